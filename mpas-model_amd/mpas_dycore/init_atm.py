@@ -1,0 +1,428 @@
+"""Synthetic initial state and mesh-coefficient precompute for the dycore.
+
+This is SURVEY.md §8(f) row 1 (the initial-state and mesh-coefficient pipeline),
+restated in numpy so the GPU box (which never sees /root/reference) can build
+the synthetic inputs of BASELINE.json's configs on its own:
+
+* vertical grid and metrics       -- core_init_atmosphere/mpas_init_atm_cases.F:615-706
+* Jablonowski-Williamson state    -- mpas_init_atm_cases.F:367-1160 (``rebalance``
+                                     replaced by the analytic JW wind, the path the
+                                     reference takes with rebalance=.false., 1005-1011)
+* zb / zb3 terrain flux metrics   -- mpas_init_atm_cases.F:1045-1093
+* deriv_two (quadratic LSQ fit)   -- core_init_atmosphere/mpas_atm_advection.F:21-394
+* defc_a / defc_b                 -- core_init_atmosphere/mpas_atm_advection.F:744-946
+* signs, zb_cell, kiteForCell     -- core_atmosphere/mpas_atm_core.F:987-1074
+* adv_coefs compression           -- core_atmosphere/mpas_atm_core.F:1121-1266
+* couple_coef_3rd_order           -- core_atmosphere/mpas_atm_core.F:1269-1288
+* damping coefficients (dss)      -- core_atmosphere/mpas_atm_core.F:1077-1118
+* mesh scaling                    -- core_atmosphere/mpas_atm_core.F:927-984
+* inverses                        -- core_atmosphere/mpas_atm_core.F:339-353
+
+These are *inputs* of the hot path; the oracle (the compiled reference Fortran)
+and the HIP product both consume exactly the arrays produced here, so their
+fidelity to the reference init affects realism, not parity.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .mesh import _normalize, arc_length
+
+# mpas_constants.F:25-36 (all promoted to double by -fdefault-real-8)
+PII = 3.141592653589793
+OMEGA = 7.29212e-5
+GRAVITY = 9.80616
+RGAS = 287.0
+RV = 461.6
+RVORD = RV / RGAS
+CP = 7.0 * RGAS / 2.0
+CV = CP - RGAS
+P0 = 1.0e5
+
+DEFAULT_CONFIG = dict(
+    config_time_integration_order=2, config_dt=720.0, config_split_dynamics_transport=True,
+    config_number_of_sub_steps=2, config_dynamics_split_steps=3,
+    config_h_mom_eddy_visc2=0.0, config_h_mom_eddy_visc4=0.0, config_v_mom_eddy_visc2=0.0,
+    config_h_theta_eddy_visc2=0.0, config_h_theta_eddy_visc4=0.0, config_v_theta_eddy_visc2=0.0,
+    config_horiz_mixing="2d_smagorinsky", config_len_disp=120000.0, config_visc4_2dsmag=0.05,
+    config_del4u_div_factor=10.0, config_scalar_advection=True, config_positive_definite=False,
+    config_monotonic=True, config_coef_3rd_order=0.25, config_smagorinsky_coef=0.125,
+    config_mix_full=True, config_epssm=0.1, config_smdiv=0.1, config_apvm_upwinding=0.5,
+    config_h_ScaleWithMesh=True, config_zd=22000.0, config_xnutr=0.2, config_mpas_cam_coef=0.0,
+    config_rayleigh_damp_u=False, config_rayleigh_damp_u_timescale_days=5.0,
+    config_number_rayleigh_damp_u_levels=6,
+)  # Registry.xml:56-290 defaults
+
+
+def vertical_grid(K: int, zt: float = 45000.0):
+    """mpas_init_atm_cases.F:615-678 (uniform dzeta, str=1.5 stretching)."""
+    nz1, nz = K, K + 1
+    dz = zt / float(nz1)
+    k = np.arange(nz)
+    sh = (k * dz / zt) ** 1.5
+    zw = k * dz
+    ah = 1.0 - np.cos(0.5 * PII * k * dz / zt) ** 6
+    dzw = zw[1:] - zw[:-1]
+    rdzw = 1.0 / dzw
+    dzu = np.zeros(nz1)
+    rdzu = np.zeros(nz1)
+    fzp = np.zeros(nz1)
+    fzm = np.zeros(nz1)
+    dzu[1:] = 0.5 * (dzw[1:] + dzw[:-1])
+    rdzu[1:] = 1.0 / dzu[1:]
+    fzp[1:] = 0.5 * dzw[1:] / dzu[1:]
+    fzm[1:] = 0.5 * dzw[:-1] / dzu[1:]
+    cof1 = (2.0 * dzu[1] + dzu[2]) / (dzu[1] + dzu[2]) * dzw[0] / dzu[1]
+    cof2 = dzu[1] / (dzu[1] + dzu[2]) * dzw[0] / dzu[2]
+    cf1 = fzp[1] + cof1
+    cf2 = fzm[1] - cof1 - cof2
+    cf3 = cof2
+    return dict(zt=zt, sh=sh, zw=zw, ah=ah, dzw=dzw, rdzw=rdzw, dzu=dzu, rdzu=rdzu,
+                fzp=fzp, fzm=fzm, cf1=cf1, cf2=cf2, cf3=cf3)
+
+
+def _jw_hx(phi, r_earth):
+    u0 = 35.0
+    etavs = (1.0 - 0.252) * PII / 2.0
+    return (u0 / GRAVITY * np.cos(etavs) ** 1.5
+            * ((-2.0 * np.sin(phi) ** 6 * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0)
+               * u0 * np.cos(etavs) ** 1.5
+               + (1.6 * np.cos(phi) ** 3 * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * r_earth * OMEGA))
+
+
+def _local_frame(c):
+    ez = np.array([0.0, 0.0, 1.0])
+    e1 = np.cross(ez, c)
+    bad = np.linalg.norm(e1, axis=-1) < 1e-8
+    if np.any(bad):
+        e1[bad] = np.cross(np.array([1.0, 0.0, 0.0]), c[bad])
+    e1 = _normalize(e1)
+    e2 = np.cross(c, e1)
+    return e1, e2
+
+
+def _azimuth(c, p, e1, e2):
+    d = p - c
+    return np.arctan2(np.sum(d * e2, -1), np.sum(d * e1, -1))
+
+
+def compute_deriv_two(m):
+    """Quadratic least-squares second derivative along each edge normal
+    (mpas_atm_advection.F:92-392, polynomial_order = 2).  deriv_two[e, side, j]:
+    j=0 the cell itself, j=i+1 its neighbour cellsOnCell(i)."""
+    nC, nE, R = m["nCells"], m["nEdges"], m["sphere_radius"]
+    xc = np.stack([m["xCell"], m["yCell"], m["zCell"]], 1) / R
+    xv = np.stack([m["xVertex"], m["yVertex"], m["zVertex"]], 1) / R
+    nEoC, coc, eoc, coe, voe = m["nEdgesOnCell"], m["cellsOnCell"], m["edgesOnCell"], m["cellsOnEdge"], m["verticesOnEdge"]
+    d2 = np.zeros((nE, 2, 15))
+    e1, e2 = _local_frame(xc)
+    for n in np.unique(nEoC):
+        cells = np.nonzero(nEoC == n)[0]
+        c = xc[cells]
+        nb = xc[coc[cells, :n]]                                  # (nc, n, 3)
+        th = _azimuth(c[:, None, :], nb, e1[cells][:, None, :], e2[cells][:, None, :])
+        dl = R * arc_length(c[:, None, :], nb)
+        xp, yp = np.cos(th) * dl, np.sin(th) * dl
+        A = np.zeros((len(cells), n + 1, 6))
+        A[:, 0, 0] = 1.0
+        A[:, 1:, 0] = 1.0
+        A[:, 1:, 1] = xp
+        A[:, 1:, 2] = yp
+        A[:, 1:, 3] = xp ** 2
+        A[:, 1:, 4] = xp * yp
+        A[:, 1:, 5] = yp ** 2
+        B = np.linalg.pinv(A)                                     # (nc, 6, n+1)
+        for i in range(n):
+            e = eoc[cells, i]
+            mid = _normalize(xv[voe[e, 0]] + xv[voe[e, 1]])       # arc_bisect of the edge's vertices
+            the = _azimuth(c, mid, e1[cells], e2[cells])
+            cs, sn = np.cos(the), np.sin(the)
+            val = 2.0 * cs[:, None] ** 2 * B[:, 3, :] + 2.0 * cs[:, None] * sn[:, None] * B[:, 4, :] \
+                + 2.0 * sn[:, None] ** 2 * B[:, 5, :]
+            side = np.where(coe[e, 0] == cells, 0, 1)
+            d2[e, side, :n + 1] = val
+    return d2
+
+
+def compute_defc(m):
+    """Deformation weights defc_a/defc_b (mpas_atm_advection.F:802-946)."""
+    nC, R = m["nCells"], m["sphere_radius"]
+    xc = np.stack([m["xCell"], m["yCell"], m["zCell"]], 1) / R
+    xv = np.stack([m["xVertex"], m["yVertex"], m["zVertex"]], 1) / R
+    nEoC, voc, eoc, coe = m["nEdgesOnCell"], m["verticesOnCell"], m["edgesOnCell"], m["cellsOnEdge"]
+    maxE = m["maxEdges"]
+    defc_a = np.zeros((nC, maxE))
+    defc_b = np.zeros((nC, maxE))
+    e1, e2 = _local_frame(xc)
+    for n in np.unique(nEoC):
+        cells = np.nonzero(nEoC == n)[0]
+        c = xc[cells]
+        vv = xv[voc[cells, :n]]
+        th = _azimuth(c[:, None, :], vv, e1[cells][:, None, :], e2[cells][:, None, :])
+        dl = R * arc_length(c[:, None, :], vv)
+        xp, yp = np.cos(th) * dl, np.sin(th) * dl
+        ip1 = (np.arange(n) + 1) % n
+        dx = xp[:, ip1] - xp
+        dy = yp[:, ip1] - yp
+        thetat = np.arctan2(dy, dx)                               # direction of segment i -> i+1
+        dls = np.sqrt(dx ** 2 + dy ** 2)
+        area = np.sum(0.25 * (xp + xp[:, ip1]) * dy - 0.25 * (yp + yp[:, ip1]) * dx, axis=1)
+        s2, c2, sc = np.sin(thetat) ** 2, np.cos(thetat) ** 2, np.sin(thetat) * np.cos(thetat)
+        a = dls * (c2 - s2) / area[:, None]
+        b = dls * 2.0 * sc / area[:, None]
+        flip = coe[eoc[cells, :n], 0] != cells[:, None]
+        a[flip] *= -1.0
+        b[flip] *= -1.0
+        defc_a[cells, :n] = a
+        defc_b[cells, :n] = b
+    return defc_a, defc_b
+
+
+def adv_coef_compression(m, d2):
+    """mpas_atm_core.F:1154-1264, vectorised over edges."""
+    nE, maxE = m["nEdges"], m["maxEdges"]
+    coe, coc, nEoC, dc, dv = m["cellsOnEdge"], m["cellsOnCell"], m["nEdgesOnCell"], m["dcEdge"], m["dvEdge"]
+    c1, c2 = coe[:, 0], coe[:, 1]
+    lst = -np.ones((nE, 15), dtype=np.int64)
+    lst[:, 0], lst[:, 1] = c1, c2
+    n = np.full(nE, 2)
+    ar = np.arange(nE)
+    for i in range(maxE):
+        cc = coc[c1, i]
+        add = (i < nEoC[c1]) & (cc != c2)
+        lst[ar[add], n[add]] = cc[add]
+        n = n + add
+    for i in range(maxE):
+        cc = coc[c2, i]
+        valid = i < nEoC[c2]
+        present = np.any(lst == cc[:, None], axis=1)
+        add = valid & ~present
+        lst[ar[add], n[add]] = cc[add]
+        n = n + add
+    coef = np.zeros((nE, 15))
+    coef3 = np.zeros((nE, 15))
+
+    def jpos(cell):
+        return np.argmax(lst == cell[:, None], axis=1)
+
+    j = jpos(c1)
+    coef[ar, j] += d2[:, 0, 0]
+    coef3[ar, j] += d2[:, 0, 0]
+    for i in range(maxE):
+        v = i < nEoC[c1]
+        j = jpos(coc[c1, i])
+        coef[ar[v], j[v]] += d2[v, 0, i + 1]
+        coef3[ar[v], j[v]] += d2[v, 0, i + 1]
+    j = jpos(c2)
+    coef[ar, j] += d2[:, 1, 0]
+    coef3[ar, j] -= d2[:, 1, 0]
+    for i in range(maxE):
+        v = i < nEoC[c2]
+        j = jpos(coc[c2, i])
+        coef[ar[v], j[v]] += d2[v, 1, i + 1]
+        coef3[ar[v], j[v]] -= d2[v, 1, i + 1]
+    coef = -(dc[:, None] ** 2) * coef / 12.0
+    coef3 = -(dc[:, None] ** 2) * coef3 / 12.0
+    coef[ar, jpos(c1)] += 0.5
+    coef[ar, jpos(c2)] += 0.5
+    coef *= dv[:, None]
+    coef3 *= dv[:, None]
+    mask = np.arange(15)[None, :] < n[:, None]
+    return n, np.where(mask, lst, -1), np.where(mask, coef, 0.0), np.where(mask, coef3, 0.0)
+
+
+def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: dict | None = None,
+               init_case: int = 2) -> dict:
+    """Build every mesh/state/diag input array of the dycore for the JW case.
+
+    Returns a flat dict keyed by MPAS field name (0-based index arrays, element-major
+    (n, K) float arrays, i.e. the transpose of the Fortran (K, n) layout)."""
+    cfg = dict(DEFAULT_CONFIG)
+    if config:
+        cfg.update(config)
+    nC, nE, nV, R = m["nCells"], m["nEdges"], m["nVertices"], m["sphere_radius"]
+    vg = vertical_grid(K)
+    nz1, nz = K, K + 1
+    lat = m["latCell"]
+    coe, voe = m["cellsOnEdge"], m["verticesOnEdge"]
+    c1, c2 = coe[:, 0], coe[:, 1]
+
+    # ---- metrics (mpas_init_atm_cases.F:603-696)
+    hx = _jw_hx(lat, R)
+    zgrid = (1.0 - vg["ah"])[None, :] * (vg["sh"][None, :] * (vg["zt"] - hx[:, None]) + hx[:, None]) \
+        + vg["ah"][None, :] * vg["sh"][None, :] * vg["zt"]                          # (nC, K+1)
+    zz = (vg["zw"][1:] - vg["zw"][:-1])[None, :] / (zgrid[:, 1:] - zgrid[:, :-1])   # (nC, K)
+    zxu = 0.5 * (zgrid[c2, :-1] - zgrid[c1, :-1] + zgrid[c2, 1:] - zgrid[c1, 1:]) / m["dcEdge"][:, None]
+
+    # ---- JW thermodynamic state (mpas_init_atm_cases.F:839-958), vectorised over cells
+    u0, t0b, t0, delta_t, dtdz, eta_t = 35.0, 250.0, 288.0, 4.8e5, 0.005, 0.2
+    znut = eta_t
+    ztemp = 0.5 * (zgrid[:, 1:] + zgrid[:, :-1])
+    ppb = P0 * np.exp(-GRAVITY * ztemp / (RGAS * t0b))
+    pb = (ppb / P0) ** (RGAS / CP)
+    rb = ppb / (RGAS * t0b * zz)
+    tb = t0b / pb
+    pp = np.zeros_like(ppb)
+    rr = np.zeros_like(ppb)
+    qv = np.zeros_like(ppb)
+    phi = lat[:, None]
+    dzw, dzu, fzp, fzm = vg["dzw"], vg["dzu"], vg["fzp"], vg["fzm"]
+    for _ in range(10):
+        eta = (ppb + pp) / P0
+        etav = (eta - 0.252) * PII / 2.0
+        teta = t0 * eta ** (RGAS * dtdz / GRAVITY) + np.where(eta >= znut, 0.0, delta_t * (znut - eta) ** 5)
+        temperature = teta + 0.75 * eta * PII * u0 / RGAS * np.sin(etav) * np.sqrt(np.cos(etav)) * (
+            (-2.0 * np.sin(phi) ** 6 * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0) * 2.0 * u0 * np.cos(etav) ** 1.5
+            + (1.6 * np.cos(phi) ** 3 * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * R * OMEGA) / (1.0 + 0.61 * qv)
+        if moist:
+            ptemp = ppb + pp
+            relhum = np.where(ptemp < 50000.0, 0.0, np.where(ptemp > P0, 1.0, 1.0 - ((P0 - ptemp) / 50000.0) ** 1.25))
+            relhum = np.minimum(0.40, relhum)
+            es = np.where(temperature > 273.15,
+                          1000.0 * 0.6112 * np.exp(17.67 * (temperature - 273.15) / (temperature - 29.65)),
+                          1000.0 * 0.6112 * np.exp(21.8745584 * (temperature - 273.15) / (temperature - 7.66)))
+            qsat = (287.04 / 461.6) * es / (ptemp - es)
+            qsat = np.where(relhum == 0.0, 0.0, qsat)
+            qv = relhum * qsat
+        tt = temperature * (1.0 + 1.61 * qv)
+        for _ in range(25):
+            rr = (pp / (RGAS * zz) - rb * (tt - t0b)) / tt
+            ppi = np.zeros_like(pp)
+            ppi[:, 0] = P0 - 0.5 * dzw[0] * GRAVITY * (1.25 * (rr[:, 0] + rb[:, 0]) * (1.0 + qv[:, 0])
+                                                       - 0.25 * (rr[:, 1] + rb[:, 1]) * (1.0 + qv[:, 1]))
+            ppi[:, 0] -= ppb[:, 0]
+            for k in range(nz1 - 1):
+                ppi[:, k + 1] = ppi[:, k] - dzu[k + 1] * GRAVITY * (
+                    (rr[:, k] + (rr[:, k] + rb[:, k]) * qv[:, k]) * fzp[k + 1]
+                    + (rr[:, k + 1] + (rr[:, k + 1] + rb[:, k + 1]) * qv[:, k + 1]) * fzm[k + 1])
+            pp = 0.2 * ppi + 0.8 * pp
+    p = ((ppb + pp) / P0) ** (RGAS / CP)
+    t = tt / p
+    rho_zz = rb + rr
+
+    # ---- wind (analytic JW flux, mpas_init_atm_cases.F:974-1019)
+    latV = m["latVertex"]
+    lat1, lat2 = latV[voe[:, 0]], latV[voe[:, 1]]
+    flux = (0.5 * (lat2 - lat1) - 0.125 * (np.sin(4.0 * lat2) - np.sin(4.0 * lat1))) * R / m["dvEdge"]
+    if init_case == 2:
+        lat_pert, lon_pert = 40.0 * PII / 180.0, 20.0 * PII / 180.0
+        le, lo = m["latEdge"], m["lonEdge"]
+        arg = np.sin(le) * np.sin(lat_pert) + np.cos(le) * np.cos(lat_pert) * np.cos(lo - lon_pert)
+        r_pert = np.arccos(np.clip(arg, -1.0, 1.0)) / 0.1
+        u_pert = 1.0 * np.exp(-r_pert ** 2) * (lat2 - lat1) * R / m["dvEdge"]
+    else:
+        u_pert = np.zeros(nE)
+    etavs = (0.5 * (ppb[c1] + ppb[c2] + pp[c1] + pp[c2]) / P0 - 0.252) * PII / 2.0
+    u = u0 * flux[:, None] * np.cos(etavs) ** 1.5 + u_pert[:, None]
+    ru = 0.5 * (rho_zz[c1] + rho_zz[c2]) * u
+
+    fEdge = 2.0 * OMEGA * np.sin(m["latEdge"])
+    fVertex = 2.0 * OMEGA * np.sin(m["latVertex"])
+
+    # ---- deriv_two, zb/zb3 (mpas_init_atm_cases.F:1045-1093, theta_adv_order = 3)
+    d2 = compute_deriv_two(m)
+    nEoC, coc, eoc = m["nEdgesOnCell"], m["cellsOnCell"], m["edgesOnCell"]
+    d2c1 = d2[:, 0, 0][:, None] * zgrid[c1]
+    d2c2 = d2[:, 1, 0][:, None] * zgrid[c2]
+    for i in range(m["maxEdges"]):
+        v1 = (i < nEoC[c1])[:, None]
+        v2 = (i < nEoC[c2])[:, None]
+        d2c1 = d2c1 + np.where(v1, d2[:, 0, i + 1][:, None] * zgrid[coc[c1, i]], 0.0)
+        d2c2 = d2c2 + np.where(v2, d2[:, 1, i + 1][:, None] * zgrid[coc[c2, i]], 0.0)
+    dcE = m["dcEdge"][:, None]
+    z_edge = 0.5 * (zgrid[c1] + zgrid[c2]) - dcE ** 2 * (d2c1 + d2c2) / 12.0
+    z_edge3 = -dcE ** 2 * (d2c1 - d2c2) / 12.0
+    dvA1 = (m["dvEdge"] / m["areaCell"][c1])[:, None]
+    dvA2 = (m["dvEdge"] / m["areaCell"][c2])[:, None]
+    zb = np.zeros((nE, 2, nz))
+    zb3 = np.zeros((nE, 2, nz))
+    zb[:, 0, :nz1] = ((z_edge - zgrid[c1]) * dvA1)[:, :nz1]
+    zb[:, 1, :nz1] = ((z_edge - zgrid[c2]) * dvA2)[:, :nz1]
+    zb3[:, 0, :nz1] = (z_edge3 * dvA1)[:, :nz1]
+    zb3[:, 1, :nz1] = (z_edge3 * dvA2)[:, :nz1]
+
+    # ---- rw / w from terrain (mpas_init_atm_cases.F:1096-1126)
+    coef3 = cfg["config_coef_3rd_order"]
+    rw = np.zeros((nC, nz))
+    for k in range(1, nz1):
+        fl = fzm[k] * ru[:, k] + fzp[k] * ru[:, k - 1]
+        z2 = fzm[k] * zz[c2, k] + fzp[k] * zz[c2, k - 1]
+        z1 = fzm[k] * zz[c1, k] + fzp[k] * zz[c1, k - 1]
+        sg = np.copysign(1.0, ru[:, k])
+        np.add.at(rw[:, k], c2, z2 * zb[:, 1, k] * fl - sg * coef3 * z2 * zb3[:, 1, k] * fl)
+        np.add.at(rw[:, k], c1, -z1 * zb[:, 0, k] * fl + sg * coef3 * z1 * zb3[:, 0, k] * fl)
+    w = np.zeros((nC, nz))
+    w[:, 1:nz1] = rw[:, 1:nz1] / (fzp[1:] * rho_zz[:, :-1] + fzm[1:] * rho_zz[:, 1:])
+
+    rho = rho_zz * zz
+    theta = t / (1.0 + 1.61 * qv)
+
+    # ---- model-init precompute (mpas_atm_core.F)
+    edgesOnCell_sign = np.zeros((nC, m["maxEdges"]))
+    zb_cell = np.zeros((nC, m["maxEdges"], nz))
+    zb3_cell = np.zeros((nC, m["maxEdges"], nz))
+    kiteForCell = np.zeros((nC, m["maxEdges"]), dtype=np.int64)
+    ac = np.arange(nC)
+    for i in range(m["maxEdges"]):
+        has = i < nEoC
+        e = np.where(has, eoc[:, i], 0)
+        first = coe[e, 0] == ac
+        edgesOnCell_sign[:, i] = np.where(has, np.where(first, 1.0, -1.0), 0.0)
+        side = np.where(first, 0, 1)
+        zb_cell[:, i, :] = np.where(has[:, None], zb[e, side, :], 0.0)
+        zb3_cell[:, i, :] = np.where(has[:, None], zb3[e, side, :], 0.0)
+        v = np.where(has, m["verticesOnCell"][:, i], 0)
+        kf = np.zeros(nC, dtype=np.int64)
+        for j in range(2, -1, -1):
+            kf = np.where(m["cellsOnVertex"][v, j] == ac, j, kf)
+        kiteForCell[:, i] = np.where(has, kf, 0)          # 0-based (Fortran value - 1)
+    eov = m["edgesOnVertex"]
+    edgesOnVertex_sign = np.where(voe[eov, 1] == np.arange(nV)[:, None], 1.0, -1.0)
+
+    nAdv, advCells, adv_coefs, adv_coefs_3rd = adv_coef_compression(m, d2)
+    adv_coefs_3rd = coef3 * adv_coefs_3rd
+    zb3_cell = coef3 * zb3_cell
+    defc_a, defc_b = compute_defc(m)
+
+    # damping (mpas_atm_core.F:1105-1116)
+    zt_c = zgrid[:, nz1]
+    zmid = 0.5 * (zgrid[:, :-1] + zgrid[:, 1:])
+    zd, xnutr = cfg["config_zd"], cfg["config_xnutr"]
+    dss = np.where(zmid > zd, xnutr * np.sin(0.5 * PII * (zmid - zd) / (zt_c[:, None] - zd)) ** 2.0, 0.0)
+    dss = dss / m["meshDensity"][:, None] ** 0.25
+    md = m["meshDensity"]
+    if cfg["config_h_ScaleWithMesh"]:
+        msd2 = 1.0 / ((md[c1] + md[c2]) / 2.0) ** 0.25
+        msd4 = 1.0 / ((md[c1] + md[c2]) / 2.0) ** 0.75
+    else:
+        msd2 = np.ones(nE)
+        msd4 = np.ones(nE)
+
+    scalars = np.zeros((nC, nz1, ns))
+    if ns >= 1:
+        scalars[:, :, 0] = qv
+    if ns > 1:
+        # smooth positive blobs so the monotonic limiter is exercised
+        xc = np.stack([m["xCell"], m["yCell"], m["zCell"]], 1) / R
+        rng = np.random.default_rng(20250202)
+        for s in range(1, ns):
+            ctr = _normalize(rng.normal(size=3))
+            d = arc_length(xc, np.broadcast_to(ctr, xc.shape))
+            prof = np.exp(-((np.arange(nz1) - nz1 * 0.3) / (0.15 * nz1)) ** 2)
+            scalars[:, :, s] = 1.0e-3 * np.exp(-(d / 0.5) ** 2)[:, None] * prof[None, :]
+
+    out = dict(m)
+    out.update(
+        nVertLevels=K, num_scalars=ns, config=cfg,
+        zgrid=zgrid, zz=zz, zxu=zxu, rdzw=vg["rdzw"], rdzu=vg["rdzu"], fzm=fzm, fzp=fzp,
+        cf1=vg["cf1"], cf2=vg["cf2"], cf3=vg["cf3"], dss=dss,
+        fEdge=fEdge, fVertex=fVertex, deriv_two=d2, zb=zb, zb3=zb3, zb_cell=zb_cell, zb3_cell=zb3_cell,
+        edgesOnCell_sign=edgesOnCell_sign, edgesOnVertex_sign=edgesOnVertex_sign, kiteForCell=kiteForCell,
+        nAdvCellsForEdge=nAdv, advCellsForEdge=advCells, adv_coefs=adv_coefs, adv_coefs_3rd=adv_coefs_3rd,
+        defc_a=defc_a, defc_b=defc_b, meshScalingDel2=msd2, meshScalingDel4=msd4,
+        invAreaCell=1.0 / m["areaCell"], invDvEdge=1.0 / m["dvEdge"], invDcEdge=1.0 / m["dcEdge"],
+        invAreaTriangle=1.0 / m["areaTriangle"],
+        # state (time level 1) and diag inputs of atm_init_coupled_diagnostics
+        u=u, w=w, theta=theta, rho=rho, scalars=scalars, rho_base=rb, theta_base=tb,
+    )
+    return out
