@@ -1,0 +1,114 @@
+/*
+ * mpas_dycore.h -- C ABI of the MI355X-native MPAS-Atmosphere dycore.
+ *
+ * This is the drop-in boundary behind the reference's Fortran operator API
+ * (module atm_time_integration, src/core_atmosphere/dynamics/
+ * mpas_atm_time_integration.F).  A Fortran shim module named
+ * atm_time_integration keeps the reference's public
+ * routines and binds these entry points with iso_c_binding:
+ *
+ *   atm_timestep(domain, dt, nowTime, itimestep)      mpas_atm_time_integration.F:87
+ *       -> mpas_dyc_timestep                          (atm_srk3, :142-1796)
+ *   atm_init_coupled_diagnostics(state, 1, diag, ...) mpas_atm_time_integration.F:5825
+ *   atm_compute_solve_diagnostics(dt, state, 1, ...)  mpas_atm_time_integration.F:5419
+ *       -> mpas_dyc_init_diagnostics                  (called at mpas_atm_core.F:390,399)
+ *   mpas_pool_shift_time_levels(state)                mpas_pool_routines.F:5541
+ *       -> mpas_dyc_shift_time_levels                 (called at mpas_atm_core.F:671)
+ *   mpas_pool_get_array(pool, name, ptr[, timeLevel])  mpas_pool_routines.F:4282
+ *       -> mpas_dyc_set_field / mpas_dyc_get_field    (pool-owned host memory <-> HBM)
+ *
+ * Conventions (match what the Fortran pools hold, so the shim passes pool
+ * pointers unchanged):
+ *   - real fields are fp64 Fortran memory images including the garbage slot:
+ *     u(nVertLevels, nEdges+1), w(nVertLevels+1, nCells+1),
+ *     scalars(num_scalars, nVertLevels, nCells+1), zb_cell(nVertLevels+1, maxEdges, nCells+1) ...
+ *   - integer fields are int32 with MPAS 1-based indices (n+1 = garbage slot);
+ *   - time_level is 1 or 2 for the state pool (ignored otherwise).
+ * All functions return 0 on success and a negative MPAS_DYC_E* code on error
+ * (the shim maps non-zero to mpas_log_write(..., MPAS_LOG_CRIT), which is how
+ * the reference reports fatal errors, mpas_log.F:612).  No torch types, no
+ * C++ types: plain pointers and sizes.
+ */
+#ifndef MPAS_DYCORE_H
+#define MPAS_DYCORE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPAS_DYC_OK 0
+#define MPAS_DYC_EINVAL -1    /* bad argument / unknown field / size mismatch */
+#define MPAS_DYC_EHIP -2      /* HIP runtime error */
+#define MPAS_DYC_ESTATE -3    /* call out of sequence */
+#define MPAS_DYC_ECOMM -4     /* halo exchange failure */
+
+typedef struct mpas_dyc_ctx mpas_dyc_ctx;
+
+/* Registry.xml dims (8-46) for one block; *Solve = owned counts (mpas_block_creator.F). */
+typedef struct {
+  int32_t nCells, nEdges, nVertices, nVertLevels, maxEdges, maxEdges2, num_scalars;
+  int32_t nCellsSolve, nEdgesSolve, nVerticesSolve;
+  int32_t moist_start, moist_end; /* 1-based, as in the state pool */
+  int32_t index_qv;               /* 1-based */
+} mpas_dyc_dims;
+
+/* nhyd_model namelist (Registry.xml:56-290).  Logicals as int 0/1;
+ * config_horiz_mixing: 1 = "2d_smagorinsky", 0 = "2d_fixed". */
+typedef struct {
+  int32_t config_time_integration_order, config_number_of_sub_steps, config_dynamics_split_steps;
+  int32_t config_number_rayleigh_damp_u_levels;
+  int32_t config_split_dynamics_transport, config_scalar_advection, config_positive_definite;
+  int32_t config_monotonic, config_mix_full, config_rayleigh_damp_u, config_horiz_mixing;
+  double config_h_mom_eddy_visc2, config_h_mom_eddy_visc4, config_v_mom_eddy_visc2;
+  double config_h_theta_eddy_visc2, config_h_theta_eddy_visc4, config_v_theta_eddy_visc2;
+  double config_len_disp, config_visc4_2dsmag, config_del4u_div_factor, config_coef_3rd_order;
+  double config_smagorinsky_coef, config_epssm, config_smdiv, config_apvm_upwinding;
+  double config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days;
+} mpas_dyc_config;
+
+/* Create a dycore context on HIP device `device` (-1 = current); allocates all
+ * device fields (mesh, state x2 time levels, diag, tend, module scratch). */
+int mpas_dyc_create(const mpas_dyc_dims* dims, const mpas_dyc_config* cfg, int device, mpas_dyc_ctx** out);
+void mpas_dyc_destroy(mpas_dyc_ctx* ctx);
+const char* mpas_dyc_last_error(const mpas_dyc_ctx* ctx);
+
+/* Host <-> device copy of one named pool field (pool: "mesh","state","diag","tend",
+ * "tend_physics"; scalars 0-d fields cf1/cf2/cf3 take 8 bytes). nbytes must match. */
+int mpas_dyc_set_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level,
+                       const void* host, int64_t nbytes);
+int mpas_dyc_get_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level,
+                       void* host, int64_t nbytes);
+/* Size in bytes of a field's Fortran memory image (0 if unknown). */
+int64_t mpas_dyc_field_bytes(const mpas_dyc_ctx* ctx, const char* pool, const char* name);
+/* Raw device pointer of a field (for zero-copy use from torch / RCCL); NULL if unknown. */
+void* mpas_dyc_field_device_ptr(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level);
+
+/* atm_init_coupled_diagnostics + atm_compute_solve_diagnostics on time level 1
+ * (model init, mpas_atm_core.F:387-404). */
+int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt);
+/* atm_timestep -> atm_srk3: advance time level 1 to time level 2 by dt. Asynchronous. */
+int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep);
+/* mpas_pool_shift_time_levels(state): swap time levels 1 and 2 (pointer swap). */
+int mpas_dyc_shift_time_levels(mpas_dyc_ctx* ctx);
+/* Block until all queued device work of the context is complete. */
+int mpas_dyc_synchronize(mpas_dyc_ctx* ctx);
+
+/* ---- measurement hooks (bench.py / tests) ---- */
+/* One acoustic sub-step (atm_advance_acoustic_step + atm_divergence_damping_3d) on the
+ * current state, repeated `reps` times, timed with HIP events on the compute stream.
+ * Returns the average time per sub-step in *ms_out and per-kernel averages in
+ * ms_kernels[3] = {edge phase, cell phase, divergence damping} (may be NULL). */
+int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_step, int32_t reps,
+                                double* ms_out, double* ms_kernels);
+/* Capture one full timestep in a hipGraph and replay it for subsequent
+ * mpas_dyc_timestep calls (1 = on, 0 = off). */
+int mpas_dyc_use_graph(mpas_dyc_ctx* ctx, int32_t on);
+/* Algorithmic HBM bytes of one acoustic sub-step (B_ac). */
+double mpas_dyc_acoustic_bytes(const mpas_dyc_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPAS_DYCORE_H */

@@ -1,0 +1,82 @@
+// MI355X-native MPAS split-explicit dycore: device data model shared by the
+// kernels (kernels.hip) and the host sequencer (dycore.hip).
+//
+// Layout in HBM: every MPAS array keeps its Fortran memory
+// image (K, n+1) == element-major [n+1][K] -- one contiguous column of K (or
+// K+1) fp64 levels per cell/edge/vertex, k the fast axis -- including the
+// garbage slot n+1 (device index n).  Index arrays are converted once to
+// 0-based int32 with "missing" -> n (the garbage slot).  A 64-lane wavefront
+// owns one column (lane = k), so every column read is a 448 B (K=56)
+// coalesced segment and neighbour gathers fetch whole columns.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mpas {
+
+// core_atmosphere constants: src/framework/mpas_constants.F:25-36 (promoted to double)
+constexpr double GRAVITY = 9.80616;
+constexpr double RGAS = 287.0;
+constexpr double RV = 461.6;
+constexpr double CP = 7.0 * RGAS / 2.0;
+constexpr double CV = CP - RGAS;
+constexpr double RVORD = RV / RGAS;
+constexpr double PRANDTL = 1.0;
+constexpr double P0 = 1.0e5;   // mpas_atm_time_integration.F:2985, 5907
+constexpr double SECONDS_PER_DAY = 86400.0;
+
+struct Dims {
+  int nCells, nEdges, nVertices, K, maxEdges, maxEdges2, ns;
+  int nCellsSolve, nEdgesSolve, nVerticesSolve;
+  int moist_start, moist_end;  // 0-based inclusive range of moist scalars
+};
+
+struct Config {
+  int time_integration_order, number_of_sub_steps, dynamics_split_steps;
+  int number_rayleigh_damp_u_levels;
+  int split_dynamics_transport, scalar_advection, positive_definite, monotonic, mix_full;
+  int rayleigh_damp_u, horiz_mixing_smag;  // horiz_mixing: 1 = 2d_smagorinsky, 0 = 2d_fixed
+  double h_mom_eddy_visc2, h_mom_eddy_visc4, v_mom_eddy_visc2;
+  double h_theta_eddy_visc2, h_theta_eddy_visc4, v_theta_eddy_visc2;
+  double len_disp, visc4_2dsmag, del4u_div_factor, coef_3rd_order, smagorinsky_coef;
+  double epssm, smdiv, apvm_upwinding, mpas_cam_coef, rayleigh_damp_u_timescale_days;
+};
+
+// Device pointers handed to every kernel (by value, in kernarg memory).
+// Time-level fields are resolved to tl1/tl2 on the host before each launch.
+struct Ptrs {
+  // ---- mesh: connectivity (0-based, missing -> n)
+  const int *nEdgesOnCell, *edgesOnCell, *cellsOnCell, *verticesOnCell, *kiteForCell;
+  const int *cellsOnEdge, *verticesOnEdge, *nEdgesOnEdge, *edgesOnEdge;
+  const int *nAdvCellsForEdge, *advCellsForEdge, *cellsOnVertex, *edgesOnVertex;
+  // ---- mesh: geometry / coefficients
+  const double *dcEdge, *dvEdge, *invDcEdge, *invDvEdge, *invAreaCell, *invAreaTriangle;
+  const double *fEdge, *fVertex, *meshScalingDel2, *meshScalingDel4, *specZoneMaskEdge, *specZoneMaskCell;
+  const double *fzm, *fzp, *rdzw, *rdzu;
+  const double *edgesOnCell_sign, *edgesOnVertex_sign, *kiteAreasOnVertex, *weightsOnEdge;
+  const double *adv_coefs, *adv_coefs_3rd, *defc_a, *defc_b;
+  const double *zgrid, *zz, *zxu, *dss, *zb_cell, *zb3_cell;
+  const double *u_init, *v_init, *t_init, *angleEdge;
+  double cf1, cf2, cf3;
+  // ---- state, two time levels resolved per launch
+  double *u1, *u2, *w1, *w2, *theta_m1, *theta_m2, *rho_zz1, *rho_zz2, *scalars1, *scalars2;
+  // ---- diag
+  double *theta, *rho, *rho_base, *theta_base, *rho_p, *rho_p_save, *rho_pp, *rho_zz_old_split;
+  double *rtheta_base, *rtheta_p, *rtheta_p_save, *rtheta_pp, *rtheta_pp_old;
+  double *exner, *exner_base, *pressure_base, *pressure_p, *h_divergence, *kdiff, *ke, *divergence;
+  double *pv_cell, *tend_rtheta_adv, *cqw, *cofwr, *cofwz, *cofwt, *coftz, *a_tri, *alpha_tri, *gamma_tri, *cofrz;
+  double *rw, *rw_p, *rw_save, *wwAvg, *wwAvg_split;
+  double *ru, *ruAvg, *ruAvg_split, *ru_p, *ru_save, *cqu, *rho_edge, *v, *pv_edge, *gradPVn, *gradPVt;
+  double *vorticity, *pv_vertex;
+  // ---- tend / tend_physics
+  double *tend_u, *tend_u_euler, *tend_w, *tend_w_euler, *tend_theta, *tend_theta_euler;
+  double *tend_rho, *rt_diabatic_tend, *scalars_tend, *rthdynten;
+  // ---- module scratch (mpas_atm_time_integration.F:35-71)
+  double *qtot, *tend_ru_physics, *tend_rtheta_physics, *tend_rho_physics;
+  double *delsq_theta, *delsq_w, *delsq_divergence, *delsq_u, *delsq_vorticity, *dpdz;
+  double *ke_vertex, *ke_edge, *horiz_flux_array;
+  double *s_max, *s_min, *scale_arr, *flux_arr, *flux_upwind_tmp, *flux_tmp, *wdtn, *rho_zz_int;
+  double *scalar_old_copy;
+};
+
+}  // namespace mpas

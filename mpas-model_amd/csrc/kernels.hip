@@ -1,0 +1,1313 @@
+// Hand-written CDNA4 (gfx950) HIP kernels for the MPAS-Atmosphere split-explicit
+// dycore time step (src/core_atmosphere/dynamics/mpas_atm_time_integration.F).
+//
+// Execution model: one 64-lane wavefront per column, lane = k.
+// Blocks are 256 threads = 4 columns.  Element indices are made wave-uniform
+// with readfirstlane so connectivity/geometry loads go through the scalar unit,
+// and every field access is a contiguous K*8-byte column segment.  Vertical
+// neighbours (k-1, k+1, k-2) come from cross-lane shuffles; the sequential
+// vertical recurrences (Thomas sweeps, alpha/gamma LU factors) are evaluated
+// in the reference operation order with v_readlane, so results track the
+// Fortran to rounding (parity bar: DESIGN.md §6).
+//
+// Each kernel cites the reference lines it implements.  Arithmetic keeps the
+// Fortran left-to-right expression trees -- the build
+// uses -ffp-contract=off so no FMA re-association happens either.
+#include "dycore.h"
+
+namespace mpas {
+
+#define WAVES_PER_BLOCK 4
+#define BLOCK_THREADS (64 * WAVES_PER_BLOCK)
+
+// element of this wavefront, wave-uniform (scalar register)
+__device__ __forceinline__ int wave_elem(int start) {
+  int e = start + blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+  return __builtin_amdgcn_readfirstlane(e);
+}
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// value held by lane-1 (k-1) / lane+1 (k+1); lanes at the ends get garbage that callers never use
+__device__ __forceinline__ double up1(double x) { return __shfl_up(x, 1, 64); }
+__device__ __forceinline__ double dn1(double x) { return __shfl_down(x, 1, 64); }
+__device__ __forceinline__ double up2(double x) { return __shfl_up(x, 2, 64); }
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// Fortran sign(1.0_RKIND, x): IEEE copysign semantics
+__device__ __forceinline__ double sgn1(double x) { return copysign(1.0, x); }
+
+// statement functions flux4/flux3, mpas_atm_time_integration.F:3326-3331 (same trees at 3717, 4655)
+__device__ __forceinline__ double flux4(double q_im2, double q_im1, double q_i, double q_ip1, double ua) {
+  return ua * (7.0 * (q_i + q_im1) - (q_ip1 + q_im2)) / 12.0;
+}
+__device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, double q_ip1, double ua, double coef3) {
+  return flux4(q_im2, q_im1, q_i, q_ip1, ua) + coef3 * fabs(ua) * ((q_ip1 - q_im2) - 3.0 * (q_i - q_im1)) / 12.0;
+}
+
+#define LD(p, i) (act ? (p)[(i)] : 0.0)
+#define LDW(p, i) (actw ? (p)[(i)] : 0.0)
+
+// ============================================================================
+// atm_compute_moist_coefficients  (mpas_atm_time_integration.F:1899-1931)
+// ============================================================================
+__global__ __launch_bounds__(BLOCK_THREADS) void k_moist_cells(Dims d, Ptrs p) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  double q = 0.0;
+  if (act) {
+    const double* s = p.scalars2 + ((size_t)c * K + k) * d.ns;
+    for (int iq = d.moist_start; iq <= d.moist_end; ++iq) q = q + s[iq];
+    p.qtot[(size_t)c * K + k] = q;
+  }
+  double qm = up1(q);
+  if (act && k >= 1) {
+    double qtotal = 0.5 * (q + qm);
+    p.cqw[(size_t)c * K + k] = 1.0 / (1.0 + qtotal);
+  }
+}
+
+__global__ __launch_bounds__(BLOCK_THREADS) void k_moist_edges(Dims d, Ptrs p) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const double* s1 = p.scalars2 + ((size_t)c1 * K + k) * d.ns;
+  const double* s2 = p.scalars2 + ((size_t)c2 * K + k) * d.ns;
+  double qtotal = 0.0;
+  for (int iq = d.moist_start; iq <= d.moist_end; ++iq) qtotal = qtotal + 0.5 * (s1[iq] + s2[iq]);
+  p.cqu[(size_t)e * K + k] = 1.0 / (1.0 + qtotal);
+}
+
+// ============================================================================
+// atm_compute_vert_imp_coefs_work  (mpas_atm_time_integration.F:2064-2129)
+// ============================================================================
+__global__ __launch_bounds__(BLOCK_THREADS) void k_vert_imp_coefs(Dims d, Ptrs p, double dts, double epssm) {
+  const int c = wave_elem(0);
+  const int k = lane_id(), K = d.K;
+  const double dtseps = .5 * dts * (1. + epssm);
+  const double rcv = RGAS / (CP - RGAS);
+  const double c2 = CP * rcv;
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)K) p.cofrz[threadIdx.x] = dtseps * p.rdzw[threadIdx.x];
+  if (c >= d.nCellsSolve) return;
+  const bool act = k < K;
+  const size_t o = (size_t)c * K + k;
+  const double zz = LD(p.zz, o), pp = LD(p.exner, o), t = LD(p.theta_m2, o);
+  const double rb = LD(p.rho_base, o), rtb = LD(p.rtheta_base, o), pb = LD(p.exner_base, o);
+  const double rt = LD(p.rtheta_p, o), cqw = LD(p.cqw, o), qtot = LD(p.qtot, o);
+  const double fzm = act ? p.fzm[k] : 0.0, fzp = act ? p.fzp[k] : 0.0;
+  const double rdzu = act ? p.rdzu[k] : 0.0, rdzw = act ? p.rdzw[k] : 0.0;
+  const double zzm = up1(zz), pm = up1(pp), tm = up1(t);
+  double cofwr = 0.0, cofwz = 0.0, coftz = 0.0;
+  if (act && k >= 1) {
+    cofwr = .5 * dtseps * GRAVITY * (fzm * zz + fzp * zzm);
+    cofwz = dtseps * c2 * (fzm * zz + fzp * zzm) * rdzu * cqw * (fzm * pp + fzp * pm);
+    coftz = dtseps * (fzm * t + fzp * tm);
+  }
+  double cofwt = 0.0;
+  if (act) cofwt = .5 * dtseps * rcv * zz * GRAVITY * rb / (1. + qtot) * pp / ((rtb + rt) * pb);
+  // k+1 / k-1 neighbours
+  const double coftz_p = dn1(coftz), coftz_m = up1(coftz);
+  const double cofwt_m = up1(cofwt), rdzw_m = up1(rdzw);
+  const double cofrz = dtseps * rdzw, cofrz_m = up1(cofrz);
+  double a = 0.0, b = 1.0, cc = 0.0;
+  if (act && k >= 1) {
+    a = -cofwz * coftz_m * rdzw_m * zzm + cofwr * cofrz_m - cofwt_m * coftz_m * rdzw_m;
+    b = 1. + cofwz * (coftz * rdzw * zz + coftz * rdzw_m * zzm) - coftz * (cofwt * rdzw - cofwt_m * rdzw_m) +
+        cofwr * (cofrz - cofrz_m);
+    cc = -cofwz * coftz_p * rdzw * zz - cofwr * cofrz + cofwt * coftz_p * rdzw;
+  }
+  // sequential LU recurrence in the reference order (2124-2127)
+  double alpha = 0.0, gamma = 0.0;
+  for (int kk = 1; kk < K; ++kk) {
+    const double gp = readlane_d(gamma, kk - 1);
+    if (k == kk) {
+      alpha = 1. / (b - a * gp);
+      gamma = cc * alpha;
+    }
+  }
+  if (act) {
+    if (k >= 1) {
+      p.cofwr[o] = cofwr;
+      p.cofwz[o] = cofwz;
+    }
+    p.cofwt[o] = cofwt;
+    p.a_tri[o] = a;
+    p.alpha_tri[o] = alpha;
+    p.gamma_tri[o] = gamma;
+  }
+  if (k <= K) p.coftz[(size_t)c * (K + 1) + k] = coftz;  // coftz(1) = coftz(K+1) = 0
+}
+
+// ============================================================================
+// atm_compute_dyn_tend_work  (mpas_atm_time_integration.F:4663-5414)
+// ============================================================================
+struct DynTendScal {
+  int rk_step;
+  double dt, invDt, h_mom_eddy_visc4, h_theta_eddy_visc4, coef_3rd_order, c_s;
+  double rayleigh_coef_inverse;
+};
+
+// cells (all): 2d Smagorinsky kdiff + cam filter (rk1, 4677-4720); h_divergence (4729-4748);
+// tend_rho and dpdz (rk1, 4755-4766)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells1(Dims d, Ptrs p, Config cf, DynTendScal s) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const size_t o = (size_t)c * K + k;
+  const int ne = p.nEdgesOnCell[c];
+  if (s.rk_step == 1 && act) {
+    double kd;
+    if (cf.horiz_mixing_smag) {
+      double d_diag = 0.0, d_off = 0.0;
+      for (int i = 0; i < ne; ++i) {
+        const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+        const double a = p.defc_a[c * d.maxEdges + i], bb = p.defc_b[c * d.maxEdges + i];
+        const double ue = p.u2[(size_t)e * K + k], ve = p.v[(size_t)e * K + k];
+        d_diag = d_diag + a * ue - bb * ve;
+        d_off = d_off + bb * ue + a * ve;
+      }
+      const double csl = s.c_s * cf.len_disp;
+      kd = fmin((csl * csl) * sqrt(d_diag * d_diag + d_off * d_off), (0.01 * (cf.len_disp * cf.len_disp)) * s.invDt);
+    } else {
+      kd = cf.h_theta_eddy_visc2;
+    }
+    if (cf.mpas_cam_coef > 0.0) {
+      if (k == K - 3) kd = fmax(kd, 2.0833 * cf.len_disp * cf.mpas_cam_coef);
+      if (k == K - 2) kd = fmax(kd, 2.0 * 2.0833 * cf.len_disp * cf.mpas_cam_coef);
+      if (k == K - 1) kd = fmax(kd, 4.0 * 2.0833 * cf.len_disp * cf.mpas_cam_coef);
+    }
+    p.kdiff[o] = kd;
+  }
+  double hd = 0.0;
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double edge_sign = p.edgesOnCell_sign[c * d.maxEdges + i] * p.dvEdge[e];
+    hd = hd + edge_sign * LD(p.ru, (size_t)e * K + k);
+  }
+  hd = hd * p.invAreaCell[c];
+  if (act) p.h_divergence[o] = hd;
+  if (s.rk_step == 1) {
+    const size_t ow = (size_t)c * (K + 1) + k;
+    const double rwk = (k <= K) ? p.rw[ow] : 0.0;
+    const double rwp = dn1(rwk);
+    if (act) {
+      p.tend_rho[o] = -hd - p.rdzw[k] * (rwp - rwk) + p.tend_rho_physics[o];
+      const double qt = p.qtot[o];
+      p.dpdz[o] = -GRAVITY * (p.rho_base[o] * (qt) + p.rho_p_save[o] * (1. + qt));
+    }
+  }
+}
+
+// edges: tend_u (edge-solve: PGF rk1 4781-4788, vertical transport 4792-4807, Coriolis/KE 4811-4838)
+// + rk1 del2 on all edges (4856-4883); finalize (Rayleigh + euler + physics, 5015-5036) when rk>1.
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges(Dims d, Ptrs p, Config cf, DynTendScal s, int finalize) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const size_t o = (size_t)e * K + k;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  const bool solve = e < d.nEdgesSolve;
+  double tue = act ? p.tend_u_euler[o] : 0.0;
+  const double uk = LD(p.u2, o);
+  if (solve) {
+    if (s.rk_step == 1 && act) {
+      const size_t o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
+      tue = -p.cqu[o] * ((p.pressure_p[o2] - p.pressure_p[o1]) * p.invDcEdge[e] / (.5 * (p.zz[o2] + p.zz[o1])) -
+                         0.5 * p.zxu[o] * (p.dpdz[o1] + p.dpdz[o2]));
+    }
+    // vertical transport of u: wduz(k), k = 1..K+1 on lanes 0..K
+    const double um1 = up1(uk), um2 = up2(uk), up1v = dn1(uk);
+    const double rwa = (k <= K) ? 0.5 * (p.rw[(size_t)c1 * (K + 1) + k] + p.rw[(size_t)c2 * (K + 1) + k]) : 0.0;
+    double wduz = 0.0;
+    if (k == 1 || k == K - 1) {
+      wduz = 0.5 * (p.rw[(size_t)c1 * (K + 1) + k] + p.rw[(size_t)c2 * (K + 1) + k]) * (p.fzm[k] * uk + p.fzp[k] * um1);
+    } else if (k >= 2 && k <= K - 2) {
+      wduz = flux3(um2, um1, uk, up1v, rwa, 1.0);
+    }
+    const double wduz_p = dn1(wduz);
+    double tu = act ? -p.rdzw[k] * (wduz_p - wduz) : 0.0;
+    // nonlinear Coriolis term (Ringler et al. 2009)
+    double q = 0.0;
+    const int neoe = p.nEdgesOnEdge[e];
+    const double pve = LD(p.pv_edge, o);
+    for (int j = 0; j < neoe; ++j) {
+      const int eoe = uni(p.edgesOnEdge[e * d.maxEdges2 + j]);
+      const double workpv = 0.5 * (pve + LD(p.pv_edge, (size_t)eoe * K + k));
+      q = q + p.weightsOnEdge[e * d.maxEdges2 + j] * LD(p.u2, (size_t)eoe * K + k) * workpv;
+    }
+    if (act) {
+      const size_t o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
+      tu = tu + p.rho_edge[o] * (q - (p.ke[o2] - p.ke[o1]) * p.invDcEdge[e]) -
+           uk * 0.5 * (p.h_divergence[o1] + p.h_divergence[o2]);
+    }
+    if (finalize && act) {
+      if (cf.rayleigh_damp_u && k >= K - cf.number_rayleigh_damp_u_levels) {
+        const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
+        tu = tu - p.rho_edge[o] * uk * coef;
+      }
+      tu = tu + tue + p.tend_ru_physics[o];
+    }
+    if (act) p.tend_u[o] = tu;
+  }
+  if (s.rk_step == 1 && act) {
+    // del^2 part of the del^4 filter, all edges (4858-4883)
+    const int v1 = p.verticesOnEdge[2 * e], v2 = p.verticesOnEdge[2 * e + 1];
+    const double r_dc = p.invDcEdge[e];
+    const double r_dv = fmin(p.invDvEdge[e], 4 * p.invDcEdge[e]);
+    const double u_diffusion = (p.divergence[(size_t)c2 * K + k] - p.divergence[(size_t)c1 * K + k]) * r_dc -
+                               (p.vorticity[(size_t)v2 * K + k] - p.vorticity[(size_t)v1 * K + k]) * r_dv;
+    p.delsq_u[o] = 0.0 + u_diffusion;
+    const double kdiffu = 0.5 * (p.kdiff[(size_t)c1 * K + k] + p.kdiff[(size_t)c2 * K + k]);
+    tue = tue + p.rho_edge[o] * kdiffu * u_diffusion * p.meshScalingDel2[e];
+  }
+  if (act && (s.rk_step == 1)) p.tend_u_euler[o] = tue;
+}
+
+// vertices: delsq_vorticity (4889-4898); cells: delsq_divergence (4900-4910)   [rk1, visc4>0]
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_delsq_vc(Dims d, Ptrs p) {
+  const int idx = wave_elem(0);
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  if (idx < d.nVertices) {
+    const int v = idx;
+    double dv = 0.0;
+    for (int i = 0; i < 3; ++i) {
+      const int e = uni(p.edgesOnVertex[3 * v + i]);
+      const double edge_sign = p.invAreaTriangle[v] * p.dcEdge[e] * p.edgesOnVertex_sign[3 * v + i];
+      dv = dv + edge_sign * LD(p.delsq_u, (size_t)e * K + k);
+    }
+    if (act) p.delsq_vorticity[(size_t)v * K + k] = dv;
+  } else {
+    const int c = idx - d.nVertices;
+    if (c >= d.nCells) return;
+    double dd = 0.0;
+    const double r = p.invAreaCell[c];
+    const int ne = p.nEdgesOnCell[c];
+    for (int i = 0; i < ne; ++i) {
+      const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+      const double edge_sign = r * p.dvEdge[e] * p.edgesOnCell_sign[c * d.maxEdges + i];
+      dd = dd + edge_sign * LD(p.delsq_u, (size_t)e * K + k);
+    }
+    if (act) p.delsq_divergence[(size_t)c * K + k] = dd;
+  }
+}
+
+// edge-solve, rk1: del^4 (4917-4942), vertical mixing of u (4949-5006), then finalize (5015-5036)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_rk1b(Dims d, Ptrs p, Config cf, DynTendScal s) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdgesSolve) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const size_t o = (size_t)e * K + k;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  double tue = LD(p.tend_u_euler, o);
+  const double uk = LD(p.u2, o);
+  if (s.h_mom_eddy_visc4 > 0.0 && act) {
+    const int v1 = p.verticesOnEdge[2 * e], v2 = p.verticesOnEdge[2 * e + 1];
+    const double u_mix_scale = p.meshScalingDel4[e] * s.h_mom_eddy_visc4;
+    const double r_dc = u_mix_scale * cf.del4u_div_factor * p.invDcEdge[e];
+    const double r_dv = u_mix_scale * fmin(p.invDvEdge[e], 4 * p.invDcEdge[e]);
+    const double u_diffusion =
+        p.rho_edge[o] * ((p.delsq_divergence[(size_t)c2 * K + k] - p.delsq_divergence[(size_t)c1 * K + k]) * r_dc -
+                         (p.delsq_vorticity[(size_t)v2 * K + k] - p.delsq_vorticity[(size_t)v1 * K + k]) * r_dv);
+    tue = tue - u_diffusion;
+  }
+  if (cf.v_mom_eddy_visc2 > 0.0) {
+    // lanes 1..K-2 (Fortran k = 2..K-1)
+    double um = up1(uk), upv = dn1(uk);
+    double mixm = 0.0, mix0 = 0.0, mixp = 0.0;
+    if (!cf.mix_full) {
+      const double ca = cos(p.angleEdge[e]), sa = sin(p.angleEdge[e]);
+      mix0 = act ? uk - p.u_init[k] * ca - p.v_init[k] * sa : 0.0;
+      mixm = up1(mix0);
+      mixp = dn1(mix0);
+    }
+    if (k >= 1 && k <= K - 2) {
+      const size_t K1 = K + 1;
+      const double z1 = 0.5 * (p.zgrid[c1 * K1 + k - 1] + p.zgrid[c2 * K1 + k - 1]);
+      const double z2 = 0.5 * (p.zgrid[c1 * K1 + k] + p.zgrid[c2 * K1 + k]);
+      const double z3 = 0.5 * (p.zgrid[c1 * K1 + k + 1] + p.zgrid[c2 * K1 + k + 1]);
+      const double z4 = 0.5 * (p.zgrid[c1 * K1 + k + 2] + p.zgrid[c2 * K1 + k + 2]);
+      const double zm = 0.5 * (z1 + z2), z0 = 0.5 * (z2 + z3), zp = 0.5 * (z3 + z4);
+      if (cf.mix_full)
+        tue = tue + p.rho_edge[o] * cf.v_mom_eddy_visc2 * ((upv - uk) / (zp - z0) - (uk - um) / (z0 - zm)) / (0.5 * (zp - zm));
+      else
+        tue = tue + p.rho_edge[o] * cf.v_mom_eddy_visc2 * ((mixp - mix0) / (zp - z0) - (mix0 - mixm) / (z0 - zm)) / (0.5 * (zp - zm));
+    }
+  }
+  if (!act) return;
+  p.tend_u_euler[o] = tue;
+  double tu = p.tend_u[o];
+  if (cf.rayleigh_damp_u && k >= K - cf.number_rayleigh_damp_u_levels) {
+    const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
+    tu = tu - p.rho_edge[o] * uk * coef;
+  }
+  p.tend_u[o] = tu + tue + p.tend_ru_physics[o];
+}
+
+// cells (all), rk1: del^2 for w (5107-5130) and theta (5278-5301)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells2(Dims d, Ptrs p) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const double r_areaCell = p.invAreaCell[c];
+  const int ne = p.nEdgesOnCell[c];
+  double dw = 0.0, tw = 0.0, dth = 0.0, tth = 0.0;
+  const double prandtl_inv = 1.0 / PRANDTL;
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+    const double sg = p.edgesOnCell_sign[c * d.maxEdges + i];
+    const double re = LD(p.rho_edge, (size_t)e * K + k);
+    const double re_m = up1(re);
+    const double kd1 = LD(p.kdiff, (size_t)c1 * K + k), kd2 = LD(p.kdiff, (size_t)c2 * K + k);
+    const double kd1m = up1(kd1), kd2m = up1(kd2);
+    if (act && k >= 1) {
+      const double edge_sign = 0.5 * r_areaCell * sg * p.dvEdge[e] * p.invDcEdge[e];
+      double w_turb_flux = edge_sign * (re + re_m) * (p.w2[(size_t)c2 * (K + 1) + k] - p.w2[(size_t)c1 * (K + 1) + k]);
+      dw = dw + w_turb_flux;
+      w_turb_flux = w_turb_flux * p.meshScalingDel2[e] * 0.25 * (kd1 + kd2 + kd1m + kd2m);
+      tw = tw + w_turb_flux;
+    }
+    if (act) {
+      const double edge_sign = r_areaCell * sg * p.dvEdge[e] * p.invDcEdge[e];
+      const double pr_scale = prandtl_inv * p.meshScalingDel2[e];
+      double ttf = edge_sign * (p.theta_m2[(size_t)c2 * K + k] - p.theta_m2[(size_t)c1 * K + k]) * re;
+      dth = dth + ttf;
+      ttf = ttf * 0.5 * (kd1 + kd2) * pr_scale;
+      tth = tth + ttf;
+    }
+  }
+  if (act) {
+    p.delsq_w[(size_t)c * K + k] = dw;
+    p.delsq_theta[(size_t)c * K + k] = dth;
+    p.tend_theta_euler[(size_t)c * K + k] = tth;
+  }
+  if (k <= K) p.tend_w_euler[(size_t)c * (K + 1) + k] = (act && k >= 1) ? tw : 0.0;
+}
+
+// cells (solve): w tendency (5046-5074, del4 5134-5152, 5167-5223) and theta tendency
+// (5231-5269, del4 5305-5323, 5331-5414)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Config cf, DynTendScal s) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const bool actw = k <= K;
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + k, ow = (size_t)c * K1 + k;
+  const int ne = p.nEdgesOnCell[c];
+  const double fzm = act ? p.fzm[k] : 0.0, fzp = act ? p.fzp[k] : 0.0;
+  const bool rk1 = s.rk_step == 1;
+  // ---------------- w: horizontal advection (5046-5074)
+  double tw = 0.0;
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double rue = LD(p.ru, (size_t)e * K + k);
+    const double rue_m = up1(rue);
+    const double ru_edge_w = fzm * rue + fzp * rue_m;
+    const double sgn = sgn1(ru_edge_w);
+    double flux = 0.0;
+    const int na = p.nAdvCellsForEdge[e];
+    for (int j = 0; j < na; ++j) {
+      const int ic = uni(p.advCellsForEdge[e * 15 + j]);
+      const double scalar_weight = p.adv_coefs[e * 15 + j] + sgn * p.adv_coefs_3rd[e * 15 + j];
+      flux = flux + scalar_weight * LDW(p.w2, (size_t)ic * K1 + k);
+    }
+    tw = tw - p.edgesOnCell_sign[c * d.maxEdges + i] * ru_edge_w * flux;
+  }
+  // ---------------- w euler tendency: del4 (rk1)
+  double twe = actw ? p.tend_w_euler[ow] : 0.0;
+  if (rk1 && s.h_mom_eddy_visc4 > 0.0) {
+    const double r_areaCell = s.h_mom_eddy_visc4 * p.invAreaCell[c];
+    for (int i = 0; i < ne; ++i) {
+      const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+      const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+      const double edge_sign = p.meshScalingDel4[e] * r_areaCell * p.dvEdge[e] *
+                               p.edgesOnCell_sign[c * d.maxEdges + i] * p.invDcEdge[e];
+      if (act && k >= 1) twe = twe - edge_sign * (p.delsq_w[(size_t)c2 * K + k] - p.delsq_w[(size_t)c1 * K + k]);
+    }
+  }
+  // ---------------- w: vertical advection, PGF/buoyancy (5167-5197)
+  const double wk = LDW(p.w2, ow), rwk = LDW(p.rw, ow);
+  const double wm1 = up1(wk), wm2 = up2(wk), wp1 = dn1(wk), rwm1 = up1(rwk);
+  double wdwz = 0.0;
+  if (k == 1 || k == K - 1) wdwz = 0.25 * (rwk + rwm1) * (wk + wm1);
+  else if (k >= 2 && k <= K - 2) wdwz = flux3(wm2, wm1, wk, wp1, 0.5 * (rwk + rwm1), 1.0);
+  const double wdwz_p = dn1(wdwz);
+  const double rdzu = act ? p.rdzu[k] : 0.0;
+  if (act && k >= 1) tw = tw * p.invAreaCell[c] - rdzu * (wdwz_p - wdwz);
+  const double ppk = LD(p.pressure_p, o), ppm = up1(ppk);
+  const double dpk = LD(p.dpdz, o), dpm = up1(dpk);
+  if (rk1 && act && k >= 1)
+    twe = twe - p.cqw[o] * (rdzu * (ppk - ppm) - (fzm * dpk + fzp * dpm));
+  if (rk1 && cf.v_mom_eddy_visc2 > 0.0) {
+    const double rz = LD(p.rho_zz2, o), rzm = up1(rz);
+    const double rdzw_k = act ? p.rdzw[k] : 0.0, rdzw_m = up1(rdzw_k);
+    if (act && k >= 1)
+      twe = twe + cf.v_mom_eddy_visc2 * 0.5 * (rz + rzm) * ((wp1 - wk) * rdzw_k - (wk - wm1) * rdzw_m) * rdzu;
+  }
+  if (act && k >= 1) tw = tw + twe;
+  if (actw) {
+    p.tend_w[ow] = (act && k >= 1) ? tw : 0.0;
+    if (rk1) p.tend_w_euler[ow] = twe;
+  }
+  // ---------------- theta: horizontal advection (5231-5252)
+  double tt = 0.0;
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double rue = LD(p.ru, (size_t)e * K + k);
+    const double sgn = sgn1(rue);
+    double flux = 0.0;
+    const int na = p.nAdvCellsForEdge[e];
+    for (int j = 0; j < na; ++j) {
+      const int ic = uni(p.advCellsForEdge[e * 15 + j]);
+      const double scalar_weight = p.adv_coefs[e * 15 + j] + sgn * p.adv_coefs_3rd[e * 15 + j];
+      flux = flux + scalar_weight * LD(p.theta_m2, (size_t)ic * K + k);
+    }
+    tt = tt - p.edgesOnCell_sign[c * d.maxEdges + i] * rue * flux;
+  }
+  if (!rk1) {  // perturbation flux for rtheta_pp (5256-5269)
+    for (int i = 0; i < ne; ++i) {
+      const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+      const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+      if (act) {
+        const double flux = p.edgesOnCell_sign[c * d.maxEdges + i] * p.dvEdge[e] *
+                            (p.ru_save[(size_t)e * K + k] - p.ru[(size_t)e * K + k]) * 0.5 *
+                            (p.theta_m1[(size_t)c2 * K + k] + p.theta_m1[(size_t)c1 * K + k]);
+        tt = tt - flux;
+      }
+    }
+  }
+  double tte = LD(p.tend_theta_euler, o);
+  if (rk1 && s.h_theta_eddy_visc4 > 0.0) {
+    const double r_areaCell = s.h_theta_eddy_visc4 * (1.0 / PRANDTL) * p.invAreaCell[c];
+    for (int i = 0; i < ne; ++i) {
+      const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+      const double edge_sign = p.meshScalingDel4[e] * r_areaCell * p.dvEdge[e] *
+                               p.edgesOnCell_sign[c * d.maxEdges + i] * p.invDcEdge[e];
+      const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+      if (act) tte = tte - edge_sign * (p.delsq_theta[(size_t)c2 * K + k] - p.delsq_theta[(size_t)c1 * K + k]);
+    }
+  }
+  // ---------------- theta: vertical advection (5331-5354)
+  const double th = LD(p.theta_m2, o), thm1 = up1(th), thm2 = up2(th), thp1 = dn1(th);
+  const double ths = LD(p.theta_m1, o), thsm1 = up1(ths);
+  const double rws = LDW(p.rw_save, ow);
+  double wdtz = 0.0;
+  if (k == 1) {
+    wdtz = rwk * (fzm * th + fzp * thm1);
+    wdtz = wdtz + (rws - rwk) * (fzm * ths + fzp * thsm1);
+  } else if (k >= 2 && k <= K - 2) {
+    wdtz = flux3(thm2, thm1, th, thp1, rwk, s.coef_3rd_order);
+    wdtz = wdtz + (rws - rwk) * (fzm * ths + fzp * thsm1);
+  } else if (k == K - 1) {
+    wdtz = rws * (fzm * th + fzp * thm1);
+  }
+  const double wdtz_p = dn1(wdtz);
+  if (rk1 && cf.v_theta_eddy_visc2 > 0.0) {
+    const double rz = LD(p.rho_zz2, o);
+    if (act && k >= 1 && k <= K - 2) {
+      const size_t zo = (size_t)c * K1;
+      const double z1 = p.zgrid[zo + k - 1], z2 = p.zgrid[zo + k], z3 = p.zgrid[zo + k + 1], z4 = p.zgrid[zo + k + 2];
+      const double zm = 0.5 * (z1 + z2), z0 = 0.5 * (z2 + z3), zp = 0.5 * (z3 + z4);
+      if (cf.mix_full) {
+        tte = tte + cf.v_theta_eddy_visc2 * (1.0 / PRANDTL) * rz *
+                        ((thp1 - th) / (zp - z0) - (th - thm1) / (z0 - zm)) / (0.5 * (zp - zm));
+      } else {
+        const double ti = p.t_init[o], tim = p.t_init[o - 1], tip = p.t_init[o + 1];
+        tte = tte + cf.v_theta_eddy_visc2 * (1.0 / PRANDTL) * rz *
+                        (((thp1 - tip) - (th - ti)) / (zp - z0) - ((th - ti) - (thm1 - tim)) / (z0 - zm)) / (0.5 * (zp - zm));
+      }
+    }
+  }
+  if (act) {
+    const double rz = p.rho_zz2[o];
+    tt = tt * p.invAreaCell[c] - p.rdzw[k] * (wdtz_p - wdtz);
+    p.tend_rtheta_adv[o] = tt;
+    p.rthdynten[o] = tt / rz;
+    tt = tt + rz * p.rt_diabatic_tend[o];
+    if (rk1) p.tend_theta_euler[o] = tte;
+    p.tend_theta[o] = tt + tte + p.tend_rtheta_physics[o];
+  }
+}
+
+// ============================================================================
+// atm_set_smlstep_pert_variables_work  (mpas_atm_time_integration.F:2290-2307)
+// ============================================================================
+__global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const size_t K1 = K + 1;
+  const double fzm = act ? p.fzm[k] : 0.0, fzp = act ? p.fzp[k] : 0.0;
+  double wt = (k <= K) ? p.tend_w[(size_t)c * K1 + k] : 0.0;
+  const int ne = p.nEdgesOnCell[c];
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double ut = LD(p.tend_u, (size_t)e * K + k), utm = up1(ut);
+    if (act && k >= 1) {
+      const double flux = p.edgesOnCell_sign[c * d.maxEdges + i] * (fzm * ut + fzp * utm);
+      const size_t zo = ((size_t)c * d.maxEdges + i) * K1 + k;
+      wt = wt - (p.zb_cell[zo] + sgn1(ut) * p.zb3_cell[zo]) * flux;
+    }
+  }
+  const double zz = LD(p.zz, (size_t)c * K + k), zzm = up1(zz);
+  if (act && k >= 1) p.tend_w[(size_t)c * K1 + k] = (fzm * zz + fzp * zzm) * wt;
+}
+
+// ============================================================================
+// atm_advance_acoustic_step_work  (mpas_atm_time_integration.F:2535-2721)
+// ============================================================================
+// edge phase (2540-2601): edges with >=1 owned cell
+__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const size_t o = (size_t)e * K + k;
+  if (small_step != 1) {
+    const double rcv = RGAS / (CP - RGAS);
+    const double c2v = CP * rcv;
+    const size_t o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
+    double pgrad = ((p.rtheta_pp[o2] - p.rtheta_pp[o1]) * p.invDcEdge[e]) / (.5 * (p.zz[o2] + p.zz[o1]));
+    pgrad = p.cqu[o] * 0.5 * c2v * (p.exner[o1] + p.exner[o2]) * pgrad;
+    pgrad = pgrad + 0.5 * p.zxu[o] * GRAVITY * (p.rho_pp[o1] + p.rho_pp[o2]);
+    const double rup = p.ru_p[o] + dts * (p.tend_u[o] - (1.0 - p.specZoneMaskEdge[e]) * pgrad);
+    p.ru_p[o] = rup;
+    p.ruAvg[o] = p.ruAvg[o] + rup;
+  } else {
+    const double rup = dts * p.tend_u[o];
+    p.ru_p[o] = rup;
+    p.ruAvg[o] = rup;
+  }
+}
+
+// cell phase (2603-2721): rtheta_pp_old for all cells, column solve for owned cells
+__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p, double dts, int small_step, double epssm) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K, actw = k <= K;
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + k, ow = (size_t)c * K1 + k;
+  double rtpp = LD(p.rtheta_pp, o);
+  if (act) p.rtheta_pp_old[o] = (small_step == 1) ? 0.0 : rtpp;
+  if (c >= d.nCellsSolve) return;
+  const double resm = (1.0 - epssm) / (1.0 + epssm);
+  double rhopp = LD(p.rho_pp, o), rwp = LDW(p.rw_p, ow), wwa = LDW(p.wwAvg, ow);
+  if (small_step == 1) { wwa = 0.0; rhopp = 0.0; rtpp = 0.0; rwp = 0.0; }
+  if (p.specZoneMaskCell[c] == 0.0) {
+    double ts = 0.0, rs = 0.0;
+    const int ne = p.nEdgesOnCell[c];
+    const double invA = p.invAreaCell[c];
+    for (int i = 0; i < ne; ++i) {
+      const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+      const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+      if (act) {
+        const double flux = p.edgesOnCell_sign[c * d.maxEdges + i] * dts * p.dvEdge[e] * p.ru_p[(size_t)e * K + k] * invA;
+        rs = rs - flux;
+        ts = ts - flux * 0.5 * (p.theta_m1[(size_t)c2 * K + k] + p.theta_m1[(size_t)c1 * K + k]);
+      }
+    }
+    const double cofrz = act ? p.cofrz[k] : 0.0, rdzw = act ? p.rdzw[k] : 0.0;
+    const double coftz = LDW(p.coftz, ow), coftz_p = dn1(coftz);
+    const double rwp_p = dn1(rwp);
+    if (act) {
+      rs = rhopp + dts * p.tend_rho[o] + rs - cofrz * resm * (rwp_p - rwp);
+      ts = rtpp + dts * p.tend_theta[o] + ts - resm * rdzw * (coftz_p * rwp_p - coftz * rwp);
+    }
+    if (act && k >= 1) wwa = wwa + 0.5 * (1.0 - epssm) * rwp;
+    // rw_p right-hand side (2660-2670)
+    const double zz = LD(p.zz, o), zzm = up1(zz);
+    const double tsm = up1(ts), rsm = up1(rs), rtppm = up1(rtpp), rhoppm = up1(rhopp);
+    const double cofwt = LD(p.cofwt, o), cofwtm = up1(cofwt);
+    if (act && k >= 1) {
+      rwp = rwp + dts * p.tend_w[ow] -
+            p.cofwz[o] * ((zz * ts - zzm * tsm) + resm * (zz * rtpp - zzm * rtppm)) -
+            p.cofwr[o] * ((rs + rsm) + resm * (rhopp + rhoppm)) + cofwt * (ts + resm * rtpp) +
+            cofwtm * (tsm + resm * rtppm);
+    }
+    // tridiagonal solve sweeping up and then down the column (2675-2682), reference order
+    const double a_tri = LD(p.a_tri, o), alpha_tri = LD(p.alpha_tri, o), gamma_tri = LD(p.gamma_tri, o);
+    for (int kk = 1; kk < K; ++kk) {
+      const double xm = readlane_d(rwp, kk - 1);
+      if (k == kk) rwp = (rwp - a_tri * xm) * alpha_tri;
+    }
+    for (int kk = K - 1; kk >= 0; --kk) {
+      const double xp = readlane_d(rwp, kk + 1);
+      if (k == kk) rwp = rwp - gamma_tri * xp;
+    }
+    // implicit Rayleigh damping of w (2687-2693)
+    if (act && k >= 1) {
+      const double fzm = p.fzm[k], fzp = p.fzp[k];
+      const double rz = p.rho_zz2[o], rzm = p.rho_zz2[o - 1];
+      const double dss = p.dss[o];
+      const double dd = p.rw_save[ow] - p.rw[ow];
+      rwp = (rwp + dd - dts * dss * (fzm * zz + fzp * zzm) * (fzm * rz + fzp * rzm) * p.w2[ow]) / (1.0 + dts * dss) - dd;
+      wwa = wwa + 0.5 * (1.0 + epssm) * rwp;
+    }
+    const double rwp_p2 = dn1(rwp);
+    if (act) {
+      p.rho_pp[o] = rs - cofrz * (rwp_p2 - rwp);
+      p.rtheta_pp[o] = ts - rdzw * (coftz_p * rwp_p2 - coftz * rwp);
+    }
+    if (actw) {
+      p.rw_p[ow] = rwp;
+      p.wwAvg[ow] = wwa;
+    }
+  } else {
+    // specified zone (2710-2719): regional only, masks are 0 for global meshes
+    if (act) {
+      rhopp = rhopp + dts * p.tend_rho[o];
+      rtpp = rtpp + dts * p.tend_theta[o];
+      rwp = rwp + dts * p.tend_w[ow];
+      wwa = wwa + 0.5 * (1.0 + epssm) * rwp;
+      p.rho_pp[o] = rhopp;
+      p.rtheta_pp[o] = rtpp;
+    }
+    if (actw) {
+      p.rw_p[ow] = rwp;
+      p.wwAvg[ow] = wwa;
+    }
+  }
+}
+
+// atm_divergence_damping_3d (2765-2793)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, double coef_divdamp) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const size_t o = (size_t)e * K + k, o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
+  const double divCell1 = -(p.rtheta_pp[o1] - p.rtheta_pp_old[o1]);
+  const double divCell2 = -(p.rtheta_pp[o2] - p.rtheta_pp_old[o2]);
+  p.ru_p[o] = p.ru_p[o] + coef_divdamp * (divCell2 - divCell1) * (1.0 - p.specZoneMaskEdge[e]) /
+                              (p.theta_m1[o1] + p.theta_m1[o2]);
+}
+
+// ============================================================================
+// atm_recover_large_step_variables_work  (mpas_atm_time_integration.F:2984-3097)
+// The edge loop (3048-3059) recomputes rho_zz of its two cells and the cell loops
+// recompute ru of their edges with the reference expressions (bit-identical), so
+// the three barrier-separated phases become two independent launches.
+// ============================================================================
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const size_t o = (size_t)e * K + k;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  auto rhozz = [&](int c) -> double {
+    if (c >= d.nCells) return 1.0;  // garbage cell (2989-2991)
+    const size_t oc = (size_t)c * K + k;
+    const double rho_p = p.rho_p_save[oc] + p.rho_pp[oc];
+    return rho_p + p.rho_base[oc];
+  };
+  p.ruAvg[o] = p.ru_save[o] + (p.ruAvg[o] * invNs);
+  const double ru = p.ru_save[o] + p.ru_p[o];
+  p.ru[o] = ru;
+  p.u2[o] = 2. * ru / (rhozz(c1) + rhozz(c2));
+}
+
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells(Dims d, Ptrs p, double dt, double invNs, int rk_step) {
+  const int c = wave_elem(0);
+  const int k = lane_id(), K = d.K;
+  const size_t K1 = K + 1;
+  if (c == d.nCells) {  // rho_zz(:, nCells+1) = 1 (2989-2991)
+    if (k < K) p.rho_zz2[(size_t)c * K + k] = 1.0;
+    return;
+  }
+  if (c > d.nCells) return;
+  const bool act = k < K;
+  const size_t o = (size_t)c * K + k, ow = (size_t)c * K1 + k;
+  const double rcv = RGAS / (CP - RGAS);
+  double rz = 0.0;
+  if (act) {
+    const double rho_p = p.rho_p_save[o] + p.rho_pp[o];
+    p.rho_p[o] = rho_p;
+    rz = rho_p + p.rho_base[o];
+    p.rho_zz2[o] = rz;
+  }
+  const double fzm = act ? p.fzm[k] : 0.0, fzp = act ? p.fzp[k] : 0.0;
+  const double zz = LD(p.zz, o), zzm = up1(zz);
+  double w = 0.0;
+  if (act && k >= 1) {
+    p.wwAvg[ow] = p.rw_save[ow] + (p.wwAvg[ow] * invNs);
+    const double rw = p.rw_save[ow] + p.rw_p[ow];
+    p.rw[ow] = rw;
+    w = rw / (fzm * zz + fzp * zzm);
+  }
+  if (act) {
+    if (rk_step == 3) {
+      const double rtp = p.rtheta_p_save[o] + p.rtheta_pp[o] - dt * rz * p.rt_diabatic_tend[o];
+      p.rtheta_p[o] = rtp;
+      p.theta_m2[o] = (rtp + p.rtheta_base[o]) / rz;
+      const double ex = pow(zz * (RGAS / P0) * (rtp + p.rtheta_base[o]), rcv);
+      p.exner[o] = ex;
+      p.pressure_p[o] = zz * RGAS * (ex * rtp + p.rtheta_base[o] * (ex - p.exner_base[o]));
+    } else {
+      const double rtp = p.rtheta_p_save[o] + p.rtheta_pp[o];
+      p.rtheta_p[o] = rtp;
+      p.theta_m2[o] = (rtp + p.rtheta_base[o]) / rz;
+    }
+  }
+  // w from the flux-divergence operator (3063-3097)
+  const int ne = p.nEdgesOnCell[c];
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double sg = p.edgesOnCell_sign[c * d.maxEdges + i];
+    const double ruk = act ? p.ru_save[(size_t)e * K + k] + p.ru_p[(size_t)e * K + k] : 0.0;
+    const double rum = up1(ruk);
+    const double ru1 = readlane_d(ruk, 0), ru2 = readlane_d(ruk, 1), ru3 = readlane_d(ruk, 2);
+    const size_t zo = ((size_t)c * d.maxEdges + i) * K1 + k;
+    if (k == 0) {
+      const double flux = (p.cf1 * ru1 + p.cf2 * ru2 + p.cf3 * ru3);
+      w = w + sg * (p.zb_cell[zo] + sgn1(flux) * p.zb3_cell[zo]) * flux;
+    } else if (act) {
+      const double flux = (fzm * ruk + fzp * rum);
+      w = w + sg * (p.zb_cell[zo] + sgn1(flux) * p.zb3_cell[zo]) * flux;
+    }
+  }
+  const double rzm = up1(rz);
+  const double r1 = readlane_d(rz, 0), r2 = readlane_d(rz, 1), r3 = readlane_d(rz, 2);
+  if (k == 0) w = w / (p.cf1 * r1 + p.cf2 * r2 + p.cf3 * r3);
+  else if (act) w = w / (fzm * rz + fzp * rzm);
+  if (k <= K) p.w2[ow] = w;  // w(K+1) = 0
+}
+
+// ============================================================================
+// atm_compute_solve_diagnostics_work  (mpas_atm_time_integration.F:5585-5820)
+// ke_edge is recomputed where it is consumed with the reference expression
+// efac*u**2 (bit-identical), collapsing the four barrier phases into three launches.
+// ============================================================================
+__device__ __forceinline__ double ke_edge_of(const Ptrs& p, const double* u, int e, int K, int k) {
+  const double efac = p.dcEdge[e] * p.dvEdge[e];
+  const double uu = u[(size_t)e * K + k];
+  return efac * (uu * uu);
+}
+
+__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_vertices(Dims d, Ptrs p, const double* __restrict__ u) {
+  const int v = wave_elem(0);
+  if (v >= d.nVertices) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  double vort = 0.0, kev = 0.0;
+  for (int i = 0; i < 3; ++i) {
+    const int e = uni(p.edgesOnVertex[3 * v + i]);
+    const double s = p.edgesOnVertex_sign[3 * v + i] * p.dcEdge[e];
+    vort = vort + s * u[(size_t)e * K + k];
+  }
+  vort = vort * p.invAreaTriangle[v];
+  const int e1 = uni(p.edgesOnVertex[3 * v]), e2 = uni(p.edgesOnVertex[3 * v + 1]), e3 = uni(p.edgesOnVertex[3 * v + 2]);
+  const double r = 0.25 * p.invAreaTriangle[v];
+  kev = (ke_edge_of(p, u, e1, K, k) + ke_edge_of(p, u, e2, K, k) + ke_edge_of(p, u, e3, K, k)) * r;
+  const size_t o = (size_t)v * K + k;
+  p.vorticity[o] = vort;
+  p.ke_vertex[o] = kev;
+  p.pv_vertex[o] = (p.fVertex[v] + vort);
+}
+
+__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells(Dims d, Ptrs p, const double* __restrict__ u, double apvm) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const int ne = p.nEdgesOnCell[c];
+  const double r = p.invAreaCell[c];
+  double div = 0.0, ke = 0.0;
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double s = p.edgesOnCell_sign[c * d.maxEdges + i] * p.dvEdge[e];
+    div = div + s * u[(size_t)e * K + k];
+  }
+  div = div * r;
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    ke = ke + 0.25 * ke_edge_of(p, u, e, K, k);
+  }
+  ke = ke * p.invAreaCell[c];
+  const double ke_fact = 1.0 - .375;
+  ke = ke_fact * ke;
+  double pvc = 0.0;
+  for (int i = 0; i < ne; ++i) {
+    const int iv = uni(p.verticesOnCell[c * d.maxEdges + i]);
+    const int j = p.kiteForCell[c * d.maxEdges + i];
+    const double kite = p.kiteAreasOnVertex[3 * iv + j];
+    ke = ke + (1. - ke_fact) * kite * p.ke_vertex[(size_t)iv * K + k] * r;
+    pvc = pvc + kite * p.pv_vertex[(size_t)iv * K + k] * r;
+  }
+  const size_t o = (size_t)c * K + k;
+  p.divergence[o] = div;
+  p.ke[o] = ke;
+  if (apvm > 0.0) p.pv_cell[o] = pvc;
+}
+
+__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges(Dims d, Ptrs p, const double* __restrict__ u,
+                                                               const double* __restrict__ h, int reconstruct_v,
+                                                               double apvm, double dt) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const size_t o = (size_t)e * K + k;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  const int v1 = p.verticesOnEdge[2 * e], v2 = p.verticesOnEdge[2 * e + 1];
+  p.rho_edge[o] = 0.5 * (h[(size_t)c1 * K + k] + h[(size_t)c2 * K + k]);
+  p.ke_edge[o] = ke_edge_of(p, u, e, K, k);
+  double vv;
+  if (reconstruct_v) {
+    vv = 0.0;
+    const int neoe = p.nEdgesOnEdge[e];
+    for (int i = 0; i < neoe; ++i) {
+      const int eoe = uni(p.edgesOnEdge[e * d.maxEdges2 + i]);
+      vv = vv + p.weightsOnEdge[e * d.maxEdges2 + i] * u[(size_t)eoe * K + k];
+    }
+    p.v[o] = vv;
+  } else {
+    vv = p.v[o];
+  }
+  const double pv1 = p.pv_vertex[(size_t)v1 * K + k], pv2 = p.pv_vertex[(size_t)v2 * K + k];
+  double pve = 0.5 * (pv1 + pv2);
+  if (apvm > 0.0) {
+    const double r = apvm * dt;
+    const double r1 = 1.0 * p.invDvEdge[e];
+    const double r2 = 1.0 * p.invDcEdge[e];
+    const double gt = (pv2 - pv1) * r1;
+    const double gn = (p.pv_cell[(size_t)c2 * K + k] - p.pv_cell[(size_t)c1 * K + k]) * r2;
+    p.gradPVt[o] = gt;
+    p.gradPVn[o] = gn;
+    pve = pve - r * (vv * gt + u[o] * gn);
+  }
+  p.pv_edge[o] = pve;
+}
+
+// ============================================================================
+// atm_init_coupled_diagnostics  (mpas_atm_time_integration.F:5906-5988)
+// ============================================================================
+// cells: theta_m, rho_zz (5909-5914)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_init_coupled_a(Dims d, Ptrs p, int index_qv) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const size_t o = (size_t)c * K + k;
+  p.theta_m1[o] = p.theta[o] * (1. + RVORD * p.scalars1[o * d.ns + index_qv]);
+  p.rho_zz1[o] = p.rho[o] / p.zz[o];
+}
+// edges: ru (5918-5924)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_init_coupled_b(Dims d, Ptrs p) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  const size_t o = (size_t)e * K + k;
+  p.ru[o] = 0.5 * p.u1[o] * (p.rho_zz1[(size_t)c1 * K + k] + p.rho_zz1[(size_t)c2 * K + k]);
+}
+// cells: rw, rho_p, rtheta_base, rtheta_p, exner, exner_base, pressure_p, pressure_base (5931-5988)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_init_coupled_c(Dims d, Ptrs p) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + k;
+  const double fzm = act ? p.fzm[k] : 0.0, fzp = act ? p.fzp[k] : 0.0;
+  const double rz = LD(p.rho_zz1, o), rzm = up1(rz);
+  const double zz = LD(p.zz, o), zzm = up1(zz);
+  double rw = 0.0;
+  if (act && k >= 1) rw = p.w1[(size_t)c * K1 + k] * (fzp * rzm + fzm * rz) * (fzp * zzm + fzm * zz);
+  const int ne = p.nEdgesOnCell[c];
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double ruk = LD(p.ru, (size_t)e * K + k), rum = up1(ruk);
+    if (act && k >= 1) {
+      const double flux = (fzm * ruk + fzp * rum);
+      const size_t zo = ((size_t)c * d.maxEdges + i) * K1 + k;
+      rw = rw - p.edgesOnCell_sign[c * d.maxEdges + i] * (p.zb_cell[zo] + sgn1(flux) * p.zb3_cell[zo]) * flux *
+                    (fzp * zzm + fzm * zz);
+    }
+  }
+  if (k <= K) p.rw[(size_t)c * K1 + k] = rw;
+  if (!act) return;
+  const double rcv = RGAS / (CP - RGAS);
+  const double rho_p = rz - p.rho_base[o];
+  p.rho_p[o] = rho_p;
+  const double rtb = p.theta_base[o] * p.rho_base[o];
+  p.rtheta_base[o] = rtb;
+  const double th = p.theta_m1[o];
+  const double rtp = th * rho_p + p.rho_base[o] * (th - p.theta_base[o]);
+  p.rtheta_p[o] = rtp;
+  const double ex = pow(zz * (RGAS / P0) * (rtp + rtb), rcv);
+  const double exb = pow(zz * (RGAS / P0) * (rtb), rcv);
+  p.exner[o] = ex;
+  p.exner_base[o] = exb;
+  p.pressure_p[o] = zz * RGAS * (ex * rtp + rtb * (ex - exb));
+  p.pressure_base[o] = zz * RGAS * exb * rtb;
+}
+
+// ============================================================================
+// atm_rk_dynamics_substep_finish  (mpas_atm_time_integration.F:6051-6079)
+// ============================================================================
+__global__ __launch_bounds__(BLOCK_THREADS) void k_substep_finish(Dims d, Ptrs p, int dynamics_substep,
+                                                                   int dynamics_split, double inv_dynamics_split) {
+  const int idx = wave_elem(0);
+  const int k = lane_id(), K = d.K;
+  const size_t K1 = K + 1;
+  if (idx < d.nEdges) {
+    const int e = idx;
+    if (k >= K) return;
+    const size_t o = (size_t)e * K + k;
+    if (dynamics_substep < dynamics_split) {
+      p.ru_save[o] = p.ru[o];
+      p.u1[o] = p.u2[o];
+    }
+    double ras = (dynamics_substep == 1) ? p.ruAvg[o] : p.ruAvg[o] + p.ruAvg_split[o];
+    p.ruAvg_split[o] = ras;
+    if (dynamics_substep == dynamics_split) p.ruAvg[o] = ras * inv_dynamics_split;
+  } else {
+    const int c = idx - d.nEdges;
+    if (c >= d.nCells) return;
+    if (k <= K) {
+      const size_t ow = (size_t)c * K1 + k;
+      if (dynamics_substep < dynamics_split) {
+        p.rw_save[ow] = p.rw[ow];
+        p.w1[ow] = p.w2[ow];
+      }
+      double was = (dynamics_substep == 1) ? p.wwAvg[ow] : p.wwAvg[ow] + p.wwAvg_split[ow];
+      p.wwAvg_split[ow] = was;
+      if (dynamics_substep == dynamics_split) p.wwAvg[ow] = was * inv_dynamics_split;
+    }
+    if (k < K) {
+      const size_t o = (size_t)c * K + k;
+      if (dynamics_substep < dynamics_split) {
+        p.rtheta_p_save[o] = p.rtheta_p[o];
+        p.rho_p_save[o] = p.rho_p[o];
+        p.theta_m1[o] = p.theta_m2[o];
+        p.rho_zz1[o] = p.rho_zz2[o];
+      }
+      if (dynamics_substep == dynamics_split) p.rho_zz1[o] = p.rho_zz_old_split[o];
+    }
+  }
+}
+
+// ============================================================================
+// atm_advance_scalars_work  (mpas_atm_time_integration.F:3346-3504)
+// ============================================================================
+// edges (all): scalar value at the edge, horiz_flux_arr(ns, K, nEdges+1)  (3357-3426)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_edges(Dims d, Ptrs p) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  if (k >= K) return;
+  const double uh = p.ruAvg[(size_t)e * K + k];
+  const double sg = sgn1(uh);
+  const int na = p.nAdvCellsForEdge[e];
+  double* hf = p.horiz_flux_array + ((size_t)e * K + k) * ns;
+  if (na == 10) {
+    // unrolled hexagon form (3363-3390): sum of ten products, left to right
+    double w[10];
+    int ica[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      w[j] = p.adv_coefs[e * 15 + j] + sg * p.adv_coefs_3rd[e * 15 + j];
+      ica[j] = uni(p.advCellsForEdge[e * 15 + j]);
+    }
+    for (int is = 0; is < ns; ++is) {
+      double acc = w[0] * p.scalars2[((size_t)ica[0] * K + k) * ns + is];
+#pragma unroll
+      for (int j = 1; j < 10; ++j) acc = acc + w[j] * p.scalars2[((size_t)ica[j] * K + k) * ns + is];
+      hf[is] = acc;
+    }
+  } else {
+    for (int is = 0; is < ns; ++is) hf[is] = 0.0;
+    for (int j = 0; j < na; ++j) {
+      const int ic = uni(p.advCellsForEdge[e * 15 + j]);
+      const double scalar_weight = p.adv_coefs[e * 15 + j] + sg * p.adv_coefs_3rd[e * 15 + j];
+      for (int is = 0; is < ns; ++is) hf[is] = hf[is] + scalar_weight * p.scalars2[((size_t)ic * K + k) * ns + is];
+    }
+  }
+}
+
+// cells (solve): flux divergence, vertical flux3 transport and update (3433-3504)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_cells(Dims d, Ptrs p, double dt, double wt_new,
+                                                                  double coef_3rd_order) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + k;
+  const double wt_old = 1. - wt_new;
+  const int ne = p.nEdgesOnCell[c];
+  const double invA = p.invAreaCell[c];
+  const double fnm = act ? p.fzm[k] : 0.0, fnp = act ? p.fzp[k] : 0.0;
+  const double wwa = (k <= K) ? p.wwAvg[(size_t)c * K1 + k] : 0.0;
+  const double rdnw = act ? p.rdzw[k] : 0.0;
+  const double rzo = LD(p.rho_zz1, o), rzn = LD(p.rho_zz2, o);
+  const double rho_zz_new_inv = act ? 1.0 / (wt_old * rzo + wt_new * rzn) : 0.0;
+  for (int is = 0; is < ns; ++is) {
+    double stc = 0.0;
+    for (int i = 0; i < ne; ++i) {
+      const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+      if (act)
+        stc = stc - p.edgesOnCell_sign[c * d.maxEdges + i] * p.ruAvg[(size_t)e * K + k] *
+                        p.horiz_flux_array[((size_t)e * K + k) * ns + is];
+    }
+    if (act) {
+      p.scalars_tend[o * ns + is] = 0.0;  // no physics: scalar_tend_save zeroed (3437-3439)
+      stc = stc * invA + 0.0;
+    }
+    const double sn = LD(p.scalars2, o * ns + is);
+    const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
+    double wdtn = 0.0;
+    if (k == 1 || k == K - 1) wdtn = wwa * (fnm * sn + fnp * snm1);
+    else if (k >= 2 && k <= K - 2) wdtn = flux3(snm2, snm1, sn, snp1, wwa, coef_3rd_order);
+    const double wdtn_p = dn1(wdtn);
+    if (act) {
+      const double so = p.scalars1[o * ns + is];
+      p.scalars2[o * ns + is] = (so * rzo + dt * (stc - rdnw * (wdtn_p - wdtn))) * rho_zz_new_inv;
+    }
+  }
+}
+
+// ============================================================================
+// atm_advance_scalars_mono_work  (mpas_atm_time_integration.F:3737-4210)
+// ============================================================================
+// cells (solve): source update of scalars_old (3737-3752) and rho_zz_int (3766-3792)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_prep(Dims d, Ptrs p, double dt, int advance_density) {
+  const int c = wave_elem(0);
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const size_t K1 = K + 1;
+  if (c >= d.nCells) return;
+  const size_t o = (size_t)c * K + k;
+  if (c >= d.nCellsSolve) {  // rho_zz_int(:,iCell) = 0 on all cells (3772-3774)
+    if (advance_density && act) p.rho_zz_int[o] = 0.0;
+    return;
+  }
+  if (act) {
+    const double rzo = p.rho_zz1[o];
+    for (int is = 0; is < ns; ++is) {
+      p.scalars_tend[o * ns + is] = 0.0;
+      p.scalars1[o * ns + is] = p.scalars1[o * ns + is] + dt * p.scalars_tend[o * ns + is] / rzo;
+      p.scalars_tend[o * ns + is] = 0.0;
+    }
+  }
+  if (advance_density) {
+    double rzi = 0.0;
+    const int ne = p.nEdgesOnCell[c];
+    for (int i = 0; i < ne; ++i) {
+      const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+      if (act)
+        rzi = rzi - p.edgesOnCell_sign[c * d.maxEdges + i] * p.ruAvg[(size_t)e * K + k] * p.dvEdge[e] * p.invAreaCell[c];
+    }
+    const double wwa = (k <= K) ? p.wwAvg[(size_t)c * K1 + k] : 0.0, wwap = dn1(wwa);
+    if (act) p.rho_zz_int[o] = p.rho_zz1[o] + dt * (rzi - p.rdzw[k] * (wwap - wwa));
+  }
+}
+
+// per scalar iScalar, cells (solve): vertical flux and min/max bounds (3843-3908)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds(Dims d, Ptrs p, int is, double coef_3rd_order) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + k;
+  auto sold = [&](int cc) -> double { return (cc < d.nCells) ? p.scalars1[((size_t)cc * K + k) * ns + is] : 0.0; };
+  const double so = act ? sold(c) : 0.0;
+  const double sn = LD(p.scalars2, o * ns + is);
+  const double som = up1(so), sop = dn1(so);
+  const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
+  const double wwa = (k <= K) ? p.wwAvg[(size_t)c * K1 + k] : 0.0;
+  const double fnm = act ? p.fzm[k] : 0.0, fnp = act ? p.fzp[k] : 0.0;
+  double wdtn = 0.0;
+  if (k == 1 || k == K - 1) wdtn = wwa * (fnm * sn + fnp * snm1);
+  else if (k >= 2 && k <= K - 2) wdtn = flux3(snm2, snm1, sn, snp1, wwa, coef_3rd_order);
+  if (k <= K) p.wdtn[(size_t)c * K1 + k] = wdtn;
+  if (!act) return;
+  double smax, smin;
+  if (k == 0) {
+    smax = fmax(so, sop);
+    smin = fmin(so, sop);
+  } else if (k == K - 1) {
+    smax = fmax(so, som);
+    smin = fmin(so, som);
+  } else {
+    smax = fmax(fmax(som, so), sop);
+    smin = fmin(fmin(som, so), sop);
+  }
+  const int ne = p.nEdgesOnCell[c];
+  for (int i = 0; i < ne; ++i) {
+    const int cc = uni(p.cellsOnCell[c * d.maxEdges + i]);
+    const double v = sold(cc);
+    smax = fmax(smax, v);
+    smin = fmin(smin, v);
+  }
+  p.s_max[o] = smax;
+  p.s_min[o] = smin;
+}
+
+// per scalar, edges: high-order flux (3916-3961), upwind flux and flux difference (4007-4022)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_edges1(Dims d, Ptrs p, int is, double dt) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  if (k >= K) return;
+  const size_t o = (size_t)e * K + k;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  auto snew = [&](int cc) -> double { return (cc < d.nCells) ? p.scalars2[((size_t)cc * K + k) * ns + is] : 0.0; };
+  auto sold = [&](int cc) -> double { return (cc < d.nCells) ? p.scalars1[((size_t)cc * K + k) * ns + is] : 0.0; };
+  const double uh = p.ruAvg[o];
+  double fa = 0.0;
+  if (c1 < d.nCellsSolve || c2 < d.nCellsSolve) {
+    const int na = p.nAdvCellsForEdge[e];
+    if (na == 10) {
+      const int ii = (uh > 0) ? 0 : 1;
+      double acc = 0.0;
+#pragma unroll
+      for (int jj = 0; jj < 10; ++jj) {
+        const double a = p.adv_coefs[e * 15 + jj], b = p.adv_coefs_3rd[e * 15 + jj];
+        const double swa = (ii == 0) ? (a + b) : (a - b);
+        const double term = swa * snew(uni(p.advCellsForEdge[e * 15 + jj]));
+        acc = (jj == 0) ? term : acc + term;
+      }
+      fa = uh * (acc);
+    } else {
+      for (int i = 0; i < na; ++i) {
+        const int ic = uni(p.advCellsForEdge[e * 15 + i]);
+        const double scalar_weight = uh * (p.adv_coefs[e * 15 + i] + sgn1(uh) * p.adv_coefs_3rd[e * 15 + i]);
+        fa = fa + scalar_weight * snew(ic);
+      }
+    }
+  }
+  p.flux_arr[o] = fa;
+  const double fu = p.dvEdge[e] * dt * (fmax(0.0, uh) * sold(c1) + fmin(0.0, uh) * sold(c2));
+  p.flux_upwind_tmp[o] = fu;
+  p.flux_tmp[o] = dt * fa - fu;
+}
+
+// per scalar, cells (solve): upwind update, in/out flux sums and limiter factors (3969-4076)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1(Dims d, Ptrs p, int is, double dt, int advance_density) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + k, ow = (size_t)c * K1 + k;
+  const double eps = 1.e-20;
+  const double so = LD(p.scalars1, o * ns + is), som = up1(so);
+  const double rzo = LD(p.rho_zz1, o);
+  const double wwa = (k <= K) ? p.wwAvg[ow] : 0.0;
+  const double rdnw = act ? p.rdzw[k] : 0.0;
+  double snew = so * rzo;
+  double fua = 0.0;  // flux_upwind_arr(k), k >= 2
+  if (act && k >= 1) fua = dt * (fmax(0.0, wwa) * som + fmin(0.0, wwa) * so);
+  const double fua_p = dn1(fua);
+  if (act && k <= K - 2) snew = snew - fua_p * rdnw;
+  double wd = (k <= K) ? p.wdtn[ow] : 0.0;
+  if (act && k >= 1) {
+    snew = snew + fua * rdnw;
+    wd = dt * wd - fua;
+  }
+  if (k <= K) p.wdtn[ow] = wd;
+  const double wdp = dn1(wd);
+  double sin_ = 0.0, sout = 0.0;
+  if (act) {
+    sin_ = -rdnw * (fmin(0.0, wdp) - fmax(0.0, wd));
+    sout = -rdnw * (fmax(0.0, wdp) - fmin(0.0, wd));
+  }
+  const int ne = p.nEdgesOnCell[c];
+  const double invA = p.invAreaCell[c];
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double sg = p.edgesOnCell_sign[c * d.maxEdges + i];
+    if (act) {
+      const double ft = p.flux_tmp[(size_t)e * K + k];
+      snew = snew - sg * p.flux_upwind_tmp[(size_t)e * K + k] * invA;
+      sout = sout - fmax(0.0, sg * ft) * invA;
+      sin_ = sin_ - fmin(0.0, sg * ft) * invA;
+    }
+  }
+  if (!act) return;
+  const double rhoref = advance_density ? p.rho_zz_int[o] : p.rho_zz2[o];
+  double scale_factor = (p.s_max[o] * rhoref - snew) / (sin_ + eps);
+  const double scale_in = fmin(1.0, fmax(0.0, scale_factor));
+  scale_factor = (p.s_min[o] * rhoref - snew) / (sout - eps);
+  const double scale_out = fmin(1.0, fmax(0.0, scale_factor));
+  p.scalar_old_copy[o] = snew;  // upwind solution (the reference's scratch scalar_new)
+  p.scale_arr[((size_t)c * 2 + 0) * K + k] = scale_in;
+  p.scale_arr[((size_t)c * 2 + 1) * K + k] = scale_out;
+}
+
+// per scalar, edges with an owned cell: flux correction and rescale (4102-4138)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_edges2(Dims d, Ptrs p, double dt) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const size_t o = (size_t)e * K + k;
+  double flux = dt * p.flux_arr[o] - p.flux_upwind_tmp[o];
+  auto sc = [&](int cc, int io) -> double { return (cc < d.nCells) ? p.scale_arr[((size_t)cc * 2 + io) * K + k] : 0.0; };
+  flux = fmax(0.0, flux) * fmin(sc(c1, 1), sc(c2, 0)) + fmin(0.0, flux) * fmin(sc(c1, 0), sc(c2, 1));
+  p.flux_arr[o] = flux;
+}
+
+// per scalar, cells: vertical flux rescale, update and positive-definite copy-back (4145-4210)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2(Dims d, Ptrs p, int is, int advance_density) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + k, ow = (size_t)c * K1 + k;
+  if (c >= d.nCellsSolve) {  // halo cells: scalars_new = max(0, scalar_new) with scalar_new = input copy
+    if (act) p.scalars2[o * ns + is] = fmax(0.0, p.scalars2[o * ns + is]);
+    return;
+  }
+  const double si = act ? p.scale_arr[((size_t)c * 2 + 0) * K + k] : 0.0;
+  const double so_ = act ? p.scale_arr[((size_t)c * 2 + 1) * K + k] : 0.0;
+  const double sim = up1(si), som = up1(so_);
+  double wd = (k <= K) ? p.wdtn[ow] : 0.0;
+  if (act && k >= 1) {
+    const double f = wd;
+    wd = fmax(0.0, f) * fmin(som, si) + fmin(0.0, f) * fmin(so_, sim);
+  }
+  const double wdp = dn1(wd);
+  if (!act) return;
+  double snew = p.scalar_old_copy[o];
+  const int ne = p.nEdgesOnCell[c];
+  const double invA = p.invAreaCell[c];
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    snew = snew - p.edgesOnCell_sign[c * d.maxEdges + i] * p.flux_arr[(size_t)e * K + k] * invA;
+  }
+  const double rhoref = advance_density ? p.rho_zz_int[o] : p.rho_zz2[o];
+  snew = (snew + (-p.rdzw[k] * (wdp - wd))) / rhoref;
+  p.scalars2[o * ns + is] = fmax(0.0, snew);
+}
+
+}  // namespace mpas

@@ -1,0 +1,87 @@
+"""ctypes binding of the C ABI in include/mpas_dycore.h (libmpas_dycore.so).
+
+The product path has exactly one implementation: the HIP kernels in
+mpas-model_amd/csrc.  If the shared library is missing this module raises --
+there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBPATH = os.path.join(os.path.dirname(HERE), "csrc", "libmpas_dycore.so")
+
+EXPORTS = (
+    "mpas_dyc_create", "mpas_dyc_destroy", "mpas_dyc_last_error", "mpas_dyc_set_field", "mpas_dyc_get_field",
+    "mpas_dyc_field_bytes", "mpas_dyc_field_device_ptr", "mpas_dyc_init_diagnostics", "mpas_dyc_timestep",
+    "mpas_dyc_shift_time_levels", "mpas_dyc_synchronize", "mpas_dyc_time_acoustic_step", "mpas_dyc_use_graph",
+    "mpas_dyc_acoustic_bytes",
+)
+
+
+class Dims(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "nCells", "nEdges", "nVertices", "nVertLevels", "maxEdges", "maxEdges2", "num_scalars",
+        "nCellsSolve", "nEdgesSolve", "nVerticesSolve", "moist_start", "moist_end", "index_qv")]
+
+
+_CFG_INT = ("config_time_integration_order", "config_number_of_sub_steps", "config_dynamics_split_steps",
+            "config_number_rayleigh_damp_u_levels", "config_split_dynamics_transport", "config_scalar_advection",
+            "config_positive_definite", "config_monotonic", "config_mix_full", "config_rayleigh_damp_u",
+            "config_horiz_mixing")
+_CFG_DBL = ("config_h_mom_eddy_visc2", "config_h_mom_eddy_visc4", "config_v_mom_eddy_visc2",
+            "config_h_theta_eddy_visc2", "config_h_theta_eddy_visc4", "config_v_theta_eddy_visc2",
+            "config_len_disp", "config_visc4_2dsmag", "config_del4u_div_factor", "config_coef_3rd_order",
+            "config_smagorinsky_coef", "config_epssm", "config_smdiv", "config_apvm_upwinding",
+            "config_mpas_cam_coef", "config_rayleigh_damp_u_timescale_days")
+
+
+class Config(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in _CFG_INT] + [(n, C.c_double) for n in _CFG_DBL]
+
+
+def make_config(cfg: dict) -> Config:
+    c = Config()
+    for n in _CFG_INT:
+        v = cfg[n]
+        if n == "config_horiz_mixing":
+            v = 1 if v == "2d_smagorinsky" else 0
+        setattr(c, n, int(v))
+    for n in _CFG_DBL:
+        setattr(c, n, float(cfg[n]))
+    return c
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIBPATH):
+        raise RuntimeError(f"MI355X dycore library not built: {LIBPATH} (run __graft_entry__.build())")
+    lib = C.CDLL(LIBPATH)
+    vp, i32, i64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    lib.mpas_dyc_create.argtypes = [C.POINTER(Dims), C.POINTER(Config), C.c_int, C.POINTER(vp)]
+    lib.mpas_dyc_destroy.argtypes = [vp]
+    lib.mpas_dyc_destroy.restype = None
+    lib.mpas_dyc_last_error.argtypes = [vp]
+    lib.mpas_dyc_last_error.restype = C.c_char_p
+    lib.mpas_dyc_set_field.argtypes = [vp, C.c_char_p, C.c_char_p, i32, vp, i64]
+    lib.mpas_dyc_get_field.argtypes = [vp, C.c_char_p, C.c_char_p, i32, vp, i64]
+    lib.mpas_dyc_field_bytes.argtypes = [vp, C.c_char_p, C.c_char_p]
+    lib.mpas_dyc_field_bytes.restype = i64
+    lib.mpas_dyc_field_device_ptr.argtypes = [vp, C.c_char_p, C.c_char_p, i32]
+    lib.mpas_dyc_field_device_ptr.restype = vp
+    lib.mpas_dyc_init_diagnostics.argtypes = [vp, dbl]
+    lib.mpas_dyc_timestep.argtypes = [vp, dbl, i32]
+    lib.mpas_dyc_shift_time_levels.argtypes = [vp]
+    lib.mpas_dyc_synchronize.argtypes = [vp]
+    lib.mpas_dyc_time_acoustic_step.argtypes = [vp, dbl, i32, i32, C.POINTER(dbl), C.POINTER(dbl)]
+    lib.mpas_dyc_use_graph.argtypes = [vp, i32]
+    lib.mpas_dyc_acoustic_bytes.argtypes = [vp]
+    lib.mpas_dyc_acoustic_bytes.restype = dbl
+    _lib = lib
+    return lib
