@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Benchmark: MPAS-Atmosphere dycore cell-updates/s on MI355X (BASELINE.json metric).
+
+One "step" = one full atm_timestep / atm_srk3 (dt) of the split-explicit dycore
+(3 dynamics substeps x RK3 x acoustic substeps + split scalar transport with the
+monotone limiter) on a synthetic x1.163842 JW baroclinic-wave state, 56 levels,
+fp64.  value = nCells * nVertLevels * (ranks) / t_dt  (cell-updates per second).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Also reported:
+  roofline      acoustic sub-step (atm_advance_acoustic_step + atm_divergence_damping_3d),
+                algorithmic bytes B_ac / measured time (HIP events on the
+                dycore's stream) vs the 8 TB/s HBM peak
+  cpu_baseline  the reference Fortran dycore (oracle/_ref, compiled from /root/reference)
+                on the host cores, bounded sample
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpas-model_amd"))
+sys.path.insert(0, ROOT)
+
+METRIC = "dycore cell-updates/sec (nCells×nVertLevels/step) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
+
+
+def _dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def cpu_baseline(case, dt, nthreads, steps):
+    """Reference dycore (compiled Fortran) timed on host cores -- the cpu_baseline leg only."""
+    from oracle import ref_runner
+    if not ref_runner.available():
+        return None
+    _, times = ref_runner.run_reference(case, nsteps=steps, dt=dt, dump_steps=[], nthreads=nthreads, timeout=1200)
+    use = times[1:] if len(times) > 1 else times  # first step pays allocation / first-touch
+    t = sum(use) / len(use)
+    return dict(value=case["nCells"] * case["nVertLevels"] / t, unit="cell-updates/s", cores=nthreads,
+                kind="reference",
+                sample=f"unmodified reference atm_srk3 (amdflang -O2, OpenMP {nthreads} threads) on the same "
+                       f"x1.{case['nCells']} x {case['nVertLevels']} JW case: {steps} dt steps, mean of steps "
+                       f"2..{steps} ({t:.2f} s/step)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--ncells", type=int, default=163842)
+    ap.add_argument("--levels", type=int, default=56)
+    ap.add_argument("--num-scalars", type=int, default=1)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--acoustic-reps", type=int, default=20)
+    args = ap.parse_args()
+
+    world, rank, local = _dist()
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = local
+
+    from mpas_dycore import Dycore
+    from mpas_dycore.cases import jw_case
+
+    t_build = time.time()
+    case = jw_case(args.ncells, K=args.levels, ns=args.num_scalars)
+    dt = case["dt"]
+    t_build = time.time() - t_build
+
+    dy = Dycore(case, device=device)
+    dy.init_diagnostics(dt)
+    if not args.no_graph:
+        dy.use_graph(True)
+
+    def step(i):
+        dy.atm_timestep(dt, i)
+        dy.shift_time_levels()
+
+    for i in range(args.warmup):
+        step(i + 1)
+    dy.synchronize()
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i + 1)
+    dy.synchronize()
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    cells_levels = case["nCells"] * case["nVertLevels"]
+    value = world * cells_levels / (ms_per_step / 1e3)
+
+    # ---- roofline of the acoustic sub-step (graded kernel), measured with HIP events
+    nss = case["config"]["config_number_of_sub_steps"]
+    dts = dt / case["config"]["config_dynamics_split_steps"] / nss
+    ms_sub, ms_k = dy.time_acoustic_step(dts, small_step=2, reps=args.acoustic_reps)
+    b_ac = dy.acoustic_bytes()
+    t_kern = sum(ms_k) / 1e3
+    achieved = b_ac / t_kern / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "acoustic_traffic.json")
+    if os.path.isfile(tf):
+        try:
+            with open(tf) as f:
+                tj = json.load(f)
+            if tj.get("ncells") == case["nCells"] and tj.get("levels") == case["nVertLevels"]:
+                traffic = tj.get("bytes_per_substep")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "cell-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (icosahedral SCVT mesh + Jablonowski-Williamson baroclinic wave, built on the box)",
+        "config": {
+            "workload": f"x1.{case['nCells']} dry dycore, {case['nVertLevels']} levels, dt={dt:g}s "
+                        f"(BASELINE.json configs[2] mesh; one full atm_srk3 per step)",
+            "nCells": case["nCells"], "nVertLevels": case["nVertLevels"], "num_scalars": case["num_scalars"],
+            "dt": dt, "time_integration_order": case["config"]["config_time_integration_order"],
+            "split_steps": case["config"]["config_dynamics_split_steps"], "acoustic_substeps": nss,
+            "parallelism": f"replicas{world}" if world > 1 else "single",
+            "hip_graph": not args.no_graph,
+        },
+        "roofline": {
+            "kernel": "acoustic sub-step (k_acoustic_edges + k_acoustic_cells + k_divdamp)",
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "bytes_per_launch": b_ac, "ms_per_substep": sum(ms_k),
+            "ms_kernels": {"edges": ms_k[0], "cells": ms_k[1], "divdamp": ms_k[2]},
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            nthreads = min(args.cpu_threads, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(case, dt, nthreads, args.cpu_steps)
+        except Exception as e:  # the measured GPU number stands on its own
+            out["cpu_baseline"] = {"error": str(e)[:200]}
+    out["build_s"] = round(t_build, 1)
+    dy.close()
+    if dist:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

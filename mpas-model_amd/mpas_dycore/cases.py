@@ -1,0 +1,53 @@
+"""Synthetic benchmark / test cases of BASELINE.json (SURVEY.md §8d "Synthetic inputs").
+
+x1.N quasi-uniform icosahedral meshes with the JW baroclinic-wave state; dt and
+config_len_disp scale with resolution as SURVEY.md §8d lists them:
+2562 -> 2880 s / 480 km, 10242 -> 1440 s / 240 km, 163842 -> 360 s / 60 km.
+Cases are cached as .npz files (they take tens of seconds to build at 163842).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+
+import numpy as np
+
+from .init_atm import build_case
+from .mesh import build_mesh
+
+CACHE = os.environ.get("MPAS_DYCORE_CACHE", "/tmp/mpas_dycore_cache")
+
+LEVEL_OF = {642: 3, 2562: 4, 10242: 5, 40962: 6, 163842: 7, 655362: 8}
+
+
+def level_for(ncells: int) -> int:
+    return LEVEL_OF[ncells]
+
+
+def jw_dt(level: int) -> float:
+    return 360.0 * 2 ** (7 - level)
+
+
+def jw_len_disp(level: int) -> float:
+    return 60000.0 * 2 ** (7 - level)
+
+
+def jw_case(ncells: int, K: int = 56, ns: int = 1, moist: bool = False, order: int = 2,
+            lloyd_iters: int = 20, cache: bool = True) -> dict:
+    level = level_for(ncells)
+    key = f"jw_l{level}_K{K}_ns{ns}_m{int(moist)}_o{order}_ll{lloyd_iters}"
+    path = os.path.join(CACHE, key + ".pkl")
+    if cache and os.path.isfile(path):
+        with open(path, "rb") as f:  # our own cache file, written below
+            return pickle.load(f)
+    m = build_mesh(level, lloyd_iters=lloyd_iters)
+    cfg = dict(config_len_disp=jw_len_disp(level), config_dt=jw_dt(level), config_time_integration_order=order)
+    case = build_case(m, K=K, ns=ns, moist=moist, config=cfg)
+    case["dt"] = jw_dt(level)
+    if cache:
+        os.makedirs(CACHE, exist_ok=True)
+        tmp = path + f".{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            pickle.dump(case, f, protocol=pickle.HIGHEST_PROTOCOL)
+        os.replace(tmp, path)
+    return case

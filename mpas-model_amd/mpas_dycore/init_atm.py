@@ -24,6 +24,8 @@ fidelity to the reference init affects realism, not parity.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from .mesh import _normalize, arc_length
@@ -254,51 +256,33 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
     zz = (vg["zw"][1:] - vg["zw"][:-1])[None, :] / (zgrid[:, 1:] - zgrid[:, :-1])   # (nC, K)
     zxu = 0.5 * (zgrid[c2, :-1] - zgrid[c1, :-1] + zgrid[c2, 1:] - zgrid[c1, 1:]) / m["dcEdge"][:, None]
 
-    # ---- JW thermodynamic state (mpas_init_atm_cases.F:839-958), vectorised over cells
-    u0, t0b, t0, delta_t, dtdz, eta_t = 35.0, 250.0, 288.0, 4.8e5, 0.005, 0.2
-    znut = eta_t
-    ztemp = 0.5 * (zgrid[:, 1:] + zgrid[:, :-1])
-    ppb = P0 * np.exp(-GRAVITY * ztemp / (RGAS * t0b))
-    pb = (ppb / P0) ** (RGAS / CP)
-    rb = ppb / (RGAS * t0b * zz)
-    tb = t0b / pb
-    pp = np.zeros_like(ppb)
-    rr = np.zeros_like(ppb)
-    qv = np.zeros_like(ppb)
-    phi = lat[:, None]
-    dzw, dzu, fzp, fzm = vg["dzw"], vg["dzu"], vg["fzp"], vg["fzm"]
-    for _ in range(10):
-        eta = (ppb + pp) / P0
-        etav = (eta - 0.252) * PII / 2.0
-        teta = t0 * eta ** (RGAS * dtdz / GRAVITY) + np.where(eta >= znut, 0.0, delta_t * (znut - eta) ** 5)
-        temperature = teta + 0.75 * eta * PII * u0 / RGAS * np.sin(etav) * np.sqrt(np.cos(etav)) * (
-            (-2.0 * np.sin(phi) ** 6 * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0) * 2.0 * u0 * np.cos(etav) ** 1.5
-            + (1.6 * np.cos(phi) ** 3 * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * R * OMEGA) / (1.0 + 0.61 * qv)
-        if moist:
-            ptemp = ppb + pp
-            relhum = np.where(ptemp < 50000.0, 0.0, np.where(ptemp > P0, 1.0, 1.0 - ((P0 - ptemp) / 50000.0) ** 1.25))
-            relhum = np.minimum(0.40, relhum)
-            es = np.where(temperature > 273.15,
-                          1000.0 * 0.6112 * np.exp(17.67 * (temperature - 273.15) / (temperature - 29.65)),
-                          1000.0 * 0.6112 * np.exp(21.8745584 * (temperature - 273.15) / (temperature - 7.66)))
-            qsat = (287.04 / 461.6) * es / (ptemp - es)
-            qsat = np.where(relhum == 0.0, 0.0, qsat)
-            qv = relhum * qsat
-        tt = temperature * (1.0 + 1.61 * qv)
-        for _ in range(25):
-            rr = (pp / (RGAS * zz) - rb * (tt - t0b)) / tt
-            ppi = np.zeros_like(pp)
-            ppi[:, 0] = P0 - 0.5 * dzw[0] * GRAVITY * (1.25 * (rr[:, 0] + rb[:, 0]) * (1.0 + qv[:, 0])
-                                                       - 0.25 * (rr[:, 1] + rb[:, 1]) * (1.0 + qv[:, 1]))
-            ppi[:, 0] -= ppb[:, 0]
-            for k in range(nz1 - 1):
-                ppi[:, k + 1] = ppi[:, k] - dzu[k + 1] * GRAVITY * (
-                    (rr[:, k] + (rr[:, k] + rb[:, k]) * qv[:, k]) * fzp[k + 1]
-                    + (rr[:, k + 1] + (rr[:, k + 1] + rb[:, k + 1]) * qv[:, k + 1]) * fzm[k + 1])
-            pp = 0.2 * ppi + 0.8 * pp
-    p = ((ppb + pp) / P0) ** (RGAS / CP)
-    t = tt / p
+    # ---- JW thermodynamic state (mpas_init_atm_cases.F:839-958), column-independent:
+    # computed over cache-sized chunks of cells with level-major work arrays.
+    u0 = 35.0
+    ppb = np.empty((nC, nz1))
+    pp = np.empty((nC, nz1))
+    rb = np.empty((nC, nz1))
+    rr = np.empty((nC, nz1))
+    tb = np.empty((nC, nz1))
+    t = np.empty((nC, nz1))
+    qv = np.empty((nC, nz1))
+    CH = 2048
+    chunks = [slice(c0, min(nC, c0 + CH)) for c0 in range(0, nC, CH)]
+    nproc = min(16, os.cpu_count() or 1, len(chunks))
+    if nproc > 1 and nC >= 20000:
+        import concurrent.futures as cf
+        import multiprocessing as mp
+        with cf.ProcessPoolExecutor(nproc, mp_context=mp.get_context("fork")) as ex:
+            results = list(ex.map(_jw_columns, [lat[sl] for sl in chunks], [zgrid[sl] for sl in chunks],
+                                  [zz[sl] for sl in chunks], [vg] * len(chunks), [R] * len(chunks),
+                                  [moist] * len(chunks)))
+    else:
+        results = [_jw_columns(lat[sl], zgrid[sl], zz[sl], vg, R, moist) for sl in chunks]
+    for sl, r in zip(chunks, results):
+        for a, b in zip((ppb, pp, rb, rr, tb, t, qv), r):
+            a[sl] = b.T
     rho_zz = rb + rr
+    fzp, fzm = vg["fzp"], vg["fzm"]
 
     # ---- wind (analytic JW flux, mpas_init_atm_cases.F:974-1019)
     latV = m["latVertex"]
@@ -349,8 +333,8 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
         z2 = fzm[k] * zz[c2, k] + fzp[k] * zz[c2, k - 1]
         z1 = fzm[k] * zz[c1, k] + fzp[k] * zz[c1, k - 1]
         sg = np.copysign(1.0, ru[:, k])
-        np.add.at(rw[:, k], c2, z2 * zb[:, 1, k] * fl - sg * coef3 * z2 * zb3[:, 1, k] * fl)
-        np.add.at(rw[:, k], c1, -z1 * zb[:, 0, k] * fl + sg * coef3 * z1 * zb3[:, 0, k] * fl)
+        rw[:, k] += np.bincount(c2, weights=z2 * zb[:, 1, k] * fl - sg * coef3 * z2 * zb3[:, 1, k] * fl, minlength=nC)
+        rw[:, k] += np.bincount(c1, weights=-z1 * zb[:, 0, k] * fl + sg * coef3 * z1 * zb3[:, 0, k] * fl, minlength=nC)
     w = np.zeros((nC, nz))
     w[:, 1:nz1] = rw[:, 1:nz1] / (fzp[1:] * rho_zz[:, :-1] + fzm[1:] * rho_zz[:, 1:])
 
@@ -426,3 +410,57 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
         u=u, w=w, theta=theta, rho=rho, scalars=scalars, rho_base=rb, theta_base=tb,
     )
     return out
+
+
+def _jw_columns(lat, zgrid, zz, vg, R, moist):
+    """JW columns for a chunk of cells (mpas_init_atm_cases.F:841-950); arrays (K, nc)."""
+    nz1 = zz.shape[1]
+    u0, t0b, t0, delta_t, dtdz, eta_t = 35.0, 250.0, 288.0, 4.8e5, 0.005, 0.2
+    znut = eta_t
+    zzT = np.ascontiguousarray(zz.T)
+    ztemp = np.ascontiguousarray(0.5 * (zgrid[:, 1:] + zgrid[:, :-1]).T)
+    ppb = P0 * np.exp(-GRAVITY * ztemp / (RGAS * t0b))
+    pb = (ppb / P0) ** (RGAS / CP)
+    rb = ppb / (RGAS * t0b * zzT)
+    tb = t0b / pb
+    pp = np.zeros_like(ppb)
+    rr = np.zeros_like(ppb)
+    qv = np.zeros_like(ppb)
+    phi = lat[None, :]
+    dzw, dzu, fzp, fzm = vg["dzw"], vg["dzu"], vg["fzp"], vg["fzm"]
+    geo = ((-2.0 * np.sin(phi) ** 6 * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0), 
+           (1.6 * np.cos(phi) ** 3 * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * R * OMEGA)
+    for _ in range(10):
+        eta = (ppb + pp) / P0
+        etav = (eta - 0.252) * PII / 2.0
+        dlt = znut - eta
+        teta = t0 * eta ** (RGAS * dtdz / GRAVITY) + np.where(eta >= znut, 0.0, delta_t * (dlt * dlt * dlt * dlt * dlt))
+        ce = np.cos(etav)
+        temperature = teta + 0.75 * eta * PII * u0 / RGAS * np.sin(etav) * np.sqrt(ce) * (
+            geo[0] * 2.0 * u0 * ce ** 1.5 + geo[1]) / (1.0 + 0.61 * qv)
+        if moist:
+            ptemp = ppb + pp
+            relhum = np.where(ptemp < 50000.0, 0.0, np.where(ptemp > P0, 1.0, 1.0 - ((P0 - ptemp) / 50000.0) ** 1.25))
+            relhum = np.minimum(0.40, relhum)
+            es = np.where(temperature > 273.15,
+                          1000.0 * 0.6112 * np.exp(17.67 * (temperature - 273.15) / (temperature - 29.65)),
+                          1000.0 * 0.6112 * np.exp(21.8745584 * (temperature - 273.15) / (temperature - 7.66)))
+            qsat = (287.04 / 461.6) * es / (ptemp - es)
+            qsat = np.where(relhum == 0.0, 0.0, qsat)
+            qv = relhum * qsat
+        tt = temperature * (1.0 + 1.61 * qv)
+        rzz = RGAS * zzT
+        rbt = rb * (tt - t0b)
+        for _ in range(25):
+            rr = (pp / rzz - rbt) / tt
+            ppi = np.empty_like(pp)
+            ppi[0] = P0 - 0.5 * dzw[0] * GRAVITY * (1.25 * (rr[0] + rb[0]) * (1.0 + qv[0])
+                                                    - 0.25 * (rr[1] + rb[1]) * (1.0 + qv[1]))
+            ppi[0] -= ppb[0]
+            term = rr + (rr + rb) * qv
+            for k in range(nz1 - 1):
+                ppi[k + 1] = ppi[k] - dzu[k + 1] * GRAVITY * (term[k] * fzp[k + 1] + term[k + 1] * fzm[k + 1])
+            pp = 0.2 * ppi + 0.8 * pp
+    p = ((ppb + pp) / P0) ** (RGAS / CP)
+    t = tt / p
+    return ppb, pp, rb, rr, tb, t, qv

@@ -37,27 +37,10 @@ def _fields():
 
 
 def to_fortran(case: dict, name: str) -> np.ndarray:
-    """Element-major numpy -> Fortran (..., n+1) memory image (C order of (n+1, ...))."""
-    F = _fields()
-    a = np.asarray(case[name])
-    if name in F.INDEX_TARGET:
-        n_tgt = case[_LOC_N[F.INDEX_TARGET[name]]]
-        a = np.where(a >= 0, a + 1, n_tgt + 1).astype(np.int32)
-    elif name in F.ONE_BASED_SMALL:
-        a = (a + 1).astype(np.int32)
-    elif a.dtype.kind in "iu":
-        a = a.astype(np.int32)
-    else:
-        a = a.astype(np.float64)
-    loc = F.LOCATION.get(name)
-    if loc is not None:
-        n = case[_LOC_N[loc]]
-        assert a.shape[0] == n, (name, a.shape, n)
-        pad = np.zeros((1,) + a.shape[1:], dtype=a.dtype)
-        if name in F.INDEX_TARGET:
-            pad[...] = case[_LOC_N[F.INDEX_TARGET[name]]] + 1
-        a = np.concatenate([a, pad], axis=0)
-    return np.ascontiguousarray(a)
+    """Element-major numpy -> Fortran (..., n+1) memory image (shared with the product's upload path)."""
+    _fields()
+    from mpas_dycore.layout import to_fortran as tf
+    return tf(case, name)
 
 
 def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthreads: int = 0,
