@@ -77,6 +77,7 @@ struct Ptrs {
   double *ke_vertex, *ke_edge, *horiz_flux_array;
   double *s_max, *s_min, *scale_arr, *flux_arr, *flux_upwind_tmp, *flux_tmp, *wdtn, *rho_zz_int;
   double *scalar_old_copy;
+  double *advflux_w, *advflux_th;  // edge values of w / theta_m for horizontal advection
 };
 
 }  // namespace mpas

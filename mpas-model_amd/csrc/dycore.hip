@@ -163,7 +163,8 @@ void build_registry(mpas_dyc_ctx* c) {
   for (const char* n : {"qtot", "tend_rtheta_physics", "tend_rho_physics", "delsq_theta", "delsq_w",
                         "delsq_divergence", "dpdz", "s_max", "s_min", "rho_zz_int", "scalar_old_copy"})
     add(c, "scratch", n, L_CELL, K);
-  for (const char* n : {"tend_ru_physics", "delsq_u", "ke_edge", "flux_arr", "flux_upwind_tmp", "flux_tmp"})
+  for (const char* n : {"tend_ru_physics", "delsq_u", "ke_edge", "flux_arr", "flux_upwind_tmp", "flux_tmp",
+                        "advflux_w", "advflux_th"})
     add(c, "scratch", n, L_EDGE, K);
   for (const char* n : {"delsq_vorticity", "ke_vertex"}) add(c, "scratch", n, L_VERTEX, K);
   add(c, "scratch", "horiz_flux_array", L_EDGE, (int64_t)ns * K);
@@ -227,6 +228,7 @@ Ptrs make_ptrs(mpas_dyc_ctx* c) {
   SC(ke_vertex); SC(ke_edge); SC(horiz_flux_array);
   SC(s_max); SC(s_min); SC(scale_arr); SC(flux_arr); SC(flux_upwind_tmp); SC(flux_tmp); SC(wdtn); SC(rho_zz_int);
   SC(scalar_old_copy);
+  SC(advflux_w); SC(advflux_th);
   // 0-d mesh fields are mirrored on the host
   p.cf1 = c->fields[c->by_name["mesh.cf1"]].buf[1] ? *(double*)c->fields[c->by_name["mesh.cf1"]].buf[1] : 0.0;
   p.cf2 = c->fields[c->by_name["mesh.cf2"]].buf[1] ? *(double*)c->fields[c->by_name["mesh.cf2"]].buf[1] : 0.0;
@@ -298,6 +300,7 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Ptrs& p, int rk_step, double dt) {
     LAUNCH(k_dyn_edges_rk1b, d.nEdgesSolve, d, p, cf, s);
     LAUNCH(k_dyn_cells2, d.nCells, d, p);
   }
+  LAUNCH(k_dyn_advflux, d.nEdges, d, p);
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
 }
 

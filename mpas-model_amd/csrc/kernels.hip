@@ -242,10 +242,25 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges(Dims d, Ptrs p, Con
     double q = 0.0;
     const int neoe = p.nEdgesOnEdge[e];
     const double pve = LD(p.pv_edge, o);
-    for (int j = 0; j < neoe; ++j) {
-      const int eoe = uni(p.edgesOnEdge[e * d.maxEdges2 + j]);
-      const double workpv = 0.5 * (pve + LD(p.pv_edge, (size_t)eoe * K + k));
-      q = q + p.weightsOnEdge[e * d.maxEdges2 + j] * LD(p.u2, (size_t)eoe * K + k) * workpv;
+    if (neoe == 10 && act) {  // hexagon-hexagon edge: all 20 gathers in flight at once
+      double pv[10], uu[10];
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const int eoe = uni(p.edgesOnEdge[e * d.maxEdges2 + j]);
+        pv[j] = p.pv_edge[(size_t)eoe * K + k];
+        uu[j] = p.u2[(size_t)eoe * K + k];
+      }
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const double workpv = 0.5 * (pve + pv[j]);
+        q = q + p.weightsOnEdge[e * d.maxEdges2 + j] * uu[j] * workpv;
+      }
+    } else {
+      for (int j = 0; j < neoe; ++j) {
+        const int eoe = uni(p.edgesOnEdge[e * d.maxEdges2 + j]);
+        const double workpv = 0.5 * (pve + LD(p.pv_edge, (size_t)eoe * K + k));
+        q = q + p.weightsOnEdge[e * d.maxEdges2 + j] * LD(p.u2, (size_t)eoe * K + k) * workpv;
+      }
     }
     if (act) {
       const size_t o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
@@ -399,6 +414,64 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells2(Dims d, Ptrs p) {
   if (k <= K) p.tend_w_euler[(size_t)c * (K + 1) + k] = (act && k >= 1) ? tw : 0.0;
 }
 
+// edges of owned cells: the 3rd/4th-order edge values of w and theta_m used by the
+// horizontal advection in atm_compute_dyn_tend_work (flux_arr at 5056-5066 and 5236-5244).
+// The reference recomputes them inside the cell loop for both cells of an edge; here each
+// edge is evaluated once (same expression, same order) and the cell kernel reads it back.
+template <int NA>
+__device__ __forceinline__ void adv_edge_sums(const Ptrs& p, int e, int K, int k, double sgn_w, double sgn_t,
+                                              double& fw, double& ft) {
+  const size_t K1 = K + 1;
+  double wv[NA], tv[NA];
+  int ic[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) ic[j] = uni(p.advCellsForEdge[e * 15 + j]);
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    wv[j] = p.w2[(size_t)ic[j] * K1 + k];
+    tv[j] = (k < K) ? p.theta_m2[(size_t)ic[j] * K + k] : 0.0;
+  }
+  fw = 0.0;
+  ft = 0.0;
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const double a = p.adv_coefs[e * 15 + j], b = p.adv_coefs_3rd[e * 15 + j];
+    fw = fw + (a + sgn_w * b) * wv[j];
+    ft = ft + (a + sgn_t * b) * tv[j];
+  }
+}
+
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_advflux(Dims d, Ptrs p) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const size_t o = (size_t)e * K + k;
+  const double rue = LD(p.ru, o), rue_m = up1(rue);
+  const double ru_edge_w = act ? p.fzm[k] * rue + p.fzp[k] * rue_m : 0.0;
+  const double sgn_w = sgn1(ru_edge_w), sgn_t = sgn1(rue);
+  const int na = p.nAdvCellsForEdge[e];
+  double fw = 0.0, ft = 0.0;
+  if (k <= K) {
+    if (na == 10) {
+      adv_edge_sums<10>(p, e, K, k, sgn_w, sgn_t, fw, ft);
+    } else {
+      for (int j = 0; j < na; ++j) {
+        const int ic = uni(p.advCellsForEdge[e * 15 + j]);
+        const double a = p.adv_coefs[e * 15 + j], b = p.adv_coefs_3rd[e * 15 + j];
+        fw = fw + (a + sgn_w * b) * p.w2[(size_t)ic * (K + 1) + k];
+        ft = ft + (a + sgn_t * b) * ((k < K) ? p.theta_m2[(size_t)ic * K + k] : 0.0);
+      }
+    }
+  }
+  if (act) {
+    p.advflux_w[o] = fw;
+    p.advflux_th[o] = ft;
+  }
+}
+
 // cells (solve): w tendency (5046-5074, del4 5134-5152, 5167-5223) and theta tendency
 // (5231-5269, del4 5305-5323, 5331-5414)
 __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Config cf, DynTendScal s) {
@@ -412,21 +485,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Co
   const int ne = p.nEdgesOnCell[c];
   const double fzm = act ? p.fzm[k] : 0.0, fzp = act ? p.fzp[k] : 0.0;
   const bool rk1 = s.rk_step == 1;
-  // ---------------- w: horizontal advection (5046-5074)
+  // ---------------- w: horizontal advection (5046-5074); edge fluxes from k_dyn_advflux
   double tw = 0.0;
   for (int i = 0; i < ne; ++i) {
     const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
     const double rue = LD(p.ru, (size_t)e * K + k);
     const double rue_m = up1(rue);
     const double ru_edge_w = fzm * rue + fzp * rue_m;
-    const double sgn = sgn1(ru_edge_w);
-    double flux = 0.0;
-    const int na = p.nAdvCellsForEdge[e];
-    for (int j = 0; j < na; ++j) {
-      const int ic = uni(p.advCellsForEdge[e * 15 + j]);
-      const double scalar_weight = p.adv_coefs[e * 15 + j] + sgn * p.adv_coefs_3rd[e * 15 + j];
-      flux = flux + scalar_weight * LDW(p.w2, (size_t)ic * K1 + k);
-    }
+    const double flux = LD(p.advflux_w, (size_t)e * K + k);
     tw = tw - p.edgesOnCell_sign[c * d.maxEdges + i] * ru_edge_w * flux;
   }
   // ---------------- w euler tendency: del4 (rk1)
@@ -465,19 +531,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Co
     p.tend_w[ow] = (act && k >= 1) ? tw : 0.0;
     if (rk1) p.tend_w_euler[ow] = twe;
   }
-  // ---------------- theta: horizontal advection (5231-5252)
+  // ---------------- theta: horizontal advection (5231-5252); edge fluxes from k_dyn_advflux
   double tt = 0.0;
   for (int i = 0; i < ne; ++i) {
     const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
     const double rue = LD(p.ru, (size_t)e * K + k);
-    const double sgn = sgn1(rue);
-    double flux = 0.0;
-    const int na = p.nAdvCellsForEdge[e];
-    for (int j = 0; j < na; ++j) {
-      const int ic = uni(p.advCellsForEdge[e * 15 + j]);
-      const double scalar_weight = p.adv_coefs[e * 15 + j] + sgn * p.adv_coefs_3rd[e * 15 + j];
-      flux = flux + scalar_weight * LD(p.theta_m2, (size_t)ic * K + k);
-    }
+    const double flux = LD(p.advflux_th, (size_t)e * K + k);
     tt = tt - p.edgesOnCell_sign[c * d.maxEdges + i] * rue * flux;
   }
   if (!rk1) {  // perturbation flux for rtheta_pp (5256-5269)
@@ -878,9 +937,17 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges(Dims d, Ptrs p, co
   if (reconstruct_v) {
     vv = 0.0;
     const int neoe = p.nEdgesOnEdge[e];
-    for (int i = 0; i < neoe; ++i) {
-      const int eoe = uni(p.edgesOnEdge[e * d.maxEdges2 + i]);
-      vv = vv + p.weightsOnEdge[e * d.maxEdges2 + i] * u[(size_t)eoe * K + k];
+    if (neoe == 10) {
+      double uu[10];
+#pragma unroll
+      for (int i = 0; i < 10; ++i) uu[i] = u[(size_t)uni(p.edgesOnEdge[e * d.maxEdges2 + i]) * K + k];
+#pragma unroll
+      for (int i = 0; i < 10; ++i) vv = vv + p.weightsOnEdge[e * d.maxEdges2 + i] * uu[i];
+    } else {
+      for (int i = 0; i < neoe; ++i) {
+        const int eoe = uni(p.edgesOnEdge[e * d.maxEdges2 + i]);
+        vv = vv + p.weightsOnEdge[e * d.maxEdges2 + i] * u[(size_t)eoe * K + k];
+      }
     }
     p.v[o] = vv;
   } else {

@@ -17,7 +17,7 @@ from .mesh import build_mesh
 
 CACHE = os.environ.get("MPAS_DYCORE_CACHE", "/tmp/mpas_dycore_cache")
 
-LEVEL_OF = {642: 3, 2562: 4, 10242: 5, 40962: 6, 163842: 7, 655362: 8}
+LEVEL_OF = {162: 2, 642: 3, 2562: 4, 10242: 5, 40962: 6, 163842: 7, 655362: 8}
 
 
 def level_for(ncells: int) -> int:

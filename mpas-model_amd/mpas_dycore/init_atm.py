@@ -440,7 +440,7 @@ def _jw_columns(lat, zgrid, zz, vg, R, moist):
             geo[0] * 2.0 * u0 * ce ** 1.5 + geo[1]) / (1.0 + 0.61 * qv)
         if moist:
             ptemp = ppb + pp
-            relhum = np.where(ptemp < 50000.0, 0.0, np.where(ptemp > P0, 1.0, 1.0 - ((P0 - ptemp) / 50000.0) ** 1.25))
+            relhum = np.where(ptemp < 50000.0, 0.0, np.where(ptemp > P0, 1.0, 1.0 - (np.maximum(P0 - ptemp, 0.0) / 50000.0) ** 1.25))
             relhum = np.minimum(0.40, relhum)
             es = np.where(temperature > 273.15,
                           1000.0 * 0.6112 * np.exp(17.67 * (temperature - 273.15) / (temperature - 29.65)),

@@ -78,6 +78,25 @@ contains
       close(u)
    end subroutine read_i
 
+   ! restore a field from a previous dump (pool.name[.tlN].bin), used by the kernel modes
+   subroutine read_dump_r(pname, name, t, ntl, a, n)
+      character(len=*), intent(in) :: pname, name
+      integer, intent(in) :: t, ntl, n
+      real(kind=RKIND), intent(inout) :: a(n)
+      character(len=8) :: tl
+      character(len=320) :: fn
+      logical :: ex
+      integer :: u
+      tl = ''
+      if (ntl > 1) write(tl, '(a,i1)') '.tl', t
+      fn = trim(indir)//'/'//trim(pname)//'.'//trim(name)//trim(tl)//'.bin'
+      inquire(file=trim(fn), exist=ex)
+      if (.not. ex) return
+      open(newunit=u, file=trim(fn), access='stream', form='unformatted', status='old')
+      read(u) a
+      close(u)
+   end subroutine read_dump_r
+
    subroutine add_r0(pool, pname, name)
       type (mpas_pool_type), pointer :: pool
       character(len=*), intent(in) :: pname, name
@@ -107,6 +126,7 @@ contains
       allocate(f % array(d1))
       f % array = 0.0_RKIND
       call read_r(name, f % array, d1)
+      call read_dump_r(pname, name, 1, 1, f % array, d1)
       call mpas_pool_add_field(pool, name, f)
       call register(pname, name, 1, 1, .false.)
    end subroutine add_r1
@@ -128,6 +148,9 @@ contains
          fa(t) % array = 0.0_RKIND
       end do
       call read_r(name, fa(1) % array, d1*d2)
+      do t = 1, ntl
+         call read_dump_r(pname, name, t, ntl, fa(t) % array, d1*d2)
+      end do
       call mpas_pool_add_field(pool, name, fa)
       call register(pname, name, 2, ntl, .false.)
    end subroutine add_r2
@@ -150,6 +173,9 @@ contains
          fa(t) % array = 0.0_RKIND
       end do
       call read_r(name, fa(1) % array, d1*d2*d3)
+      do t = 1, ntl
+         call read_dump_r(pname, name, t, ntl, fa(t) % array, d1*d2*d3)
+      end do
       call mpas_pool_add_field(pool, name, fa)
       call register(pname, name, 3, ntl, .false.)
    end subroutine add_r3
@@ -259,7 +285,10 @@ program mpas_ref_harness
    real(kind=RKIND) :: config_smagorinsky_coef, config_epssm, config_smdiv, config_apvm_upwinding
    real(kind=RKIND) :: config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days
    character(len=64) :: config_horiz_mixing
-   namelist /harness/ nCells, nEdges, nVertices, nVertLevels_in, maxEdges_in, maxEdges2_in, num_scalars_in, &
+   character(len=32) :: mode
+   integer :: kernel_small_step, kernel_rk_step
+   real(kind=RKIND) :: kernel_dts
+   namelist /harness/ mode, kernel_small_step, kernel_rk_step, kernel_dts, nCells, nEdges, nVertices, nVertLevels_in, maxEdges_in, maxEdges2_in, num_scalars_in, &
       nsteps, moist_end, nthreads_req, dump_steps, dt, sphere_radius, &
       config_time_integration_order, config_number_of_sub_steps, config_dynamics_split_steps, &
       config_number_rayleigh_damp_u_levels, config_split_dynamics_transport, config_scalar_advection, &
@@ -287,6 +316,10 @@ program mpas_ref_harness
    nthreads_req = 0
    moist_end = 1
    config_horiz_mixing = '2d_smagorinsky'
+   mode = 'run'
+   kernel_small_step = 2
+   kernel_rk_step = 1
+   kernel_dts = 0.0_RKIND
    open(newunit=u, file=trim(indir)//'/harness.nml', status='old')
    read(u, nml=harness)
    close(u)
@@ -528,6 +561,26 @@ program mpas_ref_harness
    call add_r2(tend_physics, 'tend_physics', 'rqvdynten', K, nC1, 1)
 
    allocate(plist(1))
+
+   if (trim(mode) == 'acoustic') then
+      ! kernel mode: one acoustic sub-step on a state restored from a dump
+      ! (atm_advance_acoustic_step 2312 + atm_divergence_damping_3d 2726), as srk3 calls them (794-869)
+!$OMP PARALLEL DO
+      do t = 1, nthr
+         call atm_advance_acoustic_step(state, diag, tend, mesh, configs, nCells, K, kernel_dts, kernel_small_step, &
+                                        cts(t), cte(t), vts(t), vte(t), ets(t), ete(t), &
+                                        csts(t), cste(t), vsts(t), vste(t), ests(t), este(t))
+      end do
+!$OMP END PARALLEL DO
+!$OMP PARALLEL DO
+      do t = 1, nthr
+         call atm_divergence_damping_3d(state, diag, mesh, configs, kernel_dts, ets(t), ete(t))
+      end do
+!$OMP END PARALLEL DO
+      call dump_all(trim(outdir)//'/step_0000', plist)
+      call mpas_dmpar_finalize(domain % dminfo)
+      stop
+   end if
 
    ! ---- model init (mpas_atm_core.F:365-424) ----
    allocate(ke_vertex(K, nV1))

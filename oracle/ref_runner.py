@@ -153,3 +153,30 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
         import shutil
         shutil.rmtree(tmp, ignore_errors=True)
     return res, times
+
+
+def run_reference_kernel(case: dict, restore_dir: str, mode: str, dts: float = 0.0, small_step: int = 2,
+                         rk_step: int = 1, nthreads: int = 1, timeout: int = 600) -> dict:
+    """Run one reference routine ('acoustic' = atm_advance_acoustic_step + atm_divergence_damping_3d)
+    on a state restored from a previous dump directory; returns the dumped pools."""
+    import shutil
+    tmp = tempfile.mkdtemp(prefix="mpasrefk_")
+    try:
+        ind, outd = os.path.join(tmp, "in"), os.path.join(tmp, "out")
+        write_inputs(case, ind, 0, 1.0, [], nthreads)
+        for fn in os.listdir(restore_dir):
+            if fn.endswith(".bin"):
+                shutil.copy(os.path.join(restore_dir, fn), os.path.join(ind, fn))
+        with open(os.path.join(ind, "harness.nml")) as f:
+            nml = f.read()
+        extra = f" mode='{mode}', kernel_small_step={small_step}, kernel_rk_step={rk_step}, kernel_dts={dts!r},\n"
+        nml = nml.replace("&harness\n", "&harness\n" + extra.replace("e+", "d+").replace("e-", "d-"))
+        with open(os.path.join(ind, "harness.nml"), "w") as f:
+            f.write(nml)
+        env = dict(os.environ, OMP_NUM_THREADS=str(nthreads))
+        r = subprocess.run([HARNESS, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference kernel run failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
+        return read_dump(case, os.path.join(outd, "step_0000"))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)

@@ -62,3 +62,28 @@ def test_timestep_matches_reference(small_case, ref_run, nsteps, tol, wtol):
         errs[key] = rel_linf(got.reshape(ref[key].shape), ref[key])
     bad = {k: v for k, v in errs.items() if not v <= (wtol if k == "state.w.tl1" else tol)}
     assert not bad, f"rel Linf above {tol}: {bad} (all: {errs})"
+
+
+def test_moist_trajectory_matches_reference_fixture():
+    """Moist JW + 2 tracer blobs (num_scalars=3, monotone split transport exercised) vs the
+    committed reference trajectory: rel Linf <= 1e-10 after 10 steps (north_star bar)."""
+    import os
+    from mpas_dycore import Dycore
+    from mpas_dycore.cases import jw_case
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "srk3_x1.642_K26_ns3.npz"))
+    case = jw_case(642, K=26, ns=3, moist=True, cache=False)
+    dt = float(z["dt"])
+    dy = Dycore(case, device=0)
+    dy.init_diagnostics(dt)
+    for it in range(10):
+        dy.atm_timestep(dt, it + 1)
+        dy.shift_time_levels()
+        if it + 1 in (1, 10):
+            dy.synchronize()
+            for pool, name, key in PROG + [("state", "scalars", "state.scalars.tl1")]:
+                ref = z[f"step{it + 1}_{key}"]
+                got = dy.get(pool, name, 1).reshape(ref.shape)
+                err = rel_linf(got, ref)
+                tol = 1e-10 if (it + 1 == 10 or name in ("w", "scalars")) else 1e-12
+                assert err <= tol, f"step {it + 1} {key}: rel Linf {err:.3e}"
+    dy.close()

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE dycore.
+
+Runs the unmodified reference atm_srk3 (oracle/_ref/mpas_ref_harness, built from
+/root/reference by oracle/Makefile) on deterministic synthetic cases and stores
+inputs/outputs as compressed npz (data only -- no reference source).
+
+  tests/golden/acoustic_x1.162_K16.npz
+      one atm_advance_acoustic_step + atm_divergence_damping_3d (small_step=2) on a
+      mid-run state: every input the kernel reads (pre_*) and every field it updates
+      (post_*), plus the mesh arrays it needs (0-based indices).
+  tests/golden/srk3_x1.642_K26_ns3.npz
+      moist JW + two tracer blobs (num_scalars=3): reference prognostics after 1 and
+      10 atm_timestep calls (u, w, theta_m, rho_zz, scalars) and an input checksum.
+
+Usage: python tools/make_golden.py   (needs oracle/_ref built; run in the build container)
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import shutil
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpas-model_amd"))
+sys.path.insert(0, ROOT)
+
+from mpas_dycore.cases import jw_case  # noqa: E402
+from oracle import ref_runner  # noqa: E402
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+ACOUSTIC_PRE = ["diag.ru_p", "diag.ruAvg", "diag.rho_pp", "diag.rtheta_pp", "diag.rtheta_pp_old", "diag.rw_p",
+                "diag.wwAvg", "state.theta_m.tl1", "state.rho_zz.tl2", "state.w.tl2", "diag.exner", "diag.cqu",
+                "diag.cofwr", "diag.cofwz", "diag.cofwt", "diag.coftz", "diag.cofrz", "diag.a_tri", "diag.alpha_tri",
+                "diag.gamma_tri", "tend.u", "tend.rho_zz", "tend.theta_m", "tend.w", "diag.rw", "diag.rw_save"]
+ACOUSTIC_POST = ["diag.ru_p", "diag.ruAvg", "diag.rho_pp", "diag.rtheta_pp", "diag.rtheta_pp_old", "diag.rw_p",
+                 "diag.wwAvg"]
+ACOUSTIC_MESH = ["zz", "zxu", "dss", "fzm", "fzp", "rdzw", "cellsOnEdge", "edgesOnCell", "nEdgesOnCell",
+                 "edgesOnCell_sign", "invDcEdge", "dvEdge", "invAreaCell"]
+STATE = ["state.u.tl1", "state.w.tl1", "state.theta_m.tl1", "state.rho_zz.tl1", "state.scalars.tl1"]
+
+
+def case_checksum(case: dict) -> str:
+    h = hashlib.sha256()
+    for k in sorted(case):
+        v = case[k]
+        if isinstance(v, np.ndarray):
+            h.update(k.encode())
+            h.update(np.ascontiguousarray(v).tobytes())
+    return h.hexdigest()
+
+
+def acoustic_fixture():
+    case = jw_case(162, K=16, ns=1, cache=False)
+    wd = "/tmp/golden_acoustic"
+    shutil.rmtree(wd, ignore_errors=True)
+    res, _ = ref_runner.run_reference(case, nsteps=2, dt=case["dt"], dump_steps=[2], nthreads=1, workdir=wd)
+    pre = res[2]
+    dts = case["dt"] / case["config"]["config_dynamics_split_steps"] / case["config"]["config_number_of_sub_steps"]
+    post = ref_runner.run_reference_kernel(case, os.path.join(wd, "out", "step_0002"), "acoustic", dts=dts,
+                                           small_step=2, nthreads=1)
+    out = dict(nCells=case["nCells"], nEdges=case["nEdges"], K=case["nVertLevels"], maxEdges=case["maxEdges"],
+               dts=dts, small_step=2, epssm=case["config"]["config_epssm"], smdiv=case["config"]["config_smdiv"],
+               len_disp=case["config"]["config_len_disp"])
+    for k in ACOUSTIC_PRE:
+        out["pre_" + k] = pre[k]
+    for k in ACOUSTIC_POST:
+        out["post_" + k] = post[k]
+    for k in ACOUSTIC_MESH:
+        out["mesh_" + k] = np.asarray(case[k])
+    os.makedirs(GOLD, exist_ok=True)
+    np.savez_compressed(os.path.join(GOLD, "acoustic_x1.162_K16.npz"), **out)
+    shutil.rmtree(wd, ignore_errors=True)
+
+
+def srk3_fixture():
+    case = jw_case(642, K=26, ns=3, moist=True, cache=False)
+    res, _ = ref_runner.run_reference(case, nsteps=10, dt=case["dt"], dump_steps=[1, 10], nthreads=4)
+    out = dict(checksum=case_checksum(case), dt=case["dt"])
+    for s in (1, 10):
+        for k in STATE:
+            out[f"step{s}_{k}"] = res[s][k]
+    np.savez_compressed(os.path.join(GOLD, "srk3_x1.642_K26_ns3.npz"), **out)
+
+
+if __name__ == "__main__":
+    if not ref_runner.available():
+        sys.exit("build the oracle first: make -C oracle")
+    acoustic_fixture()
+    srk3_fixture()
+    for f in sorted(os.listdir(GOLD)):
+        print(f, os.path.getsize(os.path.join(GOLD, f)))
