@@ -95,9 +95,54 @@ int mpas_dyc_shift_time_levels(mpas_dyc_ctx* ctx);
 /* Block until all queued device work of the context is complete. */
 int mpas_dyc_synchronize(mpas_dyc_ctx* ctx);
 
+/* ---- domain decomposition: several blocks per process, halo exchange ----
+ *
+ * A context holds the blocks this process owns (MPAS domain%blocklist; one per
+ * GPU in production, several per GPU in tests).  Each block has its own dims
+ * (owned-first element order, nCellsSolve etc. = owned counts, as built by
+ * mpas_block_creator.F) and its own fields, addressed with the *_block_field
+ * variants (the functions above act on block 0).  Halo exchanges happen inside
+ * mpas_dyc_timestep at the reference's mpas_dmpar_exch_halo_field points
+ * (mpas_atm_time_integration.F:329-1717, 3757, 4098): block-to-block copies
+ * inside the process, RCCL ncclSend/ncclRecv between processes. */
+#define MPAS_DYC_CELL 0
+#define MPAS_DYC_EDGE 1
+#define MPAS_DYC_VERTEX 2
+#define MPAS_DYC_SEND 0
+#define MPAS_DYC_RECV 1
+
+int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims /* [nblocks] */, const mpas_dyc_config* cfg,
+                           int device, mpas_dyc_ctx** out);
+int32_t mpas_dyc_num_blocks(const mpas_dyc_ctx* ctx);
+int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name,
+                             int32_t time_level, const void* host, int64_t nbytes);
+int mpas_dyc_get_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name,
+                             int32_t time_level, void* host, int64_t nbytes);
+int64_t mpas_dyc_block_field_bytes(const mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name);
+void* mpas_dyc_block_field_device_ptr(mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name,
+                                      int32_t time_level);
+/* One entry of a block's multihalo exchange list (mpas_dmpar.F mpas_multihalo_exchange_list:
+ * procID/blockID/nList/srcList|destList): the elements of `location` in halo layer
+ * `halo_layer` (cells 1..2, edges/vertices 1..3) that this block sends to (owned elements)
+ * or receives from (halo elements) block `peer_block` of rank `peer_rank`, as 1-based local
+ * indices in message order.  Both sides must list the same elements in the same order. */
+int mpas_dyc_set_exchange_list(mpas_dyc_ctx* ctx, int32_t block, int32_t location, int32_t halo_layer,
+                               int32_t direction, int32_t peer_rank, int32_t peer_block, const int32_t* local_index,
+                               int32_t n);
+/* RCCL communicator for exchanges between processes (one rank per GPU): rank 0 creates the
+ * id (ncclGetUniqueId), every rank passes it to mpas_dyc_comm_init (ncclCommInitRank). */
+int64_t mpas_dyc_comm_unique_id_bytes(void);
+int mpas_dyc_comm_unique_id(void* id, int64_t nbytes);
+int mpas_dyc_comm_init(mpas_dyc_ctx* ctx, const void* id, int64_t nbytes, int32_t nranks, int32_t rank);
+/* Test hook: route block-to-block exchanges inside this process through RCCL (send to self). */
+int mpas_dyc_set_transport(mpas_dyc_ctx* ctx, int32_t rccl_for_local_blocks);
+/* mpas_dmpar_exch_halo_field(field, haloLayers) for one field; layer_mask bit l-1 = layer l. */
+int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level,
+                           int32_t layer_mask);
+
 /* ---- measurement hooks (bench.py / tests) ---- */
-/* One acoustic sub-step (atm_advance_acoustic_step + atm_divergence_damping_3d) on the
- * current state, repeated `reps` times, timed with HIP events on the compute stream.
+/* One acoustic sub-step (atm_advance_acoustic_step + atm_divergence_damping_3d) of block 0 on
+ * the current state, repeated `reps` times, timed with HIP events on the compute stream.
  * Returns the average time per sub-step in *ms_out and per-kernel averages in
  * ms_kernels[3] = {edge phase, cell phase, divergence damping} (may be NULL). */
 int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_step, int32_t reps,
@@ -105,7 +150,7 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
 /* Capture one full timestep in a hipGraph and replay it for subsequent
  * mpas_dyc_timestep calls (1 = on, 0 = off). */
 int mpas_dyc_use_graph(mpas_dyc_ctx* ctx, int32_t on);
-/* Algorithmic HBM bytes of one acoustic sub-step (B_ac). */
+/* Algorithmic HBM bytes of one acoustic sub-step of block 0 (B_ac). */
 double mpas_dyc_acoustic_bytes(const mpas_dyc_ctx* ctx);
 
 #ifdef __cplusplus

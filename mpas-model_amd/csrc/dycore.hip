@@ -1,17 +1,23 @@
 // Host side of the MI355X-native dycore: field registry in HBM, the atm_srk3
-// sequencer (mpas_atm_time_integration.F:142-1796) and the C ABI declared in
-// include/mpas_dycore.h.  One translation unit with the kernels.
+// sequencer (mpas_atm_time_integration.F:142-1796), halo exchanges between
+// blocks (mpas_dmpar.F: device copies between blocks of this process, RCCL
+// send/recv between processes) and the C ABI declared in include/mpas_dycore.h.
+// One translation unit with the kernels.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/mpas_dycore.h"
 #include "kernels.hip"
+#include "halo.hip"
 
 using namespace mpas;
 
@@ -28,25 +34,77 @@ struct Field {
   Target target;
   int ntl;
   void* buf[2] = {nullptr, nullptr};
-  int64_t count() const { return inner; }
 };
+
+// One entry of a block's multihalo exchange list (mpas_multihalo_exchange_list:
+// procID, blockID, nList, srcList/destList), one per (location, halo layer,
+// direction, peer block).
+struct XList {
+  int loc, layer, dir, peer_rank, peer_block;
+  int n = 0;
+  int* d_idx = nullptr;  // 0-based local element indices, message order
+};
+
+// A block: MPAS block_type -- dims, fields and exchange lists of one patch.
+struct Block {
+  Dims d{};
+  std::vector<Field> fields;
+  std::map<std::string, int> by_name;  // "pool.name"
+  std::vector<XList> xl;
+  int64_t nEdges_act = -1;             // edges with an owned cell (from cellsOnEdge), for B_ac
+};
+
+// One message of an exchange point: a contiguous range of a block's send or receive buffer.
+struct XMsg {
+  int block, peer_rank, peer_block;
+  int64_t off, count;  // doubles
+};
+
+struct XBlockPlan {
+  XSeg* d_pack = nullptr;
+  XSeg* d_unpack = nullptr;
+  int npack = 0, nunpack = 0, maxn_pack = 0, maxn_unpack = 0;
+  double* sendbuf = nullptr;
+  double* recvbuf = nullptr;
+  int64_t nsend = 0, nrecv = 0;
+};
+
+struct XPlan {
+  std::vector<XBlockPlan> bp;
+  std::vector<std::pair<XMsg, XMsg>> local;  // (send, matching recv) between blocks of this process
+  std::vector<XMsg> rsend, rrecv;            // RCCL messages, in matching order
+};
+
+// One field of an exchange point: mpas_dmpar_exch_halo_field(field[, haloLayers]).
+struct XField {
+  const char* pool;
+  const char* name;
+  int tl;            // time level for state fields (1/2), ignored otherwise
+  unsigned layers;   // bit l-1 set = halo layer l exchanged
+};
+constexpr unsigned ALL_LAYERS = 0x7u;
 
 }  // namespace
 
 struct mpas_dyc_ctx {
-  Dims d{};
   Config cf{};
   int index_qv = 0;
   int device = 0;
   hipStream_t stream = nullptr;
-  std::vector<Field> fields;
-  std::map<std::string, int> by_name;  // "pool.name"
+  std::vector<Block> blk;
   int cur = 0;                          // time level 1 -> buf[cur], 2 -> buf[1-cur]
   std::string err;
   hipEvent_t ev[8] = {};
   bool use_graph = false;
   hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
   double graph_dt[2] = {0, 0};
+  // halo exchange
+  int rank = 0, nranks = 1;
+  ncclComm_t comm = nullptr;
+  bool rccl_local = false;              // route block-to-block copies of this process through RCCL too
+  bool planning = false;                // dry run: build exchange plans, launch nothing
+  bool planned[2] = {false, false};
+  std::map<std::string, XPlan> plans;
 };
 
 namespace {
@@ -60,22 +118,39 @@ namespace {
     }                                                                                 \
   } while (0)
 
-int64_t nloc(const mpas_dyc_ctx* c, Loc l) {
+#define NCCLCHK(x)                                                                    \
+  do {                                                                                \
+    ncclResult_t r_ = (x);                                                            \
+    if (r_ != ncclSuccess) {                                                          \
+      ctx->err = std::string(#x) + ": " + ncclGetErrorString(r_);                     \
+      return MPAS_DYC_ECOMM;                                                          \
+    }                                                                                 \
+  } while (0)
+
+#define CHK(x)                 \
+  do {                         \
+    int r__ = (x);             \
+    if (r__) return r__;       \
+  } while (0)
+
+int64_t nloc(const Block& b, Loc l) {
   switch (l) {
-    case L_CELL: return c->d.nCells + 1;
-    case L_EDGE: return c->d.nEdges + 1;
-    case L_VERTEX: return c->d.nVertices + 1;
+    case L_CELL: return b.d.nCells + 1;
+    case L_EDGE: return b.d.nEdges + 1;
+    case L_VERTEX: return b.d.nVertices + 1;
     default: return 1;
   }
 }
 
-int64_t field_elems(const mpas_dyc_ctx* c, const Field& f) { return nloc(c, f.loc) * f.inner; }
-int64_t field_bytes(const mpas_dyc_ctx* c, const Field& f) {
-  return field_elems(c, f) * (f.is_int ? 4 : 8);
+int64_t field_elems(const Block& b, const Field& f) { return nloc(b, f.loc) * f.inner; }
+int64_t field_bytes(const Block& b, const Field& f) { return field_elems(b, f) * (f.is_int ? 4 : 8); }
+
+bool is_host_0d(const Field& f) {
+  return f.pool == "mesh" && (f.name == "cf1" || f.name == "cf2" || f.name == "cf3");
 }
 
-void add(mpas_dyc_ctx* c, const char* pool, const char* name, Loc loc, int64_t inner, int ntl = 1,
-         bool is_int = false, Target t = T_NONE) {
+void add(Block& c, const char* pool, const char* name, Loc loc, int64_t inner, int ntl = 1, bool is_int = false,
+         Target t = T_NONE) {
   Field f;
   f.pool = pool;
   f.name = name;
@@ -84,13 +159,12 @@ void add(mpas_dyc_ctx* c, const char* pool, const char* name, Loc loc, int64_t i
   f.is_int = is_int;
   f.target = t;
   f.ntl = ntl;
-  c->by_name[f.pool + "." + f.name] = (int)c->fields.size();
-  c->fields.push_back(f);
+  c.by_name[f.pool + "." + f.name] = (int)c.fields.size();
+  c.fields.push_back(f);
 }
-
 // The Registry.xml var_structs the dycore touches (same list the oracle harness builds).
-void build_registry(mpas_dyc_ctx* c) {
-  const int K = c->d.K, ME = c->d.maxEdges, ME2 = c->d.maxEdges2, ns = c->d.ns;
+void build_registry(Block& c) {
+  const int K = c.d.K, ME = c.d.maxEdges, ME2 = c.d.maxEdges2, ns = c.d.ns;
   // mesh: connectivity
   add(c, "mesh", "nEdgesOnCell", L_CELL, 1, 1, true);
   add(c, "mesh", "edgesOnCell", L_CELL, ME, 1, true, T_EDGE);
@@ -172,29 +246,30 @@ void build_registry(mpas_dyc_ctx* c) {
   add(c, "scratch", "wdtn", L_CELL, K + 1);
 }
 
-Field* find(mpas_dyc_ctx* c, const char* pool, const char* name) {
-  auto it = c->by_name.find(std::string(pool) + "." + name);
-  if (it == c->by_name.end()) return nullptr;
-  return &c->fields[it->second];
+Field* find(Block& b, const char* pool, const char* name) {
+  auto it = b.by_name.find(std::string(pool) + "." + name);
+  if (it == b.by_name.end()) return nullptr;
+  return &b.fields[it->second];
 }
 
+int slot_of(const mpas_dyc_ctx* c, const Field& f, int tl) { return (f.ntl == 2) ? ((tl == 2) ? 1 - c->cur : c->cur) : 0; }
+
 template <class T>
-T* P(mpas_dyc_ctx* c, const char* pool, const char* name, int tl = 1) {
-  Field* f = find(c, pool, name);
+T* P(mpas_dyc_ctx* c, Block& b, const char* pool, const char* name, int tl = 1) {
+  Field* f = find(b, pool, name);
   if (!f) {
     fprintf(stderr, "mpas_dycore: internal: missing field %s.%s\n", pool, name);
     abort();
   }
-  int slot = (f->ntl == 2) ? ((tl == 1) ? c->cur : 1 - c->cur) : 0;
-  return (T*)f->buf[slot];
+  return (T*)f->buf[slot_of(c, *f, tl)];
 }
 
-Ptrs make_ptrs(mpas_dyc_ctx* c) {
+Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   Ptrs p{};
-#define MI(x) p.x = P<const int>(c, "mesh", #x)
-#define MR(x) p.x = P<const double>(c, "mesh", #x)
-#define DG(x) p.x = P<double>(c, "diag", #x)
-#define SC(x) p.x = P<double>(c, "scratch", #x)
+#define MI(x) p.x = P<const int>(c, b, "mesh", #x)
+#define MR(x) p.x = P<const double>(c, b, "mesh", #x)
+#define DG(x) p.x = P<double>(c, b, "diag", #x)
+#define SC(x) p.x = P<double>(c, b, "scratch", #x)
   MI(nEdgesOnCell); MI(edgesOnCell); MI(cellsOnCell); MI(verticesOnCell); MI(kiteForCell);
   MI(cellsOnEdge); MI(verticesOnEdge); MI(nEdgesOnEdge); MI(edgesOnEdge); MI(nAdvCellsForEdge);
   MI(advCellsForEdge); MI(cellsOnVertex); MI(edgesOnVertex);
@@ -205,11 +280,11 @@ Ptrs make_ptrs(mpas_dyc_ctx* c) {
   MR(adv_coefs); MR(adv_coefs_3rd); MR(defc_a); MR(defc_b);
   MR(zgrid); MR(zz); MR(zxu); MR(dss); MR(zb_cell); MR(zb3_cell);
   MR(u_init); MR(v_init); MR(t_init); MR(angleEdge);
-  p.u1 = P<double>(c, "state", "u", 1); p.u2 = P<double>(c, "state", "u", 2);
-  p.w1 = P<double>(c, "state", "w", 1); p.w2 = P<double>(c, "state", "w", 2);
-  p.theta_m1 = P<double>(c, "state", "theta_m", 1); p.theta_m2 = P<double>(c, "state", "theta_m", 2);
-  p.rho_zz1 = P<double>(c, "state", "rho_zz", 1); p.rho_zz2 = P<double>(c, "state", "rho_zz", 2);
-  p.scalars1 = P<double>(c, "state", "scalars", 1); p.scalars2 = P<double>(c, "state", "scalars", 2);
+  p.u1 = P<double>(c, b, "state", "u", 1); p.u2 = P<double>(c, b, "state", "u", 2);
+  p.w1 = P<double>(c, b, "state", "w", 1); p.w2 = P<double>(c, b, "state", "w", 2);
+  p.theta_m1 = P<double>(c, b, "state", "theta_m", 1); p.theta_m2 = P<double>(c, b, "state", "theta_m", 2);
+  p.rho_zz1 = P<double>(c, b, "state", "rho_zz", 1); p.rho_zz2 = P<double>(c, b, "state", "rho_zz", 2);
+  p.scalars1 = P<double>(c, b, "state", "scalars", 1); p.scalars2 = P<double>(c, b, "state", "scalars", 2);
   DG(theta); DG(rho); DG(rho_base); DG(theta_base); DG(rho_p); DG(rho_p_save); DG(rho_pp); DG(rho_zz_old_split);
   DG(rtheta_base); DG(rtheta_p); DG(rtheta_p_save); DG(rtheta_pp); DG(rtheta_pp_old);
   DG(exner); DG(exner_base); DG(pressure_base); DG(pressure_p); DG(h_divergence); DG(kdiff); DG(ke); DG(divergence);
@@ -218,11 +293,11 @@ Ptrs make_ptrs(mpas_dyc_ctx* c) {
   DG(rw); DG(rw_p); DG(rw_save); DG(wwAvg); DG(wwAvg_split);
   DG(ru); DG(ruAvg); DG(ruAvg_split); DG(ru_p); DG(ru_save); DG(cqu); DG(rho_edge); DG(v); DG(pv_edge);
   DG(gradPVn); DG(gradPVt); DG(vorticity); DG(pv_vertex);
-  p.tend_u = P<double>(c, "tend", "u"); p.tend_u_euler = P<double>(c, "tend", "u_euler");
-  p.tend_w = P<double>(c, "tend", "w"); p.tend_w_euler = P<double>(c, "tend", "w_euler");
-  p.tend_theta = P<double>(c, "tend", "theta_m"); p.tend_theta_euler = P<double>(c, "tend", "theta_euler");
-  p.tend_rho = P<double>(c, "tend", "rho_zz"); p.rt_diabatic_tend = P<double>(c, "tend", "rt_diabatic_tend");
-  p.scalars_tend = P<double>(c, "tend", "scalars_tend"); p.rthdynten = P<double>(c, "tend_physics", "rthdynten");
+  p.tend_u = P<double>(c, b, "tend", "u"); p.tend_u_euler = P<double>(c, b, "tend", "u_euler");
+  p.tend_w = P<double>(c, b, "tend", "w"); p.tend_w_euler = P<double>(c, b, "tend", "w_euler");
+  p.tend_theta = P<double>(c, b, "tend", "theta_m"); p.tend_theta_euler = P<double>(c, b, "tend", "theta_euler");
+  p.tend_rho = P<double>(c, b, "tend", "rho_zz"); p.rt_diabatic_tend = P<double>(c, b, "tend", "rt_diabatic_tend");
+  p.scalars_tend = P<double>(c, b, "tend", "scalars_tend"); p.rthdynten = P<double>(c, b, "tend_physics", "rthdynten");
   SC(qtot); SC(tend_ru_physics); SC(tend_rtheta_physics); SC(tend_rho_physics);
   SC(delsq_theta); SC(delsq_w); SC(delsq_divergence); SC(delsq_u); SC(delsq_vorticity); SC(dpdz);
   SC(ke_vertex); SC(ke_edge); SC(horiz_flux_array);
@@ -230,9 +305,9 @@ Ptrs make_ptrs(mpas_dyc_ctx* c) {
   SC(scalar_old_copy);
   SC(advflux_w); SC(advflux_th);
   // 0-d mesh fields are mirrored on the host
-  p.cf1 = c->fields[c->by_name["mesh.cf1"]].buf[1] ? *(double*)c->fields[c->by_name["mesh.cf1"]].buf[1] : 0.0;
-  p.cf2 = c->fields[c->by_name["mesh.cf2"]].buf[1] ? *(double*)c->fields[c->by_name["mesh.cf2"]].buf[1] : 0.0;
-  p.cf3 = c->fields[c->by_name["mesh.cf3"]].buf[1] ? *(double*)c->fields[c->by_name["mesh.cf3"]].buf[1] : 0.0;
+  p.cf1 = b.fields[b.by_name["mesh.cf1"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf1"]].buf[1] : 0.0;
+  p.cf2 = b.fields[b.by_name["mesh.cf2"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf2"]].buf[1] : 0.0;
+  p.cf3 = b.fields[b.by_name["mesh.cf3"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf3"]].buf[1] : 0.0;
 #undef MI
 #undef MR
 #undef DG
@@ -242,21 +317,204 @@ Ptrs make_ptrs(mpas_dyc_ctx* c) {
 
 inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)); }
 
-#define LAUNCH(kern, n, ...)                                                                  \
-  do {                                                                                        \
-    if ((n) > 0) hipLaunchKernelGGL(kern, grid_for(n), dim3(BLOCK_THREADS), 0, ctx->stream, __VA_ARGS__); \
+#define LAUNCH(kern, n, ...)                                                                               \
+  do {                                                                                                     \
+    if ((n) > 0 && !ctx->planning)                                                                         \
+      hipLaunchKernelGGL(kern, grid_for(n), dim3(BLOCK_THREADS), 0, ctx->stream, __VA_ARGS__);             \
   } while (0)
 
 // ---------------------------------------------------------------------------
-// reference routines, one host function each
+// halo exchange (mpas_dmpar_exch_halo_field, framework/mpas_dmpar.F)
+// ---------------------------------------------------------------------------
+bool needs_exchange(const mpas_dyc_ctx* ctx) { return ctx->blk.size() > 1 || ctx->nranks > 1; }
+
+std::string plan_key(const mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
+  std::string k = std::to_string(ctx->cur);
+  for (const auto& f : fs) k += "|" + std::string(f.pool) + "." + f.name + "." + std::to_string(f.tl) + "." + std::to_string(f.layers);
+  return k;
+}
+
+const XList* find_list(const Block& b, int loc, int layer, int dir, int peer_rank, int peer_block) {
+  for (const auto& x : b.xl)
+    if (x.loc == loc && x.layer == layer && x.dir == dir && x.peer_rank == peer_rank && x.peer_block == peer_block)
+      return &x;
+  return nullptr;
+}
+
+void free_plan(XPlan& pl) {
+  for (auto& bp : pl.bp) {
+    if (bp.d_pack) (void)hipFree(bp.d_pack);
+    if (bp.d_unpack) (void)hipFree(bp.d_unpack);
+    if (bp.sendbuf) (void)hipFree(bp.sendbuf);
+    if (bp.recvbuf) (void)hipFree(bp.recvbuf);
+  }
+  pl.bp.clear();
+}
+
+void invalidate_plans(mpas_dyc_ctx* ctx) {
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->plans) free_plan(kv.second);
+  ctx->plans.clear();
+  ctx->planned[0] = ctx->planned[1] = false;
+  for (auto& g : ctx->graph_exec)
+    if (g) {
+      (void)hipGraphExecDestroy(g);
+      g = nullptr;
+    }
+}
+
+// Message layout of one block and direction: peers in (rank, block) order; per peer,
+// the fields in call order and per field the halo layers in ascending order.
+int build_side(mpas_dyc_ctx* ctx, int bi, int dir, const std::vector<XField>& fs, std::vector<XSeg>& segs,
+               std::vector<XMsg>& msgs, int64_t& total, int& maxn) {
+  Block& b = ctx->blk[bi];
+  std::vector<std::pair<int, int>> peers;
+  for (const auto& x : b.xl)
+    if (x.dir == dir) peers.emplace_back(x.peer_rank, x.peer_block);
+  std::sort(peers.begin(), peers.end());
+  peers.erase(std::unique(peers.begin(), peers.end()), peers.end());
+  total = 0;
+  maxn = 0;
+  for (const auto& pr : peers) {
+    const int64_t start = total;
+    for (const auto& f : fs) {
+      Field* F = find(b, f.pool, f.name);
+      if (!F || F->is_int || F->loc == L_NONE) {
+        ctx->err = std::string("halo exchange of unsupported field ") + f.pool + "." + f.name;
+        return MPAS_DYC_EINVAL;
+      }
+      for (int layer = 1; layer <= 3; ++layer) {
+        if (!((f.layers >> (layer - 1)) & 1u)) continue;
+        const XList* x = find_list(b, (int)F->loc, layer, dir, pr.first, pr.second);
+        if (!x || x->n == 0) continue;
+        XSeg s;
+        s.base = (double*)F->buf[slot_of(ctx, *F, f.tl)];
+        s.idx = x->d_idx;
+        s.n = x->n;
+        s.inner = (int)F->inner;
+        s.off = total;
+        segs.push_back(s);
+        total += (int64_t)x->n * F->inner;
+        maxn = std::max(maxn, x->n);
+      }
+    }
+    if (total > start) msgs.push_back(XMsg{bi, pr.first, pr.second, start, total - start});
+  }
+  return MPAS_DYC_OK;
+}
+
+int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
+  const int nb = (int)ctx->blk.size();
+  pl.bp.assign(nb, XBlockPlan{});
+  std::vector<std::vector<XMsg>> smsg(nb), rmsg(nb);
+  for (int bi = 0; bi < nb; ++bi) {
+    XBlockPlan& bp = pl.bp[bi];
+    std::vector<XSeg> ps, us;
+    CHK(build_side(ctx, bi, 0, fs, ps, smsg[bi], bp.nsend, bp.maxn_pack));
+    CHK(build_side(ctx, bi, 1, fs, us, rmsg[bi], bp.nrecv, bp.maxn_unpack));
+    bp.npack = (int)ps.size();
+    bp.nunpack = (int)us.size();
+    if (bp.npack) {
+      HIPCHK(hipMalloc(&bp.d_pack, ps.size() * sizeof(XSeg)));
+      HIPCHK(hipMemcpy(bp.d_pack, ps.data(), ps.size() * sizeof(XSeg), hipMemcpyHostToDevice));
+      HIPCHK(hipMalloc(&bp.sendbuf, bp.nsend * sizeof(double)));
+    }
+    if (bp.nunpack) {
+      HIPCHK(hipMalloc(&bp.d_unpack, us.size() * sizeof(XSeg)));
+      HIPCHK(hipMemcpy(bp.d_unpack, us.data(), us.size() * sizeof(XSeg), hipMemcpyHostToDevice));
+      HIPCHK(hipMalloc(&bp.recvbuf, bp.nrecv * sizeof(double)));
+    }
+  }
+  for (int bi = 0; bi < nb; ++bi) {
+    for (const XMsg& s : smsg[bi]) {
+      if (s.peer_rank == ctx->rank && !ctx->rccl_local) {
+        if (s.peer_block < 0 || s.peer_block >= nb) {
+          ctx->err = "exchange list names block " + std::to_string(s.peer_block) + " not in this process";
+          return MPAS_DYC_EINVAL;
+        }
+        const XMsg* r = nullptr;
+        for (const XMsg& m : rmsg[s.peer_block])
+          if (m.peer_rank == ctx->rank && m.peer_block == bi) r = &m;
+        if (!r || r->count != s.count) {
+          ctx->err = "send/recv lists of blocks " + std::to_string(bi) + "->" + std::to_string(s.peer_block) +
+                     " disagree";
+          return MPAS_DYC_EINVAL;
+        }
+        pl.local.emplace_back(s, *r);
+      } else {
+        pl.rsend.push_back(s);
+      }
+    }
+    for (const XMsg& r : rmsg[bi])
+      if (!(r.peer_rank == ctx->rank && !ctx->rccl_local)) pl.rrecv.push_back(r);
+  }
+  if ((!pl.rsend.empty() || !pl.rrecv.empty()) && !ctx->comm) {
+    ctx->err = "exchange lists name other processes but no communicator was set (mpas_dyc_comm_init)";
+    return MPAS_DYC_ECOMM;
+  }
+  // point-to-point messages between two ranks match in issue order: order both sides by
+  // (source block, destination block)
+  std::sort(pl.rsend.begin(), pl.rsend.end(), [](const XMsg& a, const XMsg& b) {
+    return std::make_tuple(a.peer_rank, a.block, a.peer_block) < std::make_tuple(b.peer_rank, b.block, b.peer_block);
+  });
+  std::sort(pl.rrecv.begin(), pl.rrecv.end(), [](const XMsg& a, const XMsg& b) {
+    return std::make_tuple(a.peer_rank, a.peer_block, a.block) < std::make_tuple(b.peer_rank, b.peer_block, b.block);
+  });
+  return MPAS_DYC_OK;
+}
+
+int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
+  if (!needs_exchange(ctx)) return MPAS_DYC_OK;
+  const std::string key = plan_key(ctx, fs);
+  auto it = ctx->plans.find(key);
+  if (it == ctx->plans.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(ctx->stream, &cs);
+    if (cs != hipStreamCaptureStatusNone) {
+      ctx->err = "internal: exchange plan missing during graph capture";
+      return MPAS_DYC_ESTATE;
+    }
+    XPlan pl;
+    int r = build_plan(ctx, fs, pl);
+    if (r) {
+      free_plan(pl);
+      return r;
+    }
+    it = ctx->plans.emplace(key, std::move(pl)).first;
+  }
+  if (ctx->planning) return MPAS_DYC_OK;
+  XPlan& pl = it->second;
+  for (auto& bp : pl.bp)
+    if (bp.npack)
+      hipLaunchKernelGGL(k_halo_pack, dim3((bp.maxn_pack + 3) / 4, bp.npack), dim3(256), 0, ctx->stream,
+                         bp.d_pack, bp.sendbuf);
+  for (const auto& sr : pl.local)
+    HIPCHK(hipMemcpyAsync(pl.bp[sr.second.block].recvbuf + sr.second.off, pl.bp[sr.first.block].sendbuf + sr.first.off,
+                          sr.first.count * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+  if (!pl.rsend.empty() || !pl.rrecv.empty()) {
+    NCCLCHK(ncclGroupStart());
+    for (const XMsg& m : pl.rsend)
+      NCCLCHK(ncclSend(pl.bp[m.block].sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
+    for (const XMsg& m : pl.rrecv)
+      NCCLCHK(ncclRecv(pl.bp[m.block].recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
+    NCCLCHK(ncclGroupEnd());
+  }
+  for (auto& bp : pl.bp)
+    if (bp.nunpack)
+      hipLaunchKernelGGL(k_halo_unpack, dim3((bp.maxn_unpack + 3) / 4, bp.nunpack), dim3(256), 0, ctx->stream,
+                         bp.d_unpack, bp.recvbuf);
+  return MPAS_DYC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// reference routines, one host function each (per block)
 // ---------------------------------------------------------------------------
 void copy_n(mpas_dyc_ctx* ctx, double* dst, const double* src, int64_t n) {
-  (void)hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream);
+  if (!ctx->planning) (void)hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream);
 }
 
 // atm_rk_integration_setup (1847-1857): copies over owned+halo elements (not the garbage slot)
-void rk_integration_setup(mpas_dyc_ctx* ctx, const Ptrs& p) {
-  const Dims& d = ctx->d;
+void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
   const int64_t K = d.K, K1 = d.K + 1;
   copy_n(ctx, p.ru_save, p.ru, (int64_t)d.nEdges * K);
   copy_n(ctx, p.rw_save, p.rw, (int64_t)d.nCells * K1);
@@ -270,12 +528,11 @@ void rk_integration_setup(mpas_dyc_ctx* ctx, const Ptrs& p) {
   copy_n(ctx, p.scalars2, p.scalars1, (int64_t)d.nCells * K * d.ns);
 }
 
-void vert_imp_coefs(mpas_dyc_ctx* ctx, const Ptrs& p, double dts) {
-  LAUNCH(k_vert_imp_coefs, std::max(ctx->d.nCellsSolve, 1), ctx->d, p, dts, ctx->cf.epssm);
+void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
+  LAUNCH(k_vert_imp_coefs, std::max(d.nCellsSolve, 1), d, p, dts, ctx->cf.epssm);
 }
 
-void dyn_tend(mpas_dyc_ctx* ctx, const Ptrs& p, int rk_step, double dt) {
-  const Dims& d = ctx->d;
+void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, double dt) {
   const Config& cf = ctx->cf;
   DynTendScal s{};
   s.rk_step = rk_step;
@@ -304,20 +561,18 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Ptrs& p, int rk_step, double dt) {
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
 }
 
-void acoustic_step(mpas_dyc_ctx* ctx, const Ptrs& p, double dts, int small_step) {
-  const Dims& d = ctx->d;
+void acoustic_step(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
   LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step);
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
 }
 
-void divergence_damping(mpas_dyc_ctx* ctx, const Ptrs& p, double dts) {
+void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
   const double rdts = 1.0 / dts;
   const double coef_divdamp = 2.0 * ctx->cf.smdiv * ctx->cf.len_disp * rdts;
-  LAUNCH(k_divdamp, ctx->d.nEdges, ctx->d, p, coef_divdamp);
+  LAUNCH(k_divdamp, d.nEdges, d, p, coef_divdamp);
 }
 
-void solve_diagnostics(mpas_dyc_ctx* ctx, const Ptrs& p, double dt, int tl, int rk_step /*0 = absent*/) {
-  const Dims& d = ctx->d;
+void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt, int tl, int rk_step /*0 = absent*/) {
   const double* u = (tl == 1) ? p.u1 : p.u2;
   const double* h = (tl == 1) ? p.rho_zz1 : p.rho_zz2;
   const int reconstruct_v = (rk_step == 0 || rk_step == 3) ? 1 : 0;
@@ -326,8 +581,7 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Ptrs& p, double dt, int tl, int 
   LAUNCH(k_diag_edges, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
 }
 
-void advance_scalars(mpas_dyc_ctx* ctx, const Ptrs& p, double dt, int rk_step, bool advance_density) {
-  const Dims& d = ctx->d;
+void advance_scalars(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt, int rk_step, bool advance_density) {
   double wt_new = 1.0;
   if (advance_density) {
     if (rk_step == 1 && ctx->cf.time_integration_order == 3) wt_new = 1. / 3;
@@ -339,23 +593,54 @@ void advance_scalars(mpas_dyc_ctx* ctx, const Ptrs& p, double dt, int rk_step, b
   LAUNCH(k_scalars_cells, d.nCellsSolve, d, p, dt, wt_new, ctx->cf.coef_3rd_order);
 }
 
-void advance_scalars_mono(mpas_dyc_ctx* ctx, const Ptrs& p, double dt, bool advance_density) {
-  const Dims& d = ctx->d;
-  LAUNCH(k_mono_prep, d.nCells, d, p, dt, advance_density ? 1 : 0);
-  for (int is = 0; is < d.ns; ++is) {
-    LAUNCH(k_mono_bounds, d.nCellsSolve, d, p, is, ctx->cf.coef_3rd_order);
-    LAUNCH(k_mono_edges1, d.nEdges, d, p, is, dt);
-    LAUNCH(k_mono_cells1, d.nCellsSolve, d, p, is, dt, advance_density ? 1 : 0);
-    LAUNCH(k_mono_edges2, d.nEdges, d, p, dt);
-    LAUNCH(k_mono_cells2, d.nCells, d, p, is, advance_density ? 1 : 0);
+// atm_advance_scalars_mono (3548-4210) over all blocks: its two halo exchanges
+// (scalars_old at 3757, the limiter factors at 4098) sit between the block loops.
+int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt, bool advance_density) {
+  const int ad = advance_density ? 1 : 0;
+  const int nb = (int)ctx->blk.size();
+  for (int b = 0; b < nb; ++b) {
+    const Dims& d = ctx->blk[b].d;
+    LAUNCH(k_mono_prep, d.nCells, d, P[b], dt, ad);
   }
+  CHK(exchange(ctx, {{"state", "scalars", 1, ALL_LAYERS}}));
+  const int ns = ctx->blk[0].d.ns;
+  for (int is = 0; is < ns; ++is) {
+    for (int b = 0; b < nb; ++b) {
+      const Dims& d = ctx->blk[b].d;
+      LAUNCH(k_mono_bounds, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
+      LAUNCH(k_mono_edges1, d.nEdges, d, P[b], is, dt);
+      LAUNCH(k_mono_cells1, d.nCellsSolve, d, P[b], is, dt, ad);
+    }
+    CHK(exchange(ctx, {{"scratch", "scale_arr", 1, 0x1u}}));
+    for (int b = 0; b < nb; ++b) {
+      const Dims& d = ctx->blk[b].d;
+      LAUNCH(k_mono_edges2, d.nEdges, d, P[b], dt);
+      LAUNCH(k_mono_cells2, d.nCells, d, P[b], is, ad);
+    }
+  }
+  return MPAS_DYC_OK;
 }
 
-// atm_srk3 (mpas_atm_time_integration.F:142-1796), single block: halo exchanges are no-ops
+std::vector<Ptrs> block_ptrs(mpas_dyc_ctx* ctx) {
+  std::vector<Ptrs> P;
+  for (auto& b : ctx->blk) P.push_back(make_ptrs(ctx, b));
+  return P;
+}
+
+// run `body(d, p)` for every block (the reference's `block => domain % blocklist` loops)
+#define EACH(...)                                       \
+  for (size_t ib_ = 0; ib_ < ctx->blk.size(); ++ib_) {  \
+    const Dims& d = ctx->blk[ib_].d;                    \
+    const Ptrs& p = P[ib_];                             \
+    (void)d;                                            \
+    (void)p;                                            \
+    __VA_ARGS__;                                        \
+  }
+
+// atm_srk3 (mpas_atm_time_integration.F:142-1796)
 int srk3(mpas_dyc_ctx* ctx, double dt) {
-  const Dims& d = ctx->d;
   const Config& cf = ctx->cf;
-  Ptrs p = make_ptrs(ctx);
+  const std::vector<Ptrs> P = block_ptrs(ctx);
   int dynamics_split = cf.dynamics_split_steps;
   double dt_dynamics;
   if (cf.split_dynamics_transport) {
@@ -388,54 +673,66 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
     number_sub_steps[1] = std::max(1, nss / 2);
     number_sub_steps[2] = nss;
   }
-  // halo: theta_m, scalars, pressure_p, rtheta_p (329-338)
-  rk_integration_setup(ctx, p);                                   // 341-381
-  LAUNCH(k_moist_cells, d.nCells, d, p);                          // 383-422
-  LAUNCH(k_moist_edges, d.nEdges, d, p);
+  const bool scalars_in_dynamics = cf.scalar_advection && !cf.split_dynamics_transport;
+  CHK(exchange(ctx, {{"state", "theta_m", 1, ALL_LAYERS}, {"state", "scalars", 1, ALL_LAYERS},   // 329-338
+                     {"diag", "pressure_p", 0, ALL_LAYERS}, {"diag", "rtheta_p", 0, ALL_LAYERS}}));
+  EACH(rk_integration_setup(ctx, d, p));                          // 341-381
+  EACH(LAUNCH(k_moist_cells, d.nCells, d, p));                    // 383-422
+  EACH(LAUNCH(k_moist_edges, d.nEdges, d, p));
   // physics tendencies are zero without DO_PHYSICS (450-457): scratch arrays stay zero.
 
   for (int dynamics_substep = 1; dynamics_substep <= dynamics_split; ++dynamics_substep) {
-    vert_imp_coefs(ctx, p, rk_sub_timestep[0]);                   // 476-510
-    // halo: exner (513)
+    EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));         // 476-510
+    CHK(exchange(ctx, {{"diag", "exner", 0, ALL_LAYERS}}));      // 513
     for (int rk_step = 1; rk_step <= 3; ++rk_step) {
-      if (cf.time_integration_order == 3 && rk_step == 2) vert_imp_coefs(ctx, p, rk_sub_timestep[1]);
-      dyn_tend(ctx, p, rk_step, dt);                              // 561-630
-      // halo: tend_u layer 1 (642)
-      LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p);                // 644-678
+      if (cf.time_integration_order == 3 && rk_step == 2) EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[1]));
+      EACH(dyn_tend(ctx, d, p, rk_step, dt));                     // 561-630
+      CHK(exchange(ctx, {{"tend", "u", 0, 0x1u}}));               // 642
+      EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p));          // 644-678
       for (int small_step = 1; small_step <= number_sub_steps[rk_step - 1]; ++small_step) {
-        // halo: rho_pp layer 1 (792)
-        acoustic_step(ctx, p, rk_sub_timestep[rk_step - 1], small_step);  // 794-837
-        // halo: rtheta_pp layer 1 (845)
-        divergence_damping(ctx, p, rk_sub_timestep[rk_step - 1]);          // 849-869
+        CHK(exchange(ctx, {{"diag", "rho_pp", 0, 0x1u}}));        // 792
+        EACH(acoustic_step(ctx, d, p, rk_sub_timestep[rk_step - 1], small_step));  // 794-837
+        CHK(exchange(ctx, {{"diag", "rtheta_pp", 0, 0x1u}}));     // 845
+        EACH(divergence_damping(ctx, d, p, rk_sub_timestep[rk_step - 1]));          // 849-869
       }
-      // halo: rw_p, ru_p, rho_pp (all), rtheta_pp layer 2 (876-887)
+      CHK(exchange(ctx, {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},   // 876-887
+                         {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}}));
       const double invNs = 1 / (double)number_sub_steps[rk_step - 1];
-      LAUNCH(k_recover_edges, d.nEdges, d, p, invNs);             // 889-930
-      LAUNCH(k_recover_cells, d.nCells + 1, d, p, rk_timestep[rk_step - 1], invNs, rk_step);
-      // halo: u (988)
-      if (cf.scalar_advection && !cf.split_dynamics_transport) {  // 993-1185
-        if (rk_step < 3 || (!cf.monotonic && !cf.positive_definite))
-          advance_scalars(ctx, p, rk_timestep[rk_step - 1], rk_step, false);
-        else
-          advance_scalars_mono(ctx, p, rk_timestep[rk_step - 1], false);
+      EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs));       // 889-930
+      EACH(LAUNCH(k_recover_cells, d.nCells + 1, d, p, rk_timestep[rk_step - 1], invNs, rk_step));
+      CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));        // 988
+      if (scalars_in_dynamics) {                                  // 993-1185
+        if (rk_step < 3 || (!cf.monotonic && !cf.positive_definite)) {
+          EACH(advance_scalars(ctx, d, p, rk_timestep[rk_step - 1], rk_step, false));
+        } else {
+          CHK(advance_scalars_mono(ctx, P, rk_timestep[rk_step - 1], false));
+        }
       }
-      solve_diagnostics(ctx, p, dt, 2, rk_step);                  // 1187-1228
-      // halo: w, pv_edge, rho_edge (+ scalars) (1234-1249)
+      EACH(solve_diagnostics(ctx, d, p, dt, 2, rk_step));         // 1187-1228
+      if (scalars_in_dynamics)                                    // 1234-1249
+        CHK(exchange(ctx, {{"state", "w", 2, ALL_LAYERS}, {"diag", "pv_edge", 0, ALL_LAYERS},
+                           {"diag", "rho_edge", 0, ALL_LAYERS}, {"state", "scalars", 2, ALL_LAYERS}}));
+      else
+        CHK(exchange(ctx, {{"state", "w", 2, ALL_LAYERS}, {"diag", "pv_edge", 0, ALL_LAYERS},
+                           {"diag", "rho_edge", 0, ALL_LAYERS}}));
     }
-    // halo: theta_m, pressure_p, rtheta_p between dynamics substeps (1282-1297)
-    LAUNCH(k_substep_finish, d.nEdges + d.nCells, d, p, dynamics_substep, dynamics_split,
-           1.0 / (double)dynamics_split);                          // 1304-1341
+    if (dynamics_substep < dynamics_split)                        // 1282-1297
+      CHK(exchange(ctx, {{"state", "theta_m", 2, ALL_LAYERS}, {"diag", "pressure_p", 0, ALL_LAYERS},
+                         {"diag", "rtheta_p", 0, ALL_LAYERS}}));
+    EACH(LAUNCH(k_substep_finish, d.nEdges + d.nCells, d, p, dynamics_substep, dynamics_split,
+                1.0 / (double)dynamics_split));                   // 1304-1341
   }
 
   if (cf.scalar_advection && cf.split_dynamics_transport) {       // 1355-1576
     double rk_ts[3] = {dt / 3., dt / 2., dt};
     if (cf.time_integration_order == 2) rk_ts[0] = dt / 2.;
     for (int rk_step = 1; rk_step <= 3; ++rk_step) {
-      if (rk_step < 3 || (!cf.monotonic && !cf.positive_definite))
-        advance_scalars(ctx, p, rk_ts[rk_step - 1], rk_step, true);
-      else
-        advance_scalars_mono(ctx, p, rk_ts[rk_step - 1], true);
-      // halo: scalars (1571)
+      if (rk_step < 3 || (!cf.monotonic && !cf.positive_definite)) {
+        EACH(advance_scalars(ctx, d, p, rk_ts[rk_step - 1], rk_step, true));
+      } else {
+        CHK(advance_scalars_mono(ctx, P, rk_ts[rk_step - 1], true));
+      }
+      if (rk_step < 3) CHK(exchange(ctx, {{"state", "scalars", 2, ALL_LAYERS}}));  // 1569-1572
     }
   }
   // mpas_reconstruct (1581-1603) produces output-only diagnostics (uReconstruct*);
@@ -443,13 +740,16 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   return MPAS_DYC_OK;
 }
 
+// model init, mpas_atm_core.F:143-186 (exchanges) and 387-404 (the two routines)
 int init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
-  const Dims& d = ctx->d;
-  Ptrs p = make_ptrs(ctx);
-  LAUNCH(k_init_coupled_a, d.nCells, d, p, ctx->index_qv);
-  LAUNCH(k_init_coupled_b, d.nEdges, d, p);
-  LAUNCH(k_init_coupled_c, d.nCells, d, p);
-  solve_diagnostics(ctx, p, dt, 1, 0);
+  const std::vector<Ptrs> P = block_ptrs(ctx);
+  CHK(exchange(ctx, {{"state", "u", 1, ALL_LAYERS}}));           // 145
+  EACH(LAUNCH(k_init_coupled_a, d.nCells, d, p, ctx->index_qv));
+  EACH(LAUNCH(k_init_coupled_b, d.nEdges, d, p));
+  EACH(LAUNCH(k_init_coupled_c, d.nCells, d, p));
+  EACH(solve_diagnostics(ctx, d, p, dt, 1, 0));
+  CHK(exchange(ctx, {{"diag", "pv_edge", 0, ALL_LAYERS}, {"diag", "ru", 0, ALL_LAYERS},  // 180-186
+                     {"diag", "rw", 0, ALL_LAYERS}}));
   return MPAS_DYC_OK;
 }
 
@@ -458,15 +758,15 @@ int init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
 // ===========================================================================
 // C ABI
 // ===========================================================================
-extern "C" {
+namespace {
 
-int mpas_dyc_create(const mpas_dyc_dims* dims, const mpas_dyc_config* cfg, int device, mpas_dyc_ctx** out) {
-  if (!dims || !cfg || !out) return MPAS_DYC_EINVAL;
-  *out = nullptr;
+int fill_dims(Dims& d, const mpas_dyc_dims* dims) {
   if (dims->nVertLevels < 4 || dims->nVertLevels > 63) return MPAS_DYC_EINVAL;  // column = one wavefront
   if (dims->maxEdges < 3 || dims->maxEdges2 < dims->maxEdges || dims->num_scalars < 1) return MPAS_DYC_EINVAL;
-  mpas_dyc_ctx* ctx = new mpas_dyc_ctx();
-  Dims& d = ctx->d;
+  if (dims->nCells < 1 || dims->nEdges < 1 || dims->nVertices < 1) return MPAS_DYC_EINVAL;
+  if (dims->nCellsSolve < 1 || dims->nCellsSolve > dims->nCells || dims->nEdgesSolve > dims->nEdges ||
+      dims->nVerticesSolve > dims->nVertices)
+    return MPAS_DYC_EINVAL;
   d.nCells = dims->nCells;
   d.nEdges = dims->nEdges;
   d.nVertices = dims->nVertices;
@@ -479,8 +779,10 @@ int mpas_dyc_create(const mpas_dyc_dims* dims, const mpas_dyc_config* cfg, int d
   d.nVerticesSolve = dims->nVerticesSolve;
   d.moist_start = dims->moist_start - 1;
   d.moist_end = dims->moist_end - 1;
-  ctx->index_qv = dims->index_qv - 1;
-  Config& c = ctx->cf;
+  return MPAS_DYC_OK;
+}
+
+void fill_config(Config& c, const mpas_dyc_config* cfg) {
   c.time_integration_order = cfg->config_time_integration_order;
   c.number_of_sub_steps = cfg->config_number_of_sub_steps;
   c.dynamics_split_steps = cfg->config_dynamics_split_steps;
@@ -508,117 +810,187 @@ int mpas_dyc_create(const mpas_dyc_dims* dims, const mpas_dyc_config* cfg, int d
   c.apvm_upwinding = cfg->config_apvm_upwinding;
   c.mpas_cam_coef = cfg->config_mpas_cam_coef;
   c.rayleigh_damp_u_timescale_days = cfg->config_rayleigh_damp_u_timescale_days;
-  if (c.time_integration_order != 2 && c.time_integration_order != 3) {
+}
+
+int64_t target_n(const Block& b, Target t) {
+  switch (t) {
+    case T_CELL: return b.d.nCells;
+    case T_EDGE: return b.d.nEdges;
+    case T_VERTEX: return b.d.nVertices;
+    default: return 0;
+  }
+}
+
+Block* get_block(mpas_dyc_ctx* ctx, int32_t block) {
+  if (!ctx || block < 0 || block >= (int32_t)ctx->blk.size()) return nullptr;
+  return &ctx->blk[block];
+}
+
+// edges with at least one owned cell (the acoustic edge loop's active set), from MPAS 1-based cellsOnEdge
+void count_active_edges(Block& b, const int32_t* coe) {
+  int64_t n = 0;
+  for (int e = 0; e < b.d.nEdges; ++e) {
+    const int c1 = coe[2 * e] - 1, c2 = coe[2 * e + 1] - 1;
+    if ((c1 >= 0 && c1 < b.d.nCellsSolve) || (c2 >= 0 && c2 < b.d.nCellsSolve)) ++n;
+  }
+  b.nEdges_act = n;
+}
+
+// build the exchange plans of both time-level parities of a step outside graph capture
+int plan_all(mpas_dyc_ctx* ctx, double dt) {
+  if (!needs_exchange(ctx) || ctx->planned[ctx->cur]) return MPAS_DYC_OK;
+  ctx->planning = true;
+  int r = srk3(ctx, dt);
+  ctx->planning = false;
+  if (r == MPAS_DYC_OK) ctx->planned[ctx->cur] = true;
+  return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpas_dyc_config* cfg, int device,
+                           mpas_dyc_ctx** out) {
+  if (!dims || !cfg || !out || nblocks < 1) return MPAS_DYC_EINVAL;
+  *out = nullptr;
+  mpas_dyc_ctx* ctx = new mpas_dyc_ctx();
+  ctx->blk.resize(nblocks);
+  for (int b = 0; b < nblocks; ++b) {
+    if (fill_dims(ctx->blk[b].d, &dims[b]) != MPAS_DYC_OK || dims[b].nVertLevels != dims[0].nVertLevels ||
+        dims[b].num_scalars != dims[0].num_scalars) {
+      delete ctx;
+      return MPAS_DYC_EINVAL;
+    }
+  }
+  ctx->index_qv = dims[0].index_qv - 1;
+  fill_config(ctx->cf, cfg);
+  if (ctx->cf.time_integration_order != 2 && ctx->cf.time_integration_order != 3) {
     delete ctx;
     return MPAS_DYC_EINVAL;
   }
-
-  if (device >= 0) {
-    if (hipSetDevice(device) != hipSuccess) {
-      delete ctx;
-      return MPAS_DYC_EHIP;
-    }
+  if (device >= 0 && hipSetDevice(device) != hipSuccess) {
+    delete ctx;
+    return MPAS_DYC_EHIP;
   }
-  hipGetDevice(&ctx->device);
+  (void)hipGetDevice(&ctx->device);
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return MPAS_DYC_EHIP;
   }
-  for (auto& e : ctx->ev) hipEventCreate(&e);
-  build_registry(ctx);
-  for (auto& f : ctx->fields) {
-    const int64_t nb = field_bytes(ctx, f);
-    for (int t = 0; t < f.ntl; ++t) {
-      if (hipMalloc(&f.buf[t], nb) != hipSuccess || hipMemset(f.buf[t], 0, nb) != hipSuccess) {
-        mpas_dyc_destroy(ctx);
-        return MPAS_DYC_EHIP;
+  for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  for (auto& b : ctx->blk) {
+    build_registry(b);
+    for (auto& f : b.fields) {
+      const int64_t nb = field_bytes(b, f);
+      for (int t = 0; t < f.ntl; ++t) {
+        if (hipMalloc(&f.buf[t], nb) != hipSuccess || hipMemset(f.buf[t], 0, nb) != hipSuccess) {
+          mpas_dyc_destroy(ctx);
+          return MPAS_DYC_EHIP;
+        }
       }
-    }
-    if (f.pool == "mesh" && (f.name == "cf1" || f.name == "cf2" || f.name == "cf3")) {
-      f.buf[1] = new double(0.0);  // host mirror of the 0-d field
+      if (is_host_0d(f)) f.buf[1] = new double(0.0);  // host mirror of the 0-d field
     }
   }
   *out = ctx;
   return MPAS_DYC_OK;
 }
 
+int mpas_dyc_create(const mpas_dyc_dims* dims, const mpas_dyc_config* cfg, int device, mpas_dyc_ctx** out) {
+  return mpas_dyc_create_blocks(1, dims, cfg, device, out);
+}
+
 void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
   if (!ctx) return;
-  hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
-  for (auto& g : ctx->graph_exec)
-    if (g) hipGraphExecDestroy(g);
-  for (auto& f : ctx->fields) {
-    for (int t = 0; t < f.ntl; ++t)
-      if (f.buf[t]) hipFree(f.buf[t]);
-    if (f.pool == "mesh" && (f.name == "cf1" || f.name == "cf2" || f.name == "cf3")) delete (double*)f.buf[1];
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  invalidate_plans(ctx);
+  for (auto& b : ctx->blk) {
+    for (auto& f : b.fields) {
+      for (int t = 0; t < f.ntl; ++t)
+        if (f.buf[t]) (void)hipFree(f.buf[t]);
+      if (is_host_0d(f)) delete (double*)f.buf[1];
+    }
+    for (auto& x : b.xl)
+      if (x.d_idx) (void)hipFree(x.d_idx);
   }
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
-    if (e) hipEventDestroy(e);
-  if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
 
 const char* mpas_dyc_last_error(const mpas_dyc_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+int32_t mpas_dyc_num_blocks(const mpas_dyc_ctx* ctx) { return ctx ? (int32_t)ctx->blk.size() : 0; }
+
+int64_t mpas_dyc_block_field_bytes(const mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name) {
+  if (!ctx || !pool || !name || block < 0 || block >= (int32_t)ctx->blk.size()) return 0;
+  const Block& b = ctx->blk[block];
+  auto it = b.by_name.find(std::string(pool) + "." + name);
+  if (it == b.by_name.end()) return 0;
+  return field_bytes(b, b.fields[it->second]);
+}
+
 int64_t mpas_dyc_field_bytes(const mpas_dyc_ctx* ctx, const char* pool, const char* name) {
-  if (!ctx || !pool || !name) return 0;
-  auto it = ctx->by_name.find(std::string(pool) + "." + name);
-  if (it == ctx->by_name.end()) return 0;
-  return field_bytes(ctx, ctx->fields[it->second]);
+  return mpas_dyc_block_field_bytes(ctx, 0, pool, name);
+}
+
+void* mpas_dyc_block_field_device_ptr(mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name,
+                                      int32_t time_level) {
+  Block* b = get_block(ctx, block);
+  if (!b || !pool || !name) return nullptr;
+  Field* f = find(*b, pool, name);
+  if (!f) return nullptr;
+  return f->buf[slot_of(ctx, *f, time_level)];
 }
 
 void* mpas_dyc_field_device_ptr(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level) {
-  if (!ctx || !pool || !name) return nullptr;
-  Field* f = find(ctx, pool, name);
-  if (!f) return nullptr;
-  int slot = (f->ntl == 2) ? ((time_level == 2) ? 1 - ctx->cur : ctx->cur) : 0;
-  return f->buf[slot];
+  return mpas_dyc_block_field_device_ptr(ctx, 0, pool, name, time_level);
 }
 
-static int64_t target_n(const mpas_dyc_ctx* c, Target t) {
-  switch (t) {
-    case T_CELL: return c->d.nCells;
-    case T_EDGE: return c->d.nEdges;
-    case T_VERTEX: return c->d.nVertices;
-    default: return 0;
-  }
-}
-
-int mpas_dyc_set_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level,
-                       const void* host, int64_t nbytes) {
+int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name,
+                             int32_t time_level, const void* host, int64_t nbytes) {
   if (!ctx || !pool || !name || !host) return MPAS_DYC_EINVAL;
-  Field* f = find(ctx, pool, name);
+  Block* bp = get_block(ctx, block);
+  if (!bp) {
+    ctx->err = "no block " + std::to_string(block);
+    return MPAS_DYC_EINVAL;
+  }
+  Block& b = *bp;
+  Field* f = find(b, pool, name);
   if (!f) {
     ctx->err = std::string("unknown field ") + pool + "." + name;
     return MPAS_DYC_EINVAL;
   }
-  if (f->pool == "mesh" && (f->name == "cf1" || f->name == "cf2" || f->name == "cf3")) {
+  if (is_host_0d(*f)) {
     if (nbytes != 8) return MPAS_DYC_EINVAL;
     *(double*)f->buf[1] = *(const double*)host;
     HIPCHK(hipMemcpy(f->buf[0], host, 8, hipMemcpyHostToDevice));
     return MPAS_DYC_OK;
   }
-  const int64_t nb = field_bytes(ctx, *f);
+  const int64_t nb = field_bytes(b, *f);
   if (nbytes != nb) {
-    ctx->err = "size mismatch for " + f->pool + "." + f->name + ": got " + std::to_string(nbytes) +
-               " expected " + std::to_string(nb);
+    ctx->err = "size mismatch for " + f->pool + "." + f->name + ": got " + std::to_string(nbytes) + " expected " +
+               std::to_string(nb);
     return MPAS_DYC_EINVAL;
   }
-  const int slot = (f->ntl == 2) ? ((time_level == 2) ? 1 - ctx->cur : ctx->cur) : 0;
+  const int slot = slot_of(ctx, *f, time_level);
   HIPCHK(hipSetDevice(ctx->device));
   if (f->is_int && f->target != T_NONE) {
     // MPAS 1-based -> device 0-based; out-of-range / 0 -> garbage slot
-    const int64_t n = field_elems(ctx, *f);
+    const int64_t n = field_elems(b, *f);
     std::vector<int32_t> tmp(n);
     const int32_t* src = (const int32_t*)host;
-    const int64_t nt = target_n(ctx, f->target);
+    const int64_t nt = target_n(b, f->target);
     for (int64_t i = 0; i < n; ++i) {
       int32_t v = src[i] - 1;
       if (f->target == T_SMALL) v = v < 0 ? 0 : v;
       else if (v < 0 || v > nt) v = (int32_t)nt;
       tmp[i] = v;
     }
+    if (f->pool == "mesh" && f->name == "cellsOnEdge") count_active_edges(b, src);
     HIPCHK(hipMemcpyAsync(f->buf[slot], tmp.data(), nb, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   } else {
@@ -628,33 +1000,145 @@ int mpas_dyc_set_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, in
   return MPAS_DYC_OK;
 }
 
-int mpas_dyc_get_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level, void* host,
-                       int64_t nbytes) {
+int mpas_dyc_set_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level,
+                       const void* host, int64_t nbytes) {
+  return mpas_dyc_set_block_field(ctx, 0, pool, name, time_level, host, nbytes);
+}
+
+int mpas_dyc_get_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name,
+                             int32_t time_level, void* host, int64_t nbytes) {
   if (!ctx || !pool || !name || !host) return MPAS_DYC_EINVAL;
-  Field* f = find(ctx, pool, name);
+  Block* bp = get_block(ctx, block);
+  if (!bp) {
+    ctx->err = "no block " + std::to_string(block);
+    return MPAS_DYC_EINVAL;
+  }
+  Block& b = *bp;
+  Field* f = find(b, pool, name);
   if (!f) {
     ctx->err = std::string("unknown field ") + pool + "." + name;
     return MPAS_DYC_EINVAL;
   }
-  if (f->pool == "mesh" && (f->name == "cf1" || f->name == "cf2" || f->name == "cf3")) {
+  if (is_host_0d(*f)) {
     if (nbytes != 8) return MPAS_DYC_EINVAL;
     *(double*)host = *(double*)f->buf[1];
     return MPAS_DYC_OK;
   }
-  const int64_t nb = field_bytes(ctx, *f);
+  const int64_t nb = field_bytes(b, *f);
   if (nbytes != nb) {
     ctx->err = "size mismatch for " + f->pool + "." + f->name;
     return MPAS_DYC_EINVAL;
   }
-  const int slot = (f->ntl == 2) ? ((time_level == 2) ? 1 - ctx->cur : ctx->cur) : 0;
   HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(hipMemcpyAsync(host, f->buf[slot], nb, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(host, f->buf[slot_of(ctx, *f, time_level)], nb, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   if (f->is_int && f->target != T_NONE) {
     int32_t* h = (int32_t*)host;
-    const int64_t n = field_elems(ctx, *f);
+    const int64_t n = field_elems(b, *f);
     for (int64_t i = 0; i < n; ++i) h[i] += 1;
   }
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_get_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level, void* host,
+                       int64_t nbytes) {
+  return mpas_dyc_get_block_field(ctx, 0, pool, name, time_level, host, nbytes);
+}
+
+int mpas_dyc_set_exchange_list(mpas_dyc_ctx* ctx, int32_t block, int32_t location, int32_t halo_layer,
+                               int32_t direction, int32_t peer_rank, int32_t peer_block, const int32_t* local_index,
+                               int32_t n) {
+  Block* bp = get_block(ctx, block);
+  if (!bp) {
+    if (ctx) ctx->err = "no block " + std::to_string(block);
+    return MPAS_DYC_EINVAL;
+  }
+  if (location < MPAS_DYC_CELL || location > MPAS_DYC_VERTEX || halo_layer < 1 || halo_layer > 3 ||
+      (location == MPAS_DYC_CELL && halo_layer > 2) || (direction != MPAS_DYC_SEND && direction != MPAS_DYC_RECV) ||
+      peer_rank < 0 || peer_block < 0 || n < 0 || (n > 0 && !local_index)) {
+    ctx->err = "invalid exchange list arguments";
+    return MPAS_DYC_EINVAL;
+  }
+  Block& b = *bp;
+  const int64_t nl = location == MPAS_DYC_CELL ? b.d.nCells : location == MPAS_DYC_EDGE ? b.d.nEdges : b.d.nVertices;
+  const int64_t nown = location == MPAS_DYC_CELL ? b.d.nCellsSolve
+                       : location == MPAS_DYC_EDGE ? b.d.nEdgesSolve : b.d.nVerticesSolve;
+  std::vector<int32_t> idx(n);
+  for (int i = 0; i < n; ++i) {
+    const int32_t v = local_index[i] - 1;
+    // senders send owned elements; receivers fill halo elements
+    const bool ok = direction == MPAS_DYC_SEND ? (v >= 0 && v < nown) : (v >= nown && v < nl);
+    if (!ok) {
+      ctx->err = "exchange list index " + std::to_string(local_index[i]) + " out of range";
+      return MPAS_DYC_EINVAL;
+    }
+    idx[i] = v;
+  }
+  invalidate_plans(ctx);
+  XList* x = nullptr;
+  for (auto& e : b.xl)
+    if (e.loc == location && e.layer == halo_layer && e.dir == direction && e.peer_rank == peer_rank &&
+        e.peer_block == peer_block)
+      x = &e;
+  if (!x) {
+    b.xl.push_back(XList{location, halo_layer, direction, peer_rank, peer_block});
+    x = &b.xl.back();
+  }
+  if (x->d_idx) {
+    HIPCHK(hipFree(x->d_idx));
+    x->d_idx = nullptr;
+  }
+  x->n = n;
+  if (n > 0) {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMalloc(&x->d_idx, n * sizeof(int32_t)));
+    HIPCHK(hipMemcpy(x->d_idx, idx.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_comm_unique_id(void* id, int64_t nbytes) {
+  if (!id || nbytes < (int64_t)sizeof(ncclUniqueId)) return MPAS_DYC_EINVAL;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return MPAS_DYC_ECOMM;
+  memcpy(id, &u, sizeof(u));
+  return MPAS_DYC_OK;
+}
+
+int64_t mpas_dyc_comm_unique_id_bytes(void) { return (int64_t)sizeof(ncclUniqueId); }
+
+int mpas_dyc_comm_init(mpas_dyc_ctx* ctx, const void* id, int64_t nbytes, int32_t nranks, int32_t rank) {
+  if (!ctx || !id || nbytes < (int64_t)sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks)
+    return MPAS_DYC_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  invalidate_plans(ctx);
+  if (ctx->comm) {
+    ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_set_transport(mpas_dyc_ctx* ctx, int32_t rccl_for_local_blocks) {
+  if (!ctx) return MPAS_DYC_EINVAL;
+  invalidate_plans(ctx);
+  ctx->rccl_local = rccl_for_local_blocks != 0;
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level,
+                           int32_t layer_mask) {
+  if (!ctx || !pool || !name || layer_mask <= 0 || layer_mask > 7) return MPAS_DYC_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  std::string sp(pool), sn(name);
+  int r = exchange(ctx, {{sp.c_str(), sn.c_str(), time_level, (unsigned)layer_mask}});
+  if (r) return r;
+  HIPCHK(hipGetLastError());
   return MPAS_DYC_OK;
 }
 
@@ -670,17 +1154,23 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
   (void)itimestep;
   if (!ctx || !(dt > 0.0)) return MPAS_DYC_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
+  CHK(plan_all(ctx, dt));
   if (ctx->use_graph) {
     const int parity = ctx->cur;
     if (!ctx->graph_exec[parity] || ctx->graph_dt[parity] != dt) {
-      if (ctx->graph_exec[parity]) hipGraphExecDestroy(ctx->graph_exec[parity]);
+      if (ctx->graph_exec[parity]) (void)hipGraphExecDestroy(ctx->graph_exec[parity]);
+      ctx->graph_exec[parity] = nullptr;
       hipGraph_t g;
       HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
       int r = srk3(ctx, dt);
-      HIPCHK(hipStreamEndCapture(ctx->stream, &g));
+      hipError_t e = hipStreamEndCapture(ctx->stream, &g);
       if (r) return r;
+      if (e != hipSuccess) {
+        ctx->err = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
+        return MPAS_DYC_EHIP;
+      }
       HIPCHK(hipGraphInstantiate(&ctx->graph_exec[parity], g, nullptr, nullptr, 0));
-      hipGraphDestroy(g);
+      (void)hipGraphDestroy(g);
       ctx->graph_dt[parity] = dt;
     }
     HIPCHK(hipGraphLaunch(ctx->graph_exec[parity], ctx->stream));
@@ -712,11 +1202,11 @@ int mpas_dyc_use_graph(mpas_dyc_ctx* ctx, int32_t on) {
 
 double mpas_dyc_acoustic_bytes(const mpas_dyc_ctx* ctx) {
   if (!ctx) return 0.0;
-  const Dims& d = ctx->d;
-  // B_ac = 8 [K (7 nE_act + 18 nC_own) + 9 (K+1) nC_own]   (SURVEY.md §8d);
-  // single block: every edge has an owned cell.
+  // B_ac = 8 [K (7 nE_act + 18 nC_own) + 9 (K+1) nC_own]   (SURVEY.md §8d), block 0
+  const Dims& d = ctx->blk[0].d;
   const double K = d.K;
-  const double nEact = d.nEdges, nC = d.nCellsSolve;
+  const double nEact = ctx->blk[0].nEdges_act >= 0 ? (double)ctx->blk[0].nEdges_act : (double)d.nEdges;
+  const double nC = d.nCellsSolve;
   return 8.0 * (K * (7.0 * nEact + 18.0 * nC) + 9.0 * (K + 1.0) * nC);
 }
 
@@ -724,8 +1214,9 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
                                 double* ms_kernels) {
   if (!ctx || reps < 1) return MPAS_DYC_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
-  Ptrs p = make_ptrs(ctx);
-  const Dims& d = ctx->d;
+  Block& b = ctx->blk[0];
+  const Ptrs p = make_ptrs(ctx, b);
+  const Dims& d = b.d;
   double acc[3] = {0, 0, 0};
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   for (int r = 0; r < reps; ++r) {
@@ -734,16 +1225,16 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
     HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
     LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
     HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-    divergence_damping(ctx, p, dts);
+    divergence_damping(ctx, d, p, dts);
     HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
     if (ms_kernels) {
       HIPCHK(hipEventSynchronize(ctx->ev[4]));
       float t;
-      hipEventElapsedTime(&t, ctx->ev[1], ctx->ev[2]);
+      (void)hipEventElapsedTime(&t, ctx->ev[1], ctx->ev[2]);
       acc[0] += t;
-      hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
+      (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
       acc[1] += t;
-      hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]);
+      (void)hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]);
       acc[2] += t;
     }
   }

@@ -16,8 +16,13 @@ EXPORTS = (
     "mpas_dyc_create", "mpas_dyc_destroy", "mpas_dyc_last_error", "mpas_dyc_set_field", "mpas_dyc_get_field",
     "mpas_dyc_field_bytes", "mpas_dyc_field_device_ptr", "mpas_dyc_init_diagnostics", "mpas_dyc_timestep",
     "mpas_dyc_shift_time_levels", "mpas_dyc_synchronize", "mpas_dyc_time_acoustic_step", "mpas_dyc_use_graph",
-    "mpas_dyc_acoustic_bytes",
+    "mpas_dyc_acoustic_bytes", "mpas_dyc_create_blocks", "mpas_dyc_num_blocks", "mpas_dyc_set_block_field",
+    "mpas_dyc_get_block_field", "mpas_dyc_block_field_bytes", "mpas_dyc_block_field_device_ptr",
+    "mpas_dyc_set_exchange_list", "mpas_dyc_comm_unique_id_bytes", "mpas_dyc_comm_unique_id", "mpas_dyc_comm_init",
+    "mpas_dyc_set_transport", "mpas_dyc_halo_exchange",
 )
+CELL, EDGE, VERTEX = 0, 1, 2
+SEND, RECV = 0, 1
 
 
 class Dims(C.Structure):
@@ -83,5 +88,21 @@ def load() -> C.CDLL:
     lib.mpas_dyc_use_graph.argtypes = [vp, i32]
     lib.mpas_dyc_acoustic_bytes.argtypes = [vp]
     lib.mpas_dyc_acoustic_bytes.restype = dbl
+    lib.mpas_dyc_create_blocks.argtypes = [i32, C.POINTER(Dims), C.POINTER(Config), C.c_int, C.POINTER(vp)]
+    lib.mpas_dyc_num_blocks.argtypes = [vp]
+    lib.mpas_dyc_num_blocks.restype = i32
+    lib.mpas_dyc_set_block_field.argtypes = [vp, i32, C.c_char_p, C.c_char_p, i32, vp, i64]
+    lib.mpas_dyc_get_block_field.argtypes = [vp, i32, C.c_char_p, C.c_char_p, i32, vp, i64]
+    lib.mpas_dyc_block_field_bytes.argtypes = [vp, i32, C.c_char_p, C.c_char_p]
+    lib.mpas_dyc_block_field_bytes.restype = i64
+    lib.mpas_dyc_block_field_device_ptr.argtypes = [vp, i32, C.c_char_p, C.c_char_p, i32]
+    lib.mpas_dyc_block_field_device_ptr.restype = vp
+    lib.mpas_dyc_set_exchange_list.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, i32]
+    lib.mpas_dyc_comm_unique_id_bytes.argtypes = []
+    lib.mpas_dyc_comm_unique_id_bytes.restype = i64
+    lib.mpas_dyc_comm_unique_id.argtypes = [vp, i64]
+    lib.mpas_dyc_comm_init.argtypes = [vp, vp, i64, i32, i32]
+    lib.mpas_dyc_set_transport.argtypes = [vp, i32]
+    lib.mpas_dyc_halo_exchange.argtypes = [vp, C.c_char_p, C.c_char_p, i32, i32]
     _lib = lib
     return lib

@@ -1,0 +1,228 @@
+"""Horizontal domain decomposition: blocks with halos and their exchange lists.
+
+Restates how MPAS builds a block from a cell partition
+(framework/mpas_bootstrapping.F:238-268, mpas_block_creator.F,
+mpas_block_decomp.F) so one rank's dycore sees exactly what the reference's
+would.
+
+* **Cells.** A block owns the cells its partition assigns it (nCellsSolve).
+  It then adds ``nHalos`` = config_num_halos = 2 layers (Registry.xml:242).
+  Layer ``l`` is the set of cellsOnCell neighbours of layers < l that are not
+  yet in the block (mpas_block_creator_build_cell_halos, :470-716).
+* **Edges and vertices.** A block owns an edge when the first valid
+  cellsOnEdge entry is an owned cell (mpas_block_decomp_partitioned_edge_list,
+  mpas_block_decomp.F:301-356). Vertices use cellsOnVertex the same way
+  (mpas_bootstrapping.F:253).
+  * Halo layer 1 holds the remaining edges of the owned cells.
+  * Layer ``l`` > 1 holds the edges of the cell-halo layer ``l-1`` not yet in
+    the block (build_edge_halos, :734-938).
+  * Edge and vertex fields therefore have nHalos+1 = 3 exchange layers.
+* **Local order.** Owned elements come first, then each halo layer. Within a
+  group, elements are in ascending global index. The reference's own order
+  within a group is hash-discovery order. Every stencil is element-local with
+  fixed neighbour order, so this choice changes no result bit.
+* **Missing neighbours.** Connectivity is remapped to block-local indices, and
+  neighbours outside the block become -1, which is the garbage slot n+1 at the
+  C ABI (mpas_block_creator.F:1445).
+* **Exchange lists** (mpas_dmpar_get_exch_list). For every (block,
+  location, halo layer), the halo elements are grouped by owning block. The
+  owner sends its owned copies in ascending global index, and the receiver
+  unpacks them in the same order.
+* **Partition.** The default partition splits the cells into contiguous ranges
+  of the space-filling-curve order of ``mesh.py``. A METIS
+  ``graph.info.part.N`` file, as read by mpas_block_decomp.F, is accepted as
+  well.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import fields as F
+
+NHALOS = 2
+LOCS = ("cell", "edge", "vertex")
+LOC_CODE = {"cell": 0, "edge": 1, "vertex": 2}
+NLAYERS = {"cell": NHALOS, "edge": NHALOS + 1, "vertex": NHALOS + 1}
+_N = {"cell": "nCells", "edge": "nEdges", "vertex": "nVertices"}
+
+
+def partition_sfc(nCells: int, nparts: int) -> np.ndarray:
+    """Owner block of every cell: contiguous ranges of the (Hilbert-ordered) cell index."""
+    if nparts < 1 or nparts > nCells:
+        raise ValueError(f"cannot split {nCells} cells into {nparts} blocks")
+    return (np.arange(nCells, dtype=np.int64) * nparts // nCells).astype(np.int32)
+
+
+def read_partition_file(path: str, nCells: int) -> np.ndarray:
+    """graph.info.part.N: one 0-based owning block per line (mpas_block_decomp.F:106-160)."""
+    part = np.loadtxt(path, dtype=np.int64, ndmin=1)
+    if part.size != nCells:
+        raise ValueError(f"{path}: {part.size} entries for {nCells} cells")
+    return part.astype(np.int32)
+
+
+def _neighbours(idx2d: np.ndarray, counts: np.ndarray | None, rows: np.ndarray) -> np.ndarray:
+    """Unique valid entries of idx2d[rows, :counts[rows]]."""
+    if rows.size == 0:
+        return rows
+    sub = idx2d[rows]
+    if counts is not None:
+        mask = np.arange(sub.shape[1])[None, :] < counts[rows][:, None]
+        vals = sub[mask]
+    else:
+        vals = sub.ravel()
+    vals = vals[vals >= 0]
+    return np.unique(vals)
+
+
+def element_owners(case: dict, cell_part: np.ndarray) -> dict:
+    """Owning block of every cell, edge and vertex (first valid cell of cellsOnEdge / cellsOnVertex)."""
+    def first_valid(c2):
+        c = c2[:, 0].copy()
+        for j in range(1, c2.shape[1]):
+            bad = c < 0
+            c[bad] = c2[bad, j]
+        if (c < 0).any():
+            raise ValueError("element not adjacent to any valid cell")
+        return c
+    return {"cell": np.asarray(cell_part, dtype=np.int32),
+            "edge": cell_part[first_valid(np.asarray(case["cellsOnEdge"]))],
+            "vertex": cell_part[first_valid(np.asarray(case["cellsOnVertex"]))]}
+
+
+@dataclass
+class Block:
+    """One block: its local case plus the local -> global maps and halo layer sizes."""
+    part: int
+    case: dict
+    glob: dict                      # loc -> global index of every local element
+    layer_end: dict                 # loc -> cumulative counts [owned, +layer1, ...] (MPAS n*Solve arrays)
+    send: list = field(default_factory=list)   # (loc, layer, peer, local idx 0-based)
+    recv: list = field(default_factory=list)
+
+    @property
+    def solve(self) -> tuple:
+        return (self.layer_end["cell"][0], self.layer_end["edge"][0], self.layer_end["vertex"][0])
+
+    def layer_range(self, loc: str, layer: int) -> tuple:
+        """[start, end) of halo layer ``layer`` (0 = owned) of a location."""
+        e = self.layer_end[loc]
+        return (0 if layer == 0 else e[layer - 1], e[layer])
+
+
+def _block_elements(case: dict, owners: dict, p: int) -> tuple[dict, dict]:
+    nEdgesOnCell = np.asarray(case["nEdgesOnCell"])
+    cellsOnCell = np.asarray(case["cellsOnCell"])
+    owned = np.flatnonzero(owners["cell"] == p)
+    if owned.size == 0:
+        raise ValueError(f"block {p} owns no cells")
+    cell_layers = [owned]
+    seen = np.zeros(case["nCells"], dtype=bool)
+    seen[owned] = True
+    for _ in range(NHALOS):
+        nb = _neighbours(cellsOnCell, nEdgesOnCell, cell_layers[-1])
+        new = nb[~seen[nb]]
+        seen[new] = True
+        cell_layers.append(new)
+    groups = {"cell": cell_layers}
+    for loc, on_cell in (("edge", "edgesOnCell"), ("vertex", "verticesOnCell")):
+        arr = np.asarray(case[on_cell])
+        n = case[_N[loc]]
+        e0 = _neighbours(arr, nEdgesOnCell, owned)
+        own = e0[owners[loc][e0] == p]
+        lay1 = e0[owners[loc][e0] != p]
+        in_blk = np.zeros(n, dtype=bool)
+        in_blk[e0] = True
+        lays = [own, lay1]
+        for h in range(1, NHALOS + 1):
+            nb = _neighbours(arr, nEdgesOnCell, cell_layers[h])
+            new = nb[~in_blk[nb]]
+            in_blk[new] = True
+            lays.append(new)
+        groups[loc] = lays
+    glob = {loc: np.concatenate(groups[loc]).astype(np.int64) for loc in LOCS}
+    layer_end = {loc: list(np.cumsum([g.size for g in groups[loc]])) for loc in LOCS}
+    return glob, layer_end
+
+
+def _local_case(case: dict, glob: dict) -> dict:
+    g2l = {}
+    for loc in LOCS:
+        m = np.full(case[_N[loc]], -1, dtype=np.int64)
+        m[glob[loc]] = np.arange(glob[loc].size)
+        g2l[loc] = m
+    out = {}
+    for k, v in case.items():
+        loc = F.LOCATION.get(k)
+        if loc is None or not isinstance(v, np.ndarray):
+            out[k] = v
+            continue
+        sub = v[glob[loc]]
+        if k in F.INDEX_TARGET:
+            tgt = g2l[F.INDEX_TARGET[k]]
+            sub = np.where(sub >= 0, tgt[np.maximum(sub, 0)], -1)
+        out[k] = np.ascontiguousarray(sub)
+    for loc in LOCS:
+        out[_N[loc]] = int(glob[loc].size)
+    return out
+
+
+def decompose(case: dict, cell_part: np.ndarray, parts=None) -> list[Block]:
+    """Build the blocks of ``parts`` (default: all) with their send and receive lists.
+
+    The element sets of every block are computed (cheap), so a rank can build
+    only its own block(s) and still know what each neighbour expects from it."""
+    nparts = int(cell_part.max()) + 1
+    owners = element_owners(case, cell_part)
+    elems = [_block_elements(case, owners, p) for p in range(nparts)]
+    want = list(range(nparts)) if parts is None else list(parts)
+    blocks = [Block(part=p, case=_local_case(case, elems[p][0]), glob=elems[p][0], layer_end=elems[p][1])
+              for p in want]
+    for b in blocks:
+        for loc in LOCS:
+            n_owned = b.layer_end[loc][0]
+            owned_glob = b.glob[loc][:n_owned]  # ascending global ids
+            for layer in range(1, NLAYERS[loc] + 1):
+                # receive: my layer-`layer` halo elements, grouped by owner
+                s, e = b.layer_range(loc, layer)
+                own = owners[loc][b.glob[loc][s:e]]
+                for q in np.unique(own):
+                    sel = np.flatnonzero(own == q)
+                    b.recv.append((loc, layer, int(q), (s + sel).astype(np.int32)))
+                # send: every other block's layer-`layer` halo elements that I own
+                for p in range(nparts):
+                    if p == b.part:
+                        continue
+                    glob_p, lend_p = elems[p]
+                    gids = glob_p[loc][lend_p[loc][layer - 1]:lend_p[loc][layer]]
+                    gids = gids[owners[loc][gids] == b.part]
+                    if gids.size:
+                        b.send.append((loc, layer, p, np.searchsorted(owned_glob, gids).astype(np.int32)))
+    return blocks
+
+
+def gather_owned(blocks: list[Block], arrays: list, loc: str, n_global: int) -> np.ndarray:
+    """Scatter each block's owned rows of an element-major array into the global array."""
+    out = None
+    for b, a in zip(blocks, arrays):
+        a = np.asarray(a)
+        if out is None:
+            out = np.full((n_global,) + a.shape[1:], np.nan, dtype=a.dtype)
+        n_own = b.layer_end[loc][0]
+        out[b.glob[loc][:n_own]] = a[:n_own]
+    return out
+
+
+def messages(block: Block, direction: str, layers=(1, 2, 3), locs=LOCS) -> dict:
+    """Host restatement of one block's messages for an exchange: peer -> list of local index
+    arrays in message order (layers ascending), as the device plan packs them."""
+    lists = block.send if direction == "send" else block.recv
+    out = {}
+    for loc in locs:
+        for layer in sorted(layers):
+            for (l, lay, peer, idx) in lists:
+                if l == loc and lay == layer:
+                    out.setdefault(peer, []).append(idx)
+    return {p: np.concatenate(v) for p, v in sorted(out.items())}

@@ -34,29 +34,77 @@ class DycoreError(RuntimeError):
 
 
 class Dycore:
-    """One block of the MI355X dycore (all cells owned unless ``solve`` counts are given)."""
+    """The blocks of this process on one GPU (MPAS domain%blocklist).
 
-    def __init__(self, case: dict, device: int = 0, solve: tuple | None = None, moist_end: int = 1):
+    ``Dycore(case)`` is one block owning every element (the single-GPU path);
+    ``Dycore.from_blocks(...)`` takes the blocks of a decomposition
+    (``mpas_dycore.decomp``) and installs their exchange lists."""
+
+    def __init__(self, case: dict | None = None, device: int = 0, solve: tuple | None = None, moist_end: int = 1,
+                 _blocks: list | None = None):
         self.lib = _lib.load()
-        self.case = case
-        self.K = case["nVertLevels"]
-        self.ns = case["num_scalars"]
-        self.n = {"cell": case["nCells"], "edge": case["nEdges"], "vertex": case["nVertices"]}
-        d = _lib.Dims()
-        d.nCells, d.nEdges, d.nVertices = case["nCells"], case["nEdges"], case["nVertices"]
-        d.nVertLevels, d.maxEdges, d.maxEdges2 = self.K, case["maxEdges"], case["maxEdges2"]
-        d.num_scalars = self.ns
-        if solve is None:
-            solve = (case["nCells"], case["nEdges"], case["nVertices"])
-        d.nCellsSolve, d.nEdgesSolve, d.nVerticesSolve = solve
-        d.moist_start, d.moist_end, d.index_qv = 1, moist_end, 1
-        cfg = _lib.make_config(case["config"])
+        cases = [case] if _blocks is None else [b.case for b in _blocks]
+        solves = [solve] if _blocks is None else [b.solve for b in _blocks]
+        self.cases = cases
+        self.case = cases[0]
+        self.K = self.case["nVertLevels"]
+        self.ns = self.case["num_scalars"]
+        self.nblocks = len(cases)
+        self.nb = [{"cell": c["nCells"], "edge": c["nEdges"], "vertex": c["nVertices"]} for c in cases]
+        self.n = self.nb[0]
+        dims = (_lib.Dims * len(cases))()
+        for d, c, sv in zip(dims, cases, solves):
+            d.nCells, d.nEdges, d.nVertices = c["nCells"], c["nEdges"], c["nVertices"]
+            d.nVertLevels, d.maxEdges, d.maxEdges2 = self.K, c["maxEdges"], c["maxEdges2"]
+            d.num_scalars = self.ns
+            if sv is None:
+                sv = (c["nCells"], c["nEdges"], c["nVertices"])
+            d.nCellsSolve, d.nEdgesSolve, d.nVerticesSolve = (int(x) for x in sv)
+            d.moist_start, d.moist_end, d.index_qv = 1, moist_end, 1
+        cfg = _lib.make_config(self.case["config"])
         h = C.c_void_p()
-        rc = self.lib.mpas_dyc_create(C.byref(d), C.byref(cfg), int(device), C.byref(h))
+        rc = self.lib.mpas_dyc_create_blocks(len(cases), dims, C.byref(cfg), int(device), C.byref(h))
         if rc != 0 or not h.value:
-            raise DycoreError(f"mpas_dyc_create failed ({rc})")
+            raise DycoreError(f"mpas_dyc_create_blocks failed ({rc})")
         self.h = h
-        self._upload_case(case)
+        for ib, c in enumerate(cases):
+            self._upload_case(c, ib)
+
+    @classmethod
+    def from_blocks(cls, blocks: list, device: int = 0, moist_end: int = 1, placement: dict | None = None,
+                    rank: int = 0, nranks: int = 1, comm_id: bytes | None = None, rccl_local: bool = False):
+        """Blocks of this process (``decomp.decompose(..., parts=...)``) on one GPU.
+
+        ``placement`` maps every block (part) id to (rank, local block index); by
+        default all blocks live in this process, in the given order.  With
+        ``nranks`` > 1, ``comm_id`` is the RCCL unique id created on rank 0."""
+        if placement is None:
+            placement = {b.part: (0, i) for i, b in enumerate(blocks)}
+        self = cls(device=device, moist_end=moist_end, _blocks=blocks)
+        if comm_id is not None:
+            idb = C.create_string_buffer(bytes(comm_id), len(comm_id))
+            self._check(self.lib.mpas_dyc_comm_init(self.h, idb, len(comm_id), int(nranks), int(rank)), "comm_init")
+        if rccl_local:
+            self._check(self.lib.mpas_dyc_set_transport(self.h, 1), "set_transport")
+        code = {"cell": _lib.CELL, "edge": _lib.EDGE, "vertex": _lib.VERTEX}
+        for ib, b in enumerate(blocks):
+            for direction, lists in ((_lib.SEND, b.send), (_lib.RECV, b.recv)):
+                for loc, layer, peer, idx in lists:
+                    pr, pb = placement[peer]
+                    a = np.ascontiguousarray(np.asarray(idx, dtype=np.int32) + 1)
+                    self._check(self.lib.mpas_dyc_set_exchange_list(self.h, ib, code[loc], int(layer), direction,
+                                                                    int(pr), int(pb), a.ctypes.data_as(C.c_void_p),
+                                                                    int(a.size)), "set_exchange_list")
+        return self
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        lib = _lib.load()
+        n = lib.mpas_dyc_comm_unique_id_bytes()
+        buf = C.create_string_buffer(n)
+        if lib.mpas_dyc_comm_unique_id(buf, n) != 0:
+            raise DycoreError("mpas_dyc_comm_unique_id failed")
+        return buf.raw
 
     # -------------------------------------------------------------- fields
     def _check(self, rc, what):
@@ -64,46 +112,54 @@ class Dycore:
             msg = self.lib.mpas_dyc_last_error(self.h)
             raise DycoreError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
 
-    def set_raw(self, pool: str, name: str, fortran_image: np.ndarray, time_level: int = 1):
+    def set_raw(self, pool: str, name: str, fortran_image: np.ndarray, time_level: int = 1, block: int = 0):
         a = np.ascontiguousarray(fortran_image)
-        self._check(self.lib.mpas_dyc_set_field(self.h, pool.encode(), name.encode(), time_level,
-                                                a.ctypes.data_as(C.c_void_p), a.nbytes), f"set {pool}.{name}")
+        self._check(self.lib.mpas_dyc_set_block_field(self.h, block, pool.encode(), name.encode(), time_level,
+                                                      a.ctypes.data_as(C.c_void_p), a.nbytes),
+                    f"set {pool}.{name}")
 
-    def set(self, pool: str, name: str, arr, time_level: int = 1):
+    def set(self, pool: str, name: str, arr, time_level: int = 1, block: int = 0):
         """Upload an element-major array (0-based indices for index fields)."""
-        self.set_raw(pool, name, to_fortran({**self.case, name: arr}, name), time_level)
+        self.set_raw(pool, name, to_fortran({**self.cases[block], name: arr}, name), time_level, block)
 
-    def get(self, pool: str, name: str, time_level: int = 1) -> np.ndarray:
+    def get(self, pool: str, name: str, time_level: int = 1, block: int = 0) -> np.ndarray:
         """Download a real field as element-major (n, inner) numpy (garbage slot dropped)."""
-        nb = self.lib.mpas_dyc_field_bytes(self.h, pool.encode(), name.encode())
+        nb = self.lib.mpas_dyc_block_field_bytes(self.h, block, pool.encode(), name.encode())
         if nb <= 0:
             raise DycoreError(f"unknown field {pool}.{name}")
         buf = np.empty(nb // 8, dtype=np.float64)
-        self._check(self.lib.mpas_dyc_get_field(self.h, pool.encode(), name.encode(), time_level,
-                                                buf.ctypes.data_as(C.c_void_p), buf.nbytes), f"get {pool}.{name}")
+        self._check(self.lib.mpas_dyc_get_block_field(self.h, block, pool.encode(), name.encode(), time_level,
+                                                      buf.ctypes.data_as(C.c_void_p), buf.nbytes),
+                    f"get {pool}.{name}")
         loc = _loc_of(pool, name)
         if loc is None:
             return buf
-        n1 = self.n[loc] + 1
+        n1 = self.nb[block][loc] + 1
         if name in ("scalars", "scalars_tend"):
             return buf.reshape(n1, self.K, self.ns)[:-1]
         return buf.reshape(n1, buf.size // n1)[:-1]
 
-    def _upload_case(self, case: dict):
+    def halo_exchange(self, pool: str, name: str, time_level: int = 1, layers=(1, 2, 3)):
+        """mpas_dmpar_exch_halo_field(field, haloLayers) over the blocks of this process (and peers)."""
+        mask = sum(1 << (l - 1) for l in layers)
+        self._check(self.lib.mpas_dyc_halo_exchange(self.h, pool.encode(), name.encode(), time_level, mask),
+                    f"halo_exchange {pool}.{name}")
+
+    def _upload_case(self, case: dict, block: int = 0):
         for name in case:
             if name in _SKIP:
                 continue
             if name in F.LOCATION or name in F.VERTICAL_1D:
                 if name in F.VERTICAL_1D:
-                    self.set_raw("mesh", name, np.asarray(case[name], dtype=np.float64))
+                    self.set_raw("mesh", name, np.asarray(case[name], dtype=np.float64), block=block)
                 else:
-                    self.set_raw("mesh", name, to_fortran(case, name))
+                    self.set_raw("mesh", name, to_fortran(case, name), block=block)
             elif name in F.SCALARS_0D:
-                self.set_raw("mesh", name, np.asarray([case[name]], dtype=np.float64))
+                self.set_raw("mesh", name, np.asarray([case[name]], dtype=np.float64), block=block)
         for name in STATE_INPUTS:
-            self.set_raw("state", name, to_fortran(case, name), 1)
+            self.set_raw("state", name, to_fortran(case, name), 1, block)
         for name in DIAG_INPUTS:
-            self.set_raw("diag", name, to_fortran(case, name))
+            self.set_raw("diag", name, to_fortran(case, name), block=block)
 
     # -------------------------------------------------------- operators
     def init_diagnostics(self, dt: float):

@@ -31,3 +31,9 @@ def small_case():
     from mpas_dycore.init_atm import build_case
     m = build_mesh(3, lloyd_iters=20)
     return build_case(m, K=26, ns=1)
+
+
+@pytest.fixture(scope="session")
+def moist_case():
+    from mpas_dycore.cases import jw_case
+    return jw_case(642, K=26, ns=3, moist=True, cache=False)
