@@ -54,25 +54,22 @@ struct Block {
   int64_t nEdges_act = -1;             // edges with an owned cell (from cellsOnEdge), for B_ac
 };
 
-// One message of an exchange point: a contiguous range of a block's send or receive buffer.
+// One RCCL message of an exchange point: a contiguous range of the process-wide send or receive buffer.
 struct XMsg {
   int block, peer_rank, peer_block;
   int64_t off, count;  // doubles
 };
 
-struct XBlockPlan {
-  XSeg* d_pack = nullptr;
-  XSeg* d_unpack = nullptr;
-  int npack = 0, nunpack = 0, maxn_pack = 0, maxn_unpack = 0;
+// An exchange point, compiled: `pre` packs RCCL messages and copies halos between blocks of
+// this process directly (owned columns of one block -> halo columns of another); `post`
+// unpacks received RCCL messages.  One kernel launch each, whatever the number of blocks.
+struct XPlan {
+  XSeg* d_pre = nullptr;
+  XSeg* d_post = nullptr;
+  int npre = 0, npost = 0, maxn_pre = 0, maxn_post = 0;
   double* sendbuf = nullptr;
   double* recvbuf = nullptr;
-  int64_t nsend = 0, nrecv = 0;
-};
-
-struct XPlan {
-  std::vector<XBlockPlan> bp;
-  std::vector<std::pair<XMsg, XMsg>> local;  // (send, matching recv) between blocks of this process
-  std::vector<XMsg> rsend, rrecv;            // RCCL messages, in matching order
+  std::vector<XMsg> rsend, rrecv;  // in matching order
 };
 
 // One field of an exchange point: mpas_dmpar_exch_halo_field(field[, haloLayers]).
@@ -342,13 +339,9 @@ const XList* find_list(const Block& b, int loc, int layer, int dir, int peer_ran
 }
 
 void free_plan(XPlan& pl) {
-  for (auto& bp : pl.bp) {
-    if (bp.d_pack) (void)hipFree(bp.d_pack);
-    if (bp.d_unpack) (void)hipFree(bp.d_unpack);
-    if (bp.sendbuf) (void)hipFree(bp.sendbuf);
-    if (bp.recvbuf) (void)hipFree(bp.recvbuf);
-  }
-  pl.bp.clear();
+  for (void* p : {(void*)pl.d_pre, (void*)pl.d_post, (void*)pl.sendbuf, (void*)pl.recvbuf})
+    if (p) (void)hipFree(p);
+  pl = XPlan{};
 }
 
 void invalidate_plans(mpas_dyc_ctx* ctx) {
@@ -363,94 +356,130 @@ void invalidate_plans(mpas_dyc_ctx* ctx) {
     }
 }
 
-// Message layout of one block and direction: peers in (rank, block) order; per peer,
-// the fields in call order and per field the halo layers in ascending order.
-int build_side(mpas_dyc_ctx* ctx, int bi, int dir, const std::vector<XField>& fs, std::vector<XSeg>& segs,
-               std::vector<XMsg>& msgs, int64_t& total, int& maxn) {
-  Block& b = ctx->blk[bi];
+bool is_local(const mpas_dyc_ctx* ctx, int peer_rank) { return peer_rank == ctx->rank && !ctx->rccl_local; }
+
+std::vector<std::pair<int, int>> peers_of(const Block& b, int dir) {
   std::vector<std::pair<int, int>> peers;
   for (const auto& x : b.xl)
-    if (x.dir == dir) peers.emplace_back(x.peer_rank, x.peer_block);
+    if (x.dir == dir && x.n > 0) peers.emplace_back(x.peer_rank, x.peer_block);
   std::sort(peers.begin(), peers.end());
   peers.erase(std::unique(peers.begin(), peers.end()), peers.end());
-  total = 0;
-  maxn = 0;
-  for (const auto& pr : peers) {
-    const int64_t start = total;
-    for (const auto& f : fs) {
-      Field* F = find(b, f.pool, f.name);
-      if (!F || F->is_int || F->loc == L_NONE) {
-        ctx->err = std::string("halo exchange of unsupported field ") + f.pool + "." + f.name;
-        return MPAS_DYC_EINVAL;
-      }
-      for (int layer = 1; layer <= 3; ++layer) {
-        if (!((f.layers >> (layer - 1)) & 1u)) continue;
-        const XList* x = find_list(b, (int)F->loc, layer, dir, pr.first, pr.second);
-        if (!x || x->n == 0) continue;
-        XSeg s;
-        s.base = (double*)F->buf[slot_of(ctx, *F, f.tl)];
-        s.idx = x->d_idx;
-        s.n = x->n;
-        s.inner = (int)F->inner;
-        s.off = total;
-        segs.push_back(s);
-        total += (int64_t)x->n * F->inner;
-        maxn = std::max(maxn, x->n);
-      }
-    }
-    if (total > start) msgs.push_back(XMsg{bi, pr.first, pr.second, start, total - start});
-  }
-  return MPAS_DYC_OK;
+  return peers;
 }
 
+// Message layout: per block, peers in (rank, block) order; per peer, the fields in call
+// order and per field the halo layers in ascending order (both sides agree on it).
 int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   const int nb = (int)ctx->blk.size();
-  pl.bp.assign(nb, XBlockPlan{});
-  std::vector<std::vector<XMsg>> smsg(nb), rmsg(nb);
-  for (int bi = 0; bi < nb; ++bi) {
-    XBlockPlan& bp = pl.bp[bi];
-    std::vector<XSeg> ps, us;
-    CHK(build_side(ctx, bi, 0, fs, ps, smsg[bi], bp.nsend, bp.maxn_pack));
-    CHK(build_side(ctx, bi, 1, fs, us, rmsg[bi], bp.nrecv, bp.maxn_unpack));
-    bp.npack = (int)ps.size();
-    bp.nunpack = (int)us.size();
-    if (bp.npack) {
-      HIPCHK(hipMalloc(&bp.d_pack, ps.size() * sizeof(XSeg)));
-      HIPCHK(hipMemcpy(bp.d_pack, ps.data(), ps.size() * sizeof(XSeg), hipMemcpyHostToDevice));
-      HIPCHK(hipMalloc(&bp.sendbuf, bp.nsend * sizeof(double)));
+  std::vector<XSeg> pre, post;
+  std::vector<int64_t> pre_off, post_off;  // buffer offsets, patched once the buffers exist (-1: direct)
+  int64_t stotal = 0, rtotal = 0;
+  auto field_of = [&](Block& b, const XField& f) -> Field* {
+    Field* F = find(b, f.pool, f.name);
+    if (!F || F->is_int || F->loc == L_NONE) {
+      ctx->err = std::string("halo exchange of unsupported field ") + f.pool + "." + f.name;
+      return nullptr;
     }
-    if (bp.nunpack) {
-      HIPCHK(hipMalloc(&bp.d_unpack, us.size() * sizeof(XSeg)));
-      HIPCHK(hipMemcpy(bp.d_unpack, us.data(), us.size() * sizeof(XSeg), hipMemcpyHostToDevice));
-      HIPCHK(hipMalloc(&bp.recvbuf, bp.nrecv * sizeof(double)));
-    }
-  }
+    return F;
+  };
   for (int bi = 0; bi < nb; ++bi) {
-    for (const XMsg& s : smsg[bi]) {
-      if (s.peer_rank == ctx->rank && !ctx->rccl_local) {
-        if (s.peer_block < 0 || s.peer_block >= nb) {
-          ctx->err = "exchange list names block " + std::to_string(s.peer_block) + " not in this process";
-          return MPAS_DYC_EINVAL;
-        }
-        const XMsg* r = nullptr;
-        for (const XMsg& m : rmsg[s.peer_block])
-          if (m.peer_rank == ctx->rank && m.peer_block == bi) r = &m;
-        if (!r || r->count != s.count) {
-          ctx->err = "send/recv lists of blocks " + std::to_string(bi) + "->" + std::to_string(s.peer_block) +
-                     " disagree";
-          return MPAS_DYC_EINVAL;
-        }
-        pl.local.emplace_back(s, *r);
-      } else {
-        pl.rsend.push_back(s);
+    Block& b = ctx->blk[bi];
+    for (const auto& pr : peers_of(b, MPAS_DYC_SEND)) {
+      const bool local = is_local(ctx, pr.first);
+      if (local && (pr.second < 0 || pr.second >= nb)) {
+        ctx->err = "exchange list names block " + std::to_string(pr.second) + " not in this process";
+        return MPAS_DYC_EINVAL;
       }
+      const int64_t start = stotal;
+      for (const auto& f : fs) {
+        Field* F = field_of(b, f);
+        if (!F) return MPAS_DYC_EINVAL;
+        for (int layer = 1; layer <= 3; ++layer) {
+          if (!((f.layers >> (layer - 1)) & 1u)) continue;
+          const XList* sx = find_list(b, (int)F->loc, layer, MPAS_DYC_SEND, pr.first, pr.second);
+          if (!sx || sx->n == 0) continue;
+          XSeg sg{};
+          sg.src = (const double*)F->buf[slot_of(ctx, *F, f.tl)];
+          sg.sidx = sx->d_idx;
+          sg.n = sx->n;
+          sg.inner = (int)F->inner;
+          if (local) {
+            Block& pb = ctx->blk[pr.second];
+            const XList* rx = find_list(pb, (int)F->loc, layer, MPAS_DYC_RECV, ctx->rank, bi);
+            if (!rx || rx->n != sx->n) {
+              ctx->err = "send/recv lists of blocks " + std::to_string(bi) + "->" + std::to_string(pr.second) +
+                         " disagree";
+              return MPAS_DYC_EINVAL;
+            }
+            Field* PF = find(pb, f.pool, f.name);
+            sg.dst = (double*)PF->buf[slot_of(ctx, *PF, f.tl)];
+            sg.didx = rx->d_idx;
+            pre_off.push_back(-1);
+          } else {
+            sg.didx = nullptr;
+            pre_off.push_back(stotal);
+            stotal += (int64_t)sx->n * F->inner;
+          }
+          pre.push_back(sg);
+          pl.maxn_pre = std::max(pl.maxn_pre, sx->n);
+        }
+      }
+      if (!local && stotal > start) pl.rsend.push_back(XMsg{bi, pr.first, pr.second, start, stotal - start});
     }
-    for (const XMsg& r : rmsg[bi])
-      if (!(r.peer_rank == ctx->rank && !ctx->rccl_local)) pl.rrecv.push_back(r);
+    for (const auto& pr : peers_of(b, MPAS_DYC_RECV)) {
+      const bool local = is_local(ctx, pr.first);
+      const int64_t start = rtotal;
+      for (const auto& f : fs) {
+        Field* F = field_of(b, f);
+        if (!F) return MPAS_DYC_EINVAL;
+        for (int layer = 1; layer <= 3; ++layer) {
+          if (!((f.layers >> (layer - 1)) & 1u)) continue;
+          const XList* rx = find_list(b, (int)F->loc, layer, MPAS_DYC_RECV, pr.first, pr.second);
+          if (!rx || rx->n == 0) continue;
+          if (local) {  // filled by the sender's direct copy; check that one exists
+            const XList* sx = (pr.second >= 0 && pr.second < nb)
+                                  ? find_list(ctx->blk[pr.second], (int)F->loc, layer, MPAS_DYC_SEND, ctx->rank, bi)
+                                  : nullptr;
+            if (!sx || sx->n != rx->n) {
+              ctx->err = "send/recv lists of blocks " + std::to_string(pr.second) + "->" + std::to_string(bi) +
+                         " disagree";
+              return MPAS_DYC_EINVAL;
+            }
+            continue;
+          }
+          XSeg sg{};
+          sg.sidx = nullptr;
+          sg.dst = (double*)F->buf[slot_of(ctx, *F, f.tl)];
+          sg.didx = rx->d_idx;
+          sg.n = rx->n;
+          sg.inner = (int)F->inner;
+          post.push_back(sg);
+          post_off.push_back(rtotal);
+          rtotal += (int64_t)rx->n * F->inner;
+          pl.maxn_post = std::max(pl.maxn_post, rx->n);
+        }
+      }
+      if (!local && rtotal > start) pl.rrecv.push_back(XMsg{bi, pr.first, pr.second, start, rtotal - start});
+    }
   }
   if ((!pl.rsend.empty() || !pl.rrecv.empty()) && !ctx->comm) {
     ctx->err = "exchange lists name other processes but no communicator was set (mpas_dyc_comm_init)";
     return MPAS_DYC_ECOMM;
+  }
+  if (stotal) HIPCHK(hipMalloc(&pl.sendbuf, stotal * sizeof(double)));
+  if (rtotal) HIPCHK(hipMalloc(&pl.recvbuf, rtotal * sizeof(double)));
+  for (size_t i = 0; i < pre.size(); ++i)
+    if (pre_off[i] >= 0) pre[i].dst = pl.sendbuf + pre_off[i];
+  for (size_t i = 0; i < post.size(); ++i) post[i].src = pl.recvbuf + post_off[i];
+  pl.npre = (int)pre.size();
+  pl.npost = (int)post.size();
+  if (pl.npre) {
+    HIPCHK(hipMalloc(&pl.d_pre, pre.size() * sizeof(XSeg)));
+    HIPCHK(hipMemcpy(pl.d_pre, pre.data(), pre.size() * sizeof(XSeg), hipMemcpyHostToDevice));
+  }
+  if (pl.npost) {
+    HIPCHK(hipMalloc(&pl.d_post, post.size() * sizeof(XSeg)));
+    HIPCHK(hipMemcpy(pl.d_post, post.data(), post.size() * sizeof(XSeg), hipMemcpyHostToDevice));
   }
   // point-to-point messages between two ranks match in issue order: order both sides by
   // (source block, destination block)
@@ -484,48 +513,42 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   }
   if (ctx->planning) return MPAS_DYC_OK;
   XPlan& pl = it->second;
-  for (auto& bp : pl.bp)
-    if (bp.npack)
-      hipLaunchKernelGGL(k_halo_pack, dim3((bp.maxn_pack + 3) / 4, bp.npack), dim3(256), 0, ctx->stream,
-                         bp.d_pack, bp.sendbuf);
-  for (const auto& sr : pl.local)
-    HIPCHK(hipMemcpyAsync(pl.bp[sr.second.block].recvbuf + sr.second.off, pl.bp[sr.first.block].sendbuf + sr.first.off,
-                          sr.first.count * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+  if (pl.npre)
+    hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_pre + 3) / 4, pl.npre), dim3(256), 0, ctx->stream, pl.d_pre);
   if (!pl.rsend.empty() || !pl.rrecv.empty()) {
     NCCLCHK(ncclGroupStart());
     for (const XMsg& m : pl.rsend)
-      NCCLCHK(ncclSend(pl.bp[m.block].sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
+      NCCLCHK(ncclSend(pl.sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
     for (const XMsg& m : pl.rrecv)
-      NCCLCHK(ncclRecv(pl.bp[m.block].recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
+      NCCLCHK(ncclRecv(pl.recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
     NCCLCHK(ncclGroupEnd());
   }
-  for (auto& bp : pl.bp)
-    if (bp.nunpack)
-      hipLaunchKernelGGL(k_halo_unpack, dim3((bp.maxn_unpack + 3) / 4, bp.nunpack), dim3(256), 0, ctx->stream,
-                         bp.d_unpack, bp.recvbuf);
+  if (pl.npost)
+    hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_post + 3) / 4, pl.npost), dim3(256), 0, ctx->stream, pl.d_post);
   return MPAS_DYC_OK;
 }
 
 // ---------------------------------------------------------------------------
 // reference routines, one host function each (per block)
 // ---------------------------------------------------------------------------
-void copy_n(mpas_dyc_ctx* ctx, double* dst, const double* src, int64_t n) {
-  if (!ctx->planning) (void)hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream);
-}
-
 // atm_rk_integration_setup (1847-1857): copies over owned+halo elements (not the garbage slot)
 void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
   const int64_t K = d.K, K1 = d.K + 1;
-  copy_n(ctx, p.ru_save, p.ru, (int64_t)d.nEdges * K);
-  copy_n(ctx, p.rw_save, p.rw, (int64_t)d.nCells * K1);
-  copy_n(ctx, p.rtheta_p_save, p.rtheta_p, (int64_t)d.nCells * K);
-  copy_n(ctx, p.rho_p_save, p.rho_p, (int64_t)d.nCells * K);
-  copy_n(ctx, p.u2, p.u1, (int64_t)d.nEdges * K);
-  copy_n(ctx, p.w2, p.w1, (int64_t)d.nCells * K1);
-  copy_n(ctx, p.theta_m2, p.theta_m1, (int64_t)d.nCells * K);
-  copy_n(ctx, p.rho_zz2, p.rho_zz1, (int64_t)d.nCells * K);
-  copy_n(ctx, p.rho_zz_old_split, p.rho_zz1, (int64_t)d.nCells * K);
-  copy_n(ctx, p.scalars2, p.scalars1, (int64_t)d.nCells * K * d.ns);
+  CopyList c{};
+  const double* src[10] = {p.ru, p.rw, p.rtheta_p, p.rho_p, p.u1, p.w1, p.theta_m1, p.rho_zz1, p.rho_zz1, p.scalars1};
+  double* dst[10] = {p.ru_save, p.rw_save, p.rtheta_p_save, p.rho_p_save, p.u2,
+                     p.w2, p.theta_m2, p.rho_zz2, p.rho_zz_old_split, p.scalars2};
+  const int64_t n[10] = {d.nEdges * K, d.nCells * K1, d.nCells * K, d.nCells * K, d.nEdges * K,
+                         d.nCells * K1, d.nCells * K, d.nCells * K, d.nCells * K, d.nCells * K * d.ns};
+  int64_t nmax = 0;
+  for (int i = 0; i < 10; ++i) {
+    c.src[i] = src[i];
+    c.dst[i] = dst[i];
+    c.n[i] = n[i];
+    nmax = std::max(nmax, n[i]);
+  }
+  const unsigned gx = (unsigned)std::min<int64_t>((nmax + 255) / 256, 2048);
+  if (!ctx->planning) hipLaunchKernelGGL(k_copy_many, dim3(gx, 10), dim3(256), 0, ctx->stream, c);
 }
 
 void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {

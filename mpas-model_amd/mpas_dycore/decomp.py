@@ -143,7 +143,7 @@ def _block_elements(case: dict, owners: dict, p: int) -> tuple[dict, dict]:
             lays.append(new)
         groups[loc] = lays
     glob = {loc: np.concatenate(groups[loc]).astype(np.int64) for loc in LOCS}
-    layer_end = {loc: list(np.cumsum([g.size for g in groups[loc]])) for loc in LOCS}
+    layer_end = {loc: [int(x) for x in np.cumsum([g.size for g in groups[loc]])] for loc in LOCS}
     return glob, layer_end
 
 
@@ -226,3 +226,16 @@ def messages(block: Block, direction: str, layers=(1, 2, 3), locs=LOCS) -> dict:
                 if l == loc and lay == layer:
                     out.setdefault(peer, []).append(idx)
     return {p: np.concatenate(v) for p, v in sorted(out.items())}
+
+
+def rank_blocks(case: dict, nranks: int, rank: int, blocks_per_rank: int = 1, cell_part=None):
+    """Blocks of one rank and the placement of every block: block p lives on rank
+    p // blocks_per_rank as local block p % blocks_per_rank (config_number_of_blocks
+    per MPI task, mpas_block_decomp.F:65-100)."""
+    nparts = nranks * blocks_per_rank
+    if cell_part is None:
+        cell_part = partition_sfc(case["nCells"], nparts)
+    mine = list(range(rank * blocks_per_rank, (rank + 1) * blocks_per_rank))
+    blocks = decompose(case, cell_part, parts=mine)
+    placement = {p: (p // blocks_per_rank, p % blocks_per_rank) for p in range(nparts)}
+    return blocks, placement

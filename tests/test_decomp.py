@@ -138,9 +138,17 @@ def _gloo_worker(rank, world, port, q):
         from mpas_dycore.mesh import build_mesh
         from mpas_dycore.init_atm import build_case
         case = build_case(build_mesh(2, lloyd_iters=5), K=4, ns=1)
-        part = decomp.partition_sfc(case["nCells"], world)
-        (b,) = decomp.decompose(case, part, parts=[rank])
-        ok = True
+        (b,), placement = decomp.rank_blocks(case, world, rank, 1)
+        assert placement == {p: (p, 0) for p in range(world)}
+        # what I send to each rank is exactly what that rank expects to receive
+        mine = {(b.part, peer): [(l, lay, int(i.size)) for (l, lay, q, i) in b.send if q == peer]
+                for peer in range(world) if peer != rank}
+        theirs = {(peer, b.part): [(l, lay, int(i.size)) for (l, lay, q, i) in b.recv if q == peer]
+                  for peer in range(world) if peer != rank}
+        everyone = [None] * world
+        dist.all_gather_object(everyone, (mine, theirs))
+        ok = all(everyone[dst][1][(src, dst)] == lists for src in range(world)
+                 for (s_, dst), lists in everyone[src][0].items())
         for loc, key in (("cell", "nCells"), ("edge", "nEdges"), ("vertex", "nVertices")):
             g = np.random.default_rng(11).standard_normal((case[key], 3))
             a = np.full((b.glob[loc].size, 3), np.nan)
@@ -164,7 +172,8 @@ def _gloo_worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
-def test_exchange_two_gloo_ranks():
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_across_gloo_ranks(world):
     import multiprocessing as mp
     import socket
     with socket.socket() as s:
@@ -172,10 +181,10 @@ def test_exchange_two_gloo_ranks():
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: True, 1: True}, res
+    assert res == {r: True for r in range(world)}, res
