@@ -313,6 +313,9 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
 }
 
 inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)); }
+#ifndef DIVDAMP_EPW
+#define DIVDAMP_EPW 2  // edges per wavefront in k_divdamp
+#endif
 
 #define LAUNCH(kern, n, ...)                                                                               \
   do {                                                                                                     \
@@ -592,7 +595,7 @@ void acoustic_step(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, 
 void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
   const double rdts = 1.0 / dts;
   const double coef_divdamp = 2.0 * ctx->cf.smdiv * ctx->cf.len_disp * rdts;
-  LAUNCH(k_divdamp, d.nEdges, d, p, coef_divdamp);
+  LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp);
 }
 
 void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt, int tl, int rk_step /*0 = absent*/) {

@@ -20,9 +20,23 @@ namespace mpas {
 #define WAVES_PER_BLOCK 4
 #define BLOCK_THREADS (64 * WAVES_PER_BLOCK)
 
+// XCD-aware block order.  Workgroups are dealt round-robin to the 8 XCDs, each with
+// its own 4 MiB L2; remapping blockIdx so that XCD x runs one contiguous 1/8 of the
+// (space-filling-curve ordered) elements keeps every neighbour gather of an edge or
+// cell stencil inside the L2 that already holds its neighbours' columns.  The map is a
+// bijection for any grid size, so correctness never depends on the actual placement.
+__device__ __forceinline__ int xcd_block() {
+#ifdef NO_XCD_REMAP
+  return blockIdx.x;
+#endif
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int q = nb >> 3, r = nb & 7, x = bid & 7, i = bid >> 3;
+  return x * q + min(x, r) + i;
+}
+
 // element of this wavefront, wave-uniform (scalar register)
 __device__ __forceinline__ int wave_elem(int start) {
-  int e = start + blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+  int e = start + xcd_block() * WAVES_PER_BLOCK + (threadIdx.x >> 6);
   return __builtin_amdgcn_readfirstlane(e);
 }
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -748,19 +762,38 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p
   }
 }
 
-// atm_divergence_damping_3d (2765-2793)
+// atm_divergence_damping_3d (2765-2793).  EPW edges per wavefront: every load of all
+// EPW edges is issued before the first store, so each wave keeps EPW x 7 column loads
+// in flight (the kernel is latency x occupancy bound with one edge per wave).
+template <int EPW>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, double coef_divdamp) {
-  const int e = wave_elem(0);
-  if (e >= d.nEdges) return;
-  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
-  if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
+  const int e0 = wave_elem(0) * EPW;
   const int k = lane_id(), K = d.K;
-  if (k >= K) return;
-  const size_t o = (size_t)e * K + k, o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
-  const double divCell1 = -(p.rtheta_pp[o1] - p.rtheta_pp_old[o1]);
-  const double divCell2 = -(p.rtheta_pp[o2] - p.rtheta_pp_old[o2]);
-  p.ru_p[o] = p.ru_p[o] + coef_divdamp * (divCell2 - divCell1) * (1.0 - p.specZoneMaskEdge[e]) /
-                              (p.theta_m1[o1] + p.theta_m1[o2]);
+  const bool act = k < K;
+  double ru[EPW], d1[EPW], d2[EPW], th[EPW], mask[EPW];
+  bool on[EPW];
+#pragma unroll
+  for (int j = 0; j < EPW; ++j) {
+    const int e = e0 + j;
+    on[j] = false;
+    if (e < d.nEdges) {
+      const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+      on[j] = (c1 < d.nCellsSolve || c2 < d.nCellsSolve);
+      if (on[j] && act) {
+        const size_t o = (size_t)e * K + k, o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
+        ru[j] = p.ru_p[o];
+        d1[j] = -(p.rtheta_pp[o1] - p.rtheta_pp_old[o1]);
+        d2[j] = -(p.rtheta_pp[o2] - p.rtheta_pp_old[o2]);
+        th[j] = p.theta_m1[o1] + p.theta_m1[o2];
+        mask[j] = p.specZoneMaskEdge[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < EPW; ++j) {
+    if (on[j] && act)
+      p.ru_p[(size_t)(e0 + j) * K + k] = ru[j] + coef_divdamp * (d2[j] - d1[j]) * (1.0 - mask[j]) / th[j];
+  }
 }
 
 // ============================================================================

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBPATH = os.path.join(os.path.dirname(HERE), "csrc", "libmpas_dycore.so")
+LIBPATH = os.environ.get("MPAS_DYCORE_LIB") or os.path.join(os.path.dirname(HERE), "csrc", "libmpas_dycore.so")
 
 EXPORTS = (
     "mpas_dyc_create", "mpas_dyc_destroy", "mpas_dyc_last_error", "mpas_dyc_set_field", "mpas_dyc_get_field",

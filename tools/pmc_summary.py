@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Summarise the FETCH_SIZE / WRITE_SIZE passes of tools/pmc_traffic.sh per kernel.
+
+Counter values are KiB per dispatch.  FETCH_SIZE on gfx950 under-reports
+streaming reads (MI355X_MICROARCH.md "HBM"); the factor for this code's
+8-byte-per-lane column loads is calibrated on k_copy_many, whose bytes are known
+exactly (atm_rk_integration_setup: ten contiguous copies).
+Usage: python tools/pmc_summary.py gpurun_out [ncells levels ns] > profiles/...
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(path):
+    per = defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            name = r["Kernel_Name"].split("(")[0].replace("mpas::", "")
+            per[name].append((float(r["Counter_Value"]) * 1024.0,
+                              (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))
+    return per
+
+
+def main():
+    d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+    nC, K, ns = (int(x) for x in sys.argv[2:5]) if len(sys.argv) > 4 else (163842, 56, 1)
+    fetch = load(os.path.join(d, "pmc_fetch", "fetch_counter_collection.csv"))
+    write = load(os.path.join(d, "pmc_write", "write_counter_collection.csv"))
+    # calibration: k_copy_many moves (nE*K + 2 nC*(K+1) + 6 nC*K + nC*K*ns) doubles each way
+    nE = 3 * nC - 6 if nC > 12 else 0
+    known = 8.0 * (2 * nE * K + 2 * nC * (K + 1) + 5 * nC * K + nC * K * ns)
+    cf = known / (sum(v for v, _ in fetch["k_copy_many"]) / len(fetch["k_copy_many"]))
+    cw = known / (sum(v for v, _ in write["k_copy_many"]) / len(write["k_copy_many"]))
+    rows = []
+    for name in fetch:
+        if name not in write:
+            continue
+        f = sum(v for v, _ in fetch[name]) / len(fetch[name]) * cf
+        w = sum(v for v, _ in write[name]) / len(write[name]) * cw
+        rows.append(dict(kernel=name, dispatches=len(fetch[name]), read_bytes=f, write_bytes=w))
+    rows.sort(key=lambda r: -(r["read_bytes"] + r["write_bytes"]) * r["dispatches"])
+    out = dict(ncells=nC, levels=K, num_scalars=ns, fetch_calibration=cf, write_calibration=cw,
+               method="rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; per-dispatch mean; "
+                      "FETCH/WRITE scaled by the factor that makes k_copy_many (known bytes) exact",
+               kernels=rows)
+    ac = [r for r in rows if r["kernel"] in ("k_acoustic_edges", "k_acoustic_cells", "k_divdamp")]
+    out["bytes_per_substep"] = sum(r["read_bytes"] + r["write_bytes"] for r in ac)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
