@@ -690,13 +690,18 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p
     double ts = 0.0, rs = 0.0;
     const int ne = p.nEdgesOnCell[c];
     const double invA = p.invAreaCell[c];
+    // theta_m of this cell is loaded once; the edge's other cell supplies the second
+    // operand, in the reference's (cell2 + cell1) order
+    const double thc = LD(p.theta_m1, o);
     for (int i = 0; i < ne; ++i) {
       const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
       const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
       if (act) {
         const double flux = p.edgesOnCell_sign[c * d.maxEdges + i] * dts * p.dvEdge[e] * p.ru_p[(size_t)e * K + k] * invA;
         rs = rs - flux;
-        ts = ts - flux * 0.5 * (p.theta_m1[(size_t)c2 * K + k] + p.theta_m1[(size_t)c1 * K + k]);
+        const double th1 = (c1 == c) ? thc : p.theta_m1[(size_t)c1 * K + k];
+        const double th2 = (c2 == c) ? thc : p.theta_m1[(size_t)c2 * K + k];
+        ts = ts - flux * 0.5 * (th2 + th1);
       }
     }
     const double cofrz = act ? p.cofrz[k] : 0.0, rdzw = act ? p.rdzw[k] : 0.0;

@@ -17,10 +17,9 @@ would.
   * Layer ``l`` > 1 holds the edges of the cell-halo layer ``l-1`` not yet in
     the block (build_edge_halos, :734-938).
   * Edge and vertex fields therefore have nHalos+1 = 3 exchange layers.
-* **Local order.** Owned elements come first, then each halo layer. Within a
-  group, elements are in ascending global index. The reference's own order
-  within a group is hash-discovery order. Every stencil is element-local with
-  fixed neighbour order, so this choice changes no result bit.
+* **Local order** is the reference's (see ``_block_elements``): owned first,
+  then each halo layer, so the local indices and exchange lists a rank sees are
+  the ones MPAS would build from the same partition file.
 * **Missing neighbours.** Connectivity is remapped to block-local indices, and
   neighbours outside the block become -1, which is the garbage slot n+1 at the
   C ABI (mpas_block_creator.F:1445).
@@ -112,7 +111,23 @@ class Block:
         return (0 if layer == 0 else e[layer - 1], e[layer])
 
 
+def _discovery_order(idx2d: np.ndarray, counts: np.ndarray, rows: np.ndarray) -> np.ndarray:
+    """Unique valid entries of idx2d[rows, :counts[rows]] in first-encounter order
+    (mpas_block_decomp_all_edges_in_block, mpas_block_decomp.F:369-420)."""
+    sub = idx2d[rows]
+    mask = np.arange(sub.shape[1])[None, :] < counts[rows][:, None]
+    vals = sub[mask]
+    vals = vals[vals >= 0]
+    _, first = np.unique(vals, return_index=True)
+    return vals[np.sort(first)]
+
+
 def _block_elements(case: dict, owners: dict, p: int) -> tuple[dict, dict]:
+    """Local element order of block p, as mpas_block_creator builds it:
+    cells: owned in ascending global ID, then each halo layer quicksorted (:601);
+    edges/vertices: owned in discovery order over the owned cells, then layer 1 in
+    reverse discovery order (ghostEdgeStart counts down, mpas_block_decomp.F:339-341),
+    then the new edges of each cell-halo layer in discovery order (:859-876)."""
     nEdgesOnCell = np.asarray(case["nEdgesOnCell"])
     cellsOnCell = np.asarray(case["cellsOnCell"])
     owned = np.flatnonzero(owners["cell"] == p)
@@ -126,19 +141,21 @@ def _block_elements(case: dict, owners: dict, p: int) -> tuple[dict, dict]:
         new = nb[~seen[nb]]
         seen[new] = True
         cell_layers.append(new)
+    cells = np.concatenate(cell_layers)
     groups = {"cell": cell_layers}
     for loc, on_cell in (("edge", "edgesOnCell"), ("vertex", "verticesOnCell")):
         arr = np.asarray(case[on_cell])
         n = case[_N[loc]]
-        e0 = _neighbours(arr, nEdgesOnCell, owned)
-        own = e0[owners[loc][e0] == p]
-        lay1 = e0[owners[loc][e0] != p]
+        e0 = _discovery_order(arr, nEdgesOnCell, owned)
+        mine = owners[loc][e0] == p
+        lays = [e0[mine], e0[~mine][::-1]]
         in_blk = np.zeros(n, dtype=bool)
         in_blk[e0] = True
-        lays = [own, lay1]
+        ncl = owned.size
         for h in range(1, NHALOS + 1):
-            nb = _neighbours(arr, nEdgesOnCell, cell_layers[h])
-            new = nb[~in_blk[nb]]
+            ncl += cell_layers[h].size
+            found = _discovery_order(arr, nEdgesOnCell, cells[:ncl])
+            new = found[~in_blk[found]]
             in_blk[new] = True
             lays.append(new)
         groups[loc] = lays
@@ -183,7 +200,8 @@ def decompose(case: dict, cell_part: np.ndarray, parts=None) -> list[Block]:
     for b in blocks:
         for loc in LOCS:
             n_owned = b.layer_end[loc][0]
-            owned_glob = b.glob[loc][:n_owned]  # ascending global ids
+            g2own = np.full(case[_N[loc]], -1, dtype=np.int64)
+            g2own[b.glob[loc][:n_owned]] = np.arange(n_owned)
             for layer in range(1, NLAYERS[loc] + 1):
                 # receive: my layer-`layer` halo elements, grouped by owner
                 s, e = b.layer_range(loc, layer)
@@ -199,7 +217,7 @@ def decompose(case: dict, cell_part: np.ndarray, parts=None) -> list[Block]:
                     gids = glob_p[loc][lend_p[loc][layer - 1]:lend_p[loc][layer]]
                     gids = gids[owners[loc][gids] == b.part]
                     if gids.size:
-                        b.send.append((loc, layer, p, np.searchsorted(owned_glob, gids).astype(np.int32)))
+                        b.send.append((loc, layer, p, g2own[gids].astype(np.int32)))
     return blocks
 
 

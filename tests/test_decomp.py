@@ -188,3 +188,56 @@ def test_exchange_across_gloo_ranks(world):
     for p in procs:
         p.join(timeout=60)
     assert res == {r: True for r in range(world)}, res
+
+
+def _reference_edge_order(case, part, p, on_cell, owner_of):
+    """Loop-by-loop restatement of mpas_block_decomp_all_edges_in_block +
+    mpas_block_decomp_partitioned_edge_list + build_edge_halos for one block."""
+    noc = case["nEdgesOnCell"]
+    coc = case["cellsOnCell"]
+    owned = [c for c in range(case["nCells"]) if part[c] == p]
+    cells = list(owned)
+    layers = []
+    seen = set(cells)
+    for _ in range(2):
+        ring = sorted({int(n) for c in (layers[-1] if layers else owned) for n in coc[c, :noc[c]]} - seen)
+        seen |= set(ring)
+        layers.append(ring)
+    def all_in(cs):
+        out, h = [], set()
+        for c in cs:
+            for j in range(noc[c]):
+                e = int(case[on_cell][c, j])
+                if e not in h:
+                    h.add(e)
+                    out.append(e)
+        return out
+    e0 = all_in(owned)
+    lst = [None] * len(e0)
+    last, ghost = 0, len(e0)
+    for e in e0:
+        if owner_of[e] == p:
+            lst[last] = e
+            last += 1
+        else:
+            ghost -= 1
+            lst[ghost] = e
+    have = set(lst)
+    for h in range(2):
+        cs = owned + sum(layers[:h + 1], [])
+        for e in all_in(cs):
+            if e not in have:
+                have.add(e)
+                lst.append(e)
+    return cells + layers[0] + layers[1], lst
+
+
+def test_local_order_matches_reference_block_creator(small_case):
+    part = decomp.partition_sfc(small_case["nCells"], 3)
+    owners = decomp.element_owners(small_case, part)
+    for b in decomp.decompose(small_case, part):
+        cells, edges = _reference_edge_order(small_case, part, b.part, "edgesOnCell", owners["edge"])
+        assert b.glob["cell"].tolist() == cells
+        assert b.glob["edge"].tolist() == edges
+        _, verts = _reference_edge_order(small_case, part, b.part, "verticesOnCell", owners["vertex"])
+        assert b.glob["vertex"].tolist() == verts
