@@ -29,6 +29,7 @@ struct Dims {
   int nCells, nEdges, nVertices, K, maxEdges, maxEdges2, ns;
   int nCellsSolve, nEdgesSolve, nVerticesSolve;
   int moist_start, moist_end;  // 0-based inclusive range of moist scalars
+  int diabatic;                // rt_diabatic_tend holds nonzero data (else it is read as 0)
 };
 
 struct Config {

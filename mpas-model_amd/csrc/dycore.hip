@@ -1022,6 +1022,12 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
   } else {
     HIPCHK(hipMemcpyAsync(f->buf[slot], host, nb, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (f->pool == "tend" && f->name == "rt_diabatic_tend") {
+      const double* h = (const double*)host;
+      int nz = 0;
+      for (int64_t i = 0; i < nb / 8 && !nz; ++i) nz = h[i] != 0.0;
+      b.d.diabatic = nz;
+    }
   }
   return MPAS_DYC_OK;
 }

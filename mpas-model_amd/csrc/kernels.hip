@@ -40,6 +40,10 @@ __device__ __forceinline__ int wave_elem(int start) {
   return __builtin_amdgcn_readfirstlane(e);
 }
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// per-cell edge terms kept in registers up to this many edges (hexagons and pentagons);
+// larger cells take the plain loop
+constexpr int MAX_EDGES_UNROLL = 6;
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // value held by lane-1 (k-1) / lane+1 (k+1); lanes at the ends get garbage that callers never use
@@ -65,6 +69,11 @@ __device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, 
 }
 
 #define LD(p, i) (act ? (p)[(i)] : 0.0)
+
+// Physics tendencies (tend_ru_physics, tend_rtheta_physics, tend_rho_physics) are zeroed
+// by atm_srk3 when the model is built without DO_PHYSICS (mpas_atm_time_integration.F:
+// 268-279, 450-457): the kernels add the same +0.0 without streaming the zero arrays.
+#define PHYS_ZERO 0.0
 #define LDW(p, i) (actw ? (p)[(i)] : 0.0)
 
 // ============================================================================
@@ -216,7 +225,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells1(Dims d, Ptrs p, Co
     const double rwk = (k <= K) ? p.rw[ow] : 0.0;
     const double rwp = dn1(rwk);
     if (act) {
-      p.tend_rho[o] = -hd - p.rdzw[k] * (rwp - rwk) + p.tend_rho_physics[o];
+      p.tend_rho[o] = -hd - p.rdzw[k] * (rwp - rwk) + PHYS_ZERO;  // tend_rho_physics
       const double qt = p.qtot[o];
       p.dpdz[o] = -GRAVITY * (p.rho_base[o] * (qt) + p.rho_p_save[o] * (1. + qt));
     }
@@ -286,7 +295,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges(Dims d, Ptrs p, Con
         const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
         tu = tu - p.rho_edge[o] * uk * coef;
       }
-      tu = tu + tue + p.tend_ru_physics[o];
+      tu = tu + tue + PHYS_ZERO;  // tend_ru_physics
     }
     if (act) p.tend_u[o] = tu;
   }
@@ -383,7 +392,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_rk1b(Dims d, Ptrs p
     const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
     tu = tu - p.rho_edge[o] * uk * coef;
   }
-  p.tend_u[o] = tu + tue + p.tend_ru_physics[o];
+  p.tend_u[o] = tu + tue + PHYS_ZERO;  // tend_ru_physics
 }
 
 // cells (all), rk1: del^2 for w (5107-5130) and theta (5278-5301)
@@ -499,15 +508,30 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Co
   const int ne = p.nEdgesOnCell[c];
   const double fzm = act ? p.fzm[k] : 0.0, fzp = act ? p.fzp[k] : 0.0;
   const bool rk1 = s.rk_step == 1;
-  // ---------------- w: horizontal advection (5046-5074); edge fluxes from k_dyn_advflux
-  double tw = 0.0;
+  // ---------------- horizontal advection of w (5046-5074) and theta (5231-5252) from the
+  // edge fluxes of k_dyn_advflux, plus the rk>1 perturbation flux terms (5256-5269): one
+  // pass over the edges loads each edge column once.  The two theta sums keep the
+  // reference order (all advection terms, then all perturbation terms).
+  const double thc1 = LD(p.theta_m1, o);
+  double tw = 0.0, tt = 0.0;
+  double tpert[MAX_EDGES_UNROLL];
+  const bool pert = !rk1 && ne <= MAX_EDGES_UNROLL;
   for (int i = 0; i < ne; ++i) {
     const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double sg = p.edgesOnCell_sign[c * d.maxEdges + i];
     const double rue = LD(p.ru, (size_t)e * K + k);
     const double rue_m = up1(rue);
     const double ru_edge_w = fzm * rue + fzp * rue_m;
-    const double flux = LD(p.advflux_w, (size_t)e * K + k);
-    tw = tw - p.edgesOnCell_sign[c * d.maxEdges + i] * ru_edge_w * flux;
+    tw = tw - sg * ru_edge_w * LD(p.advflux_w, (size_t)e * K + k);
+    tt = tt - sg * rue * LD(p.advflux_th, (size_t)e * K + k);
+    if (pert && act) {
+      const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+      const double th1 = (c1 == c) ? thc1 : p.theta_m1[(size_t)c1 * K + k];
+      const double th2 = (c2 == c) ? thc1 : p.theta_m1[(size_t)c2 * K + k];
+#pragma unroll
+      for (int q = 0; q < MAX_EDGES_UNROLL; ++q)
+        if (q == i) tpert[q] = sg * p.dvEdge[e] * (p.ru_save[(size_t)e * K + k] - rue) * 0.5 * (th2 + th1);
+    }
   }
   // ---------------- w euler tendency: del4 (rk1)
   double twe = actw ? p.tend_w_euler[ow] : 0.0;
@@ -545,15 +569,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Co
     p.tend_w[ow] = (act && k >= 1) ? tw : 0.0;
     if (rk1) p.tend_w_euler[ow] = twe;
   }
-  // ---------------- theta: horizontal advection (5231-5252); edge fluxes from k_dyn_advflux
-  double tt = 0.0;
-  for (int i = 0; i < ne; ++i) {
-    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
-    const double rue = LD(p.ru, (size_t)e * K + k);
-    const double flux = LD(p.advflux_th, (size_t)e * K + k);
-    tt = tt - p.edgesOnCell_sign[c * d.maxEdges + i] * rue * flux;
-  }
-  if (!rk1) {  // perturbation flux for rtheta_pp (5256-5269)
+  if (pert) {
+    if (act) {
+#pragma unroll
+      for (int q = 0; q < MAX_EDGES_UNROLL; ++q)
+        if (q < ne) tt = tt - tpert[q];
+    }
+  } else if (!rk1) {  // perturbation flux for rtheta_pp (5256-5269), cells with > MAX_EDGES_UNROLL edges
     for (int i = 0; i < ne; ++i) {
       const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
       const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
@@ -612,9 +634,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Co
     tt = tt * p.invAreaCell[c] - p.rdzw[k] * (wdtz_p - wdtz);
     p.tend_rtheta_adv[o] = tt;
     p.rthdynten[o] = tt / rz;
-    tt = tt + rz * p.rt_diabatic_tend[o];
+    tt = tt + rz * (d.diabatic ? p.rt_diabatic_tend[o] : 0.0);
     if (rk1) p.tend_theta_euler[o] = tte;
-    p.tend_theta[o] = tt + tte + p.tend_rtheta_physics[o];
+    p.tend_theta[o] = tt + tte + PHYS_ZERO;  // tend_rtheta_physics
   }
 }
 
@@ -803,9 +825,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, doubl
 
 // ============================================================================
 // atm_recover_large_step_variables_work  (mpas_atm_time_integration.F:2984-3097)
-// The edge loop (3048-3059) recomputes rho_zz of its two cells and the cell loops
-// recompute ru of their edges with the reference expressions (bit-identical), so
-// the three barrier-separated phases become two independent launches.
+// The edge loop (3048-3059) recomputes rho_zz of its two cells with the reference
+// expression (bit-identical), so the three barrier-separated phases become two
+// launches: k_recover_edges, then k_recover_cells (cell phases 1 and 3, which reads
+// the ru just written).
 // ============================================================================
 __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs) {
   const int e = wave_elem(0);
@@ -856,7 +879,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells(Dims d, Ptrs p,
   }
   if (act) {
     if (rk_step == 3) {
-      const double rtp = p.rtheta_p_save[o] + p.rtheta_pp[o] - dt * rz * p.rt_diabatic_tend[o];
+      const double rtp = p.rtheta_p_save[o] + p.rtheta_pp[o] - dt * rz * (d.diabatic ? p.rt_diabatic_tend[o] : 0.0);
       p.rtheta_p[o] = rtp;
       p.theta_m2[o] = (rtp + p.rtheta_base[o]) / rz;
       const double ex = pow(zz * (RGAS / P0) * (rtp + p.rtheta_base[o]), rcv);
@@ -873,7 +896,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells(Dims d, Ptrs p,
   for (int i = 0; i < ne; ++i) {
     const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
     const double sg = p.edgesOnCell_sign[c * d.maxEdges + i];
-    const double ruk = act ? p.ru_save[(size_t)e * K + k] + p.ru_p[(size_t)e * K + k] : 0.0;
+    const double ruk = act ? p.ru[(size_t)e * K + k] : 0.0;  // written by k_recover_edges, launched first
     const double rum = up1(ruk);
     const double ru1 = readlane_d(ruk, 0), ru2 = readlane_d(ruk, 1), ru3 = readlane_d(ruk, 2);
     const size_t zo = ((size_t)c * d.maxEdges + i) * K1 + k;
@@ -932,16 +955,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells(Dims d, Ptrs p, co
   const int ne = p.nEdgesOnCell[c];
   const double r = p.invAreaCell[c];
   double div = 0.0, ke = 0.0;
+  // divergence (5626-5640) and the edge part of ke (5650-5660): independent sums, one pass
   for (int i = 0; i < ne; ++i) {
     const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
     const double s = p.edgesOnCell_sign[c * d.maxEdges + i] * p.dvEdge[e];
-    div = div + s * u[(size_t)e * K + k];
+    const double ue = u[(size_t)e * K + k];
+    div = div + s * ue;
+    ke = ke + 0.25 * (p.dcEdge[e] * p.dvEdge[e] * (ue * ue));  // ke_edge (5600)
   }
   div = div * r;
-  for (int i = 0; i < ne; ++i) {
-    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
-    ke = ke + 0.25 * ke_edge_of(p, u, e, K, k);
-  }
   ke = ke * p.invAreaCell[c];
   const double ke_fact = 1.0 - .375;
   ke = ke_fact * ke;
@@ -970,7 +992,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges(Dims d, Ptrs p, co
   const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
   const int v1 = p.verticesOnEdge[2 * e], v2 = p.verticesOnEdge[2 * e + 1];
   p.rho_edge[o] = 0.5 * (h[(size_t)c1 * K + k] + h[(size_t)c2 * K + k]);
-  p.ke_edge[o] = ke_edge_of(p, u, e, K, k);
+  // ke_edge (5600) is module scratch: it is recomputed where consumed, never stored
   double vv;
   if (reconstruct_v) {
     vv = 0.0;
