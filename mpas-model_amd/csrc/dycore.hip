@@ -724,8 +724,9 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       CHK(exchange(ctx, {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},   // 876-887
                          {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}}));
       const double invNs = 1 / (double)number_sub_steps[rk_step - 1];
-      EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs));       // 889-930
-      EACH(LAUNCH(k_recover_cells, d.nCells + 1, d, p, rk_timestep[rk_step - 1], invNs, rk_step));
+      EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rk_timestep[rk_step - 1], invNs, rk_step));  // 889-930
+      EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs));
+      EACH(LAUNCH(k_recover_cells3, d.nCells, d, p));
       CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));        // 988
       if (scalars_in_dynamics) {                                  // 993-1185
         if (rk_step < 3 || (!cf.monotonic && !cf.positive_definite)) {

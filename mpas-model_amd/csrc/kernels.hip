@@ -825,31 +825,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, doubl
 
 // ============================================================================
 // atm_recover_large_step_variables_work  (mpas_atm_time_integration.F:2984-3097)
-// The edge loop (3048-3059) recomputes rho_zz of its two cells with the reference
-// expression (bit-identical), so the three barrier-separated phases become two
-// launches: k_recover_edges, then k_recover_cells (cell phases 1 and 3, which reads
-// the ru just written).
+// Three launches for the three barrier-separated phases.
 // ============================================================================
-__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs) {
-  const int e = wave_elem(0);
-  if (e >= d.nEdges) return;
-  const int k = lane_id(), K = d.K;
-  if (k >= K) return;
-  const size_t o = (size_t)e * K + k;
-  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
-  auto rhozz = [&](int c) -> double {
-    if (c >= d.nCells) return 1.0;  // garbage cell (2989-2991)
-    const size_t oc = (size_t)c * K + k;
-    const double rho_p = p.rho_p_save[oc] + p.rho_pp[oc];
-    return rho_p + p.rho_base[oc];
-  };
-  p.ruAvg[o] = p.ru_save[o] + (p.ruAvg[o] * invNs);
-  const double ru = p.ru_save[o] + p.ru_p[o];
-  p.ru[o] = ru;
-  p.u2[o] = 2. * ru / (rhozz(c1) + rhozz(c2));
-}
-
-__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells(Dims d, Ptrs p, double dt, double invNs, int rk_step) {
+// cells (all, and the garbage slot): 2998-3040
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p, double dt, double invNs, int rk_step) {
   const int c = wave_elem(0);
   const int k = lane_id(), K = d.K;
   const size_t K1 = K + 1;
@@ -870,13 +849,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells(Dims d, Ptrs p,
   }
   const double fzm = act ? p.fzm[k] : 0.0, fzp = act ? p.fzp[k] : 0.0;
   const double zz = LD(p.zz, o), zzm = up1(zz);
-  double w = 0.0;
+  double w = 0.0;  // w(1) = w(nVertLevels+1) = 0
   if (act && k >= 1) {
     p.wwAvg[ow] = p.rw_save[ow] + (p.wwAvg[ow] * invNs);
     const double rw = p.rw_save[ow] + p.rw_p[ow];
     p.rw[ow] = rw;
-    w = rw / (fzm * zz + fzp * zzm);
+    w = rw / (fzm * zz + fzp * zzm);  // divided by density in k_recover_cells3
   }
+  if (k <= K) p.w2[ow] = w;
   if (act) {
     if (rk_step == 3) {
       const double rtp = p.rtheta_p_save[o] + p.rtheta_pp[o] - dt * rz * (d.diabatic ? p.rt_diabatic_tend[o] : 0.0);
@@ -891,12 +871,37 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells(Dims d, Ptrs p,
       p.theta_m2[o] = (rtp + p.rtheta_base[o]) / rz;
     }
   }
-  // w from the flux-divergence operator (3063-3097)
+}
+
+// edges (all): 3048-3059
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const size_t o = (size_t)e * K + k;
+  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  p.ruAvg[o] = p.ru_save[o] + (p.ruAvg[o] * invNs);
+  const double ru = p.ru_save[o] + p.ru_p[o];
+  p.ru[o] = ru;
+  p.u2[o] = 2. * ru / (p.rho_zz2[(size_t)c1 * K + k] + p.rho_zz2[(size_t)c2 * K + k]);
+}
+
+// cells (all): w from the flux-divergence operator, then divided by density (3063-3097)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3(Dims d, Ptrs p) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const size_t K1 = K + 1;
+  const bool act = k < K;
+  const size_t o = (size_t)c * K + k, ow = (size_t)c * K1 + k;
+  const double fzm = act ? p.fzm[k] : 0.0, fzp = act ? p.fzp[k] : 0.0;
+  double w = act ? p.w2[ow] : 0.0;
   const int ne = p.nEdgesOnCell[c];
   for (int i = 0; i < ne; ++i) {
     const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
     const double sg = p.edgesOnCell_sign[c * d.maxEdges + i];
-    const double ruk = act ? p.ru[(size_t)e * K + k] : 0.0;  // written by k_recover_edges, launched first
+    const double ruk = act ? p.ru[(size_t)e * K + k] : 0.0;
     const double rum = up1(ruk);
     const double ru1 = readlane_d(ruk, 0), ru2 = readlane_d(ruk, 1), ru3 = readlane_d(ruk, 2);
     const size_t zo = ((size_t)c * d.maxEdges + i) * K1 + k;
@@ -908,11 +913,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells(Dims d, Ptrs p,
       w = w + sg * (p.zb_cell[zo] + sgn1(flux) * p.zb3_cell[zo]) * flux;
     }
   }
+  const double rz = act ? p.rho_zz2[o] : 0.0;
   const double rzm = up1(rz);
   const double r1 = readlane_d(rz, 0), r2 = readlane_d(rz, 1), r3 = readlane_d(rz, 2);
   if (k == 0) w = w / (p.cf1 * r1 + p.cf2 * r2 + p.cf3 * r3);
   else if (act) w = w / (fzm * rz + fzp * rzm);
-  if (k <= K) p.w2[ow] = w;  // w(K+1) = 0
+  if (act) p.w2[ow] = w;  // w(K+1) stays 0
 }
 
 // ============================================================================
