@@ -46,8 +46,19 @@ def main():
                method="rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; per-dispatch mean; "
                       "FETCH/WRITE scaled by the factor that makes k_copy_many (known bytes) exact",
                kernels=rows)
-    ac = [r for r in rows if r["kernel"] in ("k_acoustic_edges", "k_acoustic_cells", "k_divdamp")]
-    out["bytes_per_substep"] = sum(r["read_bytes"] + r["write_bytes"] for r in ac)
+    # the roofline sub-step is the one bench.py times: the last `reps` dispatches of each
+    # acoustic kernel (time_acoustic_step, small_step = 2)
+    reps = int(os.environ.get("ACOUSTIC_REPS", "5"))
+    tot = 0.0
+    per = {}
+    for name in fetch:
+        if any(t in name for t in ("k_acoustic_edges", "k_acoustic_cells", "k_divdamp")):
+            f = sum(v for v, _ in fetch[name][-reps:]) / reps * cf
+            w = sum(v for v, _ in write[name][-reps:]) / reps * cw
+            per[name] = dict(read_bytes=f, write_bytes=w)
+            tot += f + w
+    out["acoustic_substep_kernels"] = per
+    out["bytes_per_substep"] = tot
     print(json.dumps(out, indent=1))
 
 
