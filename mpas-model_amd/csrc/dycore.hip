@@ -1193,17 +1193,25 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
     if (!ctx->graph_exec[parity] || ctx->graph_dt[parity] != dt) {
       if (ctx->graph_exec[parity]) (void)hipGraphExecDestroy(ctx->graph_exec[parity]);
       ctx->graph_exec[parity] = nullptr;
-      hipGraph_t g;
+      hipGraph_t g = nullptr;
       HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
       int r = srk3(ctx, dt);
       hipError_t e = hipStreamEndCapture(ctx->stream, &g);
-      if (r) return r;
+      if (r && r != MPAS_DYC_ECOMM) return r;
+      if (r == MPAS_DYC_ECOMM && e == hipSuccess) e = hipErrorUnknown;  // RCCL refused to be captured
+      if (e == hipSuccess) e = hipGraphInstantiate(&ctx->graph_exec[parity], g, nullptr, nullptr, 0);
+      if (g) (void)hipGraphDestroy(g);
       if (e != hipSuccess) {
-        ctx->err = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
-        return MPAS_DYC_EHIP;
+        // a runtime that cannot capture this step (e.g. its RCCL calls) runs it eagerly
+        (void)hipGetLastError();
+        ctx->graph_exec[parity] = nullptr;
+        ctx->use_graph = false;
+        fprintf(stderr, "mpas_dycore: hipGraph capture failed (%s); running the step eagerly\n",
+                hipGetErrorString(e));
+        r = srk3(ctx, dt);
+        HIPCHK(hipGetLastError());
+        return r;
       }
-      HIPCHK(hipGraphInstantiate(&ctx->graph_exec[parity], g, nullptr, nullptr, 0));
-      (void)hipGraphDestroy(g);
       ctx->graph_dt[parity] = dt;
     }
     HIPCHK(hipGraphLaunch(ctx->graph_exec[parity], ctx->stream));
