@@ -40,12 +40,13 @@ def _dist():
     return world, rank, local
 
 
-def cpu_baseline(case, dt, nthreads, steps):
+def cpu_baseline(case, dt, nthreads, steps, moist_end=1):
     """Reference dycore (compiled Fortran) timed on host cores -- the cpu_baseline leg only."""
     from oracle import ref_runner
     if not ref_runner.available():
         return None
-    _, times = ref_runner.run_reference(case, nsteps=steps, dt=dt, dump_steps=[], nthreads=nthreads, timeout=1200)
+    _, times = ref_runner.run_reference(case, nsteps=steps, dt=dt, dump_steps=[], nthreads=nthreads, timeout=1200,
+                                        moist_end=moist_end)
     use = times[1:] if len(times) > 1 else times  # first step pays allocation / first-touch
     t = sum(use) / len(use)
     return dict(value=case["nCells"] * case["nVertLevels"] / t, unit="cell-updates/s", cores=nthreads,
@@ -62,7 +63,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--ncells", type=int, default=163842)
     ap.add_argument("--levels", type=int, default=56)
-    ap.add_argument("--num-scalars", type=int, default=1)
+    ap.add_argument("--num-scalars", type=int, default=None)
+    ap.add_argument("--moist", action="store_true",
+                    help="BASELINE.json configs[3]: moist JW (qv) + tracer blobs, num_scalars=6, monotone transport")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
@@ -85,16 +88,20 @@ def main():
     from mpas_dycore.cases import jw_case
 
     # rank 0 builds (and caches) the synthetic case before any rank touches the GPU
+    if args.num_scalars is None:
+        args.num_scalars = 6 if args.moist else 1
     t_build = time.time()
     if rank == 0:
-        case = jw_case(args.ncells, K=args.levels, ns=args.num_scalars)
+        case = jw_case(args.ncells, K=args.levels, ns=args.num_scalars, moist=args.moist)
     if dist:
         dist.barrier()
     if rank != 0:
-        case = jw_case(args.ncells, K=args.levels, ns=args.num_scalars)
+        case = jw_case(args.ncells, K=args.levels, ns=args.num_scalars, moist=args.moist)
     dt = case["dt"]
     t_build = time.time() - t_build
 
+    # WSM6-like species set: every scalar is a moist species (moist_start..moist_end, qtot)
+    moist_end = case["num_scalars"] if args.moist else 1
     nparts = world * args.blocks
     if nparts > 1:
         blocks, placement = decomp.rank_blocks(case, world, rank, args.blocks)
@@ -105,11 +112,11 @@ def main():
             comm_id = obj[0]
         torch.cuda.set_device(device)
         dy = Dycore.from_blocks(blocks, device=device, placement=placement, rank=rank, nranks=world,
-                                comm_id=comm_id)
+                                comm_id=comm_id, moist_end=moist_end)
         owned = sum(b.solve[0] for b in blocks)
         halo = sum(b.case["nCells"] - b.solve[0] for b in blocks)
     else:
-        dy = Dycore(case, device=device)
+        dy = Dycore(case, device=device, moist_end=moist_end)
         owned, halo = case["nCells"], 0
     dy.init_diagnostics(dt)
     if not args.no_graph:
@@ -174,8 +181,11 @@ def main():
         "dtype": "f64",
         "data": "synthetic (icosahedral SCVT mesh + Jablonowski-Williamson baroclinic wave, built on the box)",
         "config": {
-            "workload": f"x1.{case['nCells']} dry dycore, {case['nVertLevels']} levels, dt={dt:g}s "
-                        f"(BASELINE.json configs[2] mesh; one full atm_srk3 per step)",
+            "workload": (f"x1.{case['nCells']} moist dycore + scalar transport (num_scalars={case['num_scalars']}, "
+                         f"monotone), {case['nVertLevels']} levels, dt={dt:g}s (BASELINE.json configs[3]; one full "
+                         f"atm_srk3 per step)" if args.moist else
+                         f"x1.{case['nCells']} dry dycore, {case['nVertLevels']} levels, dt={dt:g}s "
+                         f"(BASELINE.json configs[2] mesh; one full atm_srk3 per step)"),
             "nCells": case["nCells"], "nVertLevels": case["nVertLevels"], "num_scalars": case["num_scalars"],
             "dt": dt, "time_integration_order": case["config"]["config_time_integration_order"],
             "split_steps": case["config"]["config_dynamics_split_steps"], "acoustic_substeps": nss,
@@ -196,7 +206,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             nthreads = min(args.cpu_threads, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(case, dt, nthreads, args.cpu_steps)
+            out["cpu_baseline"] = cpu_baseline(case, dt, nthreads, args.cpu_steps, moist_end)
         except Exception as e:  # the measured GPU number stands on its own
             out["cpu_baseline"] = {"error": str(e)[:200]}
     out["build_s"] = round(t_build, 1)

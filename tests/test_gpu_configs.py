@@ -41,6 +41,8 @@ VARIANTS = {
     "no_limiter": (True, dict(config_monotonic=False, config_positive_definite=False)),
     "order3_transport_in_dynamics": (True, dict(config_time_integration_order=3,
                                                 config_split_dynamics_transport=False)),
+    # every scalar a moist species (moist_end = num_scalars): qtot sums them all (1899-1931)
+    "all_scalars_moist": (True, dict(moist_end=3)),
 }
 
 
@@ -60,11 +62,13 @@ def test_config_variant_matches_reference(name, small_case, moist_case, default_
     if not ref_runner.available():
         pytest.skip("oracle/_ref not built")
     moist, cfg = VARIANTS[name]
+    cfg = dict(cfg)
+    moist_end = cfg.pop("moist_end", 1)
     case = copy.copy(moist_case if moist else small_case)
     case["config"] = dict(case["config"], **cfg)
-    res, _ = ref_runner.run_reference(case, nsteps=NSTEPS, dt=DT, dump_steps=[NSTEPS], nthreads=4)
+    res, _ = ref_runner.run_reference(case, nsteps=NSTEPS, dt=DT, dump_steps=[NSTEPS], nthreads=4, moist_end=moist_end)
     ref = res[NSTEPS]
-    dy = Dycore(case, device=0)
+    dy = Dycore(case, device=0, moist_end=moist_end)
     dy.init_diagnostics(DT)
     for it in range(NSTEPS):
         dy.atm_timestep(DT, it + 1)
