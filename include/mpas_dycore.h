@@ -82,7 +82,9 @@ int mpas_dyc_get_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, in
                        void* host, int64_t nbytes);
 /* Size in bytes of a field's Fortran memory image (0 if unknown). */
 int64_t mpas_dyc_field_bytes(const mpas_dyc_ctx* ctx, const char* pool, const char* name);
-/* Raw device pointer of a field (for zero-copy use from torch / RCCL); NULL if unknown. */
+/* Raw device pointer of a field (for zero-copy use from torch / RCCL); NULL if unknown.
+ * Device layout = the Fortran image, except scalars / scalars_tend, which are
+ * scalar-major [num_scalars][n+1][nVertLevels] in HBM (set/get transpose them). */
 void* mpas_dyc_field_device_ptr(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level);
 
 /* atm_init_coupled_diagnostics + atm_compute_solve_diagnostics on time level 1

@@ -33,6 +33,7 @@ struct Field {
   bool is_int;
   Target target;
   int ntl;
+  int nsub = 1;       // > 1: scalar-major [nsub][n+1][inner/nsub] in HBM, Fortran image (nsub, inner/nsub, n+1)
   void* buf[2] = {nullptr, nullptr};
 };
 
@@ -205,6 +206,7 @@ void build_registry(Block& c) {
   add(c, "state", "theta_m", L_CELL, K, 2);
   add(c, "state", "rho_zz", L_CELL, K, 2);
   add(c, "state", "scalars", L_CELL, (int64_t)ns * K, 2);
+  c.fields.back().nsub = ns;
   // diag
   for (const char* n : {"theta", "rho", "rho_base", "theta_base", "rho_p", "rho_p_save", "rho_pp",
                         "rho_zz_old_split", "rtheta_base", "rtheta_p", "rtheta_p_save", "rtheta_pp",
@@ -229,6 +231,7 @@ void build_registry(Block& c) {
   add(c, "tend", "rho_zz", L_CELL, K);
   add(c, "tend", "rt_diabatic_tend", L_CELL, K);
   add(c, "tend", "scalars_tend", L_CELL, (int64_t)ns * K);
+  c.fields.back().nsub = ns;
   add(c, "tend_physics", "rthdynten", L_CELL, K);
   // module scratch (mpas_atm_time_integration.F:35-71)
   for (const char* n : {"qtot", "tend_rtheta_physics", "tend_rho_physics", "delsq_theta", "delsq_w",
@@ -239,6 +242,7 @@ void build_registry(Block& c) {
     add(c, "scratch", n, L_EDGE, K);
   for (const char* n : {"delsq_vorticity", "ke_vertex"}) add(c, "scratch", n, L_VERTEX, K);
   add(c, "scratch", "horiz_flux_array", L_EDGE, (int64_t)ns * K);
+  c.fields.back().nsub = ns;
   add(c, "scratch", "scale_arr", L_CELL, 2 * (int64_t)K);
   add(c, "scratch", "wdtn", L_CELL, K + 1);
 }
@@ -401,29 +405,37 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
           if (!((f.layers >> (layer - 1)) & 1u)) continue;
           const XList* sx = find_list(b, (int)F->loc, layer, MPAS_DYC_SEND, pr.first, pr.second);
           if (!sx || sx->n == 0) continue;
-          XSeg sg{};
-          sg.src = (const double*)F->buf[slot_of(ctx, *F, f.tl)];
-          sg.sidx = sx->d_idx;
-          sg.n = sx->n;
-          sg.inner = (int)F->inner;
+          const XList* rx = nullptr;
+          Field* PF = nullptr;
           if (local) {
             Block& pb = ctx->blk[pr.second];
-            const XList* rx = find_list(pb, (int)F->loc, layer, MPAS_DYC_RECV, ctx->rank, bi);
+            rx = find_list(pb, (int)F->loc, layer, MPAS_DYC_RECV, ctx->rank, bi);
             if (!rx || rx->n != sx->n) {
               ctx->err = "send/recv lists of blocks " + std::to_string(bi) + "->" + std::to_string(pr.second) +
                          " disagree";
               return MPAS_DYC_EINVAL;
             }
-            Field* PF = find(pb, f.pool, f.name);
-            sg.dst = (double*)PF->buf[slot_of(ctx, *PF, f.tl)];
-            sg.didx = rx->d_idx;
-            pre_off.push_back(-1);
-          } else {
-            sg.didx = nullptr;
-            pre_off.push_back(stotal);
-            stotal += (int64_t)sx->n * F->inner;
+            PF = find(pb, f.pool, f.name);
           }
-          pre.push_back(sg);
+          // a scalar-major field moves as nsub fields of inner/nsub doubles
+          const int64_t sub_inner = F->inner / F->nsub;
+          for (int is = 0; is < F->nsub; ++is) {
+            XSeg sg{};
+            sg.src = (const double*)F->buf[slot_of(ctx, *F, f.tl)] + (size_t)is * nloc(b, F->loc) * sub_inner;
+            sg.sidx = sx->d_idx;
+            sg.n = sx->n;
+            sg.inner = (int)sub_inner;
+            if (local) {
+              sg.dst = (double*)PF->buf[slot_of(ctx, *PF, f.tl)] + (size_t)is * nloc(ctx->blk[pr.second], PF->loc) * sub_inner;
+              sg.didx = rx->d_idx;
+              pre_off.push_back(-1);
+            } else {
+              sg.didx = nullptr;
+              pre_off.push_back(stotal);
+              stotal += (int64_t)sx->n * sub_inner;
+            }
+            pre.push_back(sg);
+          }
           pl.maxn_pre = std::max(pl.maxn_pre, sx->n);
         }
       }
@@ -450,15 +462,18 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
             }
             continue;
           }
-          XSeg sg{};
-          sg.sidx = nullptr;
-          sg.dst = (double*)F->buf[slot_of(ctx, *F, f.tl)];
-          sg.didx = rx->d_idx;
-          sg.n = rx->n;
-          sg.inner = (int)F->inner;
-          post.push_back(sg);
-          post_off.push_back(rtotal);
-          rtotal += (int64_t)rx->n * F->inner;
+          const int64_t sub_inner = F->inner / F->nsub;
+          for (int is = 0; is < F->nsub; ++is) {
+            XSeg sg{};
+            sg.sidx = nullptr;
+            sg.dst = (double*)F->buf[slot_of(ctx, *F, f.tl)] + (size_t)is * nloc(b, F->loc) * sub_inner;
+            sg.didx = rx->d_idx;
+            sg.n = rx->n;
+            sg.inner = (int)sub_inner;
+            post.push_back(sg);
+            post_off.push_back(rtotal);
+            rtotal += (int64_t)rx->n * sub_inner;
+          }
           pl.maxn_post = std::max(pl.maxn_post, rx->n);
         }
       }
@@ -542,7 +557,7 @@ void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
   double* dst[10] = {p.ru_save, p.rw_save, p.rtheta_p_save, p.rho_p_save, p.u2,
                      p.w2, p.theta_m2, p.rho_zz2, p.rho_zz_old_split, p.scalars2};
   const int64_t n[10] = {d.nEdges * K, d.nCells * K1, d.nCells * K, d.nCells * K, d.nEdges * K,
-                         d.nCells * K1, d.nCells * K, d.nCells * K, d.nCells * K, d.nCells * K * d.ns};
+                         d.nCells * K1, d.nCells * K, d.nCells * K, d.nCells * K, (d.nCells + 1) * K * d.ns};
   int64_t nmax = 0;
   for (int i = 0; i < 10; ++i) {
     c.src[i] = src[i];
@@ -1020,6 +1035,16 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
     if (f->pool == "mesh" && f->name == "cellsOnEdge") count_active_edges(b, src);
     HIPCHK(hipMemcpyAsync(f->buf[slot], tmp.data(), nb, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+  } else if (f->nsub > 1) {
+    // Fortran (nsub, inner/nsub, n+1) -> scalar-major [nsub][n+1][inner/nsub]
+    const int64_t n = nloc(b, f->loc), ns = f->nsub, m = f->inner / ns;
+    const double* src = (const double*)host;
+    std::vector<double> tmp(n * f->inner);
+    for (int64_t c = 0; c < n; ++c)
+      for (int64_t k = 0; k < m; ++k)
+        for (int64_t s = 0; s < ns; ++s) tmp[(s * n + c) * m + k] = src[(c * m + k) * ns + s];
+    HIPCHK(hipMemcpyAsync(f->buf[slot], tmp.data(), nb, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
   } else {
     HIPCHK(hipMemcpyAsync(f->buf[slot], host, nb, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -1063,6 +1088,17 @@ int mpas_dyc_get_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
     return MPAS_DYC_EINVAL;
   }
   HIPCHK(hipSetDevice(ctx->device));
+  if (f->nsub > 1) {  // scalar-major -> Fortran (nsub, inner/nsub, n+1)
+    const int64_t n = nloc(b, f->loc), ns = f->nsub, m = f->inner / ns;
+    std::vector<double> tmp(n * f->inner);
+    HIPCHK(hipMemcpyAsync(tmp.data(), f->buf[slot_of(ctx, *f, time_level)], nb, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    double* dst = (double*)host;
+    for (int64_t c = 0; c < n; ++c)
+      for (int64_t k = 0; k < m; ++k)
+        for (int64_t s = 0; s < ns; ++s) dst[(c * m + k) * ns + s] = tmp[(s * n + c) * m + k];
+    return MPAS_DYC_OK;
+  }
   HIPCHK(hipMemcpyAsync(host, f->buf[slot_of(ctx, *f, time_level)], nb, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   if (f->is_int && f->target != T_NONE) {

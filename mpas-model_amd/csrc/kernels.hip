@@ -41,6 +41,12 @@ __device__ __forceinline__ int wave_elem(int start) {
 }
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Scalar arrays are scalar-major in HBM: scalars / scalars_tend as [ns][nCells+1][K],
+// horiz_flux_array as [ns][nEdges+1][K], so every per-scalar access is a contiguous
+// column (the Fortran image (ns, K, n+1) is transposed at the C ABI).
+#define SIX(c, k, is) (((size_t)(is) * (size_t)(d.nCells + 1) + (size_t)(c)) * (size_t)K + (size_t)(k))
+#define HIX(e, k, is) (((size_t)(is) * (size_t)(d.nEdges + 1) + (size_t)(e)) * (size_t)K + (size_t)(k))
+
 // per-cell edge terms kept in registers up to this many edges (hexagons and pentagons);
 // larger cells take the plain loop
 constexpr int MAX_EDGES_UNROLL = 6;
@@ -86,8 +92,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_moist_cells(Dims d, Ptrs p) {
   const bool act = k < K;
   double q = 0.0;
   if (act) {
-    const double* s = p.scalars2 + ((size_t)c * K + k) * d.ns;
-    for (int iq = d.moist_start; iq <= d.moist_end; ++iq) q = q + s[iq];
+    for (int iq = d.moist_start; iq <= d.moist_end; ++iq) q = q + p.scalars2[SIX(c, k, iq)];
     p.qtot[(size_t)c * K + k] = q;
   }
   double qm = up1(q);
@@ -104,10 +109,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_moist_edges(Dims d, Ptrs p) {
   if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
   const int k = lane_id(), K = d.K;
   if (k >= K) return;
-  const double* s1 = p.scalars2 + ((size_t)c1 * K + k) * d.ns;
-  const double* s2 = p.scalars2 + ((size_t)c2 * K + k) * d.ns;
   double qtotal = 0.0;
-  for (int iq = d.moist_start; iq <= d.moist_end; ++iq) qtotal = qtotal + 0.5 * (s1[iq] + s2[iq]);
+  for (int iq = d.moist_start; iq <= d.moist_end; ++iq)
+    qtotal = qtotal + 0.5 * (p.scalars2[SIX(c1, k, iq)] + p.scalars2[SIX(c2, k, iq)]);
   p.cqu[(size_t)e * K + k] = 1.0 / (1.0 + qtotal);
 }
 
@@ -1044,7 +1048,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_init_coupled_a(Dims d, Ptrs p
   const int k = lane_id(), K = d.K;
   if (k >= K) return;
   const size_t o = (size_t)c * K + k;
-  p.theta_m1[o] = p.theta[o] * (1. + RVORD * p.scalars1[o * d.ns + index_qv]);
+  p.theta_m1[o] = p.theta[o] * (1. + RVORD * p.scalars1[SIX(c, k, index_qv)]);
   p.rho_zz1[o] = p.rho[o] / p.zz[o];
 }
 // edges: ru (5918-5924)
@@ -1156,7 +1160,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_edges(Dims d, Ptrs p)
   const double uh = p.ruAvg[(size_t)e * K + k];
   const double sg = sgn1(uh);
   const int na = p.nAdvCellsForEdge[e];
-  double* hf = p.horiz_flux_array + ((size_t)e * K + k) * ns;
   if (na == 10) {
     // unrolled hexagon form (3363-3390): sum of ten products, left to right
     double w[10];
@@ -1167,17 +1170,20 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_edges(Dims d, Ptrs p)
       ica[j] = uni(p.advCellsForEdge[e * 15 + j]);
     }
     for (int is = 0; is < ns; ++is) {
-      double acc = w[0] * p.scalars2[((size_t)ica[0] * K + k) * ns + is];
+      double acc = w[0] * p.scalars2[SIX(ica[0], k, is)];
 #pragma unroll
-      for (int j = 1; j < 10; ++j) acc = acc + w[j] * p.scalars2[((size_t)ica[j] * K + k) * ns + is];
-      hf[is] = acc;
+      for (int j = 1; j < 10; ++j) acc = acc + w[j] * p.scalars2[SIX(ica[j], k, is)];
+      p.horiz_flux_array[HIX(e, k, is)] = acc;
     }
   } else {
-    for (int is = 0; is < ns; ++is) hf[is] = 0.0;
-    for (int j = 0; j < na; ++j) {
-      const int ic = uni(p.advCellsForEdge[e * 15 + j]);
-      const double scalar_weight = p.adv_coefs[e * 15 + j] + sg * p.adv_coefs_3rd[e * 15 + j];
-      for (int is = 0; is < ns; ++is) hf[is] = hf[is] + scalar_weight * p.scalars2[((size_t)ic * K + k) * ns + is];
+    for (int is = 0; is < ns; ++is) {
+      double acc = 0.0;
+      for (int j = 0; j < na; ++j) {
+        const int ic = uni(p.advCellsForEdge[e * 15 + j]);
+        const double scalar_weight = p.adv_coefs[e * 15 + j] + sg * p.adv_coefs_3rd[e * 15 + j];
+        acc = acc + scalar_weight * p.scalars2[SIX(ic, k, is)];
+      }
+      p.horiz_flux_array[HIX(e, k, is)] = acc;
     }
   }
 }
@@ -1199,27 +1205,48 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_cells(Dims d, Ptrs p,
   const double rdnw = act ? p.rdzw[k] : 0.0;
   const double rzo = LD(p.rho_zz1, o), rzn = LD(p.rho_zz2, o);
   const double rho_zz_new_inv = act ? 1.0 / (wt_old * rzo + wt_new * rzn) : 0.0;
+  // edgesOnCell_sign * uhAvg of every edge, loaded once for all scalars
+  double sru[MAX_EDGES_UNROLL];
+  int eid[MAX_EDGES_UNROLL];
+  const bool reg = ne <= MAX_EDGES_UNROLL;
+  if (reg) {
+#pragma unroll
+    for (int i = 0; i < MAX_EDGES_UNROLL; ++i) {
+      eid[i] = 0;
+      sru[i] = 0.0;
+      if (i < ne) {
+        eid[i] = uni(p.edgesOnCell[c * d.maxEdges + i]);
+        if (act) sru[i] = p.edgesOnCell_sign[c * d.maxEdges + i] * p.ruAvg[(size_t)eid[i] * K + k];
+      }
+    }
+  }
   for (int is = 0; is < ns; ++is) {
     double stc = 0.0;
-    for (int i = 0; i < ne; ++i) {
-      const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
-      if (act)
-        stc = stc - p.edgesOnCell_sign[c * d.maxEdges + i] * p.ruAvg[(size_t)e * K + k] *
-                        p.horiz_flux_array[((size_t)e * K + k) * ns + is];
+    if (reg) {
+#pragma unroll
+      for (int i = 0; i < MAX_EDGES_UNROLL; ++i)
+        if (i < ne && act) stc = stc - sru[i] * p.horiz_flux_array[HIX(eid[i], k, is)];
+    } else {
+      for (int i = 0; i < ne; ++i) {
+        const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+        if (act)
+          stc = stc - p.edgesOnCell_sign[c * d.maxEdges + i] * p.ruAvg[(size_t)e * K + k] *
+                          p.horiz_flux_array[HIX(e, k, is)];
+      }
     }
     if (act) {
-      p.scalars_tend[o * ns + is] = 0.0;  // no physics: scalar_tend_save zeroed (3437-3439)
+      p.scalars_tend[SIX(c, k, is)] = 0.0;  // no physics: scalar_tend_save zeroed (3437-3439)
       stc = stc * invA + 0.0;
     }
-    const double sn = LD(p.scalars2, o * ns + is);
+    const double sn = LD(p.scalars2, SIX(c, k, is));
     const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
     double wdtn = 0.0;
     if (k == 1 || k == K - 1) wdtn = wwa * (fnm * sn + fnp * snm1);
     else if (k >= 2 && k <= K - 2) wdtn = flux3(snm2, snm1, sn, snp1, wwa, coef_3rd_order);
     const double wdtn_p = dn1(wdtn);
     if (act) {
-      const double so = p.scalars1[o * ns + is];
-      p.scalars2[o * ns + is] = (so * rzo + dt * (stc - rdnw * (wdtn_p - wdtn))) * rho_zz_new_inv;
+      const double so = p.scalars1[SIX(c, k, is)];
+      p.scalars2[SIX(c, k, is)] = (so * rzo + dt * (stc - rdnw * (wdtn_p - wdtn))) * rho_zz_new_inv;
     }
   }
 }
@@ -1242,9 +1269,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_prep(Dims d, Ptrs p, dou
   if (act) {
     const double rzo = p.rho_zz1[o];
     for (int is = 0; is < ns; ++is) {
-      p.scalars_tend[o * ns + is] = 0.0;
-      p.scalars1[o * ns + is] = p.scalars1[o * ns + is] + dt * p.scalars_tend[o * ns + is] / rzo;
-      p.scalars_tend[o * ns + is] = 0.0;
+      const size_t so = SIX(c, k, is);
+      p.scalars_tend[so] = 0.0;
+      p.scalars1[so] = p.scalars1[so] + dt * p.scalars_tend[so] / rzo;
+      p.scalars_tend[so] = 0.0;
     }
   }
   if (advance_density) {
@@ -1268,9 +1296,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds(Dims d, Ptrs p, i
   const bool act = k < K;
   const size_t K1 = K + 1;
   const size_t o = (size_t)c * K + k;
-  auto sold = [&](int cc) -> double { return (cc < d.nCells) ? p.scalars1[((size_t)cc * K + k) * ns + is] : 0.0; };
+  auto sold = [&](int cc) -> double { return (cc < d.nCells) ? p.scalars1[SIX(cc, k, is)] : 0.0; };
   const double so = act ? sold(c) : 0.0;
-  const double sn = LD(p.scalars2, o * ns + is);
+  const double sn = LD(p.scalars2, SIX(c, k, is));
   const double som = up1(so), sop = dn1(so);
   const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
   const double wwa = (k <= K) ? p.wwAvg[(size_t)c * K1 + k] : 0.0;
@@ -1310,8 +1338,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_edges1(Dims d, Ptrs p, i
   if (k >= K) return;
   const size_t o = (size_t)e * K + k;
   const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
-  auto snew = [&](int cc) -> double { return (cc < d.nCells) ? p.scalars2[((size_t)cc * K + k) * ns + is] : 0.0; };
-  auto sold = [&](int cc) -> double { return (cc < d.nCells) ? p.scalars1[((size_t)cc * K + k) * ns + is] : 0.0; };
+  auto snew = [&](int cc) -> double { return (cc < d.nCells) ? p.scalars2[SIX(cc, k, is)] : 0.0; };
+  auto sold = [&](int cc) -> double { return (cc < d.nCells) ? p.scalars1[SIX(cc, k, is)] : 0.0; };
   const double uh = p.ruAvg[o];
   double fa = 0.0;
   if (c1 < d.nCellsSolve || c2 < d.nCellsSolve) {
@@ -1350,7 +1378,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1(Dims d, Ptrs p, i
   const size_t K1 = K + 1;
   const size_t o = (size_t)c * K + k, ow = (size_t)c * K1 + k;
   const double eps = 1.e-20;
-  const double so = LD(p.scalars1, o * ns + is), som = up1(so);
+  const double so = LD(p.scalars1, SIX(c, k, is)), som = up1(so);
   const double rzo = LD(p.rho_zz1, o);
   const double wwa = (k <= K) ? p.wwAvg[ow] : 0.0;
   const double rdnw = act ? p.rdzw[k] : 0.0;
@@ -1418,7 +1446,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2(Dims d, Ptrs p, i
   const size_t K1 = K + 1;
   const size_t o = (size_t)c * K + k, ow = (size_t)c * K1 + k;
   if (c >= d.nCellsSolve) {  // halo cells: scalars_new = max(0, scalar_new) with scalar_new = input copy
-    if (act) p.scalars2[o * ns + is] = fmax(0.0, p.scalars2[o * ns + is]);
+    if (act) p.scalars2[SIX(c, k, is)] = fmax(0.0, p.scalars2[SIX(c, k, is)]);
     return;
   }
   const double si = act ? p.scale_arr[((size_t)c * 2 + 0) * K + k] : 0.0;
@@ -1440,7 +1468,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2(Dims d, Ptrs p, i
   }
   const double rhoref = advance_density ? p.rho_zz_int[o] : p.rho_zz2[o];
   snew = (snew + (-p.rdzw[k] * (wdp - wd))) / rhoref;
-  p.scalars2[o * ns + is] = fmax(0.0, snew);
+  p.scalars2[SIX(c, k, is)] = fmax(0.0, snew);
 }
 
 }  // namespace mpas
