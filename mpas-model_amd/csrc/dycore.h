@@ -58,6 +58,7 @@ struct Ptrs {
   const double *adv_coefs, *adv_coefs_3rd, *defc_a, *defc_b;
   const double *zgrid, *zz, *zxu, *dss, *zb_cell, *zb3_cell;
   const double *u_init, *v_init, *t_init, *angleEdge;
+  const double *latCell, *lonCell, *coeffs_reconstruct;
   double cf1, cf2, cf3;
   // ---- state, two time levels resolved per launch
   double *u1, *u2, *w1, *w2, *theta_m1, *theta_m2, *rho_zz1, *rho_zz2, *scalars1, *scalars2;
@@ -69,6 +70,7 @@ struct Ptrs {
   double *rw, *rw_p, *rw_save, *wwAvg, *wwAvg_split;
   double *ru, *ruAvg, *ruAvg_split, *ru_p, *ru_save, *cqu, *rho_edge, *v, *pv_edge, *gradPVn, *gradPVt;
   double *vorticity, *pv_vertex;
+  double *uReconstructX, *uReconstructY, *uReconstructZ, *uReconstructZonal, *uReconstructMeridional;
   // ---- tend / tend_physics
   double *tend_u, *tend_u_euler, *tend_w, *tend_w_euler, *tend_theta, *tend_theta_euler;
   double *tend_rho, *rt_diabatic_tend, *scalars_tend, *rthdynten;

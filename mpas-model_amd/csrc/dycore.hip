@@ -181,7 +181,8 @@ void build_registry(Block& c) {
   for (const char* n : {"dcEdge", "dvEdge", "invDcEdge", "invDvEdge", "fEdge", "meshScalingDel2",
                         "meshScalingDel4", "specZoneMaskEdge", "angleEdge"})
     add(c, "mesh", n, L_EDGE, 1);
-  for (const char* n : {"invAreaCell", "specZoneMaskCell"}) add(c, "mesh", n, L_CELL, 1);
+  for (const char* n : {"invAreaCell", "specZoneMaskCell", "latCell", "lonCell"}) add(c, "mesh", n, L_CELL, 1);
+  add(c, "mesh", "coeffs_reconstruct", L_CELL, 3 * (int64_t)ME);
   for (const char* n : {"invAreaTriangle", "fVertex"}) add(c, "mesh", n, L_VERTEX, 1);
   for (const char* n : {"fzm", "fzp", "rdzw", "rdzu", "u_init", "v_init"}) add(c, "mesh", n, L_NONE, K);
   for (const char* n : {"cf1", "cf2", "cf3"}) add(c, "mesh", n, L_NONE, 1);
@@ -221,6 +222,9 @@ void build_registry(Block& c) {
                         "gradPVn", "gradPVt"})
     add(c, "diag", n, L_EDGE, K);
   for (const char* n : {"vorticity", "pv_vertex"}) add(c, "diag", n, L_VERTEX, K);
+  for (const char* n : {"uReconstructX", "uReconstructY", "uReconstructZ", "uReconstructZonal",
+                        "uReconstructMeridional"})
+    add(c, "diag", n, L_CELL, K);
   // tend / tend_physics
   add(c, "tend", "u", L_EDGE, K);
   add(c, "tend", "u_euler", L_EDGE, K);
@@ -281,6 +285,8 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   MR(adv_coefs); MR(adv_coefs_3rd); MR(defc_a); MR(defc_b);
   MR(zgrid); MR(zz); MR(zxu); MR(dss); MR(zb_cell); MR(zb3_cell);
   MR(u_init); MR(v_init); MR(t_init); MR(angleEdge);
+  MR(latCell); MR(lonCell); MR(coeffs_reconstruct);
+  DG(uReconstructX); DG(uReconstructY); DG(uReconstructZ); DG(uReconstructZonal); DG(uReconstructMeridional);
   p.u1 = P<double>(c, b, "state", "u", 1); p.u2 = P<double>(c, b, "state", "u", 2);
   p.w1 = P<double>(c, b, "state", "w", 1); p.w2 = P<double>(c, b, "state", "w", 2);
   p.theta_m1 = P<double>(c, b, "state", "theta_m", 1); p.theta_m2 = P<double>(c, b, "state", "theta_m", 2);
@@ -777,8 +783,8 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       if (rk_step < 3) CHK(exchange(ctx, {{"state", "scalars", 2, ALL_LAYERS}}));  // 1569-1572
     }
   }
-  // mpas_reconstruct (1581-1603) produces output-only diagnostics (uReconstruct*);
-  // summarize_timestep (1794) only logs: both outside the hot path.
+  EACH(LAUNCH(k_reconstruct, d.nCellsSolve, d, p, p.u2));          // mpas_reconstruct (1581-1603)
+  // summarize_timestep (1794) only logs: outside the hot path.
   return MPAS_DYC_OK;
 }
 
@@ -790,6 +796,7 @@ int init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
   EACH(LAUNCH(k_init_coupled_b, d.nEdges, d, p));
   EACH(LAUNCH(k_init_coupled_c, d.nCells, d, p));
   EACH(solve_diagnostics(ctx, d, p, dt, 1, 0));
+  EACH(LAUNCH(k_reconstruct, d.nCellsSolve, d, p, p.u1));          // mpas_atm_core.F:411-421
   CHK(exchange(ctx, {{"diag", "pv_edge", 0, ALL_LAYERS}, {"diag", "ru", 0, ALL_LAYERS},  // 180-186
                      {"diag", "rw", 0, ALL_LAYERS}}));
   return MPAS_DYC_OK;

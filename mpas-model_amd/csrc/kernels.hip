@@ -1471,4 +1471,34 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2(Dims d, Ptrs p, i
   p.scalars2[SIX(c, k, is)] = fmax(0.0, snew);
 }
 
+// ============================================================================
+// mpas_reconstruct_2d  (operators/mpas_vector_reconstruction.F:245-294), owned cells:
+// cell-centre velocity from the edge normals with the precomputed RBF weights
+// coeffs_reconstruct(R3, maxEdges, nCells), then its zonal / meridional components.
+// ============================================================================
+__global__ __launch_bounds__(BLOCK_THREADS) void k_reconstruct(Dims d, Ptrs p, const double* __restrict__ u) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  double x = 0.0, y = 0.0, z = 0.0;
+  const int ne = p.nEdgesOnCell[c];
+  for (int i = 0; i < ne; ++i) {
+    const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
+    const double* cf = p.coeffs_reconstruct + ((size_t)c * d.maxEdges + i) * 3;
+    const double ue = u[(size_t)e * K + k];
+    x = x + cf[0] * ue;
+    y = y + cf[1] * ue;
+    z = z + cf[2] * ue;
+  }
+  const size_t o = (size_t)c * K + k;
+  p.uReconstructX[o] = x;
+  p.uReconstructY[o] = y;
+  p.uReconstructZ[o] = z;
+  const double clat = cos(p.latCell[c]), slat = sin(p.latCell[c]);
+  const double clon = cos(p.lonCell[c]), slon = sin(p.lonCell[c]);
+  p.uReconstructZonal[o] = -x * slon + y * clon;
+  p.uReconstructMeridional[o] = -(x * clon + y * slon) * slat + z * clat;
+}
+
 }  // namespace mpas

@@ -35,7 +35,7 @@ def jw_len_disp(level: int) -> float:
 def jw_case(ncells: int, K: int = 56, ns: int = 1, moist: bool = False, order: int = 2,
             lloyd_iters: int = 20, cache: bool = True) -> dict:
     level = level_for(ncells)
-    key = f"jw_l{level}_K{K}_ns{ns}_m{int(moist)}_o{order}_ll{lloyd_iters}"
+    key = f"jw_l{level}_K{K}_ns{ns}_m{int(moist)}_o{order}_ll{lloyd_iters}_v2"
     path = os.path.join(CACHE, key + ".pkl")
     if cache and os.path.isfile(path):
         with open(path, "rb") as f:  # our own cache file, written below

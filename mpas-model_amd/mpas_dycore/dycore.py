@@ -24,7 +24,7 @@ from .layout import LOC_N, to_fortran
 STATE_INPUTS = ("u", "w", "scalars")
 DIAG_INPUTS = ("theta", "rho", "rho_base", "theta_base")
 _SKIP = set(STATE_INPUTS) | set(DIAG_INPUTS) | {"xCell", "yCell", "zCell", "xEdge", "yEdge", "zEdge", "xVertex",
-                                                "yVertex", "zVertex", "latCell", "lonCell", "latEdge", "lonEdge",
+                                                "yVertex", "zVertex", "latEdge", "lonEdge",
                                                 "latVertex", "lonVertex", "areaCell", "areaTriangle",
                                                 "meshDensity", "indexToCellID", "deriv_two", "zb", "zb3"}
 
@@ -207,7 +207,8 @@ for _n in ("theta_m", "rho_zz", "rho_p", "rtheta_p", "exner", "pressure_p", "kdi
            "wwAvg", "cqw", "h_divergence", "pv_cell", "rho_pp", "rtheta_pp", "rw_p", "exner_base", "pressure_base",
            "rtheta_base", "coftz", "cofwz", "cofwr", "cofwt", "a_tri", "alpha_tri", "gamma_tri", "rw_save",
            "tend_rtheta_adv", "rho_p_save", "rtheta_p_save", "rho_zz_old_split", "rtheta_pp_old", "wwAvg_split",
-           "scalars_tend", "rthdynten", "rt_diabatic_tend", "theta_euler", "w_euler"):
+           "scalars_tend", "rthdynten", "rt_diabatic_tend", "theta_euler", "w_euler", "uReconstructX",
+           "uReconstructY", "uReconstructZ", "uReconstructZonal", "uReconstructMeridional"):
     _LOCS[_n] = "cell"
 for _n in ("ru", "ruAvg", "ru_p", "ru_save", "cqu", "rho_edge", "v", "pv_edge", "gradPVn", "gradPVt",
            "ruAvg_split", "u_euler"):

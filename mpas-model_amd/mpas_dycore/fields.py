@@ -12,7 +12,7 @@ from __future__ import annotations
 LOCATION = {}
 for n in ("latCell lonCell xCell yCell zCell areaCell invAreaCell meshDensity nEdgesOnCell indexToCellID "
           "edgesOnCell cellsOnCell verticesOnCell kiteForCell edgesOnCell_sign defc_a defc_b zgrid zz dss "
-          "zb_cell zb3_cell theta rho scalars rho_base theta_base w").split():
+          "zb_cell zb3_cell theta rho scalars rho_base theta_base w coeffs_reconstruct").split():
     LOCATION[n] = "cell"
 for n in ("latEdge lonEdge xEdge yEdge zEdge dcEdge dvEdge invDcEdge invDvEdge angleEdge fEdge "
           "meshScalingDel2 meshScalingDel4 nEdgesOnEdge nAdvCellsForEdge cellsOnEdge verticesOnEdge "

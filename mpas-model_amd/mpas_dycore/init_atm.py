@@ -28,6 +28,8 @@ import os
 
 import numpy as np
 
+from .reconstruct import init_reconstruct
+
 from .mesh import _normalize, arc_length
 
 # mpas_constants.F:25-36 (all promoted to double by -fdefault-real-8)
@@ -409,6 +411,8 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
         # state (time level 1) and diag inputs of atm_init_coupled_diagnostics
         u=u, w=w, theta=theta, rho=rho, scalars=scalars, rho_base=rb, theta_base=tb,
     )
+    # model-init precompute of the velocity reconstruction (mpas_atm_core.F:408-409)
+    out["coeffs_reconstruct"] = init_reconstruct(out)
     return out
 
 

@@ -14,6 +14,9 @@ from conftest import rel_linf
 pytestmark = pytest.mark.gpu
 
 DT = 2880.0  # x1.642 (~960 km): SURVEY.md §8d scales dt with resolution (2562 -> 2880 s)
+# mpas_reconstruct outputs (cos/sin of lat/lon come from the device math library)
+RECON = [("diag", n, "diag." + n) for n in ("uReconstructX", "uReconstructY", "uReconstructZ", "uReconstructZonal",
+                                             "uReconstructMeridional")]
 PROG = [("state", "u", "state.u.tl1"), ("state", "theta_m", "state.theta_m.tl1"),
         ("state", "rho_zz", "state.rho_zz.tl1"), ("state", "w", "state.w.tl1")]
 
@@ -37,11 +40,12 @@ def ref_run(small_case):
 def test_init_diagnostics_match_reference(small_case, ref_run):
     dy = _dycore(small_case)
     ref = ref_run[0]
-    for pool, name, key in PROG + [("diag", "exner", "diag.exner"), ("diag", "pressure_p", "diag.pressure_p"),
+    for pool, name, key in (PROG + [("diag", "exner", "diag.exner"), ("diag", "pressure_p", "diag.pressure_p"),
                                    ("diag", "ru", "diag.ru"), ("diag", "rw", "diag.rw"),
                                    ("diag", "pv_edge", "diag.pv_edge"), ("diag", "ke", "diag.ke"),
                                    ("diag", "v", "diag.v"), ("diag", "rho_edge", "diag.rho_edge"),
-                                   ("diag", "divergence", "diag.divergence"), ("diag", "vorticity", "diag.vorticity")]:
+                                   ("diag", "divergence", "diag.divergence"), ("diag", "vorticity", "diag.vorticity")]
+                                  + RECON):
         got = dy.get(pool, name, 1)
         err = rel_linf(got, ref[key])
         assert err <= 1e-13, f"{key}: rel Linf {err:.3e}"
@@ -57,10 +61,13 @@ def test_timestep_matches_reference(small_case, ref_run, nsteps, tol, wtol):
     dy.synchronize()
     ref = ref_run[nsteps]
     errs = {}
-    for pool, name, key in PROG + [("state", "scalars", "state.scalars.tl1")]:
+    for pool, name, key in PROG + [("state", "scalars", "state.scalars.tl1")] + RECON:
         got = dy.get(pool, name, 1)
         errs[key] = rel_linf(got.reshape(ref[key].shape), ref[key])
-    bad = {k: v for k, v in errs.items() if not v <= (wtol if k == "state.w.tl1" else tol)}
+    # w and the reconstructed Z / meridional components are small for the zonal JW flow, so
+    # their error relative to their own (small) maximum is looser by construction
+    loose = {"state.w.tl1"} | {k for _, _, k in RECON}
+    bad = {k: v for k, v in errs.items() if not v <= (wtol if k in loose else tol)}
     assert not bad, f"rel Linf above {tol}: {bad} (all: {errs})"
 
 

@@ -13,7 +13,11 @@ inputs/outputs as compressed npz (data only -- no reference source).
       moist JW + two tracer blobs (num_scalars=3): reference prognostics after 1 and
       10 atm_timestep calls (u, w, theta_m, rho_zz, scalars) and an input checksum.
 
-Usage: python tools/make_golden.py   (needs oracle/_ref built; run in the build container)
+  tests/golden/reconstruct_x1.642.npz
+      mpas_rbf_interp_initialize + mpas_init_reconstruct outputs (edgeNormalVectors,
+      cellTangentPlane, coeffs_reconstruct) on x1.642.
+
+Usage: python tools/make_golden.py [acoustic|srk3|reconstruct ...]   (needs oracle/_ref built)
 """
 from __future__ import annotations
 
@@ -87,10 +91,28 @@ def srk3_fixture():
     np.savez_compressed(os.path.join(GOLD, "srk3_x1.642_K26_ns3.npz"), **out)
 
 
+def reconstruct_fixture():
+    """mpas_rbf_interp_initialize + mpas_init_reconstruct outputs of the reference on x1.642."""
+    case = jw_case(642, K=8, ns=1, cache=False)
+    res, _ = ref_runner.run_reference(case, nsteps=1, dt=case["dt"], dump_steps=[0], nthreads=2)
+    r0 = res[0]
+    nC, nE, ME = case["nCells"], case["nEdges"], case["maxEdges"]
+    np.savez_compressed(os.path.join(GOLD, "reconstruct_x1.642.npz"),
+                        checksum=case_checksum(case),
+                        coeffs_reconstruct=r0["mesh.coeffs_reconstruct"].reshape(nC + 1, ME, 3)[:-1],
+                        edgeNormalVectors=r0["mesh.edgeNormalVectors"].reshape(nE + 1, 3)[:-1],
+                        cellTangentPlane=r0["mesh.cellTangentPlane"].reshape(nC + 1, 2, 3)[:-1])
+
+
 if __name__ == "__main__":
     if not ref_runner.available():
         sys.exit("build the oracle first: make -C oracle")
-    acoustic_fixture()
-    srk3_fixture()
+    only = sys.argv[1:]
+    if not only or "acoustic" in only:
+        acoustic_fixture()
+    if not only or "srk3" in only:
+        srk3_fixture()
+    if not only or "reconstruct" in only:
+        reconstruct_fixture()
     for f in sorted(os.listdir(GOLD)):
         print(f, os.path.getsize(os.path.join(GOLD, f)))
