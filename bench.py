@@ -72,6 +72,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--acoustic-reps", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=1, help="blocks per GPU (MPAS blocks with halos)")
+    ap.add_argument("--rccl-local", action="store_true", help="route in-process block exchanges through RCCL")
     args = ap.parse_args()
 
     world, rank, local = _dist()
@@ -106,13 +107,16 @@ def main():
     if nparts > 1:
         blocks, placement = decomp.rank_blocks(case, world, rank, args.blocks)
         comm_id = None
-        if world > 1:
+        # --rccl-local: blocks of this process also exchange through RCCL (send to self), to
+        # measure the cost of the RCCL path on one GPU
+        if world > 1 or args.rccl_local:
             obj = [Dycore.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
+            if dist:
+                dist.broadcast_object_list(obj, src=0)
             comm_id = obj[0]
         torch.cuda.set_device(device)
         dy = Dycore.from_blocks(blocks, device=device, placement=placement, rank=rank, nranks=world,
-                                comm_id=comm_id, moist_end=moist_end)
+                                comm_id=comm_id, moist_end=moist_end, rccl_local=args.rccl_local)
         owned = sum(b.solve[0] for b in blocks)
         halo = sum(b.case["nCells"] - b.solve[0] for b in blocks)
     else:

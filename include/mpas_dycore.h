@@ -138,6 +138,10 @@ int mpas_dyc_comm_unique_id(void* id, int64_t nbytes);
 int mpas_dyc_comm_init(mpas_dyc_ctx* ctx, const void* id, int64_t nbytes, int32_t nranks, int32_t rank);
 /* Test hook: route block-to-block exchanges inside this process through RCCL (send to self). */
 int mpas_dyc_set_transport(mpas_dyc_ctx* ctx, int32_t rccl_for_local_blocks);
+/* Split-phase exchanges: at the tend_u, rho_pp and rtheta_pp exchanges the interior
+ * elements are computed while the halo traffic runs on a second stream.  on = 1 / 0;
+ * -1 (default) = automatic: on when exchanges go through RCCL (more than one rank). */
+int mpas_dyc_set_overlap(mpas_dyc_ctx* ctx, int32_t on);
 /* mpas_dmpar_exch_halo_field(field, haloLayers) for one field; layer_mask bit l-1 = layer l. */
 int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level,
                            int32_t layer_mask);

@@ -81,6 +81,7 @@ struct Ptrs {
   double *s_max, *s_min, *scale_arr, *flux_arr, *flux_upwind_tmp, *flux_tmp, *wdtn, *rho_zz_int;
   double *scalar_old_copy;
   double *advflux_w, *advflux_th;  // edge values of w / theta_m for horizontal advection
+  const int *edge_bnd, *cell_bnd;  // 1 = reads halo data (edge: a halo cell; owned cell: a halo edge)
 };
 
 }  // namespace mpas

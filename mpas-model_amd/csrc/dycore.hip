@@ -53,6 +53,7 @@ struct Block {
   std::map<std::string, int> by_name;  // "pool.name"
   std::vector<XList> xl;
   int64_t nEdges_act = -1;             // edges with an owned cell (from cellsOnEdge), for B_ac
+  std::vector<int32_t> h_coe, h_eoc, h_noc;  // host copies (0-based) for the halo-boundary flags
 };
 
 // One RCCL message of an exchange point: a contiguous range of the process-wide send or receive buffer.
@@ -103,6 +104,12 @@ struct mpas_dyc_ctx {
   bool planning = false;                // dry run: build exchange plans, launch nothing
   bool planned[2] = {false, false};
   std::map<std::string, XPlan> plans;
+  // split-phase exchanges: packs, RCCL and unpacks run on the exchange stream while the
+  // compute stream works on elements that read no halo data
+  hipStream_t xstream = nullptr;
+  hipEvent_t xfork = nullptr, xjoin = nullptr;
+  int overlap = -1;                     // 1 on, 0 off, -1 auto: on when exchanges go through RCCL
+  bool bnd_ready = false;
 };
 
 namespace {
@@ -249,6 +256,8 @@ void build_registry(Block& c) {
   c.fields.back().nsub = ns;
   add(c, "scratch", "scale_arr", L_CELL, 2 * (int64_t)K);
   add(c, "scratch", "wdtn", L_CELL, K + 1);
+  add(c, "scratch", "edge_bnd", L_EDGE, 1, 1, true);
+  add(c, "scratch", "cell_bnd", L_CELL, 1, 1, true);
 }
 
 Field* find(Block& b, const char* pool, const char* name) {
@@ -311,6 +320,8 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   SC(s_max); SC(s_min); SC(scale_arr); SC(flux_arr); SC(flux_upwind_tmp); SC(flux_tmp); SC(wdtn); SC(rho_zz_int);
   SC(scalar_old_copy);
   SC(advflux_w); SC(advflux_th);
+  p.edge_bnd = P<const int>(c, b, "scratch", "edge_bnd");
+  p.cell_bnd = P<const int>(c, b, "scratch", "cell_bnd");
   // 0-d mesh fields are mirrored on the host
   p.cf1 = b.fields[b.by_name["mesh.cf1"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf1"]].buf[1] : 0.0;
   p.cf2 = b.fields[b.by_name["mesh.cf2"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf2"]].buf[1] : 0.0;
@@ -552,6 +563,61 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   return MPAS_DYC_OK;
 }
 
+// Halo-boundary flags of the split-phase exchanges: an edge is "boundary" when one of its
+// cells is a halo cell (it reads exchanged cell data); an owned cell is "boundary" when
+// one of its edges is a halo edge (it reads exchanged edge data).
+int compute_bnd(mpas_dyc_ctx* ctx) {
+  for (auto& b : ctx->blk) {
+    const Dims& d = b.d;
+    if ((int64_t)b.h_coe.size() < 2LL * d.nEdges || (int64_t)b.h_eoc.size() < (int64_t)d.maxEdges * d.nCells ||
+        (int64_t)b.h_noc.size() < d.nCells) {
+      ctx->err = "mesh connectivity (cellsOnEdge, edgesOnCell, nEdgesOnCell) not set";
+      return MPAS_DYC_ESTATE;
+    }
+    std::vector<int32_t> eb(d.nEdges + 1, 1), cb(d.nCells + 1, 1);
+    for (int e = 0; e < d.nEdges; ++e)
+      eb[e] = (b.h_coe[2 * e] >= d.nCellsSolve || b.h_coe[2 * e + 1] >= d.nCellsSolve) ? 1 : 0;
+    for (int c = 0; c < d.nCells; ++c) {
+      int bnd = 0;
+      for (int i = 0; i < b.h_noc[c]; ++i) bnd |= b.h_eoc[(size_t)c * d.maxEdges + i] >= d.nEdgesSolve;
+      cb[c] = bnd;
+    }
+    HIPCHK(hipMemcpy(find(b, "scratch", "edge_bnd")->buf[0], eb.data(), eb.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(find(b, "scratch", "cell_bnd")->buf[0], cb.data(), cb.size() * 4, hipMemcpyHostToDevice));
+  }
+  ctx->bnd_ready = true;
+  return MPAS_DYC_OK;
+}
+
+// Auto mode splits only when halo traffic goes through RCCL: block-to-block copies inside
+// one GPU are a single short kernel, and splitting them only adds launches.
+bool split_phase(const mpas_dyc_ctx* ctx) {
+  if (!needs_exchange(ctx)) return false;
+  if (ctx->overlap >= 0) return ctx->overlap != 0;
+  return ctx->nranks > 1 || ctx->rccl_local;
+}
+
+// First half of a split-phase exchange: after everything queued on the compute stream,
+// the exchange stream packs, talks RCCL and unpacks; exchange_wait joins it back.
+int exchange_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
+  if (ctx->planning) return exchange(ctx, fs);
+  HIPCHK(hipEventRecord(ctx->xfork, ctx->stream));
+  HIPCHK(hipStreamWaitEvent(ctx->xstream, ctx->xfork, 0));
+  hipStream_t s = ctx->stream;
+  ctx->stream = ctx->xstream;  // exchange() issues on ctx->stream
+  const int r = exchange(ctx, fs);
+  ctx->stream = s;
+  if (r) return r;
+  HIPCHK(hipEventRecord(ctx->xjoin, ctx->xstream));
+  return MPAS_DYC_OK;
+}
+
+int exchange_wait(mpas_dyc_ctx* ctx) {
+  if (ctx->planning) return MPAS_DYC_OK;
+  HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->xjoin, 0));
+  return MPAS_DYC_OK;
+}
+
 // ---------------------------------------------------------------------------
 // reference routines, one host function each (per block)
 // ---------------------------------------------------------------------------
@@ -608,15 +674,18 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
 }
 
-void acoustic_step(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
-  LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step);
+void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int phase) {
+  LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step, phase);
+}
+
+void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
 }
 
-void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
+void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase) {
   const double rdts = 1.0 / dts;
   const double coef_divdamp = 2.0 * ctx->cf.smdiv * ctx->cf.len_disp * rdts;
-  LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp);
+  LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp, phase);
 }
 
 void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt, int tl, int rk_step /*0 = absent*/) {
@@ -721,6 +790,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
     number_sub_steps[2] = nss;
   }
   const bool scalars_in_dynamics = cf.scalar_advection && !cf.split_dynamics_transport;
+  const bool split = split_phase(ctx);
   CHK(exchange(ctx, {{"state", "theta_m", 1, ALL_LAYERS}, {"state", "scalars", 1, ALL_LAYERS},   // 329-338
                      {"diag", "pressure_p", 0, ALL_LAYERS}, {"diag", "rtheta_p", 0, ALL_LAYERS}}));
   EACH(rk_integration_setup(ctx, d, p));                          // 341-381
@@ -734,13 +804,36 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
     for (int rk_step = 1; rk_step <= 3; ++rk_step) {
       if (cf.time_integration_order == 3 && rk_step == 2) EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[1]));
       EACH(dyn_tend(ctx, d, p, rk_step, dt));                     // 561-630
-      CHK(exchange(ctx, {{"tend", "u", 0, 0x1u}}));               // 642
-      EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p));          // 644-678
+      const double dts = rk_sub_timestep[rk_step - 1];
+      if (split) {  // 642 | 644-678: interior cells overlap the tend_u exchange
+        CHK(exchange_async(ctx, {{"tend", "u", 0, 0x1u}}));
+        EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, 1));
+        CHK(exchange_wait(ctx));
+        EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, 2));
+      } else {
+        CHK(exchange(ctx, {{"tend", "u", 0, 0x1u}}));             // 642
+        EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, 0));     // 644-678
+      }
       for (int small_step = 1; small_step <= number_sub_steps[rk_step - 1]; ++small_step) {
-        CHK(exchange(ctx, {{"diag", "rho_pp", 0, 0x1u}}));        // 792
-        EACH(acoustic_step(ctx, d, p, rk_sub_timestep[rk_step - 1], small_step));  // 794-837
-        CHK(exchange(ctx, {{"diag", "rtheta_pp", 0, 0x1u}}));     // 845
-        EACH(divergence_damping(ctx, d, p, rk_sub_timestep[rk_step - 1]));          // 849-869
+        if (split) {  // 792 | 794-837: interior edges overlap the rho_pp exchange
+          CHK(exchange_async(ctx, {{"diag", "rho_pp", 0, 0x1u}}));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1));
+          CHK(exchange_wait(ctx));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 2));
+        } else {
+          CHK(exchange(ctx, {{"diag", "rho_pp", 0, 0x1u}}));      // 792
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 0));    // 794-837
+        }
+        EACH(acoustic_cells(ctx, d, p, dts, small_step));
+        if (split) {  // 845 | 849-869: interior edges overlap the rtheta_pp exchange
+          CHK(exchange_async(ctx, {{"diag", "rtheta_pp", 0, 0x1u}}));
+          EACH(divergence_damping(ctx, d, p, dts, 1));
+          CHK(exchange_wait(ctx));
+          EACH(divergence_damping(ctx, d, p, dts, 2));
+        } else {
+          CHK(exchange(ctx, {{"diag", "rtheta_pp", 0, 0x1u}}));   // 845
+          EACH(divergence_damping(ctx, d, p, dts, 0));            // 849-869
+        }
       }
       CHK(exchange(ctx, {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},   // 876-887
                          {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}}));
@@ -888,6 +981,7 @@ void count_active_edges(Block& b, const int32_t* coe) {
 // build the exchange plans of both time-level parities of a step outside graph capture
 int plan_all(mpas_dyc_ctx* ctx, double dt) {
   if (!needs_exchange(ctx) || ctx->planned[ctx->cur]) return MPAS_DYC_OK;
+  if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
   ctx->planning = true;
   int r = srk3(ctx, dt);
   ctx->planning = false;
@@ -928,6 +1022,12 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
     return MPAS_DYC_EHIP;
   }
   for (auto& e : ctx->ev) (void)hipEventCreate(&e);
+  if (hipStreamCreateWithFlags(&ctx->xstream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->xfork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->xjoin, hipEventDisableTiming) != hipSuccess) {
+    mpas_dyc_destroy(ctx);
+    return MPAS_DYC_EHIP;
+  }
   for (auto& b : ctx->blk) {
     build_registry(b);
     for (auto& f : b.fields) {
@@ -966,6 +1066,9 @@ void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->xfork) (void)hipEventDestroy(ctx->xfork);
+  if (ctx->xjoin) (void)hipEventDestroy(ctx->xjoin);
+  if (ctx->xstream) (void)hipStreamDestroy(ctx->xstream);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1039,7 +1142,15 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
       else if (v < 0 || v > nt) v = (int32_t)nt;
       tmp[i] = v;
     }
-    if (f->pool == "mesh" && f->name == "cellsOnEdge") count_active_edges(b, src);
+    if (f->pool == "mesh" && f->name == "cellsOnEdge") {
+      count_active_edges(b, src);
+      b.h_coe = tmp;
+      ctx->bnd_ready = false;
+    }
+    if (f->pool == "mesh" && f->name == "edgesOnCell") {
+      b.h_eoc = tmp;
+      ctx->bnd_ready = false;
+    }
     HIPCHK(hipMemcpyAsync(f->buf[slot], tmp.data(), nb, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   } else if (f->nsub > 1) {
@@ -1055,6 +1166,10 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
   } else {
     HIPCHK(hipMemcpyAsync(f->buf[slot], host, nb, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (f->pool == "mesh" && f->name == "nEdgesOnCell") {
+      b.h_noc.assign((const int32_t*)host, (const int32_t*)host + nb / 4);
+      ctx->bnd_ready = false;
+    }
     if (f->pool == "tend" && f->name == "rt_diabatic_tend") {
       const double* h = (const double*)host;
       int nz = 0;
@@ -1275,6 +1390,14 @@ int mpas_dyc_synchronize(mpas_dyc_ctx* ctx) {
   if (!ctx) return MPAS_DYC_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->xstream));
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_set_overlap(mpas_dyc_ctx* ctx, int32_t on) {
+  if (!ctx) return MPAS_DYC_EINVAL;
+  invalidate_plans(ctx);
+  ctx->overlap = on < 0 ? -1 : (on != 0);
   return MPAS_DYC_OK;
 }
 
@@ -1305,11 +1428,11 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   for (int r = 0; r < reps; ++r) {
     HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-    LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step);
+    LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step, 0);
     HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
     LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
     HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-    divergence_damping(ctx, d, p, dts);
+    divergence_damping(ctx, d, p, dts, 0);
     HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
     if (ms_kernels) {
       HIPCHK(hipEventSynchronize(ctx->ev[4]));

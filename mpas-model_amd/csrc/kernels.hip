@@ -647,9 +647,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Co
 // ============================================================================
 // atm_set_smlstep_pert_variables_work  (mpas_atm_time_integration.F:2290-2307)
 // ============================================================================
-__global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p) {
+// phase: 0 = every cell; 1 / 2 = only cells without / with a halo edge (split around the
+// tend_u halo exchange, which then overlaps the interior cells)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p, int phase) {
   const int c = wave_elem(0);
   if (c >= d.nCellsSolve) return;
+  if (phase && ((p.cell_bnd[c] != 0) != (phase == 2))) return;
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
   const size_t K1 = K + 1;
@@ -673,9 +676,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p) 
 // atm_advance_acoustic_step_work  (mpas_atm_time_integration.F:2535-2721)
 // ============================================================================
 // edge phase (2540-2601): edges with >=1 owned cell
-__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step) {
+// phase: 0 = every edge; 1 / 2 = only edges without / with a halo cell (split around the
+// rho_pp halo exchange, which then overlaps the interior edges)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step, int phase) {
   const int e = wave_elem(0);
   if (e >= d.nEdges) return;
+  if (phase && ((p.edge_bnd[e] != 0) != (phase == 2))) return;
   const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
   if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
   const int k = lane_id(), K = d.K;
@@ -797,7 +803,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p
 // EPW edges is issued before the first store, so each wave keeps EPW x 7 column loads
 // in flight (the kernel is latency x occupancy bound with one edge per wave).
 template <int EPW>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, double coef_divdamp) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, double coef_divdamp, int phase) {
   const int e0 = wave_elem(0) * EPW;
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
@@ -809,7 +815,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, doubl
     on[j] = false;
     if (e < d.nEdges) {
       const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
-      on[j] = (c1 < d.nCellsSolve || c2 < d.nCellsSolve);
+      on[j] = (c1 < d.nCellsSolve || c2 < d.nCellsSolve) &&
+              (phase == 0 || ((p.edge_bnd[e] != 0) == (phase == 2)));  // phases as in k_acoustic_edges
       if (on[j] && act) {
         const size_t o = (size_t)e * K + k, o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
         ru[j] = p.ru_p[o];

@@ -139,6 +139,11 @@ class Dycore:
             return buf.reshape(n1, self.K, self.ns)[:-1]
         return buf.reshape(n1, buf.size // n1)[:-1]
 
+    def set_overlap(self, on: bool | None = None):
+        """Split-phase exchanges (interior elements overlap the halo traffic): True / False,
+        or None for the library's automatic choice (on when exchanges go through RCCL)."""
+        self._check(self.lib.mpas_dyc_set_overlap(self.h, -1 if on is None else (1 if on else 0)), "set_overlap")
+
     def halo_exchange(self, pool: str, name: str, time_level: int = 1, layers=(1, 2, 3)):
         """mpas_dmpar_exch_halo_field(field, haloLayers) over the blocks of this process (and peers)."""
         mask = sum(1 << (l - 1) for l in layers)

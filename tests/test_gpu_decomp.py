@@ -37,12 +37,13 @@ def _single(case, nsteps, graph=False):
     return out
 
 
-def _blocks(case, nblocks, nsteps, graph=False, rccl_local=False):
+def _blocks(case, nblocks, nsteps, graph=False, rccl_local=False, overlap=True):
     from mpas_dycore import Dycore, decomp
     part = decomp.partition_sfc(case["nCells"], nblocks)
     blocks = decomp.decompose(case, part)
     comm_id = Dycore.comm_unique_id() if rccl_local else None
     dy = Dycore.from_blocks(blocks, device=0, comm_id=comm_id, nranks=1, rank=0, rccl_local=rccl_local)
+    dy.set_overlap(overlap)
     dy.use_graph(graph)
     _run(dy, nsteps)
     n_glob = {"cell": case["nCells"], "edge": case["nEdges"]}
@@ -92,6 +93,18 @@ def test_blocks_moist_mono_transport_bitwise(moist_case):
     got = _blocks(moist_case, 3, 2, graph=True)
     for name in ref:
         assert np.array_equal(got[name], ref[name]), f"{name}: max diff {np.nanmax(np.abs(got[name] - ref[name]))}"
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_split_phase_exchange_bitwise(small_case, graph):
+    """Interior/boundary split around the tend_u / rho_pp / rtheta_pp exchanges (exchange
+    stream overlapping the interior kernels) changes no bit."""
+    ref = _single(small_case, 3)
+    got = _blocks(small_case, 4, 3, graph=graph, overlap=True)
+    seq = _blocks(small_case, 4, 3, graph=graph, overlap=False)
+    for name in ref:
+        assert np.array_equal(got[name], ref[name]), name
+        assert np.array_equal(seq[name], ref[name]), name
 
 
 def test_rccl_transport_matches_device_copies(small_case):
