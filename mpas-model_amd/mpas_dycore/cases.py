@@ -13,7 +13,7 @@ import pickle
 import numpy as np
 
 from .init_atm import build_case
-from .mesh import build_mesh
+from .mesh import build_mesh, build_varres_mesh
 
 CACHE = os.environ.get("MPAS_DYCORE_CACHE", "/tmp/mpas_dycore_cache")
 
@@ -44,6 +44,34 @@ def jw_case(ncells: int, K: int = 56, ns: int = 1, moist: bool = False, order: i
     cfg = dict(config_len_disp=jw_len_disp(level), config_dt=jw_dt(level), config_time_integration_order=order)
     case = build_case(m, K=K, ns=ns, moist=moist, config=cfg)
     case["dt"] = jw_dt(level)
+    if cache:
+        os.makedirs(CACHE, exist_ok=True)
+        tmp = path + f".{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            pickle.dump(case, f, protocol=pickle.HIGHEST_PROTOCOL)
+        os.replace(tmp, path)
+    return case
+
+
+def varres_case(ncells: int, ratio: float = 20.0, K: int = 56, ns: int = 1, moist: bool = False,
+                lloyd_iters: int | None = None, cache: bool = True) -> dict:
+    """JW state on a variable-resolution SCVT (BASELINE.json configs[4] analogue).
+
+    dt and config_len_disp follow the finest spacing, as MPAS variable-resolution runs do
+    (dt ~ 5 s per km of the finest cells, len_disp = finest spacing)."""
+    if lloyd_iters is None:
+        lloyd_iters = 40 if ncells <= 200000 else 20
+    key = f"vr_n{ncells}_r{ratio:g}_K{K}_ns{ns}_m{int(moist)}_ll{lloyd_iters}_v2"
+    path = os.path.join(CACHE, key + ".pkl")
+    if cache and os.path.isfile(path):
+        with open(path, "rb") as f:  # our own cache file, written below
+            return pickle.load(f)
+    m = build_varres_mesh(ncells, ratio=ratio, lloyd_iters=lloyd_iters)
+    dx_min = float(m["dcEdge"].min())
+    dt = float(max(1.0, round(5.0 * dx_min / 1000.0)))
+    cfg = dict(config_len_disp=dx_min, config_dt=dt)
+    case = build_case(m, K=K, ns=ns, moist=moist, config=cfg)
+    case["dt"] = dt
     if cache:
         os.makedirs(CACHE, exist_ok=True)
         tmp = path + f".{os.getpid()}.tmp"

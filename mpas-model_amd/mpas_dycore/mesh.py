@@ -155,24 +155,103 @@ def build_mesh(level: int, lloyd_iters: int = 0, radius: float = SPHERE_RADIUS, 
     return _topology_and_geometry(p, f, radius)
 
 
-def _lloyd_step(p, f):
+def _lloyd_step(p, f, density=None):
+    """One Lloyd step: every generator moves to the (density-weighted) centroid of its
+    Voronoi cell, integrated over the fan of triangles (generator, v_j, v_j+1)."""
     vc = _circumcenters(p, f)
     cnt, vof = _cells_vertices_ccw(p, f)
+    W = vof.shape[1]
     num = np.zeros_like(p)
     idx = np.arange(len(p))
-    for j in range(6):
+    for j in range(W):
         ok = j < cnt
         v0 = vof[ok, j]
-        v1 = vof[ok, (j + 1) % 6]
+        v1 = vof[ok, (j + 1) % W]
         v1 = np.where((j + 1) < cnt[ok], v1, vof[ok, 0])
         tA, tB, tC = p[idx[ok]], vc[v0], vc[v1]
         ar = tri_area(tA, tB, tC)
-        num[idx[ok]] += ar[:, None] * _normalize(tA + tB + tC)
+        cen = _normalize(tA + tB + tC)
+        if density is not None:
+            ar = ar * density(cen)
+        num[idx[ok]] += ar[:, None] * cen
     return _normalize(num)
 
 
-def _cells_vertices_ccw(p, f):
-    """For each cell, its incident faces (=Voronoi vertices) sorted CCW; -1 padded to 6."""
+def _delaunay(p):
+    """Spherical Delaunay triangulation = convex hull of the unit generators, faces CCW."""
+    from scipy.spatial import ConvexHull
+    f = ConvexHull(p).simplices.astype(np.int64)
+    a, b, c = p[f[:, 0]], p[f[:, 1]], p[f[:, 2]]
+    flip = np.sum(np.cross(b - a, c - a) * a, axis=1) < 0
+    f[flip] = f[flip][:, [0, 2, 1]]
+    return f
+
+
+def varres_density(center_latlon=(30.0, -90.0), radius_deg=20.0, width_deg=10.0, ratio=20.0):
+    """MPAS-style refinement density rho(x) = (1-g)/2 (tanh((beta - d)/alpha) + 1) + g with
+    g = ratio^-4, so the cell spacing dx ~ rho^-1/4 varies by ``ratio`` between the
+    refined disc (radius beta around the centre) and the far field."""
+    lat, lon = np.radians(center_latlon[0]), np.radians(center_latlon[1])
+    xc = np.array([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)])
+    beta, alpha, g = np.radians(radius_deg), np.radians(width_deg), float(ratio) ** -4
+
+    def rho(x):
+        d = np.arccos(np.clip(x @ xc, -1.0, 1.0))
+        return (1.0 - g) / 2.0 * (np.tanh((beta - d) / alpha) + 1.0) + g
+    return rho
+
+
+def _fibonacci_sphere(n):
+    i = np.arange(n) + 0.5
+    z = 1.0 - 2.0 * i / n
+    r = np.sqrt(1.0 - z * z)
+    phi = np.pi * (3.0 - np.sqrt(5.0)) * i
+    return np.stack([r * np.cos(phi), r * np.sin(phi), z], axis=1)
+
+
+def _schmidt(p, center_latlon, c):
+    """Schmidt transform: colatitude theta about the centre -> 2 atan(tan(theta/2) / c),
+    which refines the spacing by c near the centre and coarsens it by c at the antipode."""
+    lat, lon = np.radians(center_latlon[0]), np.radians(center_latlon[1])
+    zc = np.array([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)])
+    a = np.cross(zc, [0.0, 0.0, 1.0]) if abs(zc[2]) < 0.9 else np.cross(zc, [1.0, 0.0, 0.0])
+    xa = a / np.linalg.norm(a)
+    ya = np.cross(zc, xa)
+    pz, px, py = p @ zc, p @ xa, p @ ya
+    th = np.arccos(np.clip(pz, -1.0, 1.0))
+    ph = np.arctan2(py, px)
+    th2 = 2.0 * np.arctan(np.tan(th / 2.0) / c)
+    return (np.sin(th2) * np.cos(ph))[:, None] * xa + (np.sin(th2) * np.sin(ph))[:, None] * ya + np.cos(th2)[:, None] * zc
+
+
+def build_varres_mesh(ncells: int, ratio: float = 20.0, lloyd_iters: int = 10, seed: int = 20250415,
+                      radius: float = SPHERE_RADIUS, sfc: bool = True, **density_kw) -> dict:
+    """Variable-resolution spherical centroidal Voronoi mesh (BASELINE.json configs[4]:
+    x20.835586-like 60-3 km meshes).  A Fibonacci lattice of ``ncells`` generators is
+    pulled towards the refinement centre by a Schmidt transform (stretch sqrt(ratio)),
+    then relaxed by density-weighted Lloyd iterations on the spherical Delaunay
+    triangulation, which is rebuilt every step so the topology (pentagons / hexagons /
+    heptagons in the transition zone) is free to change."""
+    rho = varres_density(ratio=ratio, **density_kw)
+    center = density_kw.get("center_latlon", (30.0, -90.0))
+    p = _schmidt(_fibonacci_sphere(ncells), center, np.sqrt(ratio))
+    for _ in range(lloyd_iters):
+        p = _lloyd_step(p, _delaunay(p), rho)
+    f = _delaunay(p)
+    if sfc:
+        order = np.argsort(_hilbert3d_keys(p), kind="stable")
+        rank = np.empty_like(order)
+        rank[order] = np.arange(len(order))
+        p = p[order]
+        f = rank[f]
+    m = _topology_and_geometry(p, f, radius)
+    m["meshDensity"] = rho(p)
+    return m
+
+
+def _cells_vertices_ccw(p, f, width=None):
+    """For each cell, its incident faces (=Voronoi vertices) sorted CCW; -1 padded to
+    ``width`` (default: the largest cell degree)."""
     nC = len(p)
     cell = f.reshape(-1)
     face = np.repeat(np.arange(len(f)), 3)
@@ -192,16 +271,16 @@ def _cells_vertices_ccw(p, f):
     cnt = np.bincount(cell_s, minlength=nC)
     start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
     pos = np.arange(len(cell_s)) - start[cell_s]
-    vof = -np.ones((nC, 6), dtype=np.int64)
+    vof = -np.ones((nC, int(cnt.max()) if width is None else width), dtype=np.int64)
     vof[cell_s, pos] = face_s
     return cnt, vof
 
 
 def _topology_and_geometry(p, f, radius):
     nC, nV = len(p), len(f)
-    maxEdges = 6
     xv = _circumcenters(p, f)
     nEoC, voc = _cells_vertices_ccw(p, f)
+    maxEdges = voc.shape[1]  # 6 for icosahedral meshes; 7+ for variable-resolution SCVTs
 
     # edges: unique (cell,cell) pairs of the Delaunay triangles
     pairs = np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]])

@@ -37,3 +37,10 @@ def small_case():
 def moist_case():
     from mpas_dycore.cases import jw_case
     return jw_case(642, K=26, ns=3, moist=True, cache=False)
+
+
+@pytest.fixture(scope="session")
+def varres_case_small():
+    """Variable-resolution SCVT (4x refinement, pentagons/hexagons/heptagons, maxEdges=7)."""
+    from mpas_dycore.cases import varres_case
+    return varres_case(2562, ratio=4.0, K=26, ns=3, moist=True, lloyd_iters=30, cache=False)

@@ -122,6 +122,17 @@ def test_exchange_lists_make_halos_exact(small_case, blocks_by_n, n, loc, key):
         assert np.all(np.isnan(a[e:]))
 
 
+def test_exchange_lists_on_variable_resolution_mesh():
+    """Irregular halos (5/6/7-gons) still give exact halos on every layer."""
+    from mpas_dycore.mesh import build_varres_mesh
+    m = build_varres_mesh(2562, ratio=4.0, lloyd_iters=30)
+    blocks = decomp.decompose(m, decomp.partition_sfc(m["nCells"], 6))
+    for loc, key in (("cell", "nCells"), ("edge", "nEdges"), ("vertex", "nVertices")):
+        g = np.random.default_rng(5).standard_normal((m[key], 2))
+        for b, a in zip(blocks, _exchange_in_process(blocks, loc, g)):
+            assert np.array_equal(a, g[b.glob[loc]])
+
+
 def test_partition_file_round_trip(tmp_path, small_case):
     part = decomp.partition_sfc(small_case["nCells"], 4)
     p = tmp_path / "graph.info.part.4"

@@ -73,3 +73,24 @@ def test_sfc_locality(mesh):
     """Cells are Hilbert-ordered: neighbours are close in index space (coalesced gathers)."""
     c1, c2 = mesh["cellsOnEdge"].T
     assert np.median(np.abs(c1 - c2)) < mesh["nCells"] / 8
+
+
+@pytest.fixture(scope="module")
+def vr_mesh():
+    from mpas_dycore.mesh import build_varres_mesh
+    return build_varres_mesh(2562, ratio=4.0, lloyd_iters=30)
+
+
+def test_varres_mesh_conventions(vr_mesh):
+    """Variable-resolution SCVT: valid Voronoi topology with 5/6/7-gons, MPAS orientation
+    conventions, positive kites, near-exact tiling and antisymmetric TRiSK weights."""
+    m = vr_mesh
+    assert m["nCells"] - m["nEdges"] + m["nVertices"] == 2
+    counts = np.bincount(m["nEdgesOnCell"])
+    assert m["maxEdges"] == 7 and counts[5] > 0 and counts[7] > 0 and counts[6] > 0.8 * m["nCells"]
+    assert (m["kiteAreasOnVertex"] > 0).all()
+    R = m["sphere_radius"]
+    assert abs(m["areaCell"].sum() / (4 * np.pi * R * R) - 1) < 2e-3
+    assert m["dcEdge"].max() / m["dcEdge"].min() > 3.0           # really variable resolution
+    test_edge_orientation_conventions(m)
+    test_trisk_weights(m)
