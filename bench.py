@@ -64,6 +64,9 @@ def main():
     ap.add_argument("--ncells", type=int, default=163842)
     ap.add_argument("--levels", type=int, default=56)
     ap.add_argument("--num-scalars", type=int, default=None)
+    ap.add_argument("--varres", type=int, default=0, metavar="NCELLS",
+                    help="BASELINE.json configs[4]: variable-resolution SCVT (20x refinement) with NCELLS cells, "
+                         "e.g. 835586")
     ap.add_argument("--moist", action="store_true",
                     help="BASELINE.json configs[3]: moist JW (qv) + tracer blobs, num_scalars=6, monotone transport")
     ap.add_argument("--no-graph", action="store_true")
@@ -91,13 +94,19 @@ def main():
     # rank 0 builds (and caches) the synthetic case before any rank touches the GPU
     if args.num_scalars is None:
         args.num_scalars = 6 if args.moist else 1
+    def make_case():
+        if args.varres:
+            from mpas_dycore.cases import varres_case
+            return varres_case(args.varres, ratio=20.0, K=args.levels, ns=args.num_scalars, moist=args.moist)
+        return jw_case(args.ncells, K=args.levels, ns=args.num_scalars, moist=args.moist)
+
     t_build = time.time()
     if rank == 0:
-        case = jw_case(args.ncells, K=args.levels, ns=args.num_scalars, moist=args.moist)
+        case = make_case()
     if dist:
         dist.barrier()
     if rank != 0:
-        case = jw_case(args.ncells, K=args.levels, ns=args.num_scalars, moist=args.moist)
+        case = make_case()
     dt = case["dt"]
     t_build = time.time() - t_build
 
@@ -185,7 +194,11 @@ def main():
         "dtype": "f64",
         "data": "synthetic (icosahedral SCVT mesh + Jablonowski-Williamson baroclinic wave, built on the box)",
         "config": {
-            "workload": (f"x1.{case['nCells']} moist dycore + scalar transport (num_scalars={case['num_scalars']}, "
+            "workload": (f"variable-resolution SCVT, {case['nCells']} cells (20x refinement, "
+                         f"{case['dcEdge'].min() / 1e3:.1f}-{case['dcEdge'].max() / 1e3:.0f} km, maxEdges="
+                         f"{case['maxEdges']}), {case['nVertLevels']} levels, dt={dt:g}s (BASELINE.json configs[4] "
+                         f"analogue; one full atm_srk3 per step)" if args.varres else
+                         f"x1.{case['nCells']} moist dycore + scalar transport (num_scalars={case['num_scalars']}, "
                          f"monotone), {case['nVertLevels']} levels, dt={dt:g}s (BASELINE.json configs[3]; one full "
                          f"atm_srk3 per step)" if args.moist else
                          f"x1.{case['nCells']} dry dycore, {case['nVertLevels']} levels, dt={dt:g}s "

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import os
 import pickle
+import sys
 
 import numpy as np
 
@@ -60,7 +61,7 @@ def varres_case(ncells: int, ratio: float = 20.0, K: int = 56, ns: int = 1, mois
     dt and config_len_disp follow the finest spacing, as MPAS variable-resolution runs do
     (dt ~ 5 s per km of the finest cells, len_disp = finest spacing)."""
     if lloyd_iters is None:
-        lloyd_iters = 40 if ncells <= 200000 else 20
+        lloyd_iters = 40 if ncells <= 200000 else 12
     key = f"vr_n{ncells}_r{ratio:g}_K{K}_ns{ns}_m{int(moist)}_ll{lloyd_iters}_v2"
     path = os.path.join(CACHE, key + ".pkl")
     if cache and os.path.isfile(path):
@@ -70,9 +71,11 @@ def varres_case(ncells: int, ratio: float = 20.0, K: int = 56, ns: int = 1, mois
     dx_min = float(m["dcEdge"].min())
     dt = float(max(1.0, round(5.0 * dx_min / 1000.0)))
     cfg = dict(config_len_disp=dx_min, config_dt=dt)
+    if ncells > 200000:
+        print(f"varres case: mesh done ({m['nCells']} cells), building the JW state", file=sys.stderr, flush=True)
     case = build_case(m, K=K, ns=ns, moist=moist, config=cfg)
     case["dt"] = dt
-    if cache:
+    if cache and ncells <= 400000:  # larger cases are rebuilt rather than pickled to /tmp
         os.makedirs(CACHE, exist_ok=True)
         tmp = path + f".{os.getpid()}.tmp"
         with open(tmp, "wb") as f:

@@ -26,6 +26,8 @@ are local in memory (north_star: "index arrays reordered by SFC").
 """
 from __future__ import annotations
 
+import sys
+
 import numpy as np
 
 SPHERE_RADIUS = 6371229.0  # mpas_constants.F: a = 6371229
@@ -235,8 +237,10 @@ def build_varres_mesh(ncells: int, ratio: float = 20.0, lloyd_iters: int = 10, s
     rho = varres_density(ratio=ratio, **density_kw)
     center = density_kw.get("center_latlon", (30.0, -90.0))
     p = _schmidt(_fibonacci_sphere(ncells), center, np.sqrt(ratio))
-    for _ in range(lloyd_iters):
+    for it in range(lloyd_iters):
         p = _lloyd_step(p, _delaunay(p), rho)
+        if ncells > 200000:  # long builds report progress (a silent GPU-box job looks hung)
+            print(f"varres mesh: Lloyd iteration {it + 1}/{lloyd_iters}", file=sys.stderr, flush=True)
     f = _delaunay(p)
     if sfc:
         order = np.argsort(_hilbert3d_keys(p), kind="stable")
