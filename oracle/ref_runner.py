@@ -19,12 +19,15 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HARNESS = os.path.join(HERE, "_ref", "mpas_ref_harness")
+# the same harness driver linked against the Fortran drop-in module + libmpas_dycore.so
+# (make -C oracle dropin): the product behind the reference's own Fortran API, not an oracle
+DROPIN_HARNESS = os.path.join(HERE, "_ref", "mpas_dropin_harness")
 
 _LOC_N = {"cell": "nCells", "edge": "nEdges", "vertex": "nVertices"}
 
 
-def available() -> bool:
-    return os.path.isfile(HARNESS) and os.access(HARNESS, os.X_OK)
+def available(binary: str = HARNESS) -> bool:
+    return os.path.isfile(binary) and os.access(binary, os.X_OK)
 
 
 def _fields():
@@ -124,10 +127,11 @@ def read_dump(case: dict, stepdir: str) -> dict:
 
 
 def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads: int = 0,
-                  workdir: str | None = None, moist_end: int = 1, timeout: int = 3000):
-    """Run the reference dycore; returns ({step: {field: array}}, [step wall times])."""
-    if not available():
-        raise RuntimeError("oracle/_ref/mpas_ref_harness not built (make -C oracle)")
+                  workdir: str | None = None, moist_end: int = 1, timeout: int = 3000, binary: str = HARNESS):
+    """Run the reference dycore; returns ({step: {field: array}}, [step wall times]).
+    ``binary=DROPIN_HARNESS`` runs the same driver on the drop-in module instead."""
+    if not available(binary):
+        raise RuntimeError(f"{binary} not built (make -C oracle)")
     if dump_steps is None:
         dump_steps = [nsteps]
     own = workdir is None
@@ -137,9 +141,9 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     env = dict(os.environ)
     if nthreads:
         env["OMP_NUM_THREADS"] = str(nthreads)
-    r = subprocess.run([HARNESS, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout)
+    r = subprocess.run([binary, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout)
     if r.returncode != 0:
-        raise RuntimeError(f"reference harness failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
+        raise RuntimeError(f"{os.path.basename(binary)} failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
     res = {}
     for s in dump_steps:
         sd = os.path.join(outd, f"step_{s:04d}")
