@@ -45,6 +45,8 @@ struct Config {
 
 // Device pointers handed to every kernel (by value, in kernarg memory).
 // Time-level fields are resolved to tl1/tl2 on the host before each launch.
+constexpr int CELL_HALO_EDGE = 1, CELL_BND_EDGE = 2;
+
 struct Ptrs {
   // ---- mesh: connectivity (0-based, missing -> n)
   const int *nEdgesOnCell, *edgesOnCell, *cellsOnCell, *verticesOnCell, *kiteForCell;
@@ -81,7 +83,10 @@ struct Ptrs {
   double *s_max, *s_min, *scale_arr, *flux_arr, *flux_upwind_tmp, *flux_tmp, *wdtn, *rho_zz_int;
   double *scalar_old_copy;
   double *advflux_w, *advflux_th;  // edge values of w / theta_m for horizontal advection
-  const int *edge_bnd, *cell_bnd;  // 1 = reads halo data (edge: a halo cell; owned cell: a halo edge)
+  // split-phase flags.  edge_bnd: 1 = a cell of the edge is a halo cell.  cell_bnd bits:
+  // CELL_HALO_EDGE = an edge of the cell is a halo edge, CELL_BND_EDGE = an edge of the cell has
+  // edge_bnd set; halo cells have both bits.
+  const int *edge_bnd, *cell_bnd;
 };
 
 }  // namespace mpas

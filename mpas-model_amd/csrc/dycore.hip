@@ -578,8 +578,12 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
     for (int e = 0; e < d.nEdges; ++e)
       eb[e] = (b.h_coe[2 * e] >= d.nCellsSolve || b.h_coe[2 * e + 1] >= d.nCellsSolve) ? 1 : 0;
     for (int c = 0; c < d.nCells; ++c) {
-      int bnd = 0;
-      for (int i = 0; i < b.h_noc[c]; ++i) bnd |= b.h_eoc[(size_t)c * d.maxEdges + i] >= d.nEdgesSolve;
+      int bnd = c >= d.nCellsSolve ? CELL_HALO_EDGE | CELL_BND_EDGE : 0;
+      for (int i = 0; i < b.h_noc[c]; ++i) {
+        const int e = b.h_eoc[(size_t)c * d.maxEdges + i];
+        if (e >= d.nEdgesSolve) bnd |= CELL_HALO_EDGE;
+        if (e >= d.nEdges || eb[e]) bnd |= CELL_BND_EDGE;
+      }
       cb[c] = bnd;
     }
     HIPCHK(hipMemcpy(find(b, "scratch", "edge_bnd")->buf[0], eb.data(), eb.size() * 4, hipMemcpyHostToDevice));
@@ -674,8 +678,8 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
 }
 
-void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int phase) {
-  LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step, phase);
+void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
+  LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step);
 }
 
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
@@ -791,8 +795,11 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   }
   const bool scalars_in_dynamics = cf.scalar_advection && !cf.split_dynamics_transport;
   const bool split = split_phase(ctx);
-  CHK(exchange(ctx, {{"state", "theta_m", 1, ALL_LAYERS}, {"state", "scalars", 1, ALL_LAYERS},   // 329-338
-                     {"diag", "pressure_p", 0, ALL_LAYERS}, {"diag", "rtheta_p", 0, ALL_LAYERS}}));
+  // 329-338, plus the exner exchange of the first dynamics substep (513): nothing writes exner
+  // in between (vert_imp_coefs reads it on owned cells only), so the halo values are the same
+  CHK(exchange(ctx, {{"state", "theta_m", 1, ALL_LAYERS}, {"state", "scalars", 1, ALL_LAYERS},
+                     {"diag", "pressure_p", 0, ALL_LAYERS}, {"diag", "rtheta_p", 0, ALL_LAYERS},
+                     {"diag", "exner", 0, ALL_LAYERS}}));
   EACH(rk_integration_setup(ctx, d, p));                          // 341-381
   EACH(LAUNCH(k_moist_cells, d.nCells, d, p));                    // 383-422
   EACH(LAUNCH(k_moist_edges, d.nEdges, d, p));
@@ -800,7 +807,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
 
   for (int dynamics_substep = 1; dynamics_substep <= dynamics_split; ++dynamics_substep) {
     EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));         // 476-510
-    CHK(exchange(ctx, {{"diag", "exner", 0, ALL_LAYERS}}));      // 513
+    // 513 (exner): carried by the step-start exchange and by the 1282-1297 exchange below
     for (int rk_step = 1; rk_step <= 3; ++rk_step) {
       if (cf.time_integration_order == 3 && rk_step == 2) EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[1]));
       EACH(dyn_tend(ctx, d, p, rk_step, dt));                     // 561-630
@@ -814,33 +821,48 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         CHK(exchange(ctx, {{"tend", "u", 0, 0x1u}}));             // 642
         EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, 0));     // 644-678
       }
-      for (int small_step = 1; small_step <= number_sub_steps[rk_step - 1]; ++small_step) {
-        if (split) {  // 792 | 794-837: interior edges overlap the rho_pp exchange
-          CHK(exchange_async(ctx, {{"diag", "rho_pp", 0, 0x1u}}));
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1));
-          CHK(exchange_wait(ctx));
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 2));
-        } else {
-          CHK(exchange(ctx, {{"diag", "rho_pp", 0, 0x1u}}));      // 792
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 0));    // 794-837
-        }
+      // Acoustic sub-steps (788-870).  The reference exchanges rho_pp before every sub-step
+      // (792) and rtheta_pp after it (845).  Here the rho_pp exchange of sub-step n+1 travels
+      // with the rtheta_pp exchange of sub-step n: divergence damping, which runs in between,
+      // does not touch rho_pp, so the halo values are the same.  The exchange before sub-step 1
+      // is dropped: that sub-step's edge phase does not read rho_pp (2580-2599), and the cell phase
+      // reads and zeroes only owned columns (2617-2622).  The halo values it would have set are
+      // overwritten by the all-layer exchange at 876 before anything reads them.
+      const int nsub = number_sub_steps[rk_step - 1];
+      for (int small_step = 1; small_step <= nsub; ++small_step) {
+        EACH(acoustic_edges(ctx, d, p, dts, small_step));         // 794-837
         EACH(acoustic_cells(ctx, d, p, dts, small_step));
-        if (split) {  // 845 | 849-869: interior edges overlap the rtheta_pp exchange
-          CHK(exchange_async(ctx, {{"diag", "rtheta_pp", 0, 0x1u}}));
+        std::vector<XField> xf = {{"diag", "rtheta_pp", 0, 0x1u}};  // 845
+        if (small_step < nsub) xf.push_back({"diag", "rho_pp", 0, 0x1u});  // 792 of the next sub-step
+        if (split) {  // 849-869: interior edges overlap the exchange
+          CHK(exchange_async(ctx, xf));
           EACH(divergence_damping(ctx, d, p, dts, 1));
           CHK(exchange_wait(ctx));
           EACH(divergence_damping(ctx, d, p, dts, 2));
         } else {
-          CHK(exchange(ctx, {{"diag", "rtheta_pp", 0, 0x1u}}));   // 845
+          CHK((exchange)(ctx, xf));  // parenthesised: no ADL lookup of std::exchange
           EACH(divergence_damping(ctx, d, p, dts, 0));            // 849-869
         }
       }
-      CHK(exchange(ctx, {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},   // 876-887
-                         {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}}));
+      const std::vector<XField> xrec = {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},  // 876-887
+                                        {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};
       const double invNs = 1 / (double)number_sub_steps[rk_step - 1];
-      EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rk_timestep[rk_step - 1], invNs, rk_step));  // 889-930
-      EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs));
-      EACH(LAUNCH(k_recover_cells3, d.nCells, d, p));
+      const double rdt = rk_timestep[rk_step - 1];
+      if (split) {  // 889-988: owned cells, interior edges and cells overlap the exchange
+        CHK(exchange_async(ctx, xrec));
+        EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 1));
+        EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1));
+        EACH(LAUNCH(k_recover_cells3, d.nCells, d, p, 1));
+        CHK(exchange_wait(ctx));
+        EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 2));
+        EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
+        EACH(LAUNCH(k_recover_cells3, d.nCells, d, p, 2));
+      } else {
+        CHK((exchange)(ctx, xrec));
+        EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0));  // 889-930
+        EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0));
+        EACH(LAUNCH(k_recover_cells3, d.nCells, d, p, 0));
+      }
       CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));        // 988
       if (scalars_in_dynamics) {                                  // 993-1185
         if (rk_step < 3 || (!cf.monotonic && !cf.positive_definite)) {
@@ -857,9 +879,9 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         CHK(exchange(ctx, {{"state", "w", 2, ALL_LAYERS}, {"diag", "pv_edge", 0, ALL_LAYERS},
                            {"diag", "rho_edge", 0, ALL_LAYERS}}));
     }
-    if (dynamics_substep < dynamics_split)                        // 1282-1297
+    if (dynamics_substep < dynamics_split)                        // 1282-1297 + 513 of the next substep
       CHK(exchange(ctx, {{"state", "theta_m", 2, ALL_LAYERS}, {"diag", "pressure_p", 0, ALL_LAYERS},
-                         {"diag", "rtheta_p", 0, ALL_LAYERS}}));
+                         {"diag", "rtheta_p", 0, ALL_LAYERS}, {"diag", "exner", 0, ALL_LAYERS}}));
     EACH(LAUNCH(k_substep_finish, d.nEdges + d.nCells, d, p, dynamics_substep, dynamics_split,
                 1.0 / (double)dynamics_split));                   // 1304-1341
   }
@@ -1428,7 +1450,7 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   for (int r = 0; r < reps; ++r) {
     HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-    LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step, 0);
+    LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step);
     HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
     LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
     HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));

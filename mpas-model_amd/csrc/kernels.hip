@@ -652,7 +652,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Co
 __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p, int phase) {
   const int c = wave_elem(0);
   if (c >= d.nCellsSolve) return;
-  if (phase && ((p.cell_bnd[c] != 0) != (phase == 2))) return;
+  if (phase && (((p.cell_bnd[c] & CELL_HALO_EDGE) != 0) != (phase == 2))) return;
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
   const size_t K1 = K + 1;
@@ -676,12 +676,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p, 
 // atm_advance_acoustic_step_work  (mpas_atm_time_integration.F:2535-2721)
 // ============================================================================
 // edge phase (2540-2601): edges with >=1 owned cell
-// phase: 0 = every edge; 1 / 2 = only edges without / with a halo cell (split around the
-// rho_pp halo exchange, which then overlaps the interior edges)
-__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step, int phase) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step) {
   const int e = wave_elem(0);
   if (e >= d.nEdges) return;
-  if (phase && ((p.edge_bnd[e] != 0) != (phase == 2))) return;
   const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
   if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
   const int k = lane_id(), K = d.K;
@@ -816,7 +813,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, doubl
     if (e < d.nEdges) {
       const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
       on[j] = (c1 < d.nCellsSolve || c2 < d.nCellsSolve) &&
-              (phase == 0 || ((p.edge_bnd[e] != 0) == (phase == 2)));  // phases as in k_acoustic_edges
+              (phase == 0 || ((p.edge_bnd[e] != 0) == (phase == 2)));  // 1 / 2: edges without / with a halo cell
       if (on[j] && act) {
         const size_t o = (size_t)e * K + k, o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
         ru[j] = p.ru_p[o];
@@ -836,11 +833,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, doubl
 
 // ============================================================================
 // atm_recover_large_step_variables_work  (mpas_atm_time_integration.F:2984-3097)
-// Three launches for the three barrier-separated phases.
+// Three launches for the three barrier-separated phases.  phase 0 = every element; around the
+// 876-887 exchange, phase 1 takes the elements that read no halo data (owned cells; edges with
+// two owned cells; owned cells whose edges all have two owned cells) and phase 2 the rest.
 // ============================================================================
 // cells (all, and the garbage slot): 2998-3040
-__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p, double dt, double invNs, int rk_step) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p, double dt, double invNs, int rk_step,
+                                                                  int phase) {
   const int c = wave_elem(0);
+  if (phase && ((c >= d.nCellsSolve) != (phase == 2))) return;
   const int k = lane_id(), K = d.K;
   const size_t K1 = K + 1;
   if (c == d.nCells) {  // rho_zz(:, nCells+1) = 1 (2989-2991)
@@ -885,9 +886,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p
 }
 
 // edges (all): 3048-3059
-__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs, int phase) {
   const int e = wave_elem(0);
   if (e >= d.nEdges) return;
+  if (phase && ((p.edge_bnd[e] != 0) != (phase == 2))) return;
   const int k = lane_id(), K = d.K;
   if (k >= K) return;
   const size_t o = (size_t)e * K + k;
@@ -899,9 +901,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p,
 }
 
 // cells (all): w from the flux-divergence operator, then divided by density (3063-3097)
-__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3(Dims d, Ptrs p) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3(Dims d, Ptrs p, int phase) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
+  if (phase && (((p.cell_bnd[c] & CELL_BND_EDGE) != 0) != (phase == 2))) return;
   const int k = lane_id(), K = d.K;
   const size_t K1 = K + 1;
   const bool act = k < K;
