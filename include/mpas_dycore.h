@@ -147,10 +147,14 @@ int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name
                            int32_t layer_mask);
 
 /* ---- measurement hooks (bench.py / tests) ---- */
-/* One acoustic sub-step (atm_advance_acoustic_step + atm_divergence_damping_3d) of block 0 on
- * the current state, repeated `reps` times, timed with HIP events on the compute stream.
- * Returns the average time per sub-step in *ms_out and per-kernel averages in
- * ms_kernels[3] = {edge phase, cell phase, divergence damping} (may be NULL). */
+/* A `reps`-sub-step acoustic loop (atm_advance_acoustic_step + atm_divergence_damping_3d per
+ * sub-step, srk3 :788-870) of block 0 on the current state, all sub-steps numbered
+ * `small_step`, timed with HIP events on the compute stream.  The launches are the ones srk3
+ * issues: the edge phase, the cell phase, and for every further sub-step the edge phase with
+ * the previous sub-step's damping fused in.  The last sub-step's damping is its own kernel.
+ * reps = 1 is exactly one sub-step followed by its damping.
+ * Returns the average time per sub-step in *ms_out.  ms_kernels[3] (may be NULL) gets
+ * {edge phases, cell phases, the standalone damping}, each summed and divided by reps. */
 int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_step, int32_t reps,
                                 double* ms_out, double* ms_kernels);
 /* Capture one full timestep in a hipGraph and replay it for subsequent

@@ -668,7 +668,10 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     s.rayleigh_coef_inverse = 1.0 / ((double)cf.number_rayleigh_damp_u_levels *
                                      (cf.rayleigh_damp_u_timescale_days * SECONDS_PER_DAY));
   LAUNCH(k_dyn_cells1, d.nCells, d, p, cf, s);
-  LAUNCH(k_dyn_edges, d.nEdges, d, p, cf, s, rk_step > 1 ? 1 : 0);
+  if (rk_step == 1)
+    LAUNCH(k_dyn_edges<true>, d.nEdges, d, p, cf, s, 0);
+  else
+    LAUNCH(k_dyn_edges<false>, d.nEdges, d, p, cf, s, 1);
   if (rk_step == 1) {
     if (s.h_mom_eddy_visc4 > 0.0) LAUNCH(k_dyn_delsq_vc, d.nVertices + d.nCells, d, p);
     LAUNCH(k_dyn_edges_rk1b, d.nEdgesSolve, d, p, cf, s);
@@ -678,8 +681,19 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
 }
 
-void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
-  LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step);
+double coef_divdamp(const mpas_dyc_ctx* ctx, double dts) {  // 2761-2763
+  const double rdts = 1.0 / dts;
+  return 2.0 * ctx->cf.smdiv * ctx->cf.len_disp * rdts;
+}
+
+// edge phase of acoustic sub-step `small_step`; damp = 1 also applies the divergence damping of
+// the previous sub-step (k_acoustic_edges<true>)
+void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int damp,
+                    int phase) {
+  if (damp)
+    LAUNCH(k_acoustic_edges<true>, d.nEdges, d, p, dts, small_step, coef_divdamp(ctx, dts), phase);
+  else
+    LAUNCH(k_acoustic_edges<false>, d.nEdges, d, p, dts, small_step, 0.0, phase);
 }
 
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
@@ -687,9 +701,7 @@ void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
 }
 
 void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase) {
-  const double rdts = 1.0 / dts;
-  const double coef_divdamp = 2.0 * ctx->cf.smdiv * ctx->cf.len_disp * rdts;
-  LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp, phase);
+  LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase);
 }
 
 void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt, int tl, int rk_step /*0 = absent*/) {
@@ -821,28 +833,43 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         CHK(exchange(ctx, {{"tend", "u", 0, 0x1u}}));             // 642
         EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, 0));     // 644-678
       }
-      // Acoustic sub-steps (788-870).  The reference exchanges rho_pp before every sub-step
-      // (792) and rtheta_pp after it (845).  Here the rho_pp exchange of sub-step n+1 travels
-      // with the rtheta_pp exchange of sub-step n: divergence damping, which runs in between,
-      // does not touch rho_pp, so the halo values are the same.  The exchange before sub-step 1
-      // is dropped: that sub-step's edge phase does not read rho_pp (2580-2599), and the cell phase
-      // reads and zeroes only owned columns (2617-2622).  The halo values it would have set are
-      // overwritten by the all-layer exchange at 876 before anything reads them.
+      // Acoustic sub-steps (788-870).
+      // * Exchanges.  The reference exchanges rho_pp before every sub-step (792) and rtheta_pp
+      //   after it (845).  Here the rho_pp exchange of sub-step n+1 travels with the rtheta_pp
+      //   exchange of sub-step n.  Divergence damping, which runs in between, does not touch
+      //   rho_pp, so the halo values are the same.  The exchange before sub-step 1 is dropped:
+      //   that sub-step's edge phase does not read rho_pp (2580-2599), the cell phase reads and
+      //   zeroes only owned columns (2617-2622), and the all-layer exchange at 876 overwrites
+      //   those halo values before anything reads them.
+      // * Damping.  The divergence damping of sub-step n (849-869) is fused into the edge phase
+      //   of sub-step n+1 (k_acoustic_edges<true>).  Only the last sub-step's damping is a
+      //   kernel of its own.
       const int nsub = number_sub_steps[rk_step - 1];
       for (int small_step = 1; small_step <= nsub; ++small_step) {
-        EACH(acoustic_edges(ctx, d, p, dts, small_step));         // 794-837
+        if (small_step == 1) {
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 0, 0));   // 794-837
+        } else if (split) {  // interior edges overlap the exchange issued after the last cell phase
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 1));
+          CHK(exchange_wait(ctx));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 2));
+        } else {
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0));
+        }
         EACH(acoustic_cells(ctx, d, p, dts, small_step));
         std::vector<XField> xf = {{"diag", "rtheta_pp", 0, 0x1u}};  // 845
         if (small_step < nsub) xf.push_back({"diag", "rho_pp", 0, 0x1u});  // 792 of the next sub-step
-        if (split) {  // 849-869: interior edges overlap the exchange
+        if (split) {
           CHK(exchange_async(ctx, xf));
-          EACH(divergence_damping(ctx, d, p, dts, 1));
-          CHK(exchange_wait(ctx));
-          EACH(divergence_damping(ctx, d, p, dts, 2));
         } else {
           CHK((exchange)(ctx, xf));  // parenthesised: no ADL lookup of std::exchange
-          EACH(divergence_damping(ctx, d, p, dts, 0));            // 849-869
         }
+      }
+      if (split) {  // the last sub-step's damping (849-869), interior edges overlapping the exchange
+        EACH(divergence_damping(ctx, d, p, dts, 1));
+        CHK(exchange_wait(ctx));
+        EACH(divergence_damping(ctx, d, p, dts, 2));
+      } else {
+        EACH(divergence_damping(ctx, d, p, dts, 0));
       }
       const std::vector<XField> xrec = {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},  // 876-887
                                         {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};
@@ -1446,31 +1473,33 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
   Block& b = ctx->blk[0];
   const Ptrs p = make_ptrs(ctx, b);
   const Dims& d = b.d;
+  // the sequence srk3 runs for a `reps`-sub-step acoustic loop: edges, cells, then per further
+  // sub-step the damped edge phase and cells, and the last sub-step's damping on its own
   double acc[3] = {0, 0, 0};
+  float t;
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   for (int r = 0; r < reps; ++r) {
     HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-    LAUNCH(k_acoustic_edges, d.nEdges, d, p, dts, small_step);
+    acoustic_edges(ctx, d, p, dts, small_step, r > 0 ? 1 : 0, 0);
     HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-    LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
+    acoustic_cells(ctx, d, p, dts, small_step);
     HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-    divergence_damping(ctx, d, p, dts, 0);
-    HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
     if (ms_kernels) {
-      HIPCHK(hipEventSynchronize(ctx->ev[4]));
-      float t;
+      HIPCHK(hipEventSynchronize(ctx->ev[3]));
       (void)hipEventElapsedTime(&t, ctx->ev[1], ctx->ev[2]);
       acc[0] += t;
       (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
       acc[1] += t;
-      (void)hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]);
-      acc[2] += t;
     }
   }
-  HIPCHK(hipEventRecord(ctx->ev[5], ctx->stream));
-  HIPCHK(hipEventSynchronize(ctx->ev[5]));
+  HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
+  divergence_damping(ctx, d, p, dts, 0);
+  HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
+  HIPCHK(hipEventSynchronize(ctx->ev[4]));
+  (void)hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]);
+  acc[2] += t;
   float tot;
-  HIPCHK(hipEventElapsedTime(&tot, ctx->ev[0], ctx->ev[5]));
+  HIPCHK(hipEventElapsedTime(&tot, ctx->ev[0], ctx->ev[4]));
   if (ms_out) *ms_out = tot / reps;
   if (ms_kernels)
     for (int i = 0; i < 3; ++i) ms_kernels[i] = acc[i] / reps;

@@ -238,28 +238,77 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells1(Dims d, Ptrs p, Co
 
 // edges: tend_u (edge-solve: PGF rk1 4781-4788, vertical transport 4792-4807, Coriolis/KE 4811-4838)
 // + rk1 del2 on all edges (4856-4883); finalize (Rayleigh + euler + physics, 5015-5036) when rk>1.
+// Like k_dyn_advflux this is latency bound: every column the edge reads is loaded before the
+// first use (RK1 adds the PGF and del2 operands), then the reference expressions are evaluated.
+template <bool RK1>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges(Dims d, Ptrs p, Config cf, DynTendScal s, int finalize) {
   const int e = wave_elem(0);
   if (e >= d.nEdges) return;
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
+  const size_t K1 = K + 1;
   const size_t o = (size_t)e * K + k;
   const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  const size_t o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
   const bool solve = e < d.nEdgesSolve;
-  double tue = act ? p.tend_u_euler[o] : 0.0;
+  const int neoe = solve ? p.nEdgesOnEdge[e] : 0;
+  const bool hex = neoe == 10;  // hexagon-hexagon edge: the 20 TRiSK gathers go out together
+  // ---- loads
   const double uk = LD(p.u2, o);
-  if (solve) {
-    if (s.rk_step == 1 && act) {
-      const size_t o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
-      tue = -p.cqu[o] * ((p.pressure_p[o2] - p.pressure_p[o1]) * p.invDcEdge[e] / (.5 * (p.zz[o2] + p.zz[o1])) -
-                         0.5 * p.zxu[o] * (p.dpdz[o1] + p.dpdz[o2]));
+  double tue = (act && !(RK1 && solve)) ? p.tend_u_euler[o] : 0.0;  // rk1 recomputes it on solve edges
+  double rw1 = 0.0, rw2 = 0.0, pve = 0.0, re = 0.0, ke1 = 0.0, ke2 = 0.0, hd1 = 0.0, hd2 = 0.0;
+  double pv[10], uu[10];
+  if (solve && k <= K) {
+    rw1 = p.rw[(size_t)c1 * K1 + k];
+    rw2 = p.rw[(size_t)c2 * K1 + k];
+  }
+  if (act && (solve || RK1)) re = p.rho_edge[o];
+  if (solve && act) {
+    pve = p.pv_edge[o];
+    if (hex) {
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const int eoe = uni(p.edgesOnEdge[e * d.maxEdges2 + j]);
+        pv[j] = p.pv_edge[(size_t)eoe * K + k];
+        uu[j] = p.u2[(size_t)eoe * K + k];
+      }
     }
+    ke1 = p.ke[o1];
+    ke2 = p.ke[o2];
+    hd1 = p.h_divergence[o1];
+    hd2 = p.h_divergence[o2];
+  }
+  double cqu = 0.0, pp1 = 0.0, pp2 = 0.0, zz1 = 0.0, zz2 = 0.0, zxu = 0.0, dpz1 = 0.0, dpz2 = 0.0;
+  double dv1 = 0.0, dv2 = 0.0, vo1 = 0.0, vo2 = 0.0, kd1 = 0.0, kd2 = 0.0;
+  if (RK1 && act) {
+    if (solve) {
+      cqu = p.cqu[o];
+      pp1 = p.pressure_p[o1];
+      pp2 = p.pressure_p[o2];
+      zz1 = p.zz[o1];
+      zz2 = p.zz[o2];
+      zxu = p.zxu[o];
+      dpz1 = p.dpdz[o1];
+      dpz2 = p.dpdz[o2];
+    }
+    const int v1 = p.verticesOnEdge[2 * e], v2 = p.verticesOnEdge[2 * e + 1];
+    dv1 = p.divergence[o1];
+    dv2 = p.divergence[o2];
+    vo1 = p.vorticity[(size_t)v1 * K + k];
+    vo2 = p.vorticity[(size_t)v2 * K + k];
+    kd1 = p.kdiff[o1];
+    kd2 = p.kdiff[o2];
+  }
+  // ---- tend_u
+  if (solve) {
+    if (RK1 && act)
+      tue = -cqu * ((pp2 - pp1) * p.invDcEdge[e] / (.5 * (zz2 + zz1)) - 0.5 * zxu * (dpz1 + dpz2));
     // vertical transport of u: wduz(k), k = 1..K+1 on lanes 0..K
     const double um1 = up1(uk), um2 = up2(uk), up1v = dn1(uk);
-    const double rwa = (k <= K) ? 0.5 * (p.rw[(size_t)c1 * (K + 1) + k] + p.rw[(size_t)c2 * (K + 1) + k]) : 0.0;
+    const double rwa = (k <= K) ? 0.5 * (rw1 + rw2) : 0.0;
     double wduz = 0.0;
     if (k == 1 || k == K - 1) {
-      wduz = 0.5 * (p.rw[(size_t)c1 * (K + 1) + k] + p.rw[(size_t)c2 * (K + 1) + k]) * (p.fzm[k] * uk + p.fzp[k] * um1);
+      wduz = 0.5 * (rw1 + rw2) * (p.fzm[k] * uk + p.fzp[k] * um1);
     } else if (k >= 2 && k <= K - 2) {
       wduz = flux3(um2, um1, uk, up1v, rwa, 1.0);
     }
@@ -267,16 +316,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges(Dims d, Ptrs p, Con
     double tu = act ? -p.rdzw[k] * (wduz_p - wduz) : 0.0;
     // nonlinear Coriolis term (Ringler et al. 2009)
     double q = 0.0;
-    const int neoe = p.nEdgesOnEdge[e];
-    const double pve = LD(p.pv_edge, o);
-    if (neoe == 10 && act) {  // hexagon-hexagon edge: all 20 gathers in flight at once
-      double pv[10], uu[10];
-#pragma unroll
-      for (int j = 0; j < 10; ++j) {
-        const int eoe = uni(p.edgesOnEdge[e * d.maxEdges2 + j]);
-        pv[j] = p.pv_edge[(size_t)eoe * K + k];
-        uu[j] = p.u2[(size_t)eoe * K + k];
-      }
+    if (hex && act) {
 #pragma unroll
       for (int j = 0; j < 10; ++j) {
         const double workpv = 0.5 * (pve + pv[j]);
@@ -289,32 +329,26 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges(Dims d, Ptrs p, Con
         q = q + p.weightsOnEdge[e * d.maxEdges2 + j] * LD(p.u2, (size_t)eoe * K + k) * workpv;
       }
     }
-    if (act) {
-      const size_t o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
-      tu = tu + p.rho_edge[o] * (q - (p.ke[o2] - p.ke[o1]) * p.invDcEdge[e]) -
-           uk * 0.5 * (p.h_divergence[o1] + p.h_divergence[o2]);
-    }
+    if (act) tu = tu + re * (q - (ke2 - ke1) * p.invDcEdge[e]) - uk * 0.5 * (hd1 + hd2);
     if (finalize && act) {
       if (cf.rayleigh_damp_u && k >= K - cf.number_rayleigh_damp_u_levels) {
         const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
-        tu = tu - p.rho_edge[o] * uk * coef;
+        tu = tu - re * uk * coef;
       }
       tu = tu + tue + PHYS_ZERO;  // tend_ru_physics
     }
     if (act) p.tend_u[o] = tu;
   }
-  if (s.rk_step == 1 && act) {
+  if (RK1 && act) {
     // del^2 part of the del^4 filter, all edges (4858-4883)
-    const int v1 = p.verticesOnEdge[2 * e], v2 = p.verticesOnEdge[2 * e + 1];
     const double r_dc = p.invDcEdge[e];
     const double r_dv = fmin(p.invDvEdge[e], 4 * p.invDcEdge[e]);
-    const double u_diffusion = (p.divergence[(size_t)c2 * K + k] - p.divergence[(size_t)c1 * K + k]) * r_dc -
-                               (p.vorticity[(size_t)v2 * K + k] - p.vorticity[(size_t)v1 * K + k]) * r_dv;
+    const double u_diffusion = (dv2 - dv1) * r_dc - (vo2 - vo1) * r_dv;
     p.delsq_u[o] = 0.0 + u_diffusion;
-    const double kdiffu = 0.5 * (p.kdiff[(size_t)c1 * K + k] + p.kdiff[(size_t)c2 * K + k]);
-    tue = tue + p.rho_edge[o] * kdiffu * u_diffusion * p.meshScalingDel2[e];
+    const double kdiffu = 0.5 * (kd1 + kd2);
+    tue = tue + re * kdiffu * u_diffusion * p.meshScalingDel2[e];
+    p.tend_u_euler[o] = tue;
   }
-  if (act && (s.rk_step == 1)) p.tend_u_euler[o] = tue;
 }
 
 // vertices: delsq_vorticity (4889-4898); cells: delsq_divergence (4900-4910)   [rk1, visc4>0]
@@ -445,19 +479,34 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells2(Dims d, Ptrs p) {
 // horizontal advection in atm_compute_dyn_tend_work (flux_arr at 5056-5066 and 5236-5244).
 // The reference recomputes them inside the cell loop for both cells of an edge; here each
 // edge is evaluated once (same expression, same order) and the cell kernel reads it back.
+// Latency, not bandwidth, bounds these gathers (one wave per edge, 20 neighbour columns
+// mostly from L2): every load the edge needs is issued before the first wait, index loads
+// first, then the 20 gathers, then the edge's own ru, so one memory round trip covers them.
 template <int NA>
-__device__ __forceinline__ void adv_edge_sums(const Ptrs& p, int e, int K, int k, double sgn_w, double sgn_t,
-                                              double& fw, double& ft) {
+__device__ __forceinline__ void adv_edge_sums(const Ptrs& p, int e, int K, int k, size_t o, bool act, double& fw,
+                                              double& ft) {
   const size_t K1 = K + 1;
-  double wv[NA], tv[NA];
   int ic[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) ic[j] = uni(p.advCellsForEdge[e * 15 + j]);
+  double wv[NA], tv[NA];
+  if (k <= K) {
 #pragma unroll
-  for (int j = 0; j < NA; ++j) {
-    wv[j] = p.w2[(size_t)ic[j] * K1 + k];
-    tv[j] = (k < K) ? p.theta_m2[(size_t)ic[j] * K + k] : 0.0;
+    for (int j = 0; j < NA; ++j) wv[j] = p.w2[(size_t)ic[j] * K1 + k];
+  } else {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) wv[j] = 0.0;
   }
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) tv[j] = p.theta_m2[(size_t)ic[j] * K + k];
+  } else {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) tv[j] = 0.0;
+  }
+  const double rue = LD(p.ru, o), rue_m = up1(rue);
+  const double ru_edge_w = act ? p.fzm[k] * rue + p.fzp[k] * rue_m : 0.0;
+  const double sgn_w = sgn1(ru_edge_w), sgn_t = sgn1(rue);
   fw = 0.0;
   ft = 0.0;
 #pragma unroll
@@ -476,15 +525,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_advflux(Dims d, Ptrs p) {
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
   const size_t o = (size_t)e * K + k;
-  const double rue = LD(p.ru, o), rue_m = up1(rue);
-  const double ru_edge_w = act ? p.fzm[k] * rue + p.fzp[k] * rue_m : 0.0;
-  const double sgn_w = sgn1(ru_edge_w), sgn_t = sgn1(rue);
   const int na = p.nAdvCellsForEdge[e];
   double fw = 0.0, ft = 0.0;
-  if (k <= K) {
-    if (na == 10) {
-      adv_edge_sums<10>(p, e, K, k, sgn_w, sgn_t, fw, ft);
-    } else {
+  if (na == 10) {
+    adv_edge_sums<10>(p, e, K, k, o, act, fw, ft);
+  } else {
+    const double rue = LD(p.ru, o), rue_m = up1(rue);
+    const double ru_edge_w = act ? p.fzm[k] * rue + p.fzp[k] * rue_m : 0.0;
+    const double sgn_w = sgn1(ru_edge_w), sgn_t = sgn1(rue);
+    if (k <= K) {
       for (int j = 0; j < na; ++j) {
         const int ic = uni(p.advCellsForEdge[e * 15 + j]);
         const double a = p.adv_coefs[e * 15 + j], b = p.adv_coefs_3rd[e * 15 + j];
@@ -675,10 +724,19 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p, 
 // ============================================================================
 // atm_advance_acoustic_step_work  (mpas_atm_time_integration.F:2535-2721)
 // ============================================================================
-// edge phase (2540-2601): edges with >=1 owned cell
-__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step) {
+// edge phase (2540-2601): edges with >=1 owned cell.
+// DD: first apply the divergence damping of the previous sub-step (atm_divergence_damping_3d,
+// 2765-2793, same expression), then this sub-step's update.  srk3 calls damping and the next
+// edge phase back to back on the same edges (849-869, then 794-837), with only the rtheta_pp /
+// rho_pp halo exchange in between, so one pass over ru_p does both.  The sum is the same
+// double either way: the damped ru_p is rounded before the update adds to it.
+// phase: 0 = every edge; 1 / 2 = edges without / with a halo cell (split around that exchange).
+template <bool DD>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step,
+                                                                  double coef_divdamp, int phase) {
   const int e = wave_elem(0);
   if (e >= d.nEdges) return;
+  if (phase && ((p.edge_bnd[e] != 0) != (phase == 2))) return;
   const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
   if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
   const int k = lane_id(), K = d.K;
@@ -688,10 +746,17 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p
     const double rcv = RGAS / (CP - RGAS);
     const double c2v = CP * rcv;
     const size_t o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
-    double pgrad = ((p.rtheta_pp[o2] - p.rtheta_pp[o1]) * p.invDcEdge[e]) / (.5 * (p.zz[o2] + p.zz[o1]));
+    const double rt1 = p.rtheta_pp[o1], rt2 = p.rtheta_pp[o2];
+    double rup = p.ru_p[o];
+    if (DD) {
+      const double d1 = -(rt1 - p.rtheta_pp_old[o1]);
+      const double d2 = -(rt2 - p.rtheta_pp_old[o2]);
+      rup = rup + coef_divdamp * (d2 - d1) * (1.0 - p.specZoneMaskEdge[e]) / (p.theta_m1[o1] + p.theta_m1[o2]);
+    }
+    double pgrad = ((rt2 - rt1) * p.invDcEdge[e]) / (.5 * (p.zz[o2] + p.zz[o1]));
     pgrad = p.cqu[o] * 0.5 * c2v * (p.exner[o1] + p.exner[o2]) * pgrad;
     pgrad = pgrad + 0.5 * p.zxu[o] * GRAVITY * (p.rho_pp[o1] + p.rho_pp[o2]);
-    const double rup = p.ru_p[o] + dts * (p.tend_u[o] - (1.0 - p.specZoneMaskEdge[e]) * pgrad);
+    rup = rup + dts * (p.tend_u[o] - (1.0 - p.specZoneMaskEdge[e]) * pgrad);
     p.ru_p[o] = rup;
     p.ruAvg[o] = p.ruAvg[o] + rup;
   } else {

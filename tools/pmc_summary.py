@@ -20,7 +20,8 @@ def load(path):
         for r in csv.DictReader(f):
             name = r["Kernel_Name"].split("(")[0].replace("mpas::", "")
             per[name].append((float(r["Counter_Value"]) * 1024.0,
-                              (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))
+                              (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9,
+                              int(r["Dispatch_Id"])))
     return per
 
 
@@ -32,31 +33,33 @@ def main():
     # calibration: k_copy_many moves (nE*K + 2 nC*(K+1) + 6 nC*K + nC*K*ns) doubles each way
     nE = 3 * nC - 6 if nC > 12 else 0
     known = 8.0 * (2 * nE * K + 2 * nC * (K + 1) + 5 * nC * K + nC * K * ns)
-    cf = known / (sum(v for v, _ in fetch["k_copy_many"]) / len(fetch["k_copy_many"]))
-    cw = known / (sum(v for v, _ in write["k_copy_many"]) / len(write["k_copy_many"]))
+    cf = known / (sum(x[0] for x in fetch["k_copy_many"]) / len(fetch["k_copy_many"]))
+    cw = known / (sum(x[0] for x in write["k_copy_many"]) / len(write["k_copy_many"]))
     rows = []
     for name in fetch:
         if name not in write:
             continue
-        f = sum(v for v, _ in fetch[name]) / len(fetch[name]) * cf
-        w = sum(v for v, _ in write[name]) / len(write[name]) * cw
+        f = sum(x[0] for x in fetch[name]) / len(fetch[name]) * cf
+        w = sum(x[0] for x in write[name]) / len(write[name]) * cw
         rows.append(dict(kernel=name, dispatches=len(fetch[name]), read_bytes=f, write_bytes=w))
     rows.sort(key=lambda r: -(r["read_bytes"] + r["write_bytes"]) * r["dispatches"])
     out = dict(ncells=nC, levels=K, num_scalars=ns, fetch_calibration=cf, write_calibration=cw,
                method="rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; per-dispatch mean; "
                       "FETCH/WRITE scaled by the factor that makes k_copy_many (known bytes) exact",
                kernels=rows)
-    # the roofline sub-step is the one bench.py times: the last `reps` dispatches of each
-    # acoustic kernel (time_acoustic_step, small_step = 2)
+    # the roofline sub-step is the one bench.py times: the acoustic loop of time_acoustic_step
+    # (small_step = 2), selected as in tools/acoustic_from_trace.py, per sub-step
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from acoustic_from_trace import tail_dispatches
     reps = int(os.environ.get("ACOUSTIC_REPS", "5"))
     tot = 0.0
     per = {}
-    for name in fetch:
-        if any(t in name for t in ("k_acoustic_edges", "k_acoustic_cells", "k_divdamp")):
-            f = sum(v for v, _ in fetch[name][-reps:]) / reps * cf
-            w = sum(v for v, _ in write[name][-reps:]) / reps * cw
-            per[name] = dict(read_bytes=f, write_bytes=w)
-            tot += f + w
+    for src, scale, key in ((fetch, cf, "read_bytes"), (write, cw, "write_bytes")):
+        rows = [(x[2], name, x[0]) for name, v in src.items() for x in v]
+        for fam, vals in tail_dispatches(rows, reps).items():
+            b = sum(vals) / reps * scale
+            per.setdefault(fam, {})[key] = b
+            tot += b
     out["acoustic_substep_kernels"] = per
     out["bytes_per_substep"] = tot
     print(json.dumps(out, indent=1))
