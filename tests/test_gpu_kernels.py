@@ -1,6 +1,6 @@
-"""Per-kernel GPU parity: the HIP acoustic sub-step (k_acoustic_edges + k_acoustic_cells +
-k_divdamp, through the C ABI) on the committed reference fixture.  Every input the kernels
-read is uploaded from the fixture, so the comparison is independent of the host that built it."""
+"""Per-kernel GPU parity: the HIP acoustic sub-step (k_acoustic_edges + k_acoustic_cells + k_divdamp,
+through the C ABI) on the committed reference fixture.  Every input the kernels read is uploaded
+from the fixture, so the comparison is independent of the host that built it."""
 import os
 
 import numpy as np
@@ -17,7 +17,7 @@ def _pad(a):
     return np.ascontiguousarray(np.concatenate([a, np.zeros((1,) + a.shape[1:])], 0))
 
 
-def test_acoustic_substep_matches_reference_fixture():
+def _fixture_dycore():
     from mpas_dycore import Dycore
     from mpas_dycore.cases import jw_case
     z = np.load(os.path.join(GOLD, "acoustic_x1.162_K16.npz"))
@@ -36,11 +36,36 @@ def test_acoustic_substep_matches_reference_fixture():
         a = z[k]
         img = np.ascontiguousarray(a, dtype=np.float64) if name == "cofrz" else _pad(a)
         dy.set_raw(pool, name, img, tl)
+    return z, dy
+
+
+POST = ("ru_p", "ruAvg", "rho_pp", "rtheta_pp", "rtheta_pp_old", "rw_p", "wwAvg")
+
+
+def test_acoustic_substep_matches_reference_fixture():
+    z, dy = _fixture_dycore()
     dy.time_acoustic_step(float(z["dts"]), small_step=int(z["small_step"]), reps=1)
     dy.synchronize()
-    for n in ("ru_p", "ruAvg", "rho_pp", "rtheta_pp", "rtheta_pp_old", "rw_p", "wwAvg"):
+    for n in POST:
         got = dy.get("diag", n)
         ref = z["post_diag." + n]
         err = rel_linf(got.reshape(ref.shape), ref)
         assert err <= 1e-14, f"{n}: rel Linf {err:.3e}"
     dy.close()
+
+
+def test_fused_substep_loop_equals_substeps_with_damping():
+    """A 3-sub-step loop (each damping fused into the next sub-step's edge phase) gives the same
+    bits as three single sub-steps each followed by its own damping kernel (the reference order)."""
+    z, a = _fixture_dycore()
+    for _ in range(3):
+        a.time_acoustic_step(float(z["dts"]), small_step=int(z["small_step"]), reps=1)
+    a.synchronize()
+    want = {n: a.get("diag", n) for n in POST}
+    a.close()
+    z, b = _fixture_dycore()
+    b.time_acoustic_step(float(z["dts"]), small_step=int(z["small_step"]), reps=3)
+    b.synchronize()
+    for n in POST:
+        assert np.array_equal(b.get("diag", n), want[n]), n
+    b.close()
