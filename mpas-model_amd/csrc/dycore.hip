@@ -649,7 +649,9 @@ void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts)
   LAUNCH(k_vert_imp_coefs, std::max(d.nCellsSolve, 1), d, p, dts, ctx->cf.epssm);
 }
 
-void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, double dt) {
+// part: 0 = all kernels; 1 = only k_dyn_cells1, which reads nothing the exchange after the
+// diagnostics (1234-1249) or at the substep boundary (1282-1297) delivers; 2 = the rest
+void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, double dt, int part = 0) {
   const Config& cf = ctx->cf;
   DynTendScal s{};
   s.rk_step = rk_step;
@@ -667,7 +669,8 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   if (cf.rayleigh_damp_u)
     s.rayleigh_coef_inverse = 1.0 / ((double)cf.number_rayleigh_damp_u_levels *
                                      (cf.rayleigh_damp_u_timescale_days * SECONDS_PER_DAY));
-  LAUNCH(k_dyn_cells1, d.nCells, d, p, cf, s);
+  if (part != 2) LAUNCH(k_dyn_cells1, d.nCells, d, p, cf, s);
+  if (part == 1) return;
   if (rk_step == 1)
     LAUNCH(k_dyn_edges<true>, d.nEdges, d, p, cf, s, 0);
   else
@@ -817,12 +820,26 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   EACH(LAUNCH(k_moist_edges, d.nEdges, d, p));
   // physics tendencies are zero without DO_PHYSICS (450-457): scratch arrays stay zero.
 
+  // Deferred exchanges.  With split-phase exchanges, the exchange after the diagnostics
+  // (1234-1249) runs on the exchange stream while the next kernels that do not read its fields
+  // run: the next stage's k_dyn_cells1, and vert_imp_coefs where it comes first.  Without
+  // split-phase exchanges, xchg blocks and xwait is a no-op, and the launch order is the same.
+  auto xchg = [&](const std::vector<XField>& fs) { return split ? exchange_async(ctx, fs) : (exchange)(ctx, fs); };
+  auto xwait = [&]() { return split ? exchange_wait(ctx) : MPAS_DYC_OK; };
+  bool pending = false;  // an xchg whose xwait is still due
+  EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));           // 476-510 of dynamics substep 1
   for (int dynamics_substep = 1; dynamics_substep <= dynamics_split; ++dynamics_substep) {
-    EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));         // 476-510
     // 513 (exner): carried by the step-start exchange and by the 1282-1297 exchange below
     for (int rk_step = 1; rk_step <= 3; ++rk_step) {
       if (cf.time_integration_order == 3 && rk_step == 2) EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[1]));
-      EACH(dyn_tend(ctx, d, p, rk_step, dt));                     // 561-630
+      if (pending) {  // 561-630, k_dyn_cells1 overlapping the exchange
+        EACH(dyn_tend(ctx, d, p, rk_step, dt, 1));
+        CHK(xwait());
+        pending = false;
+        EACH(dyn_tend(ctx, d, p, rk_step, dt, 2));
+      } else {
+        EACH(dyn_tend(ctx, d, p, rk_step, dt));                   // 561-630
+      }
       const double dts = rk_sub_timestep[rk_step - 1];
       if (split) {  // 642 | 644-678: interior cells overlap the tend_u exchange
         CHK(exchange_async(ctx, {{"tend", "u", 0, 0x1u}}));
@@ -875,22 +892,25 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
                                         {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};
       const double invNs = 1 / (double)number_sub_steps[rk_step - 1];
       const double rdt = rk_timestep[rk_step - 1];
-      if (split) {  // 889-988: owned cells, interior edges and cells overlap the exchange
+      if (split) {
+        // 889-1185: owned cells and interior edges overlap the 876-887 exchange; once every
+        // owned u is final, the u exchange (988) overlaps the w recovery, which does not read u
         CHK(exchange_async(ctx, xrec));
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 1));
         EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1));
-        EACH(LAUNCH(k_recover_cells3, d.nCells, d, p, 1));
         CHK(exchange_wait(ctx));
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 2));
         EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
-        EACH(LAUNCH(k_recover_cells3, d.nCells, d, p, 2));
+        CHK(exchange_async(ctx, {{"state", "u", 2, ALL_LAYERS}}));
+        EACH(LAUNCH(k_recover_cells3, d.nCells, d, p, 0));
+        CHK(exchange_wait(ctx));
       } else {
         CHK((exchange)(ctx, xrec));
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0));  // 889-930
         EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0));
         EACH(LAUNCH(k_recover_cells3, d.nCells, d, p, 0));
+        CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));      // 988
       }
-      CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));        // 988
       if (scalars_in_dynamics) {                                  // 993-1185
         if (rk_step < 3 || (!cf.monotonic && !cf.positive_definite)) {
           EACH(advance_scalars(ctx, d, p, rk_timestep[rk_step - 1], rk_step, false));
@@ -899,16 +919,26 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         }
       }
       EACH(solve_diagnostics(ctx, d, p, dt, 2, rk_step));         // 1187-1228
-      if (scalars_in_dynamics)                                    // 1234-1249
-        CHK(exchange(ctx, {{"state", "w", 2, ALL_LAYERS}, {"diag", "pv_edge", 0, ALL_LAYERS},
-                           {"diag", "rho_edge", 0, ALL_LAYERS}, {"state", "scalars", 2, ALL_LAYERS}}));
-      else
-        CHK(exchange(ctx, {{"state", "w", 2, ALL_LAYERS}, {"diag", "pv_edge", 0, ALL_LAYERS},
-                           {"diag", "rho_edge", 0, ALL_LAYERS}}));
+      std::vector<XField> xd = {{"state", "w", 2, ALL_LAYERS}, {"diag", "pv_edge", 0, ALL_LAYERS},  // 1234-1249
+                                {"diag", "rho_edge", 0, ALL_LAYERS}};
+      if (scalars_in_dynamics) xd.push_back({"state", "scalars", 2, ALL_LAYERS});
+      if (rk_step < 3) {
+        CHK(xchg(xd));  // waited for inside the next stage's dyn_tend
+        pending = true;
+      } else if (dynamics_substep < dynamics_split) {
+        // 1282-1297 follows 1234-1249 with nothing in between: one exchange carries both
+        // (plus the next substep's 513, exner).  The next substep's vert_imp_coefs overlaps it:
+        // it reads none of these fields' halos, and substep_finish, which now runs after it,
+        // writes nothing it reads.
+        xd.insert(xd.end(), {{"state", "theta_m", 2, ALL_LAYERS}, {"diag", "pressure_p", 0, ALL_LAYERS},
+                             {"diag", "rtheta_p", 0, ALL_LAYERS}, {"diag", "exner", 0, ALL_LAYERS}});
+        CHK(xchg(xd));
+        EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));     // 476-510 of the next substep
+        CHK(xwait());
+      } else {
+        CHK((exchange)(ctx, xd));
+      }
     }
-    if (dynamics_substep < dynamics_split)                        // 1282-1297 + 513 of the next substep
-      CHK(exchange(ctx, {{"state", "theta_m", 2, ALL_LAYERS}, {"diag", "pressure_p", 0, ALL_LAYERS},
-                         {"diag", "rtheta_p", 0, ALL_LAYERS}, {"diag", "exner", 0, ALL_LAYERS}}));
     EACH(LAUNCH(k_substep_finish, d.nEdges + d.nCells, d, p, dynamics_substep, dynamics_split,
                 1.0 / (double)dynamics_split));                   // 1304-1341
   }
