@@ -87,6 +87,14 @@ struct Ptrs {
   // CELL_HALO_EDGE = an edge of the cell is a halo edge, CELL_BND_EDGE = an edge of the cell has
   // edge_bnd set; halo cells have both bits.
   const int *edge_bnd, *cell_bnd;
+  // per-cell stencil records (built on the device from edgesOnCell / cellsOnEdge / dvEdge,
+  // k_build_cell_rec): cell_rec = 16 int32 per cell, [0, 7) edgesOnCell, [7, 14) the cell across
+  // each of those edges, [14] nEdgesOnCell, unused slots -> garbage element; cell_sdv =
+  // edgesOnCell_sign * dvEdge (maxEdges doubles per cell).  A cell reads its whole stencil with
+  // one scalar load.
+  const int* cell_rec;
+  const double* cell_sdv;
 };
+constexpr int CELL_REC = 16, CELL_REC_ME = 7;
 
 }  // namespace mpas

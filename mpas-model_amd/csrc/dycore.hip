@@ -258,6 +258,8 @@ void build_registry(Block& c) {
   add(c, "scratch", "wdtn", L_CELL, K + 1);
   add(c, "scratch", "edge_bnd", L_EDGE, 1, 1, true);
   add(c, "scratch", "cell_bnd", L_CELL, 1, 1, true);
+  add(c, "scratch", "cell_rec", L_CELL, CELL_REC, 1, true);
+  add(c, "scratch", "cell_sdv", L_CELL, ME);
 }
 
 Field* find(Block& b, const char* pool, const char* name) {
@@ -322,6 +324,8 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   SC(advflux_w); SC(advflux_th);
   p.edge_bnd = P<const int>(c, b, "scratch", "edge_bnd");
   p.cell_bnd = P<const int>(c, b, "scratch", "cell_bnd");
+  p.cell_rec = P<const int>(c, b, "scratch", "cell_rec");
+  p.cell_sdv = P<const double>(c, b, "scratch", "cell_sdv");
   // 0-d mesh fields are mirrored on the host
   p.cf1 = b.fields[b.by_name["mesh.cf1"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf1"]].buf[1] : 0.0;
   p.cf2 = b.fields[b.by_name["mesh.cf2"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf2"]].buf[1] : 0.0;
@@ -588,6 +592,13 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
     }
     HIPCHK(hipMemcpy(find(b, "scratch", "edge_bnd")->buf[0], eb.data(), eb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(find(b, "scratch", "cell_bnd")->buf[0], cb.data(), cb.size() * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_build_cell_rec, dim3((d.nCells + 1 + 255) / 256), dim3(256), 0, ctx->stream, d,
+                       P<const int>(ctx, b, "mesh", "nEdgesOnCell"), P<const int>(ctx, b, "mesh", "edgesOnCell"),
+                       P<const int>(ctx, b, "mesh", "cellsOnEdge"), P<const double>(ctx, b, "mesh", "dvEdge"),
+                       P<const double>(ctx, b, "mesh", "edgesOnCell_sign"), P<int>(ctx, b, "scratch", "cell_rec"),
+                       P<double>(ctx, b, "scratch", "cell_sdv"));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
   }
   ctx->bnd_ready = true;
   return MPAS_DYC_OK;
@@ -681,6 +692,15 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     LAUNCH(k_dyn_cells2, d.nCells, d, p);
   }
   LAUNCH(k_dyn_advflux, d.nEdges, d, p);
+#ifndef MPAS_NO_CELL_REC
+  if (d.maxEdges == 6 || d.maxEdges == 7) {
+    if (d.maxEdges == 6 && rk_step == 1) LAUNCH((k_dyn_cells3_r<6, true>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 6 && rk_step != 1) LAUNCH((k_dyn_cells3_r<6, false>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 7 && rk_step == 1) LAUNCH((k_dyn_cells3_r<7, true>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 7 && rk_step != 1) LAUNCH((k_dyn_cells3_r<7, false>), d.nCellsSolve, d, p, cf, s);
+    return;
+  }
+#endif
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
 }
 
@@ -700,6 +720,16 @@ void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
 }
 
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
+#ifndef MPAS_NO_CELL_REC
+  if (d.maxEdges == 6) {
+    LAUNCH(k_acoustic_cells_r<6>, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
+    return;
+  }
+  if (d.maxEdges == 7) {
+    LAUNCH(k_acoustic_cells_r<7>, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
+    return;
+  }
+#endif
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
 }
 
@@ -1059,8 +1089,8 @@ void count_active_edges(Block& b, const int32_t* coe) {
 
 // build the exchange plans of both time-level parities of a step outside graph capture
 int plan_all(mpas_dyc_ctx* ctx, double dt) {
-  if (!needs_exchange(ctx) || ctx->planned[ctx->cur]) return MPAS_DYC_OK;
   if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
+  if (!needs_exchange(ctx) || ctx->planned[ctx->cur]) return MPAS_DYC_OK;
   ctx->planning = true;
   int r = srk3(ctx, dt);
   ctx->planning = false;
@@ -1415,6 +1445,7 @@ int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name
 int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
   if (!ctx) return MPAS_DYC_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
+  if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
   int r = init_diagnostics(ctx, dt);
   HIPCHK(hipGetLastError());
   return r;
@@ -1500,6 +1531,7 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
                                 double* ms_kernels) {
   if (!ctx || reps < 1) return MPAS_DYC_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
+  if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
   Block& b = ctx->blk[0];
   const Ptrs p = make_ptrs(ctx, b);
   const Dims& d = b.d;

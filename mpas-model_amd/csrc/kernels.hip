@@ -57,6 +57,14 @@ __device__ __forceinline__ double up1(double x) { return __shfl_up(x, 1, 64); }
 __device__ __forceinline__ double dn1(double x) { return __shfl_down(x, 1, 64); }
 __device__ __forceinline__ double up2(double x) { return __shfl_up(x, 2, 64); }
 
+// A wave-uniform fp64 mesh value read as two int32 halves: integer loads cannot alias the
+// kernel's fp64 stores (TBAA), so the compiler proves them unclobbered and issues them on the
+// scalar unit (SGPRs) instead of spending vector registers on a broadcast.
+__device__ __forceinline__ double ld_uniform_f64(const double* a) {
+  const int* q = reinterpret_cast<const int*>(a);
+  return __hiloint2double(q[1], q[0]);
+}
+
 __device__ __forceinline__ double readlane_d(double v, int l) {
   int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
@@ -81,6 +89,72 @@ __device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, 
 // 268-279, 450-457): the kernels add the same +0.0 without streaming the zero arrays.
 #define PHYS_ZERO 0.0
 #define LDW(p, i) (actw ? (p)[(i)] : 0.0)
+
+// Per-cell stencil records (dycore.h, Ptrs::cell_rec / cell_sdv), one thread per cell.  The
+// cell across edge i is the other entry of cellsOnEdge, exactly the operand the reference
+// loops pick with their cellsOnEdge(1/2,iEdge) tests.  cell_sdv = edgesOnCell_sign * dvEdge:
+// the sign is +-1, so edgesOnCell_sign * x * dvEdge == x * cell_sdv bit for bit for any x.
+__global__ void k_build_cell_rec(Dims d, const int* __restrict__ noc, const int* __restrict__ eoc,
+                                 const int* __restrict__ coe, const double* __restrict__ dvEdge,
+                                 const double* __restrict__ sign, int* rec, double* cdv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > d.nCells) return;
+  const int ne = (c < d.nCells) ? noc[c] : 0;
+  for (int i = 0; i < CELL_REC_ME; ++i) {
+    int e = d.nEdges, o = d.nCells;
+    if (i < ne && i < d.maxEdges) {
+      e = eoc[(size_t)c * d.maxEdges + i];
+      if (e >= 0 && e < d.nEdges) {
+        const int c1 = coe[2 * e], c2 = coe[2 * e + 1];
+        o = (c1 == c) ? c2 : c1;
+      } else {
+        e = d.nEdges;
+      }
+    }
+    rec[(size_t)c * CELL_REC + i] = e;
+    rec[(size_t)c * CELL_REC + CELL_REC_ME + i] = o;
+    if (i < d.maxEdges)
+      cdv[(size_t)c * d.maxEdges + i] = (i < ne) ? sign[(size_t)c * d.maxEdges + i] * dvEdge[e] : 0.0;
+  }
+  // bits 2i..2i+1: edgesOnCell_sign code (0: +1, 1: -1, 2: 0, mpas_atm_core.F:1041-1050);
+  // bit 16+i: this cell is cellsOnEdge(1) of edge i
+  int bits = 0;
+  for (int i = 0; i < CELL_REC_ME && i < d.maxEdges; ++i) {
+    if (i >= ne) continue;
+    const double sg = sign[(size_t)c * d.maxEdges + i];
+    bits |= (sg > 0.0 ? 0 : (sg < 0.0 ? 1 : 2)) << (2 * i);
+    const int e = rec[(size_t)c * CELL_REC + i];
+    if (e < d.nEdges && coe[2 * e] == c) bits |= 1 << (16 + i);
+  }
+  rec[(size_t)c * CELL_REC + 14] = ne;
+  rec[(size_t)c * CELL_REC + 15] = bits;
+}
+
+// A cell's stencil from its record: one scalar round trip (see k_build_cell_rec).
+template <int ME>
+struct CellSten {
+  int e[ME], o[ME];
+  int ne, bits;
+  // edgesOnCell_sign(i): exactly +1, -1 or 0, as atm_compute_signs stores it
+  __device__ __forceinline__ double sg(int i) const {
+    const int s = (bits >> (2 * i)) & 3;
+    return s == 0 ? 1.0 : (s == 1 ? -1.0 : 0.0);
+  }
+  __device__ __forceinline__ bool first(int i) const { return (bits >> (16 + i)) & 1; }
+};
+template <int ME>
+__device__ __forceinline__ CellSten<ME> load_sten(const Ptrs& p, int c) {
+  CellSten<ME> s;
+  const int* r = p.cell_rec + (size_t)c * CELL_REC;
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    s.e[i] = r[i];
+    s.o[i] = r[CELL_REC_ME + i];
+  }
+  s.ne = r[14];
+  s.bits = r[15];
+  return s;
+}
 
 // ============================================================================
 // atm_compute_moist_coefficients  (mpas_atm_time_integration.F:1899-1931)
@@ -548,6 +622,162 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_advflux(Dims d, Ptrs p) {
   }
 }
 
+// k_dyn_cells3 on the per-cell stencil record (ME = maxEdges <= 7, RK1 = rk_step == 1): the
+// edge columns of every edge of the cell (and the cells across them) are loaded in one batch
+// after a single scalar round trip; the sums keep the reference order edge by edge.
+template <int ME, bool RK1>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3_r(Dims d, Ptrs p, Config cf, DynTendScal s) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const bool actw = k <= K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
+  const CellSten<ME> st = load_sten<ME>(p, c);
+  const bool del4w = RK1 && s.h_mom_eddy_visc4 > 0.0, del4t = RK1 && s.h_theta_eddy_visc4 > 0.0;
+  // ---- every load up front
+  double rue[ME], afw[ME], aft[ME], x1[ME], x2[ME];  // x1/x2: rk>1 ru_save, theta_m across; rk1 delsq_w / delsq_theta across
+  double sdv[ME], msi[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const size_t oe = (size_t)st.e[i] * K + kc, oc = (size_t)st.o[i] * K + kc;
+    rue[i] = p.ru[oe];
+    afw[i] = p.advflux_w[oe];
+    aft[i] = p.advflux_th[oe];
+    if (RK1) {
+      x1[i] = del4w ? p.delsq_w[oc] : 0.0;
+      x2[i] = del4t ? p.delsq_theta[oc] : 0.0;
+      sdv[i] = ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i);
+      msi[i] = 0.0;
+      if (del4w || del4t) msi[i] = ld_uniform_f64(p.meshScalingDel4 + st.e[i]);
+    } else {
+      x1[i] = p.ru_save[oe];
+      x2[i] = p.theta_m1[oc];
+      sdv[i] = ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i);
+    }
+  }
+  double idc[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) idc[i] = RK1 && (del4w || del4t) ? ld_uniform_f64(p.invDcEdge + st.e[i]) : 0.0;
+  const double invA = ld_uniform_f64(p.invAreaCell + c);
+  const double fzm = p.fzm[kc], fzp = p.fzp[kc], rdzu = p.rdzu[kc], rdzw_k = p.rdzw[kc];
+  const double thc1 = p.theta_m1[o];
+  const double twe0 = p.tend_w_euler[ow];
+  const double wk = p.w2[ow], rwk = p.rw[ow];
+  const double ppk = p.pressure_p[o], dpk = p.dpdz[o], cqw = p.cqw[o];
+  const double rz = p.rho_zz2[o];
+  const double dsw = del4w ? p.delsq_w[o] : 0.0, dst = del4t ? p.delsq_theta[o] : 0.0;
+  const double tte0 = p.tend_theta_euler[o];
+  const double th = p.theta_m2[o], rws = p.rw_save[ow];
+  const double rtd = d.diabatic ? p.rt_diabatic_tend[o] : 0.0;
+  // ---- horizontal advection of w (5046-5074) and theta (5231-5252)
+  double tw = 0.0, tt = 0.0;
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const double rue_m = up1(rue[i]);
+    if (i < st.ne) {
+      const double sg = st.sg(i);
+      const double ru_edge_w = fzm * rue[i] + fzp * rue_m;
+      tw = tw - sg * ru_edge_w * afw[i];
+      tt = tt - sg * rue[i] * aft[i];
+    }
+  }
+  // ---- w euler tendency: del4 (rk1, 5134-5152)
+  double twe = twe0;
+  if (del4w) {
+    const double r_areaCell = s.h_mom_eddy_visc4 * invA;
+#pragma unroll
+    for (int i = 0; i < ME; ++i) {
+      if (i < st.ne) {
+        const double edge_sign = msi[i] * r_areaCell * sdv[i] * idc[i];
+        const double dd = st.first(i) ? (x1[i] - dsw) : (dsw - x1[i]);  // delsq_w(cell2) - delsq_w(cell1)
+        if (act && k >= 1) twe = twe - edge_sign * dd;
+      }
+    }
+  }
+  // ---- w: vertical advection, PGF/buoyancy (5167-5197)
+  const double wm1 = up1(wk), wm2 = up2(wk), wp1 = dn1(wk), rwm1 = up1(rwk);
+  double wdwz = 0.0;
+  if (k == 1 || k == K - 1) wdwz = 0.25 * (rwk + rwm1) * (wk + wm1);
+  else if (k >= 2 && k <= K - 2) wdwz = flux3(wm2, wm1, wk, wp1, 0.5 * (rwk + rwm1), 1.0);
+  const double wdwz_p = dn1(wdwz);
+  if (act && k >= 1) tw = tw * invA - rdzu * (wdwz_p - wdwz);
+  const double ppm = up1(ppk), dpm = up1(dpk);
+  if (RK1 && act && k >= 1) twe = twe - cqw * (rdzu * (ppk - ppm) - (fzm * dpk + fzp * dpm));
+  const double rzm = up1(rz), rdzw_m = up1(rdzw_k);
+  if (RK1 && cf.v_mom_eddy_visc2 > 0.0) {
+    if (act && k >= 1)
+      twe = twe + cf.v_mom_eddy_visc2 * 0.5 * (rz + rzm) * ((wp1 - wk) * rdzw_k - (wk - wm1) * rdzw_m) * rdzu;
+  }
+  if (act && k >= 1) tw = tw + twe;
+  // ---- perturbation flux for rtheta_pp (rk > 1, 5256-5269), after all advection terms
+  if (!RK1) {
+#pragma unroll
+    for (int i = 0; i < ME; ++i) {
+      if (i < st.ne) {
+        const double flux = sdv[i] * (x1[i] - rue[i]) * 0.5 * (x2[i] + thc1);  // sign*dvEdge*(ru_save-ru)*0.5*(th2+th1)
+        if (act) tt = tt - flux;
+      }
+    }
+  }
+  // ---- theta euler tendency: del4 (rk1, 5305-5323)
+  double tte = tte0;
+  if (del4t) {
+    const double r_areaCell = s.h_theta_eddy_visc4 * (1.0 / PRANDTL) * invA;
+#pragma unroll
+    for (int i = 0; i < ME; ++i) {
+      if (i < st.ne) {
+        const double edge_sign = msi[i] * r_areaCell * sdv[i] * idc[i];
+        const double dd = st.first(i) ? (x2[i] - dst) : (dst - x2[i]);
+        if (act) tte = tte - edge_sign * dd;
+      }
+    }
+  }
+  // ---- theta: vertical advection (5331-5354)
+  const double thm1 = up1(th), thm2 = up2(th), thp1 = dn1(th);
+  const double ths = thc1, thsm1 = up1(ths);
+  double wdtz = 0.0;
+  if (k == 1) {
+    wdtz = rwk * (fzm * th + fzp * thm1);
+    wdtz = wdtz + (rws - rwk) * (fzm * ths + fzp * thsm1);
+  } else if (k >= 2 && k <= K - 2) {
+    wdtz = flux3(thm2, thm1, th, thp1, rwk, s.coef_3rd_order);
+    wdtz = wdtz + (rws - rwk) * (fzm * ths + fzp * thsm1);
+  } else if (k == K - 1) {
+    wdtz = rws * (fzm * th + fzp * thm1);
+  }
+  const double wdtz_p = dn1(wdtz);
+  if (RK1 && cf.v_theta_eddy_visc2 > 0.0) {
+    if (act && k >= 1 && k <= K - 2) {
+      const size_t zo = (size_t)c * K1;
+      const double z1 = p.zgrid[zo + k - 1], z2 = p.zgrid[zo + k], z3 = p.zgrid[zo + k + 1], z4 = p.zgrid[zo + k + 2];
+      const double zm = 0.5 * (z1 + z2), z0 = 0.5 * (z2 + z3), zp = 0.5 * (z3 + z4);
+      if (cf.mix_full) {
+        tte = tte + cf.v_theta_eddy_visc2 * (1.0 / PRANDTL) * rz *
+                        ((thp1 - th) / (zp - z0) - (th - thm1) / (z0 - zm)) / (0.5 * (zp - zm));
+      } else {
+        const double ti = p.t_init[o], tim = p.t_init[o - 1], tip = p.t_init[o + 1];
+        tte = tte + cf.v_theta_eddy_visc2 * (1.0 / PRANDTL) * rz *
+                        (((thp1 - tip) - (th - ti)) / (zp - z0) - ((th - ti) - (thm1 - tim)) / (z0 - zm)) / (0.5 * (zp - zm));
+      }
+    }
+  }
+  if (actw) {
+    p.tend_w[ow] = (act && k >= 1) ? tw : 0.0;
+    if (RK1) p.tend_w_euler[ow] = twe;
+  }
+  if (act) {
+    tt = tt * invA - rdzw_k * (wdtz_p - wdtz);
+    p.tend_rtheta_adv[o] = tt;
+    p.rthdynten[o] = tt / rz;
+    tt = tt + rz * rtd;
+    if (RK1) p.tend_theta_euler[o] = tte;
+    p.tend_theta[o] = tt + tte + PHYS_ZERO;  // tend_rtheta_physics
+  }
+}
+
 // cells (solve): w tendency (5046-5074, del4 5134-5152, 5167-5223) and theta tendency
 // (5231-5269, del4 5305-5323, 5331-5414)
 __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Config cf, DynTendScal s) {
@@ -736,33 +966,160 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p
                                                                   double coef_divdamp, int phase) {
   const int e = wave_elem(0);
   if (e >= d.nEdges) return;
-  if (phase && ((p.edge_bnd[e] != 0) != (phase == 2))) return;
-  const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
-  if (!(c1 < d.nCellsSolve || c2 < d.nCellsSolve)) return;
   const int k = lane_id(), K = d.K;
-  if (k >= K) return;
-  const size_t o = (size_t)e * K + k;
-  if (small_step != 1) {
-    const double rcv = RGAS / (CP - RGAS);
-    const double c2v = CP * rcv;
-    const size_t o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
-    const double rt1 = p.rtheta_pp[o1], rt2 = p.rtheta_pp[o2];
-    double rup = p.ru_p[o];
-    if (DD) {
-      const double d1 = -(rt1 - p.rtheta_pp_old[o1]);
-      const double d2 = -(rt2 - p.rtheta_pp_old[o2]);
-      rup = rup + coef_divdamp * (d2 - d1) * (1.0 - p.specZoneMaskEdge[e]) / (p.theta_m1[o1] + p.theta_m1[o2]);
+  const bool act = k < K;
+  const size_t o = (size_t)e * K + min(k, K - 1);  // lanes >= K load level K-1 and store nothing
+  // one scalar round trip for the edge's metadata, with its own columns already in flight
+  const int2 ce = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * e);
+  const int bnd = phase ? p.edge_bnd[e] : 0;
+  const double tu = p.tend_u[o];
+  if (small_step == 1) {
+    if (!(ce.x < d.nCellsSolve || ce.y < d.nCellsSolve) || (phase && ((bnd != 0) != (phase == 2)))) return;
+    const double rup = dts * tu;
+    if (act) {
+      p.ru_p[o] = rup;
+      p.ruAvg[o] = rup;
     }
-    double pgrad = ((rt2 - rt1) * p.invDcEdge[e]) / (.5 * (p.zz[o2] + p.zz[o1]));
-    pgrad = p.cqu[o] * 0.5 * c2v * (p.exner[o1] + p.exner[o2]) * pgrad;
-    pgrad = pgrad + 0.5 * p.zxu[o] * GRAVITY * (p.rho_pp[o1] + p.rho_pp[o2]);
-    rup = rup + dts * (p.tend_u[o] - (1.0 - p.specZoneMaskEdge[e]) * pgrad);
+    return;
+  }
+  double rup = p.ru_p[o];
+  const double rua = p.ruAvg[o], cqu = p.cqu[o], zxu = p.zxu[o];
+  const double mask = p.specZoneMaskEdge[e], invDc = p.invDcEdge[e];
+  if (!(ce.x < d.nCellsSolve || ce.y < d.nCellsSolve) || (phase && ((bnd != 0) != (phase == 2)))) return;
+  const int c1 = uni(ce.x), c2 = uni(ce.y);
+  const double rcv = RGAS / (CP - RGAS);
+  const double c2v = CP * rcv;
+  const size_t o1 = (size_t)c1 * K + min(k, K - 1), o2 = (size_t)c2 * K + min(k, K - 1);
+  const double rt1 = p.rtheta_pp[o1], rt2 = p.rtheta_pp[o2];
+  const double zz1 = p.zz[o1], zz2 = p.zz[o2], ex1 = p.exner[o1], ex2 = p.exner[o2];
+  const double rp1 = p.rho_pp[o1], rp2 = p.rho_pp[o2];
+  if (DD) {
+    const double d1 = -(rt1 - p.rtheta_pp_old[o1]);
+    const double d2 = -(rt2 - p.rtheta_pp_old[o2]);
+    rup = rup + coef_divdamp * (d2 - d1) * (1.0 - mask) / (p.theta_m1[o1] + p.theta_m1[o2]);
+  }
+  double pgrad = ((rt2 - rt1) * invDc) / (.5 * (zz2 + zz1));
+  pgrad = cqu * 0.5 * c2v * (ex1 + ex2) * pgrad;
+  pgrad = pgrad + 0.5 * zxu * GRAVITY * (rp1 + rp2);
+  rup = rup + dts * (tu - (1.0 - mask) * pgrad);
+  if (act) {
     p.ru_p[o] = rup;
-    p.ruAvg[o] = p.ruAvg[o] + rup;
+    p.ruAvg[o] = rua + rup;
+  }
+}
+
+// cell phase (2603-2721) on the per-cell stencil record (ME = maxEdges <= 7): every load the
+// column needs -- the record, its own 22 columns, the ru_p of its edges and theta_m of the cells
+// across them -- is issued before the first use, so one wave waits for two memory round trips
+// (record, then gathers) instead of a chain per edge.  Same expressions, same order as below.
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs p, double dts, int small_step,
+                                                                    double epssm) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K, actw = k <= K;
+  const int kc = min(k, K - 1), kw = min(k, K);  // clamped lanes load in bounds and store nothing
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
+  double rtpp = p.rtheta_pp[o];
+  if (c >= d.nCellsSolve) {
+    if (act) p.rtheta_pp_old[o] = (small_step == 1) ? 0.0 : rtpp;
+    return;
+  }
+  int re[ME], rc[ME];
+  double sdv[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    re[i] = p.cell_rec[(size_t)c * CELL_REC + i];
+    rc[i] = p.cell_rec[(size_t)c * CELL_REC + CELL_REC_ME + i];
+    sdv[i] = ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i);
+  }
+  const int ne = p.cell_rec[(size_t)c * CELL_REC + 14];
+  const double invA = p.invAreaCell[c], spec = p.specZoneMaskCell[c];
+  double rhopp = p.rho_pp[o], rwp = p.rw_p[ow], wwa = p.wwAvg[ow];
+  const double thc = p.theta_m1[o], trho = p.tend_rho[o], tth = p.tend_theta[o], tw = p.tend_w[ow];
+  double ru[ME], th[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    ru[i] = p.ru_p[(size_t)re[i] * K + kc];
+    th[i] = p.theta_m1[(size_t)rc[i] * K + kc];
+  }
+  const double coftz = p.coftz[ow], zz = p.zz[o], cofwt = p.cofwt[o], cofwz = p.cofwz[o], cofwr = p.cofwr[o];
+  const double a_tri = p.a_tri[o], alpha_tri = p.alpha_tri[o], gamma_tri = p.gamma_tri[o];
+  const double rz = p.rho_zz2[o], dss = p.dss[o], rws = p.rw_save[ow], rw = p.rw[ow], w2 = p.w2[ow];
+  const double cofrz = p.cofrz[kc], rdzw = p.rdzw[kc], fzm = p.fzm[kc], fzp = p.fzp[kc];
+  const double rtpp_old = (small_step == 1) ? 0.0 : rtpp;
+  const double resm = (1.0 - epssm) / (1.0 + epssm);
+  if (small_step == 1) { wwa = 0.0; rhopp = 0.0; rtpp = 0.0; rwp = 0.0; }
+  if (!act) { rhopp = 0.0; rtpp = 0.0; }  // the column's k = K+1 lane: zero, as a masked load gives
+  if (spec == 0.0) {
+    double ts = 0.0, rs = 0.0;
+#pragma unroll
+    for (int i = 0; i < ME; ++i) {
+      if (i < ne) {
+        const double flux = dts * sdv[i] * ru[i] * invA;  // == sign * dts * dvEdge * ru_p * invAreaCell
+        rs = rs - flux;
+        ts = ts - flux * 0.5 * (th[i] + thc);  // (th2 + th1): the sum commutes exactly
+      }
+    }
+    const double coftz_p = dn1(coftz);
+    const double rwp_p = dn1(rwp);
+    if (act) {
+      rs = rhopp + dts * trho + rs - cofrz * resm * (rwp_p - rwp);
+      ts = rtpp + dts * tth + ts - resm * rdzw * (coftz_p * rwp_p - coftz * rwp);
+    }
+    if (act && k >= 1) wwa = wwa + 0.5 * (1.0 - epssm) * rwp;
+    // rw_p right-hand side (2660-2670)
+    const double zzm = up1(zz);
+    const double tsm = up1(ts), rsm = up1(rs), rtppm = up1(rtpp), rhoppm = up1(rhopp);
+    const double cofwtm = up1(cofwt);
+    if (act && k >= 1) {
+      rwp = rwp + dts * tw - cofwz * ((zz * ts - zzm * tsm) + resm * (zz * rtpp - zzm * rtppm)) -
+            cofwr * ((rs + rsm) + resm * (rhopp + rhoppm)) + cofwt * (ts + resm * rtpp) +
+            cofwtm * (tsm + resm * rtppm);
+    }
+    // tridiagonal solve sweeping up and then down the column (2675-2682), reference order
+    for (int kk = 1; kk < K; ++kk) {
+      const double xm = readlane_d(rwp, kk - 1);
+      if (k == kk) rwp = (rwp - a_tri * xm) * alpha_tri;
+    }
+    for (int kk = K - 1; kk >= 0; --kk) {
+      const double xp = readlane_d(rwp, kk + 1);
+      if (k == kk) rwp = rwp - gamma_tri * xp;
+    }
+    // implicit Rayleigh damping of w (2687-2693)
+    const double rzm = up1(rz);
+    if (act && k >= 1) {
+      const double dd = rws - rw;
+      rwp = (rwp + dd - dts * dss * (fzm * zz + fzp * zzm) * (fzm * rz + fzp * rzm) * w2) / (1.0 + dts * dss) - dd;
+      wwa = wwa + 0.5 * (1.0 + epssm) * rwp;
+    }
+    const double rwp_p2 = dn1(rwp);
+    if (act) {
+      p.rtheta_pp_old[o] = rtpp_old;  // stored last: no store precedes the loads above
+      p.rho_pp[o] = rs - cofrz * (rwp_p2 - rwp);
+      p.rtheta_pp[o] = ts - rdzw * (coftz_p * rwp_p2 - coftz * rwp);
+    }
+    if (actw) {
+      p.rw_p[ow] = rwp;
+      p.wwAvg[ow] = wwa;
+    }
   } else {
-    const double rup = dts * p.tend_u[o];
-    p.ru_p[o] = rup;
-    p.ruAvg[o] = rup;
+    // specified zone (2710-2719): regional only, masks are 0 for global meshes
+    if (act) {
+      rhopp = rhopp + dts * trho;
+      rtpp = rtpp + dts * tth;
+      rwp = rwp + dts * tw;
+      wwa = wwa + 0.5 * (1.0 + epssm) * rwp;
+      p.rtheta_pp_old[o] = rtpp_old;
+      p.rho_pp[o] = rhopp;
+      p.rtheta_pp[o] = rtpp;
+    }
+    if (actw) {
+      p.rw_p[ow] = rwp;
+      p.wwAvg[ow] = wwa;
+    }
   }
 }
 
