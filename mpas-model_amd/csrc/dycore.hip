@@ -656,6 +656,16 @@ void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
   if (!ctx->planning) hipLaunchKernelGGL(k_copy_many, dim3(gx, 10), dim3(256), 0, ctx->stream, c);
 }
 
+// batched-load kernel variants (k_*_b / k_*_r) cover meshes with maxEdges 6 or 7; other meshes
+// take the general kernels
+inline bool batched(const Dims& d) {
+#ifdef MPAS_NO_CELL_REC
+  return false;
+#else
+  return (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
+#endif
+}
+
 void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
   LAUNCH(k_vert_imp_coefs, std::max(d.nCellsSolve, 1), d, p, dts, ctx->cf.epssm);
 }
@@ -680,18 +690,43 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   if (cf.rayleigh_damp_u)
     s.rayleigh_coef_inverse = 1.0 / ((double)cf.number_rayleigh_damp_u_levels *
                                      (cf.rayleigh_damp_u_timescale_days * SECONDS_PER_DAY));
-  if (part != 2) LAUNCH(k_dyn_cells1, d.nCells, d, p, cf, s);
+  const bool bt = batched(d), m6 = d.maxEdges == 6;
+  if (part != 2) {
+    if (!bt) LAUNCH(k_dyn_cells1, d.nCells, d, p, cf, s);
+    else if (m6) LAUNCH(k_dyn_cells1_b<6>, d.nCells, d, p, cf, s);
+    else LAUNCH(k_dyn_cells1_b<7>, d.nCells, d, p, cf, s);
+  }
   if (part == 1) return;
+#ifndef MPAS_NO_CELL_REC
+  if ((d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2) {
+    if (d.maxEdges == 6 && rk_step == 1) LAUNCH((k_dyn_edges_b<true, 10>), d.nEdges, d, p, cf, s, 0);
+    if (d.maxEdges == 6 && rk_step != 1) LAUNCH((k_dyn_edges_b<false, 10>), d.nEdges, d, p, cf, s, 1);
+    if (d.maxEdges == 7 && rk_step == 1) LAUNCH((k_dyn_edges_b<true, 12>), d.nEdges, d, p, cf, s, 0);
+    if (d.maxEdges == 7 && rk_step != 1) LAUNCH((k_dyn_edges_b<false, 12>), d.nEdges, d, p, cf, s, 1);
+  } else
+#endif
   if (rk_step == 1)
     LAUNCH(k_dyn_edges<true>, d.nEdges, d, p, cf, s, 0);
   else
     LAUNCH(k_dyn_edges<false>, d.nEdges, d, p, cf, s, 1);
   if (rk_step == 1) {
-    if (s.h_mom_eddy_visc4 > 0.0) LAUNCH(k_dyn_delsq_vc, d.nVertices + d.nCells, d, p);
-    LAUNCH(k_dyn_edges_rk1b, d.nEdgesSolve, d, p, cf, s);
-    LAUNCH(k_dyn_cells2, d.nCells, d, p);
+    if (!bt) {
+      if (s.h_mom_eddy_visc4 > 0.0) LAUNCH(k_dyn_delsq_vc, d.nVertices + d.nCells, d, p);
+      LAUNCH(k_dyn_edges_rk1b, d.nEdgesSolve, d, p, cf, s);
+      LAUNCH(k_dyn_cells2, d.nCells, d, p);
+    } else {
+      if (s.h_mom_eddy_visc4 > 0.0) {
+        if (m6) LAUNCH(k_dyn_delsq_vc_b<6>, d.nVertices + d.nCells, d, p);
+        else LAUNCH(k_dyn_delsq_vc_b<7>, d.nVertices + d.nCells, d, p);
+      }
+      LAUNCH(k_dyn_edges_rk1b_b, d.nEdgesSolve, d, p, cf, s);
+      if (m6) LAUNCH(k_dyn_cells2_b<6>, d.nCells, d, p);
+      else LAUNCH(k_dyn_cells2_b<7>, d.nCells, d, p);
+    }
   }
-  LAUNCH(k_dyn_advflux, d.nEdges, d, p);
+  if (!batched(d)) LAUNCH(k_dyn_advflux, d.nEdges, d, p);
+  else if (d.maxEdges == 6) LAUNCH(k_dyn_advflux_b<10>, d.nEdges, d, p);
+  else LAUNCH(k_dyn_advflux_b<12>, d.nEdges, d, p);
 #ifndef MPAS_NO_CELL_REC
   if (d.maxEdges == 6 || d.maxEdges == 7) {
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH((k_dyn_cells3_r<6, true>), d.nCellsSolve, d, p, cf, s);
@@ -702,6 +737,18 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   }
 #endif
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
+}
+
+void smlstep_pert(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int phase) {
+  if (!batched(d)) LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, phase);
+  else if (d.maxEdges == 6) LAUNCH(k_smlstep_pert_b<6>, d.nCellsSolve, d, p, phase);
+  else LAUNCH(k_smlstep_pert_b<7>, d.nCellsSolve, d, p, phase);
+}
+
+void recover_cells3(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int phase) {
+  if (!batched(d)) LAUNCH(k_recover_cells3, d.nCells, d, p, phase);
+  else if (d.maxEdges == 6) LAUNCH(k_recover_cells3_b<6>, d.nCells, d, p, phase);
+  else LAUNCH(k_recover_cells3_b<7>, d.nCells, d, p, phase);
 }
 
 double coef_divdamp(const mpas_dyc_ctx* ctx, double dts) {  // 2761-2763
@@ -734,6 +781,7 @@ void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
 }
 
 void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase) {
+  // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
   LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase);
 }
 
@@ -741,9 +789,20 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double d
   const double* u = (tl == 1) ? p.u1 : p.u2;
   const double* h = (tl == 1) ? p.rho_zz1 : p.rho_zz2;
   const int reconstruct_v = (rk_step == 0 || rk_step == 3) ? 1 : 0;
-  LAUNCH(k_diag_vertices, d.nVertices, d, p, u);
-  LAUNCH(k_diag_cells, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
-  LAUNCH(k_diag_edges, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
+  if (!batched(d)) {
+    LAUNCH(k_diag_vertices, d.nVertices, d, p, u);
+    LAUNCH(k_diag_cells, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
+    LAUNCH(k_diag_edges, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
+    return;
+  }
+  LAUNCH(k_diag_vertices, d.nVertices, d, p, u);  // the batched variant measured slower
+  if (d.maxEdges == 6) {
+    LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
+    LAUNCH(k_diag_edges_b<10>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
+  } else {
+    LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
+    LAUNCH(k_diag_edges_b<12>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
+  }
 }
 
 void advance_scalars(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt, int rk_step, bool advance_density) {
@@ -873,12 +932,12 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       const double dts = rk_sub_timestep[rk_step - 1];
       if (split) {  // 642 | 644-678: interior cells overlap the tend_u exchange
         CHK(exchange_async(ctx, {{"tend", "u", 0, 0x1u}}));
-        EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, 1));
+        EACH(smlstep_pert(ctx, d, p, 1));
         CHK(exchange_wait(ctx));
-        EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, 2));
+        EACH(smlstep_pert(ctx, d, p, 2));
       } else {
         CHK(exchange(ctx, {{"tend", "u", 0, 0x1u}}));             // 642
-        EACH(LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, 0));     // 644-678
+        EACH(smlstep_pert(ctx, d, p, 0));     // 644-678
       }
       // Acoustic sub-steps (788-870).
       // * Exchanges.  The reference exchanges rho_pp before every sub-step (792) and rtheta_pp
@@ -932,13 +991,13 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 2));
         EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
         CHK(exchange_async(ctx, {{"state", "u", 2, ALL_LAYERS}}));
-        EACH(LAUNCH(k_recover_cells3, d.nCells, d, p, 0));
+        EACH(recover_cells3(ctx, d, p, 0));
         CHK(exchange_wait(ctx));
       } else {
         CHK((exchange)(ctx, xrec));
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0));  // 889-930
         EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0));
-        EACH(LAUNCH(k_recover_cells3, d.nCells, d, p, 0));
+        EACH(recover_cells3(ctx, d, p, 0));
         CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));      // 988
       }
       if (scalars_in_dynamics) {                                  // 993-1185

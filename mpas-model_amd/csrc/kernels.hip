@@ -310,6 +310,80 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells1(Dims d, Ptrs p, Co
   }
 }
 
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells1_b(Dims d, Ptrs p, Config cf, DynTendScal s) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t o = (size_t)c * K + kc;
+  const bool rk1 = s.rk_step == 1, smag = rk1 && cf.horiz_mixing_smag;
+  const CellSten<ME> st = load_sten<ME>(p, c);
+  double sdv[ME], da[ME], db[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    sdv[i] = ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i);
+    da[i] = smag ? ld_uniform_f64(p.defc_a + (size_t)c * ME + i) : 0.0;
+    db[i] = smag ? ld_uniform_f64(p.defc_b + (size_t)c * ME + i) : 0.0;
+  }
+  const double invA = ld_uniform_f64(p.invAreaCell + c);
+  double rwk = 0.0, qt = 0.0, rb = 0.0, rps = 0.0;
+  if (rk1) {
+    rwk = p.rw[(size_t)c * (K + 1) + kw];
+    qt = p.qtot[o];
+    rb = p.rho_base[o];
+    rps = p.rho_p_save[o];
+  }
+  double rue[ME], ue[ME], ve[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const size_t oe = (size_t)uni(st.e[i]) * K + kc;
+    rue[i] = p.ru[oe];
+    ue[i] = smag ? p.u2[oe] : 0.0;
+    ve[i] = smag ? p.v[oe] : 0.0;
+  }
+  // 2d Smagorinsky kdiff + cam filter (rk1, 4677-4720)
+  if (rk1 && act) {
+    double kd;
+    if (smag) {
+      double d_diag = 0.0, d_off = 0.0;
+#pragma unroll
+      for (int i = 0; i < ME; ++i) {
+        if (i < st.ne) {
+          d_diag = d_diag + da[i] * ue[i] - db[i] * ve[i];
+          d_off = d_off + db[i] * ue[i] + da[i] * ve[i];
+        }
+      }
+      const double csl = s.c_s * cf.len_disp;
+      kd = fmin((csl * csl) * sqrt(d_diag * d_diag + d_off * d_off), (0.01 * (cf.len_disp * cf.len_disp)) * s.invDt);
+    } else {
+      kd = cf.h_theta_eddy_visc2;
+    }
+    if (cf.mpas_cam_coef > 0.0) {
+      if (k == K - 3) kd = fmax(kd, 2.0833 * cf.len_disp * cf.mpas_cam_coef);
+      if (k == K - 2) kd = fmax(kd, 2.0 * 2.0833 * cf.len_disp * cf.mpas_cam_coef);
+      if (k == K - 1) kd = fmax(kd, 4.0 * 2.0833 * cf.len_disp * cf.mpas_cam_coef);
+    }
+    p.kdiff[o] = kd;
+  }
+  // h_divergence (4729-4748)
+  double hd = 0.0;
+#pragma unroll
+  for (int i = 0; i < ME; ++i)
+    if (i < st.ne) hd = hd + sdv[i] * rue[i];  // edgesOnCell_sign * dvEdge * ru
+  hd = hd * invA;
+  if (act) p.h_divergence[o] = hd;
+  // tend_rho and dpdz (rk1, 4755-4766)
+  if (rk1) {
+    const double rwp = dn1(rwk);
+    if (act) {
+      p.tend_rho[o] = -hd - p.rdzw[k] * (rwp - rwk) + PHYS_ZERO;  // tend_rho_physics
+      p.dpdz[o] = -GRAVITY * (rb * (qt) + rps * (1. + qt));
+    }
+  }
+}
+
 // edges: tend_u (edge-solve: PGF rk1 4781-4788, vertical transport 4792-4807, Coriolis/KE 4811-4838)
 // + rk1 del2 on all edges (4856-4883); finalize (Rayleigh + euler + physics, 5015-5036) when rk>1.
 // Like k_dyn_advflux this is latency bound: every column the edge reads is loaded before the
@@ -423,6 +497,129 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges(Dims d, Ptrs p, Con
     tue = tue + re * kdiffu * u_diffusion * p.meshScalingDel2[e];
     p.tend_u_euler[o] = tue;
   }
+}
+
+// k_dyn_edges with batched loads (NE2 = 2*maxEdges-2 >= nEdgesOnEdge): the edge's metadata
+// (cellsOnEdge, verticesOnEdge, edgesOnEdge, weightsOnEdge) and own columns go out first, then
+// every gather at once, so a wave waits for two memory round trips.  Same expressions and order
+// as k_dyn_edges; solve edges (tend_u and, at rk1, del2) and halo edges (rk1 del2 only) are
+// separate paths so that neither issues the other's loads.
+template <bool RK1, int NE2>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_b(Dims d, Ptrs p, Config cf, DynTendScal s,
+                                                               int finalize) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)e * K + kc;
+  const bool solve = e < d.nEdgesSolve;
+  const int2 ce = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * e);
+  const double invDc = ld_uniform_f64(p.invDcEdge + e);
+  const double re = p.rho_edge[o];
+  // rk1 del^2 of u (4856-4883), all edges
+  auto del2 = [&](double tue, double dv1, double dv2, double vo1, double vo2, double kd1, double kd2, double invDv,
+                  double msd2) {
+    const double r_dc = invDc;
+    const double r_dv = fmin(invDv, 4 * invDc);
+    const double u_diffusion = (dv2 - dv1) * r_dc - (vo2 - vo1) * r_dv;
+    if (act) p.delsq_u[o] = 0.0 + u_diffusion;
+    const double kdiffu = 0.5 * (kd1 + kd2);
+    tue = tue + re * kdiffu * u_diffusion * msd2;
+    if (act) p.tend_u_euler[o] = tue;
+  };
+  if (!solve) {
+    if (!RK1) return;
+    const int2 ve = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * e);
+    const double invDv = ld_uniform_f64(p.invDvEdge + e), msd2 = ld_uniform_f64(p.meshScalingDel2 + e);
+    const double tue = p.tend_u_euler[o];
+    const int c1 = uni(ce.x), c2 = uni(ce.y), v1 = uni(ve.x), v2 = uni(ve.y);
+    const size_t o1 = (size_t)c1 * K + kc, o2 = (size_t)c2 * K + kc;
+    del2(tue, p.divergence[o1], p.divergence[o2], p.vorticity[(size_t)v1 * K + kc],
+         p.vorticity[(size_t)v2 * K + kc], p.kdiff[o1], p.kdiff[o2], invDv, msd2);
+    return;
+  }
+  // ---- solve edges: batch 1
+  const int neoe = p.nEdgesOnEdge[e];
+  int eoe[NE2];
+  double wgt[NE2];
+#pragma unroll
+  for (int j = 0; j < NE2; ++j) {
+    eoe[j] = p.edgesOnEdge[(size_t)e * d.maxEdges2 + j];
+    wgt[j] = ld_uniform_f64(p.weightsOnEdge + (size_t)e * d.maxEdges2 + j);
+  }
+  int2 ve = make_int2(0, 0);
+  double invDv = 0.0, msd2 = 0.0, cqu = 0.0, zxu = 0.0;
+  if (RK1) {
+    ve = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * e);
+    invDv = ld_uniform_f64(p.invDvEdge + e);
+    msd2 = ld_uniform_f64(p.meshScalingDel2 + e);
+    cqu = p.cqu[o];
+    zxu = p.zxu[o];
+  }
+  const double uk = p.u2[o], pve = p.pv_edge[o];
+  double tue = RK1 ? 0.0 : p.tend_u_euler[o];  // rk1 recomputes it on solve edges
+  // ---- batch 2: gathers
+  const int c1 = uni(ce.x), c2 = uni(ce.y);
+  const size_t o1 = (size_t)c1 * K + kc, o2 = (size_t)c2 * K + kc;
+  const double rw1 = p.rw[(size_t)c1 * K1 + kw], rw2 = p.rw[(size_t)c2 * K1 + kw];
+  const double ke1 = p.ke[o1], ke2 = p.ke[o2], hd1 = p.h_divergence[o1], hd2 = p.h_divergence[o2];
+  double pv[NE2], uu[NE2];
+#pragma unroll
+  for (int j = 0; j < NE2; ++j) {
+    const size_t oj = (size_t)uni(eoe[j]) * K + kc;
+    pv[j] = p.pv_edge[oj];
+    uu[j] = p.u2[oj];
+  }
+  double pp1 = 0.0, pp2 = 0.0, zz1 = 0.0, zz2 = 0.0, dpz1 = 0.0, dpz2 = 0.0;
+  double dv1 = 0.0, dv2 = 0.0, vo1 = 0.0, vo2 = 0.0, kd1 = 0.0, kd2 = 0.0;
+  if (RK1) {
+    const int v1 = uni(ve.x), v2 = uni(ve.y);
+    pp1 = p.pressure_p[o1];
+    pp2 = p.pressure_p[o2];
+    zz1 = p.zz[o1];
+    zz2 = p.zz[o2];
+    dpz1 = p.dpdz[o1];
+    dpz2 = p.dpdz[o2];
+    dv1 = p.divergence[o1];
+    dv2 = p.divergence[o2];
+    vo1 = p.vorticity[(size_t)v1 * K + kc];
+    vo2 = p.vorticity[(size_t)v2 * K + kc];
+    kd1 = p.kdiff[o1];
+    kd2 = p.kdiff[o2];
+  }
+  const double fzm = p.fzm[kc], fzp = p.fzp[kc], rdzw = p.rdzw[kc];
+  // ---- tend_u (PGF rk1 4781-4788, vertical transport 4792-4807, Coriolis/KE 4811-4838)
+  if (RK1) tue = -cqu * ((pp2 - pp1) * invDc / (.5 * (zz2 + zz1)) - 0.5 * zxu * (dpz1 + dpz2));
+  const double um1 = up1(uk), um2 = up2(uk), up1v = dn1(uk);
+  const double rwa = 0.5 * (rw1 + rw2);
+  double wduz = 0.0;
+  if (k == 1 || k == K - 1) {
+    wduz = 0.5 * (rw1 + rw2) * (fzm * uk + fzp * um1);
+  } else if (k >= 2 && k <= K - 2) {
+    wduz = flux3(um2, um1, uk, up1v, rwa, 1.0);
+  }
+  const double wduz_p = dn1(wduz);
+  double tu = -rdzw * (wduz_p - wduz);
+  double q = 0.0;
+#pragma unroll
+  for (int j = 0; j < NE2; ++j) {
+    if (j < neoe) {
+      const double workpv = 0.5 * (pve + pv[j]);
+      q = q + wgt[j] * uu[j] * workpv;
+    }
+  }
+  tu = tu + re * (q - (ke2 - ke1) * invDc) - uk * 0.5 * (hd1 + hd2);
+  if (finalize) {
+    if (cf.rayleigh_damp_u && k >= K - cf.number_rayleigh_damp_u_levels) {
+      const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
+      tu = tu - re * uk * coef;
+    }
+    tu = tu + tue + PHYS_ZERO;  // tend_ru_physics
+  }
+  if (act) p.tend_u[o] = tu;
+  if (RK1) del2(tue, dv1, dv2, vo1, vo2, kd1, kd2, invDv, msd2);
 }
 
 // vertices: delsq_vorticity (4889-4898); cells: delsq_divergence (4900-4910)   [rk1, visc4>0]
@@ -547,6 +744,184 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells2(Dims d, Ptrs p) {
     p.tend_theta_euler[(size_t)c * K + k] = tth;
   }
   if (k <= K) p.tend_w_euler[(size_t)c * (K + 1) + k] = (act && k >= 1) ? tw : 0.0;
+}
+
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_delsq_vc_b(Dims d, Ptrs p) {
+  const int idx = wave_elem(0);
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  if (idx < d.nVertices) {
+    const int v = idx;
+    int ei[3];
+    double sg[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      ei[i] = p.edgesOnVertex[3 * v + i];
+      sg[i] = ld_uniform_f64(p.edgesOnVertex_sign + 3 * v + i);
+    }
+    const double iat = ld_uniform_f64(p.invAreaTriangle + v);
+    double dc[3], du[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = uni(ei[i]);
+      dc[i] = ld_uniform_f64(p.dcEdge + e);
+      du[i] = p.delsq_u[(size_t)e * K + k];
+    }
+    double dv = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dv = dv + (iat * dc[i] * sg[i]) * du[i];
+    p.delsq_vorticity[(size_t)v * K + k] = dv;
+  } else {
+    const int c = idx - d.nVertices;
+    if (c >= d.nCells) return;
+    const CellSten<ME> st = load_sten<ME>(p, c);
+    double sdv[ME], du[ME];
+#pragma unroll
+    for (int i = 0; i < ME; ++i) sdv[i] = ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i);
+    const double r = ld_uniform_f64(p.invAreaCell + c);
+#pragma unroll
+    for (int i = 0; i < ME; ++i) du[i] = p.delsq_u[(size_t)uni(st.e[i]) * K + k];
+    double dd = 0.0;
+#pragma unroll
+    for (int i = 0; i < ME; ++i)
+      if (i < st.ne) dd = dd + (r * sdv[i]) * du[i];  // r * dvEdge * edgesOnCell_sign
+    p.delsq_divergence[(size_t)c * K + k] = dd;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_rk1b_b(Dims d, Ptrs p, Config cf, DynTendScal s) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdgesSolve) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const int kc = min(k, K - 1);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)e * K + kc;
+  const int2 ce = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * e);
+  const int2 ve = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * e);
+  const bool del4 = s.h_mom_eddy_visc4 > 0.0, vmix = cf.v_mom_eddy_visc2 > 0.0;
+  const double msd4 = ld_uniform_f64(p.meshScalingDel4 + e), invDc = ld_uniform_f64(p.invDcEdge + e);
+  const double invDv = ld_uniform_f64(p.invDvEdge + e);
+  const double ang = (vmix && !cf.mix_full) ? ld_uniform_f64(p.angleEdge + e) : 0.0;
+  double tue = p.tend_u_euler[o];
+  const double uk = p.u2[o], re = p.rho_edge[o], tu0 = p.tend_u[o];
+  const int c1 = uni(ce.x), c2 = uni(ce.y), v1 = uni(ve.x), v2 = uni(ve.y);
+  double dd1 = 0.0, dd2 = 0.0, dv1 = 0.0, dv2 = 0.0;
+  if (del4) {
+    dd1 = p.delsq_divergence[(size_t)c1 * K + kc];
+    dd2 = p.delsq_divergence[(size_t)c2 * K + kc];
+    dv1 = p.delsq_vorticity[(size_t)v1 * K + kc];
+    dv2 = p.delsq_vorticity[(size_t)v2 * K + kc];
+  }
+  // zgrid levels k-1 .. k+2 of both cells, lanes 1..K-2 (Fortran k = 2..K-1)
+  const int kz = max(1, min(k, K - 2));
+  double zg1[4], zg2[4];
+  if (vmix) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      zg1[j] = p.zgrid[(size_t)c1 * K1 + kz - 1 + j];
+      zg2[j] = p.zgrid[(size_t)c2 * K1 + kz - 1 + j];
+    }
+  }
+  if (del4 && act) {
+    const double u_mix_scale = msd4 * s.h_mom_eddy_visc4;
+    const double r_dc = u_mix_scale * cf.del4u_div_factor * invDc;
+    const double r_dv = u_mix_scale * fmin(invDv, 4 * invDc);
+    const double u_diffusion = re * ((dd2 - dd1) * r_dc - (dv2 - dv1) * r_dv);
+    tue = tue - u_diffusion;
+  }
+  if (vmix) {
+    const double um = up1(uk), upv = dn1(uk);
+    double mixm = 0.0, mix0 = 0.0, mixp = 0.0;
+    if (!cf.mix_full) {
+      const double ca = cos(ang), sa = sin(ang);
+      mix0 = act ? uk - p.u_init[kc] * ca - p.v_init[kc] * sa : 0.0;
+      mixm = up1(mix0);
+      mixp = dn1(mix0);
+    }
+    if (k >= 1 && k <= K - 2) {
+      const double z1 = 0.5 * (zg1[0] + zg2[0]);
+      const double z2 = 0.5 * (zg1[1] + zg2[1]);
+      const double z3 = 0.5 * (zg1[2] + zg2[2]);
+      const double z4 = 0.5 * (zg1[3] + zg2[3]);
+      const double zm = 0.5 * (z1 + z2), z0 = 0.5 * (z2 + z3), zp = 0.5 * (z3 + z4);
+      if (cf.mix_full)
+        tue = tue + re * cf.v_mom_eddy_visc2 * ((upv - uk) / (zp - z0) - (uk - um) / (z0 - zm)) / (0.5 * (zp - zm));
+      else
+        tue = tue + re * cf.v_mom_eddy_visc2 * ((mixp - mix0) / (zp - z0) - (mix0 - mixm) / (z0 - zm)) / (0.5 * (zp - zm));
+    }
+  }
+  if (!act) return;
+  p.tend_u_euler[o] = tue;
+  double tu = tu0;
+  if (cf.rayleigh_damp_u && k >= K - cf.number_rayleigh_damp_u_levels) {
+    const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
+    tu = tu - re * uk * coef;
+  }
+  p.tend_u[o] = tu + tue + PHYS_ZERO;  // tend_ru_physics
+}
+
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells2_b(Dims d, Ptrs p) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const int kc = min(k, K - 1);
+  const size_t K1 = K + 1;
+  const CellSten<ME> st = load_sten<ME>(p, c);
+  double sdv[ME], idc[ME], msd2[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) sdv[i] = ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i);
+  const double r_areaCell = ld_uniform_f64(p.invAreaCell + c);
+  const double kds = p.kdiff[(size_t)c * K + kc], ws = p.w2[(size_t)c * K1 + kc], ths = p.theta_m2[(size_t)c * K + kc];
+  double re[ME], kdo[ME], wo[ME], tho[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const int e = uni(st.e[i]), co = uni(st.o[i]);
+    idc[i] = ld_uniform_f64(p.invDcEdge + e);
+    msd2[i] = ld_uniform_f64(p.meshScalingDel2 + e);
+    re[i] = p.rho_edge[(size_t)e * K + kc];
+    kdo[i] = p.kdiff[(size_t)co * K + kc];
+    wo[i] = p.w2[(size_t)co * K1 + kc];
+    tho[i] = p.theta_m2[(size_t)co * K + kc];
+  }
+  double dw = 0.0, tw = 0.0, dth = 0.0, tth = 0.0;
+  const double prandtl_inv = 1.0 / PRANDTL;
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    // cellsOnEdge(1/2) of edge i: this cell and the one across, in the edge's order
+    const bool f = st.first(i);
+    const double kd1 = f ? kds : kdo[i], kd2 = f ? kdo[i] : kds;
+    const double w1 = f ? ws : wo[i], w2 = f ? wo[i] : ws;
+    const double t1 = f ? ths : tho[i], t2 = f ? tho[i] : ths;
+    const double re_m = up1(re[i]);
+    const double kd1m = up1(kd1), kd2m = up1(kd2);
+    if (i < st.ne) {
+      if (act && k >= 1) {
+        const double edge_sign = 0.5 * r_areaCell * sdv[i] * idc[i];  // 0.5*r_areaCell*sign*dvEdge*invDcEdge
+        double w_turb_flux = edge_sign * (re[i] + re_m) * (w2 - w1);
+        dw = dw + w_turb_flux;
+        w_turb_flux = w_turb_flux * msd2[i] * 0.25 * (kd1 + kd2 + kd1m + kd2m);
+        tw = tw + w_turb_flux;
+      }
+      if (act) {
+        const double edge_sign = r_areaCell * sdv[i] * idc[i];
+        const double pr_scale = prandtl_inv * msd2[i];
+        double ttf = edge_sign * (t2 - t1) * re[i];
+        dth = dth + ttf;
+        ttf = ttf * 0.5 * (kd1 + kd2) * pr_scale;
+        tth = tth + ttf;
+      }
+    }
+  }
+  if (act) {
+    p.delsq_w[(size_t)c * K + k] = dw;
+    p.delsq_theta[(size_t)c * K + k] = dth;
+    p.tend_theta_euler[(size_t)c * K + k] = tth;
+  }
+  if (k <= K) p.tend_w_euler[(size_t)c * K1 + k] = (act && k >= 1) ? tw : 0.0;
 }
 
 // edges of owned cells: the 3rd/4th-order edge values of w and theta_m used by the
@@ -778,6 +1153,63 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3_r(Dims d, Ptrs p, 
   }
 }
 
+// k_dyn_advflux with batched loads (NA = 2*maxEdges-2 >= nAdvCellsForEdge): the edge's index
+// and coefficient rows and its ru column go out together, then the 2*NA neighbour columns.
+template <int NA>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_advflux_b(Dims d, Ptrs p) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)e * K + kc;
+  const int2 ce = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * e);
+  const int na = p.nAdvCellsForEdge[e];
+  int ic[NA];
+  double a[NA], b[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    ic[j] = p.advCellsForEdge[(size_t)e * 15 + j];
+    a[j] = ld_uniform_f64(p.adv_coefs + (size_t)e * 15 + j);
+    b[j] = ld_uniform_f64(p.adv_coefs_3rd + (size_t)e * 15 + j);
+  }
+  const double rue = p.ru[o];
+  if (!(ce.x < d.nCellsSolve || ce.y < d.nCellsSolve)) return;
+  double wv[NA], tv[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int cj = uni(ic[j]);
+    wv[j] = p.w2[(size_t)cj * K1 + kw];
+    tv[j] = p.theta_m2[(size_t)cj * K + kc];
+  }
+  const double fzm = p.fzm[kc], fzp = p.fzp[kc];
+  const double rue_m = up1(rue);
+  const double ru_edge_w = act ? fzm * rue + fzp * rue_m : 0.0;
+  const double sgn_w = sgn1(ru_edge_w), sgn_t = sgn1(rue);
+  double fw = 0.0, ft = 0.0;
+  if (na <= NA) {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      if (j < na) {
+        fw = fw + (a[j] + sgn_w * b[j]) * wv[j];
+        ft = ft + (a[j] + sgn_t * b[j]) * tv[j];
+      }
+    }
+  } else {  // not produced by meshes with maxEdges <= 7; kept for completeness
+    for (int j = 0; j < na; ++j) {
+      const int cj = uni(p.advCellsForEdge[(size_t)e * 15 + j]);
+      const double aj = p.adv_coefs[(size_t)e * 15 + j], bj = p.adv_coefs_3rd[(size_t)e * 15 + j];
+      fw = fw + (aj + sgn_w * bj) * p.w2[(size_t)cj * K1 + kw];
+      ft = ft + (aj + sgn_t * bj) * p.theta_m2[(size_t)cj * K + kc];
+    }
+  }
+  if (act) {
+    p.advflux_w[o] = fw;
+    p.advflux_th[o] = ft;
+  }
+}
+
 // cells (solve): w tendency (5046-5074, del4 5134-5152, 5167-5223) and theta tendency
 // (5231-5269, del4 5305-5323, 5331-5414)
 __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Config cf, DynTendScal s) {
@@ -948,6 +1380,42 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p, 
     }
   }
   const double zz = LD(p.zz, (size_t)c * K + k), zzm = up1(zz);
+  if (act && k >= 1) p.tend_w[(size_t)c * K1 + k] = (fzm * zz + fzp * zzm) * wt;
+}
+
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert_b(Dims d, Ptrs p, int phase) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t K1 = K + 1;
+  const int bnd = phase ? p.cell_bnd[c] : 0;
+  const CellSten<ME> st = load_sten<ME>(p, c);
+  double zb[ME], zb3[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const size_t zo = ((size_t)c * ME + i) * K1 + kw;
+    zb[i] = p.zb_cell[zo];
+    zb3[i] = p.zb3_cell[zo];
+  }
+  double wt = p.tend_w[(size_t)c * K1 + kw];
+  const double zz = p.zz[(size_t)c * K + kc];
+  const double fzm = p.fzm[kc], fzp = p.fzp[kc];
+  if (phase && (((bnd & CELL_HALO_EDGE) != 0) != (phase == 2))) return;
+  double ut[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) ut[i] = p.tend_u[(size_t)uni(st.e[i]) * K + kc];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const double utm = up1(ut[i]);
+    if (i < st.ne && act && k >= 1) {
+      const double flux = st.sg(i) * (fzm * ut[i] + fzp * utm);
+      wt = wt - (zb[i] + sgn1(ut[i]) * zb3[i]) * flux;
+    }
+  }
+  const double zzm = up1(zz);
   if (act && k >= 1) p.tend_w[(size_t)c * K1 + k] = (fzm * zz + fzp * zzm) * wt;
 }
 
@@ -1466,6 +1934,178 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges(Dims d, Ptrs p, co
     p.gradPVt[o] = gt;
     p.gradPVn[o] = gn;
     pve = pve - r * (vv * gt + u[o] * gn);
+  }
+  p.pv_edge[o] = pve;
+}
+
+// batched variants of the recover / diagnostics kernels (maxEdges <= 7, see k_acoustic_cells_r)
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs p, int phase) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  const size_t K1 = K + 1;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
+  const int bnd = phase ? p.cell_bnd[c] : 0;
+  const int ne = p.nEdgesOnCell[c];
+  int ei[ME];
+  double sg[ME], zb[ME], zb3[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    ei[i] = p.edgesOnCell[(size_t)c * ME + i];
+    sg[i] = ld_uniform_f64(p.edgesOnCell_sign + (size_t)c * ME + i);
+    const size_t zo = ((size_t)c * ME + i) * K1 + kw;
+    zb[i] = p.zb_cell[zo];
+    zb3[i] = p.zb3_cell[zo];
+  }
+  double w = p.w2[ow];
+  const double rz = p.rho_zz2[o];
+  const double fzm = p.fzm[kc], fzp = p.fzp[kc];
+  if (phase && (((bnd & CELL_BND_EDGE) != 0) != (phase == 2))) return;
+  double ru[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) ru[i] = p.ru[(size_t)uni(ei[i]) * K + kc];
+  if (!act) w = 0.0;
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const double ruk = ru[i];
+    const double rum = up1(ruk);
+    const double ru1 = readlane_d(ruk, 0), ru2 = readlane_d(ruk, 1), ru3 = readlane_d(ruk, 2);
+    if (i < ne) {
+      if (k == 0) {
+        const double flux = (p.cf1 * ru1 + p.cf2 * ru2 + p.cf3 * ru3);
+        w = w + sg[i] * (zb[i] + sgn1(flux) * zb3[i]) * flux;
+      } else if (act) {
+        const double flux = (fzm * ruk + fzp * rum);
+        w = w + sg[i] * (zb[i] + sgn1(flux) * zb3[i]) * flux;
+      }
+    }
+  }
+  const double rzm = up1(rz);
+  const double r1 = readlane_d(rz, 0), r2 = readlane_d(rz, 1), r3 = readlane_d(rz, 2);
+  if (k == 0) w = w / (p.cf1 * r1 + p.cf2 * r2 + p.cf3 * r3);
+  else if (act) w = w / (fzm * rz + fzp * rzm);
+  if (act) p.w2[ow] = w;  // w(K+1) stays 0
+}
+
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells_b(Dims d, Ptrs p, const double* __restrict__ u,
+                                                                double apvm) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const int ne = p.nEdgesOnCell[c];
+  int ei[ME], vi[ME], kj[ME];
+  double sg[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    ei[i] = p.edgesOnCell[(size_t)c * ME + i];
+    vi[i] = p.verticesOnCell[(size_t)c * ME + i];
+    kj[i] = p.kiteForCell[(size_t)c * ME + i];
+    sg[i] = ld_uniform_f64(p.edgesOnCell_sign + (size_t)c * ME + i);
+  }
+  const double r = ld_uniform_f64(p.invAreaCell + c);
+  double dc[ME], dv[ME], kite[ME], ue[ME], kv[ME], pvv[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const int e = uni(ei[i]), iv = uni(vi[i]);
+    dc[i] = ld_uniform_f64(p.dcEdge + e);
+    dv[i] = ld_uniform_f64(p.dvEdge + e);
+    kite[i] = ld_uniform_f64(p.kiteAreasOnVertex + 3 * iv + kj[i]);
+    ue[i] = u[(size_t)e * K + k];
+    kv[i] = p.ke_vertex[(size_t)iv * K + k];
+    pvv[i] = apvm > 0.0 ? p.pv_vertex[(size_t)iv * K + k] : 0.0;
+  }
+  double div = 0.0, ke = 0.0;
+  // divergence (5626-5640) and the edge part of ke (5650-5660)
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    if (i < ne) {
+      div = div + (sg[i] * dv[i]) * ue[i];
+      ke = ke + 0.25 * (dc[i] * dv[i] * (ue[i] * ue[i]));  // ke_edge (5600)
+    }
+  }
+  div = div * r;
+  ke = ke * r;
+  const double ke_fact = 1.0 - .375;
+  ke = ke_fact * ke;
+  double pvc = 0.0;
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    if (i < ne) {
+      ke = ke + (1. - ke_fact) * kite[i] * kv[i] * r;
+      pvc = pvc + kite[i] * pvv[i] * r;
+    }
+  }
+  const size_t o = (size_t)c * K + k;
+  p.divergence[o] = div;
+  p.ke[o] = ke;
+  if (apvm > 0.0) p.pv_cell[o] = pvc;
+}
+
+template <int NE2>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges_b(Dims d, Ptrs p, const double* __restrict__ u,
+                                                                const double* __restrict__ h, int reconstruct_v,
+                                                                double apvm, double dt) {
+  const int e = wave_elem(0);
+  if (e >= d.nEdges) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const size_t o = (size_t)e * K + k;
+  const int2 ce = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * e);
+  const int2 ve = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * e);
+  int neoe = 0;
+  int eoe[NE2];
+  double wgt[NE2];
+  if (reconstruct_v) {
+    neoe = p.nEdgesOnEdge[e];
+#pragma unroll
+    for (int j = 0; j < NE2; ++j) {
+      eoe[j] = p.edgesOnEdge[(size_t)e * d.maxEdges2 + j];
+      wgt[j] = ld_uniform_f64(p.weightsOnEdge + (size_t)e * d.maxEdges2 + j);
+    }
+  }
+  double invDv = 0.0, invDc = 0.0, ue = 0.0;
+  if (apvm > 0.0) {
+    invDv = ld_uniform_f64(p.invDvEdge + e);
+    invDc = ld_uniform_f64(p.invDcEdge + e);
+    ue = u[o];
+  }
+  const int c1 = uni(ce.x), c2 = uni(ce.y), v1 = uni(ve.x), v2 = uni(ve.y);
+  const double h1 = h[(size_t)c1 * K + k], h2 = h[(size_t)c2 * K + k];
+  const double pv1 = p.pv_vertex[(size_t)v1 * K + k], pv2 = p.pv_vertex[(size_t)v2 * K + k];
+  double pc1 = 0.0, pc2 = 0.0;
+  if (apvm > 0.0) {
+    pc1 = p.pv_cell[(size_t)c1 * K + k];
+    pc2 = p.pv_cell[(size_t)c2 * K + k];
+  }
+  double vv;
+  if (reconstruct_v) {
+    double uu[NE2];
+#pragma unroll
+    for (int j = 0; j < NE2; ++j) uu[j] = u[(size_t)uni(eoe[j]) * K + k];
+    vv = 0.0;
+#pragma unroll
+    for (int j = 0; j < NE2; ++j)
+      if (j < neoe) vv = vv + wgt[j] * uu[j];
+    p.v[o] = vv;
+  } else {
+    vv = p.v[o];
+  }
+  p.rho_edge[o] = 0.5 * (h1 + h2);
+  double pve = 0.5 * (pv1 + pv2);
+  if (apvm > 0.0) {
+    const double r = apvm * dt;
+    const double r1 = 1.0 * invDv;
+    const double r2 = 1.0 * invDc;
+    const double gt = (pv2 - pv1) * r1;
+    const double gn = (pc2 - pc1) * r2;
+    p.gradPVt[o] = gt;
+    p.gradPVn[o] = gn;
+    pve = pve - r * (vv * gt + ue * gn);
   }
   p.pv_edge[o] = pve;
 }
