@@ -52,10 +52,55 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 constexpr int MAX_EDGES_UNROLL = 6;
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// value held by lane-1 (k-1) / lane+1 (k+1); lanes at the ends get garbage that callers never use
+// value held by lane-1 (k-1) / lane+1 (k+1); the end lanes keep their own value (as __shfl_up /
+// __shfl_down do).  DPP wavefront shifts (wave_shr:1 / wave_shl:1, GFX9 DPP controls 0x138 /
+// 0x130) move the two halves of a double through the VALU, without the LDS round trip of
+// ds_bpermute.
+#ifndef MPAS_SHFL_BPERMUTE
+__device__ __forceinline__ double up1(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x138, 0xf, 0xf, false),
+                          __builtin_amdgcn_update_dpp(lo, lo, 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double dn1(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x130, 0xf, 0xf, false),
+                          __builtin_amdgcn_update_dpp(lo, lo, 0x130, 0xf, 0xf, false));
+}
+#else
 __device__ __forceinline__ double up1(double x) { return __shfl_up(x, 1, 64); }
 __device__ __forceinline__ double dn1(double x) { return __shfl_down(x, 1, 64); }
+#endif
 __device__ __forceinline__ double up2(double x) { return __shfl_up(x, 2, 64); }
+// lane-1 / lane+1 value with 0.0 shifted in at the end lane
+// (bound_ctrl: the out-of-range lane reads 0)
+__device__ __forceinline__ double up1z(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, 0x138, 0xf, 0xf, true),
+                          __builtin_amdgcn_mov_dpp(lo, 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ double dn1z(double x) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, 0x130, 0xf, 0xf, true),
+                          __builtin_amdgcn_mov_dpp(lo, 0x130, 0xf, 0xf, true));
+}
+
+// The column's tridiagonal sweeps (mpas_atm_time_integration.F:2675-2682) with lane = level.
+// Forward x(k) = (x(k) - a(k) x(k-1)) alpha(k), k = 2..K (lanes 1..K-1), then backward
+// x(k) = x(k) - gamma(k) x(k+1), k = K..1 (lanes K-1..0).  Instead of one lane per iteration,
+// every lane re-evaluates its update from its neighbour's current value each iteration: after
+// iteration j lanes <= j (forward) / >= K-1-j (backward) hold their final values, and each is
+// computed from exactly the operands the sequential recurrence uses, so the result is the same
+// bit for bit.  Lanes outside the sweep take a = 0, alpha = 1 / gamma = 0 and keep their value.
+__device__ __forceinline__ double thomas_column(double r, double a, double alpha, double gamma, int k, int K) {
+  const bool fwd = k >= 1 && k < K, bwd = k < K;
+  const double af = fwd ? a : 0.0, alf = fwd ? alpha : 1.0, gb = bwd ? gamma : 0.0;
+  double x = r;
+  for (int it = 1; it < K; ++it) x = (r - af * up1z(x)) * alf;
+  const double xf = x;
+  for (int it = 0; it < K; ++it) x = xf - gb * dn1z(x);
+  return x;
+}
 
 // A wave-uniform fp64 mesh value read as two int32 halves: integer loads cannot alias the
 // kernel's fp64 stores (TBAA), so the compiler proves them unclobbered and issues them on the
@@ -1548,14 +1593,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
             cofwtm * (tsm + resm * rtppm);
     }
     // tridiagonal solve sweeping up and then down the column (2675-2682), reference order
-    for (int kk = 1; kk < K; ++kk) {
-      const double xm = readlane_d(rwp, kk - 1);
-      if (k == kk) rwp = (rwp - a_tri * xm) * alpha_tri;
-    }
-    for (int kk = K - 1; kk >= 0; --kk) {
-      const double xp = readlane_d(rwp, kk + 1);
-      if (k == kk) rwp = rwp - gamma_tri * xp;
-    }
+    rwp = thomas_column(rwp, a_tri, alpha_tri, gamma_tri, k, K);
     // implicit Rayleigh damping of w (2687-2693)
     const double rzm = up1(rz);
     if (act && k >= 1) {
