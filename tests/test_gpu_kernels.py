@@ -69,3 +69,18 @@ def test_fused_substep_loop_equals_substeps_with_damping():
     for n in POST:
         assert np.array_equal(b.get("diag", n), want[n]), n
     b.close()
+
+
+def test_acoustic_substep_bitwise_vs_reference_fixture():
+    """The acoustic sub-step is +,-,*,/ only (no pow / transcendental), evaluated in the reference's
+    operation order with FMA contraction off, so it reproduces the reference's doubles exactly --
+    including the tridiagonal sweeps, which run as DPP wavefront-shift iterations."""
+    z, dy = _fixture_dycore()
+    dy.time_acoustic_step(float(z["dts"]), small_step=int(z["small_step"]), reps=1)
+    dy.synchronize()
+    for n in POST:
+        got = dy.get("diag", n).reshape(z["post_diag." + n].shape)
+        ref = z["post_diag." + n]
+        nd = int(np.count_nonzero(got != ref))
+        assert nd == 0, f"{n}: {nd} values differ, max abs {np.max(np.abs(got - ref)):.3e}"
+    dy.close()
