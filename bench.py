@@ -67,6 +67,11 @@ def main():
     ap.add_argument("--varres", type=int, default=0, metavar="NCELLS",
                     help="BASELINE.json configs[4]: variable-resolution SCVT (20x refinement) with NCELLS cells, "
                          "e.g. 835586")
+    ap.add_argument("--init", default=None, metavar="FILE",
+                    help="start from an MPAS init file (x1.N.init.nc, netCDF CDF-1/2/5) instead of the synthetic "
+                         "JW case; needs --dt and --len-disp (namelist config_dt / config_len_disp)")
+    ap.add_argument("--dt", type=float, default=None)
+    ap.add_argument("--len-disp", type=float, default=None)
     ap.add_argument("--moist", action="store_true",
                     help="BASELINE.json configs[3]: moist JW (qv) + tracer blobs, num_scalars=6, monotone transport")
     ap.add_argument("--no-graph", action="store_true")
@@ -95,6 +100,11 @@ def main():
     if args.num_scalars is None:
         args.num_scalars = 6 if args.moist else 1
     def make_case():
+        if args.init:
+            from mpas_dycore.mpas_files import read_init
+            if args.dt is None or args.len_disp is None:
+                raise SystemExit("--init needs --dt and --len-disp")
+            return read_init(args.init, config=dict(config_dt=args.dt, config_len_disp=args.len_disp))
         if args.varres:
             from mpas_dycore.cases import varres_case
             return varres_case(args.varres, ratio=20.0, K=args.levels, ns=args.num_scalars, moist=args.moist)
@@ -111,7 +121,7 @@ def main():
     t_build = time.time() - t_build
 
     # WSM6-like species set: every scalar is a moist species (moist_start..moist_end, qtot)
-    moist_end = case["num_scalars"] if args.moist else 1
+    moist_end = case["num_scalars"] if (args.moist or args.init) else 1
     nparts = world * args.blocks
     if nparts > 1:
         blocks, placement = decomp.rank_blocks(case, world, rank, args.blocks)
@@ -192,9 +202,13 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (icosahedral SCVT mesh + Jablonowski-Williamson baroclinic wave, built on the box)",
+        "data": (f"MPAS init file {args.init}" if args.init else
+                 "synthetic (icosahedral SCVT mesh + Jablonowski-Williamson baroclinic wave, built on the box)"),
         "config": {
-            "workload": (f"variable-resolution SCVT, {case['nCells']} cells (20x refinement, "
+            "workload": (f"MPAS init file {os.path.basename(args.init)}: {case['nCells']} cells, "
+                         f"{case['nVertLevels']} levels, {case['num_scalars']} scalars, dt={dt:g}s "
+                         f"(one full atm_srk3 per step)" if args.init else
+                         f"variable-resolution SCVT, {case['nCells']} cells (20x refinement, "
                          f"{case['dcEdge'].min() / 1e3:.1f}-{case['dcEdge'].max() / 1e3:.0f} km, maxEdges="
                          f"{case['maxEdges']}), {case['nVertLevels']} levels, dt={dt:g}s (BASELINE.json configs[4] "
                          f"analogue; one full atm_srk3 per step)" if args.varres else

@@ -12,7 +12,7 @@ from __future__ import annotations
 LOCATION = {}
 for n in ("latCell lonCell xCell yCell zCell areaCell invAreaCell meshDensity nEdgesOnCell indexToCellID "
           "edgesOnCell cellsOnCell verticesOnCell kiteForCell edgesOnCell_sign defc_a defc_b zgrid zz dss "
-          "zb_cell zb3_cell theta rho scalars rho_base theta_base w coeffs_reconstruct").split():
+          "zb_cell zb3_cell theta rho scalars rho_base theta_base w coeffs_reconstruct t_init").split():
     LOCATION[n] = "cell"
 for n in ("latEdge lonEdge xEdge yEdge zEdge dcEdge dvEdge invDcEdge invDvEdge angleEdge fEdge "
           "meshScalingDel2 meshScalingDel4 nEdgesOnEdge nAdvCellsForEdge cellsOnEdge verticesOnEdge "
@@ -32,7 +32,7 @@ INDEX_TARGET = {
 ONE_BASED_SMALL = {"kiteForCell"}
 COUNTS = {"nEdgesOnCell", "nEdgesOnEdge", "nAdvCellsForEdge", "indexToCellID"}
 
-VERTICAL_1D = ("fzm", "fzp", "rdzw", "rdzu")
+VERTICAL_1D = ("fzm", "fzp", "rdzw", "rdzu", "u_init", "v_init")
 SCALARS_0D = ("cf1", "cf2", "cf3")
 
 

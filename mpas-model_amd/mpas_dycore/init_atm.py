@@ -343,7 +343,49 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
     rho = rho_zz * zz
     theta = t / (1.0 + 1.61 * qv)
 
-    # ---- model-init precompute (mpas_atm_core.F)
+    scalars = np.zeros((nC, nz1, ns))
+    if ns >= 1:
+        scalars[:, :, 0] = qv
+    if ns > 1:
+        # smooth positive blobs so the monotonic limiter is exercised (SURVEY.md §8d)
+        xc = np.stack([m["xCell"], m["yCell"], m["zCell"]], 1) / R
+        rng = np.random.default_rng(20250202)
+        for s in range(1, ns):
+            ctr = _normalize(rng.normal(size=3))
+            d = arc_length(xc, np.broadcast_to(ctr, xc.shape))
+            prof = np.exp(-((np.arange(nz1) - nz1 * 0.3) / (0.15 * nz1)) ** 2)
+            scalars[:, :, s] = 1.0e-3 * np.exp(-(d / 0.5) ** 2)[:, None] * prof[None, :]
+
+    out = dict(m)
+    out.update(
+        nVertLevels=K, num_scalars=ns, config=cfg,
+        zgrid=zgrid, zz=zz, zxu=zxu, rdzw=vg["rdzw"], rdzu=vg["rdzu"], fzm=fzm, fzp=fzp,
+        cf1=vg["cf1"], cf2=vg["cf2"], cf3=vg["cf3"],
+        fEdge=fEdge, fVertex=fVertex, deriv_two=d2, zb=zb, zb3=zb3,
+        # state (time level 1) and diag inputs of atm_init_coupled_diagnostics
+        u=u, w=w, theta=theta, rho=rho, scalars=scalars, rho_base=rb, theta_base=tb,
+    )
+    return model_init(out, cfg)
+
+
+def model_init(out: dict, cfg: dict) -> dict:
+    """The dycore's model-init precompute on the fields of an MPAS input stream
+    (mpas_atm_core.F:311-463 and 927-1288): edge signs, zb_cell/zb3_cell, kiteForCell,
+    adv_coefs compression and 3rd-order coupling, damping coefficients, mesh scaling,
+    inverses, and -- when the input does not carry them -- defc_a/defc_b and
+    coeffs_reconstruct.  ``out`` holds the mesh, zgrid, zb/zb3, deriv_two and the state;
+    it is updated in place and returned."""
+    m = out
+    nC, nE, nV = m["nCells"], m["nEdges"], m["nVertices"]
+    nz1 = m["nVertLevels"]
+    nz = nz1 + 1
+    coe, voe = m["cellsOnEdge"], m["verticesOnEdge"]
+    c1, c2 = coe[:, 0], coe[:, 1]
+    nEoC, eoc = m["nEdgesOnCell"], m["edgesOnCell"]
+    zgrid, zb, zb3, d2 = m["zgrid"], m["zb"], m["zb3"], m["deriv_two"]
+    coef3 = cfg["config_coef_3rd_order"]
+
+    # ---- signs, zb_cell, kiteForCell (mpas_atm_core.F:987-1074)
     edgesOnCell_sign = np.zeros((nC, m["maxEdges"]))
     zb_cell = np.zeros((nC, m["maxEdges"], nz))
     zb3_cell = np.zeros((nC, m["maxEdges"], nz))
@@ -365,10 +407,14 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
     eov = m["edgesOnVertex"]
     edgesOnVertex_sign = np.where(voe[eov, 1] == np.arange(nV)[:, None], 1.0, -1.0)
 
+    # ---- adv_coefs compression and 3rd-order coupling (1121-1288)
     nAdv, advCells, adv_coefs, adv_coefs_3rd = adv_coef_compression(m, d2)
     adv_coefs_3rd = coef3 * adv_coefs_3rd
     zb3_cell = coef3 * zb3_cell
-    defc_a, defc_b = compute_defc(m)
+    if "defc_a" in m and "defc_b" in m:
+        defc_a, defc_b = m["defc_a"], m["defc_b"]
+    else:
+        defc_a, defc_b = compute_defc(m)
 
     # damping (mpas_atm_core.F:1105-1116)
     zt_c = zgrid[:, nz1]
@@ -384,35 +430,17 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
         msd2 = np.ones(nE)
         msd4 = np.ones(nE)
 
-    scalars = np.zeros((nC, nz1, ns))
-    if ns >= 1:
-        scalars[:, :, 0] = qv
-    if ns > 1:
-        # smooth positive blobs so the monotonic limiter is exercised (SURVEY.md §8d)
-        xc = np.stack([m["xCell"], m["yCell"], m["zCell"]], 1) / R
-        rng = np.random.default_rng(20250202)
-        for s in range(1, ns):
-            ctr = _normalize(rng.normal(size=3))
-            d = arc_length(xc, np.broadcast_to(ctr, xc.shape))
-            prof = np.exp(-((np.arange(nz1) - nz1 * 0.3) / (0.15 * nz1)) ** 2)
-            scalars[:, :, s] = 1.0e-3 * np.exp(-(d / 0.5) ** 2)[:, None] * prof[None, :]
-
-    out = dict(m)
     out.update(
-        nVertLevels=K, num_scalars=ns, config=cfg,
-        zgrid=zgrid, zz=zz, zxu=zxu, rdzw=vg["rdzw"], rdzu=vg["rdzu"], fzm=fzm, fzp=fzp,
-        cf1=vg["cf1"], cf2=vg["cf2"], cf3=vg["cf3"], dss=dss,
-        fEdge=fEdge, fVertex=fVertex, deriv_two=d2, zb=zb, zb3=zb3, zb_cell=zb_cell, zb3_cell=zb3_cell,
+        config=cfg, dss=dss, zb_cell=zb_cell, zb3_cell=zb3_cell,
         edgesOnCell_sign=edgesOnCell_sign, edgesOnVertex_sign=edgesOnVertex_sign, kiteForCell=kiteForCell,
         nAdvCellsForEdge=nAdv, advCellsForEdge=advCells, adv_coefs=adv_coefs, adv_coefs_3rd=adv_coefs_3rd,
         defc_a=defc_a, defc_b=defc_b, meshScalingDel2=msd2, meshScalingDel4=msd4,
         invAreaCell=1.0 / m["areaCell"], invDvEdge=1.0 / m["dvEdge"], invDcEdge=1.0 / m["dcEdge"],
         invAreaTriangle=1.0 / m["areaTriangle"],
-        # state (time level 1) and diag inputs of atm_init_coupled_diagnostics
-        u=u, w=w, theta=theta, rho=rho, scalars=scalars, rho_base=rb, theta_base=tb,
     )
     # model-init precompute of the velocity reconstruction (mpas_atm_core.F:408-409)
-    out["coeffs_reconstruct"] = init_reconstruct(out)
+    if "coeffs_reconstruct" not in out:
+        out["coeffs_reconstruct"] = init_reconstruct(out)
     return out
 
 
