@@ -96,6 +96,10 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep);
 int mpas_dyc_shift_time_levels(mpas_dyc_ctx* ctx);
 /* Block until all queued device work of the context is complete. */
 int mpas_dyc_synchronize(mpas_dyc_ctx* ctx);
+/* atm_compute_output_diagnostics(state, time_level, diag, mesh) (mpas_atm_core.F:753, called
+ * before history writes at :544 and :694): diag theta, rho and pressure from theta_m, rho_zz,
+ * scalars(index_qv) of the time level, zz, pressure_base and pressure_p.  Asynchronous. */
+int mpas_dyc_output_diagnostics(mpas_dyc_ctx* ctx, int32_t time_level);
 
 /* ---- domain decomposition: several blocks per process, halo exchange ----
  *

@@ -67,7 +67,7 @@ struct Ptrs {
   // ---- diag
   double *theta, *rho, *rho_base, *theta_base, *rho_p, *rho_p_save, *rho_pp, *rho_zz_old_split;
   double *rtheta_base, *rtheta_p, *rtheta_p_save, *rtheta_pp, *rtheta_pp_old;
-  double *exner, *exner_base, *pressure_base, *pressure_p, *h_divergence, *kdiff, *ke, *divergence;
+  double *exner, *exner_base, *pressure_base, *pressure_p, *pressure, *h_divergence, *kdiff, *ke, *divergence;
   double *pv_cell, *tend_rtheta_adv, *cqw, *cofwr, *cofwz, *cofwt, *coftz, *a_tri, *alpha_tri, *gamma_tri, *cofrz;
   double *rw, *rw_p, *rw_save, *wwAvg, *wwAvg_split;
   double *ru, *ruAvg, *ruAvg_split, *ru_p, *ru_save, *cqu, *rho_edge, *v, *pv_edge, *gradPVn, *gradPVt;

@@ -218,7 +218,7 @@ void build_registry(Block& c) {
   // diag
   for (const char* n : {"theta", "rho", "rho_base", "theta_base", "rho_p", "rho_p_save", "rho_pp",
                         "rho_zz_old_split", "rtheta_base", "rtheta_p", "rtheta_p_save", "rtheta_pp",
-                        "rtheta_pp_old", "exner", "exner_base", "pressure_base", "pressure_p", "h_divergence",
+                        "rtheta_pp_old", "exner", "exner_base", "pressure_base", "pressure_p", "pressure", "h_divergence",
                         "kdiff", "ke", "divergence", "pv_cell", "tend_rtheta_adv", "cqw", "cofwr", "cofwz",
                         "cofwt", "a_tri", "alpha_tri", "gamma_tri"})
     add(c, "diag", n, L_CELL, K);
@@ -305,7 +305,7 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   p.scalars1 = P<double>(c, b, "state", "scalars", 1); p.scalars2 = P<double>(c, b, "state", "scalars", 2);
   DG(theta); DG(rho); DG(rho_base); DG(theta_base); DG(rho_p); DG(rho_p_save); DG(rho_pp); DG(rho_zz_old_split);
   DG(rtheta_base); DG(rtheta_p); DG(rtheta_p_save); DG(rtheta_pp); DG(rtheta_pp_old);
-  DG(exner); DG(exner_base); DG(pressure_base); DG(pressure_p); DG(h_divergence); DG(kdiff); DG(ke); DG(divergence);
+  DG(exner); DG(exner_base); DG(pressure_base); DG(pressure_p); DG(pressure); DG(h_divergence); DG(kdiff); DG(ke); DG(divergence);
   DG(pv_cell); DG(tend_rtheta_adv); DG(cqw); DG(cofwr); DG(cofwz); DG(cofwt); DG(coftz); DG(a_tri); DG(alpha_tri);
   DG(gamma_tri); DG(cofrz);
   DG(rw); DG(rw_p); DG(rw_save); DG(wwAvg); DG(wwAvg_split);
@@ -1508,6 +1508,18 @@ int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
   int r = init_diagnostics(ctx, dt);
   HIPCHK(hipGetLastError());
   return r;
+}
+
+int mpas_dyc_output_diagnostics(mpas_dyc_ctx* ctx, int32_t time_level) {
+  if (!ctx || (time_level != 1 && time_level != 2)) return MPAS_DYC_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  for (auto& b : ctx->blk) {
+    const Ptrs p = make_ptrs(ctx, b);
+    const Dims& d = b.d;
+    LAUNCH(k_output_diagnostics, d.nCells, d, p, (int)time_level, ctx->index_qv);
+  }
+  HIPCHK(hipGetLastError());
+  return MPAS_DYC_OK;
 }
 
 int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {

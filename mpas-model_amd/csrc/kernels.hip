@@ -2149,6 +2149,24 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges_b(Dims d, Ptrs p, 
 }
 
 // ============================================================================
+// atm_compute_output_diagnostics  (core_atmosphere/mpas_atm_core.F:753-800): theta, rho and
+// pressure of the history output from the prognostic state of time level `tl`
+// ============================================================================
+__global__ __launch_bounds__(BLOCK_THREADS) void k_output_diagnostics(Dims d, Ptrs p, int tl, int index_qv) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  const size_t o = (size_t)c * K + k;
+  const double* theta_m = tl == 1 ? p.theta_m1 : p.theta_m2;
+  const double* rho_zz = tl == 1 ? p.rho_zz1 : p.rho_zz2;
+  const double* scalars = tl == 1 ? p.scalars1 : p.scalars2;
+  p.theta[o] = theta_m[o] / (1.0 + RVORD * scalars[SIX(c, k, index_qv)]);
+  p.rho[o] = rho_zz[o] * p.zz[o];
+  p.pressure[o] = p.pressure_base[o] + p.pressure_p[o];
+}
+
+// ============================================================================
 // atm_init_coupled_diagnostics  (mpas_atm_time_integration.F:5906-5988)
 // ============================================================================
 // cells: theta_m, rho_zz (5909-5914)

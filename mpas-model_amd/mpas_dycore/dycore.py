@@ -175,6 +175,10 @@ class Dycore:
         """atm_timestep -> atm_srk3 (mpas_atm_time_integration.F:87-139); asynchronous."""
         self._check(self.lib.mpas_dyc_timestep(self.h, float(dt), int(itimestep)), "atm_timestep")
 
+    def output_diagnostics(self, time_level: int = 1):
+        """atm_compute_output_diagnostics (mpas_atm_core.F:753-800): diag theta, rho, pressure."""
+        self._check(self.lib.mpas_dyc_output_diagnostics(self.h, int(time_level)), "output_diagnostics")
+
     def shift_time_levels(self):
         self._check(self.lib.mpas_dyc_shift_time_levels(self.h), "shift_time_levels")
 
@@ -208,7 +212,7 @@ class Dycore:
 
 # horizontal location of device fields not in fields.LOCATION
 _LOCS = {}
-for _n in ("theta_m", "rho_zz", "rho_p", "rtheta_p", "exner", "pressure_p", "kdiff", "ke", "divergence", "rw",
+for _n in ("theta_m", "rho_zz", "rho_p", "rtheta_p", "exner", "pressure_p", "pressure", "kdiff", "ke", "divergence", "rw",
            "wwAvg", "cqw", "h_divergence", "pv_cell", "rho_pp", "rtheta_pp", "rw_p", "exner_base", "pressure_base",
            "rtheta_base", "coftz", "cofwz", "cofwr", "cofwt", "a_tri", "alpha_tri", "gamma_tri", "rw_save",
            "tend_rtheta_adv", "rho_p_save", "rtheta_p_save", "rho_zz_old_split", "rtheta_pp_old", "wwAvg_split",

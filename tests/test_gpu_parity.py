@@ -94,3 +94,21 @@ def test_moist_trajectory_matches_reference_fixture():
                 tol = 1e-10 if (it + 1 == 10 or name in ("w", "scalars")) else 1e-12
                 assert err <= tol, f"step {it + 1} {key}: rel Linf {err:.3e}"
     dy.close()
+
+
+def test_output_diagnostics(small_case):
+    """atm_compute_output_diagnostics (mpas_atm_core.F:753-800) after one step, against the
+    routine's three expressions evaluated in numpy on the downloaded state (bitwise)."""
+    dy = _dycore(small_case)
+    dy.atm_timestep(DT, 1)
+    dy.shift_time_levels()
+    dy.output_diagnostics(1)
+    dy.synchronize()
+    rvord = 461.6 / 287.0
+    th_m, rzz, q = dy.get("state", "theta_m", 1), dy.get("state", "rho_zz", 1), dy.get("state", "scalars", 1)
+    pb, pp = dy.get("diag", "pressure_base"), dy.get("diag", "pressure_p")
+    zz = np.asarray(small_case["zz"])
+    assert np.array_equal(dy.get("diag", "theta"), th_m / (1.0 + rvord * q[:, :, 0]))
+    assert np.array_equal(dy.get("diag", "rho"), rzz * zz)
+    assert np.array_equal(dy.get("diag", "pressure"), pb + pp)
+    dy.close()
