@@ -342,6 +342,12 @@ inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + WAVES_PER_BLOCK - 
 #define DIVDAMP_EPW 2  // edges per wavefront in k_divdamp
 #endif
 
+#define LAUNCH_E(kern, n, ...)                                                                             \
+  do {                                                                                                     \
+    if ((n) > 0 && !ctx->planning)                                                                         \
+      hipLaunchKernelGGL(kern, dim3((unsigned)(((n) + EDGE_WPB - 1) / EDGE_WPB)), dim3(EDGE_THREADS), 0,    \
+                         ctx->stream, __VA_ARGS__);                                                        \
+  } while (0)
 #define LAUNCH(kern, n, ...)                                                                               \
   do {                                                                                                     \
     if ((n) > 0 && !ctx->planning)                                                                         \
@@ -670,6 +676,15 @@ void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts)
   LAUNCH(k_vert_imp_coefs, std::max(d.nCellsSolve, 1), d, p, dts, ctx->cf.epssm);
 }
 
+// pair-layout edge kernels (k_*_p: two edges per wave, two levels per lane) need an even K
+inline bool pair_layout(const Dims& d) {
+#ifdef MPAS_NO_PAIR
+  return false;
+#else
+  return d.K % 2 == 0 && d.K <= 64;
+#endif
+}
+
 // part: 0 = all kernels; 1 = only k_dyn_cells1, which reads nothing the exchange after the
 // diagnostics (1234-1249) or at the substep boundary (1282-1297) delivers; 2 = the rest
 void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, double dt, int part = 0) {
@@ -698,11 +713,17 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   }
   if (part == 1) return;
 #ifndef MPAS_NO_CELL_REC
-  if ((d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2) {
-    if (d.maxEdges == 6 && rk_step == 1) LAUNCH((k_dyn_edges_b<true, 10>), d.nEdges, d, p, cf, s, 0);
-    if (d.maxEdges == 6 && rk_step != 1) LAUNCH((k_dyn_edges_b<false, 10>), d.nEdges, d, p, cf, s, 1);
-    if (d.maxEdges == 7 && rk_step == 1) LAUNCH((k_dyn_edges_b<true, 12>), d.nEdges, d, p, cf, s, 0);
-    if (d.maxEdges == 7 && rk_step != 1) LAUNCH((k_dyn_edges_b<false, 12>), d.nEdges, d, p, cf, s, 1);
+  if (batched(d) && pair_layout(d)) {
+    const int64_t nw = (d.nEdges + 1) / 2;
+    if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 10>), nw, d, p, cf, s, 0);
+    if (d.maxEdges == 6 && rk_step != 1) LAUNCH_E((k_dyn_edges_p<false, 10>), nw, d, p, cf, s, 1);
+    if (d.maxEdges == 7 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 12>), nw, d, p, cf, s, 0);
+    if (d.maxEdges == 7 && rk_step != 1) LAUNCH_E((k_dyn_edges_p<false, 12>), nw, d, p, cf, s, 1);
+  } else if ((d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2) {
+    if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_b<true, 10>), d.nEdges, d, p, cf, s, 0);
+    if (d.maxEdges == 6 && rk_step != 1) LAUNCH_E((k_dyn_edges_b<false, 10>), d.nEdges, d, p, cf, s, 1);
+    if (d.maxEdges == 7 && rk_step == 1) LAUNCH_E((k_dyn_edges_b<true, 12>), d.nEdges, d, p, cf, s, 0);
+    if (d.maxEdges == 7 && rk_step != 1) LAUNCH_E((k_dyn_edges_b<false, 12>), d.nEdges, d, p, cf, s, 1);
   } else
 #endif
   if (rk_step == 1)
@@ -725,8 +746,8 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     }
   }
   if (!batched(d)) LAUNCH(k_dyn_advflux, d.nEdges, d, p);
-  else if (d.maxEdges == 6) LAUNCH(k_dyn_advflux_b<10>, d.nEdges, d, p);
-  else LAUNCH(k_dyn_advflux_b<12>, d.nEdges, d, p);
+  else if (d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_b<10>, d.nEdges, d, p);
+  else LAUNCH_E(k_dyn_advflux_b<12>, d.nEdges, d, p);
 #ifndef MPAS_NO_CELL_REC
   if (d.maxEdges == 6 || d.maxEdges == 7) {
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH((k_dyn_cells3_r<6, true>), d.nCellsSolve, d, p, cf, s);
@@ -760,10 +781,18 @@ double coef_divdamp(const mpas_dyc_ctx* ctx, double dts) {  // 2761-2763
 // the previous sub-step (k_acoustic_edges<true>)
 void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int damp,
                     int phase) {
+  if (pair_layout(d)) {
+    const int64_t nw = (d.nEdges + 1) / 2;
+    if (damp)
+      LAUNCH_E(k_acoustic_edges_p<true>, nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase);
+    else
+      LAUNCH_E(k_acoustic_edges_p<false>, nw, d, p, dts, small_step, 0.0, phase);
+    return;
+  }
   if (damp)
-    LAUNCH(k_acoustic_edges<true>, d.nEdges, d, p, dts, small_step, coef_divdamp(ctx, dts), phase);
+    LAUNCH_E(k_acoustic_edges<true>, d.nEdges, d, p, dts, small_step, coef_divdamp(ctx, dts), phase);
   else
-    LAUNCH(k_acoustic_edges<false>, d.nEdges, d, p, dts, small_step, 0.0, phase);
+    LAUNCH_E(k_acoustic_edges<false>, d.nEdges, d, p, dts, small_step, 0.0, phase);
 }
 
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
@@ -798,10 +827,10 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double d
   LAUNCH(k_diag_vertices, d.nVertices, d, p, u);  // the batched variant measured slower
   if (d.maxEdges == 6) {
     LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
-    LAUNCH(k_diag_edges_b<10>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
+    LAUNCH_E(k_diag_edges_b<10>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
   } else {
     LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
-    LAUNCH(k_diag_edges_b<12>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
+    LAUNCH_E(k_diag_edges_b<12>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
   }
 }
 
@@ -1199,7 +1228,8 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   for (auto& b : ctx->blk) {
     build_registry(b);
     for (auto& f : b.fields) {
-      const int64_t nb = field_bytes(b, f);
+      // 256 B of slack: the two-levels-per-lane kernels read 16 B at the last level of the last column
+      const int64_t nb = field_bytes(b, f) + 256;
       for (int t = 0; t < f.ntl; ++t) {
         if (hipMalloc(&f.buf[t], nb) != hipSuccess || hipMemset(f.buf[t], 0, nb) != hipSuccess) {
           mpas_dyc_destroy(ctx);

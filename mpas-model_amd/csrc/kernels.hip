@@ -41,6 +41,17 @@ __device__ __forceinline__ int wave_elem(int start) {
 }
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// edge-stencil kernels (TRiSK / advection / acoustic edge phases) run EDGE_WPB waves per
+// workgroup: consecutive (SFC-ordered) edges of one workgroup share neighbour columns in the CU's L1
+#ifndef EDGE_WPB
+#define EDGE_WPB 4
+#endif
+#define EDGE_THREADS (64 * EDGE_WPB)
+__device__ __forceinline__ int wave_elem_e() {
+  int e = xcd_block() * EDGE_WPB + (threadIdx.x >> 6);
+  return __builtin_amdgcn_readfirstlane(e);
+}
+
 // Scalar arrays are scalar-major in HBM: scalars / scalars_tend as [ns][nCells+1][K],
 // horiz_flux_array as [ns][nEdges+1][K], so every per-scalar access is a contiguous
 // column (the Fortran image (ns, K, n+1) is transposed at the C ABI).
@@ -550,9 +561,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges(Dims d, Ptrs p, Con
 // as k_dyn_edges; solve edges (tend_u and, at rk1, del2) and halo edges (rk1 del2 only) are
 // separate paths so that neither issues the other's loads.
 template <bool RK1, int NE2>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_b(Dims d, Ptrs p, Config cf, DynTendScal s,
+__global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_b(Dims d, Ptrs p, Config cf, DynTendScal s,
                                                                int finalize) {
-  const int e = wave_elem(0);
+  const int e = wave_elem_e();
   if (e >= d.nEdges) return;
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
@@ -1201,8 +1212,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3_r(Dims d, Ptrs p, 
 // k_dyn_advflux with batched loads (NA = 2*maxEdges-2 >= nAdvCellsForEdge): the edge's index
 // and coefficient rows and its ru column go out together, then the 2*NA neighbour columns.
 template <int NA>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_advflux_b(Dims d, Ptrs p) {
-  const int e = wave_elem(0);
+__global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_b(Dims d, Ptrs p) {
+  const int e = wave_elem_e();
   if (e >= d.nEdges) return;
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
@@ -1475,9 +1486,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert_b(Dims d, Ptrs p
 // double either way: the damped ru_p is rounded before the update adds to it.
 // phase: 0 = every edge; 1 / 2 = edges without / with a halo cell (split around that exchange).
 template <bool DD>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step,
+__global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step,
                                                                   double coef_divdamp, int phase) {
-  const int e = wave_elem(0);
+  const int e = wave_elem_e();
   if (e >= d.nEdges) return;
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
@@ -1518,6 +1529,268 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_edges(Dims d, Ptrs p
   if (act) {
     p.ru_p[o] = rup;
     p.ruAvg[o] = rua + rup;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pair layout for gather-heavy edge kernels: one wavefront carries TWO edges (lanes 0-31 edge
+// 2w, lanes 32-63 edge 2w+1) and each lane TWO consecutive levels (2l, 2l+1), so every column
+// access is one 16-byte load per lane.  On MI355X a scattered 64-lane vector load costs about
+// the same ~14 CU cycles whether it moves 8 or 16 bytes per lane (exp microbenchmark, DESIGN.md
+// §4), so this halves the instruction cost of the neighbour gathers.  Needs an even K.
+struct d2 {
+  double x, y;
+};
+__device__ __forceinline__ d2 ld2(const double* __restrict__ a) {
+  d2 r;
+  __builtin_memcpy(&r, a, 16);
+  return r;
+}
+__device__ __forceinline__ void st2(double* a, d2 v) { __builtin_memcpy(a, &v, 16); }
+__device__ __forceinline__ int pair_wave() {
+  return __builtin_amdgcn_readfirstlane(xcd_block() * EDGE_WPB + (threadIdx.x >> 6));
+}
+__device__ __forceinline__ int pair_half() { return (threadIdx.x >> 5) & 1; }
+__device__ __forceinline__ int sel(int h, int a, int b) { return h ? b : a; }
+__device__ __forceinline__ double sel(int h, double a, double b) { return h ? b : a; }
+
+// vertical neighbours in the pair layout (levels 2l, 2l+1 on lane l of each half-wave), with the
+// end-of-column behaviour of up1 / up2 / dn1 (a lane with no neighbour keeps its own value)
+__device__ __forceinline__ double lane_shr1(double v) {  // value of lane-1 (own at lane 0)
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x138, 0xf, 0xf, false),
+                          __builtin_amdgcn_update_dpp(lo, lo, 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double lane_shl1(double v) {  // value of lane+1 (own at lane 63)
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x130, 0xf, 0xf, false),
+                          __builtin_amdgcn_update_dpp(lo, lo, 0x130, 0xf, 0xf, false));
+}
+__device__ __forceinline__ d2 km1(d2 v, int l) {  // levels (k-1) of (2l, 2l+1)
+  const double t = lane_shr1(v.y);
+  return d2{l == 0 ? v.x : t, v.x};
+}
+__device__ __forceinline__ d2 km2(d2 v, int l) {  // levels (k-2)
+  const double tx = lane_shr1(v.x), ty = lane_shr1(v.y);
+  return d2{l == 0 ? v.x : tx, l == 0 ? v.y : ty};
+}
+__device__ __forceinline__ d2 kp1(d2 v) {  // levels (k+1)
+  return d2{v.y, lane_shl1(v.x)};
+}
+
+// k_dyn_edges_b in the pair layout (NE2 = 2*maxEdges-2 TRiSK neighbours)
+template <bool RK1, int NE2>
+__global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Config cf, DynTendScal s,
+                                                              int finalize) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  const int e = sel(h, eA, eB);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)e * K + 2 * lc;
+  const bool solveA = eA < d.nEdgesSolve, solveB = hasB && eB < d.nEdgesSolve;
+  const bool solve = h ? solveB : solveA;
+  const bool mine = h == 0 || hasB;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const double invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
+  const d2 re = ld2(p.rho_edge + o);
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
+  const size_t o1 = (size_t)c1 * K + 2 * lc, o2 = (size_t)c2 * K + 2 * lc;
+  const int kx = 2 * l, ky = 2 * l + 1;  // true levels of the two components
+  const bool stx = mine && kx < K, sty = mine && ky < K;
+  auto store = [&](double* a, d2 v) {
+    if (stx && sty) st2(a + o, v);
+  };
+  // rk1 del^2 of u (4856-4883), all edges
+  auto del2 = [&](d2 tue, d2 dv1, d2 dv2, d2 vo1, d2 vo2, d2 kd1, d2 kd2, double invDv, double msd2) {
+    const double r_dc = invDc;
+    const double r_dv = fmin(invDv, 4 * invDc);
+    d2 ud, out;
+    ud.x = (dv2.x - dv1.x) * r_dc - (vo2.x - vo1.x) * r_dv;
+    ud.y = (dv2.y - dv1.y) * r_dc - (vo2.y - vo1.y) * r_dv;
+    store(p.delsq_u, d2{0.0 + ud.x, 0.0 + ud.y});
+    out.x = tue.x + re.x * (0.5 * (kd1.x + kd2.x)) * ud.x * msd2;
+    out.y = tue.y + re.y * (0.5 * (kd1.y + kd2.y)) * ud.y * msd2;
+    store(p.tend_u_euler, out);
+  };
+  if (!solveA && !solveB) {  // halo pair: rk1 del2 only
+    if (!RK1) return;
+    const int2 veA = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eA);
+    const int2 veB = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eB);
+    const double invDv = sel(h, ld_uniform_f64(p.invDvEdge + eA), ld_uniform_f64(p.invDvEdge + eB));
+    const double msd2 = sel(h, ld_uniform_f64(p.meshScalingDel2 + eA), ld_uniform_f64(p.meshScalingDel2 + eB));
+    const d2 tue = ld2(p.tend_u_euler + o);
+    const int v1 = sel(h, veA.x, veB.x), v2 = sel(h, veA.y, veB.y);
+    del2(tue, ld2(p.divergence + o1), ld2(p.divergence + o2), ld2(p.vorticity + (size_t)v1 * K + 2 * lc),
+         ld2(p.vorticity + (size_t)v2 * K + 2 * lc), ld2(p.kdiff + o1), ld2(p.kdiff + o2), invDv, msd2);
+    return;
+  }
+  // ---- batch 1: metadata of both edges, own columns
+  const int neoe = sel(h, p.nEdgesOnEdge[eA], p.nEdgesOnEdge[eB]);
+  int eoe[NE2];
+  double wgt[NE2];
+#pragma unroll
+  for (int j = 0; j < NE2; ++j) {
+    eoe[j] = sel(h, p.edgesOnEdge[(size_t)eA * d.maxEdges2 + j], p.edgesOnEdge[(size_t)eB * d.maxEdges2 + j]);
+    wgt[j] = sel(h, ld_uniform_f64(p.weightsOnEdge + (size_t)eA * d.maxEdges2 + j),
+                 ld_uniform_f64(p.weightsOnEdge + (size_t)eB * d.maxEdges2 + j));
+  }
+  int v1 = 0, v2 = 0;
+  double invDv = 0.0, msd2 = 0.0;
+  d2 cqu{}, zxu{};
+  if (RK1) {
+    const int2 veA = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eA);
+    const int2 veB = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eB);
+    v1 = sel(h, veA.x, veB.x);
+    v2 = sel(h, veA.y, veB.y);
+    invDv = sel(h, ld_uniform_f64(p.invDvEdge + eA), ld_uniform_f64(p.invDvEdge + eB));
+    msd2 = sel(h, ld_uniform_f64(p.meshScalingDel2 + eA), ld_uniform_f64(p.meshScalingDel2 + eB));
+    cqu = ld2(p.cqu + o);
+    zxu = ld2(p.zxu + o);
+  }
+  const d2 uk = ld2(p.u2 + o), pve = ld2(p.pv_edge + o);
+  d2 tue = RK1 ? d2{0.0, 0.0} : ld2(p.tend_u_euler + o);
+  if (RK1 && !solve) tue = ld2(p.tend_u_euler + o);  // the halo edge of a mixed pair
+  // ---- batch 2: gathers
+  const d2 rw1 = ld2(p.rw + (size_t)c1 * K1 + 2 * lw), rw2 = ld2(p.rw + (size_t)c2 * K1 + 2 * lw);
+  const d2 ke1 = ld2(p.ke + o1), ke2 = ld2(p.ke + o2), hd1 = ld2(p.h_divergence + o1), hd2 = ld2(p.h_divergence + o2);
+  d2 pv[NE2], uu[NE2];
+#pragma unroll
+  for (int j = 0; j < NE2; ++j) {
+    const size_t oj = (size_t)eoe[j] * K + 2 * lc;
+    pv[j] = ld2(p.pv_edge + oj);
+    uu[j] = ld2(p.u2 + oj);
+  }
+  d2 pp1{}, pp2{}, zz1{}, zz2{}, dpz1{}, dpz2{}, dv1{}, dv2{}, vo1{}, vo2{}, kd1{}, kd2{};
+  if (RK1) {
+    pp1 = ld2(p.pressure_p + o1);
+    pp2 = ld2(p.pressure_p + o2);
+    zz1 = ld2(p.zz + o1);
+    zz2 = ld2(p.zz + o2);
+    dpz1 = ld2(p.dpdz + o1);
+    dpz2 = ld2(p.dpdz + o2);
+    dv1 = ld2(p.divergence + o1);
+    dv2 = ld2(p.divergence + o2);
+    vo1 = ld2(p.vorticity + (size_t)v1 * K + 2 * lc);
+    vo2 = ld2(p.vorticity + (size_t)v2 * K + 2 * lc);
+    kd1 = ld2(p.kdiff + o1);
+    kd2 = ld2(p.kdiff + o2);
+  }
+  const d2 fzm = ld2(p.fzm + 2 * lc), fzp = ld2(p.fzp + 2 * lc), rdzw = ld2(p.rdzw + 2 * lc);
+  // ---- tend_u (PGF rk1 4781-4788, vertical transport 4792-4807, Coriolis/KE 4811-4838)
+  if (RK1 && solve) {
+    tue.x = -cqu.x * ((pp2.x - pp1.x) * invDc / (.5 * (zz2.x + zz1.x)) - 0.5 * zxu.x * (dpz1.x + dpz2.x));
+    tue.y = -cqu.y * ((pp2.y - pp1.y) * invDc / (.5 * (zz2.y + zz1.y)) - 0.5 * zxu.y * (dpz1.y + dpz2.y));
+  }
+  const d2 um1 = km1(uk, l), um2 = km2(uk, l), up1v = kp1(uk);
+  auto wduz_at = [&](int k, double rw1_, double rw2_, double fzm_, double fzp_, double u0, double um1_, double um2_,
+                     double up1_) {
+    const double rwa = 0.5 * (rw1_ + rw2_);
+    if (k == 1 || k == K - 1) return 0.5 * (rw1_ + rw2_) * (fzm_ * u0 + fzp_ * um1_);
+    if (k >= 2 && k <= K - 2) return flux3(um2_, um1_, u0, up1_, rwa, 1.0);
+    return 0.0;
+  };
+  d2 wduz;
+  wduz.x = wduz_at(kx, rw1.x, rw2.x, fzm.x, fzp.x, uk.x, um1.x, um2.x, up1v.x);
+  wduz.y = wduz_at(ky, rw1.y, rw2.y, fzm.y, fzp.y, uk.y, um1.y, um2.y, up1v.y);
+  const d2 wduz_p = kp1(wduz);
+  d2 tu;
+  tu.x = -rdzw.x * (wduz_p.x - wduz.x);
+  tu.y = -rdzw.y * (wduz_p.y - wduz.y);
+  d2 q{0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < NE2; ++j) {
+    if (j < neoe) {
+      q.x = q.x + wgt[j] * uu[j].x * (0.5 * (pve.x + pv[j].x));
+      q.y = q.y + wgt[j] * uu[j].y * (0.5 * (pve.y + pv[j].y));
+    }
+  }
+  tu.x = tu.x + re.x * (q.x - (ke2.x - ke1.x) * invDc) - uk.x * 0.5 * (hd1.x + hd2.x);
+  tu.y = tu.y + re.y * (q.y - (ke2.y - ke1.y) * invDc) - uk.y * 0.5 * (hd1.y + hd2.y);
+  if (finalize) {
+    if (cf.rayleigh_damp_u) {
+      const int k0 = K - cf.number_rayleigh_damp_u_levels;
+      if (kx >= k0) tu.x = tu.x - re.x * uk.x * ((double)(kx + 1 - k0) * s.rayleigh_coef_inverse);
+      if (ky >= k0) tu.y = tu.y - re.y * uk.y * ((double)(ky + 1 - k0) * s.rayleigh_coef_inverse);
+    }
+    tu.x = tu.x + tue.x + PHYS_ZERO;  // tend_ru_physics
+    tu.y = tu.y + tue.y + PHYS_ZERO;
+  }
+  if (solve) store(p.tend_u, tu);
+  if (RK1) del2(tue, dv1, dv2, vo1, vo2, kd1, kd2, invDv, msd2);
+}
+
+// k_acoustic_edges in the pair layout (same expressions, per level)
+template <bool DD>
+__global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,
+                                                                   double coef_divdamp, int phase) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const int eB = min(eA + 1, d.nEdges - 1);
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const bool lev = 2 * l < K;                     // this lane holds levels 2l, 2l+1
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const int bA = phase ? p.edge_bnd[eA] : 0, bB = phase ? p.edge_bnd[eB] : 0;
+  const d2 tu = ld2(p.tend_u + o);
+  auto active = [&](int2 ce, int bnd) {
+    return (ce.x < d.nCellsSolve || ce.y < d.nCellsSolve) && !(phase && ((bnd != 0) != (phase == 2)));
+  };
+  const bool onA = active(ceA, bA), onB = eA + 1 < d.nEdges && active(ceB, bB);
+  if (!onA && !onB) return;
+  const bool st = lev && (h ? onB : onA);
+  if (small_step == 1) {
+    const d2 rup = {dts * tu.x, dts * tu.y};
+    if (st) {
+      st2(p.ru_p + o, rup);
+      st2(p.ruAvg + o, rup);
+    }
+    return;
+  }
+  d2 rup = ld2(p.ru_p + o);
+  const d2 rua = ld2(p.ruAvg + o), cqu = ld2(p.cqu + o), zxu = ld2(p.zxu + o);
+  const double mask = sel(h, ld_uniform_f64(p.specZoneMaskEdge + eA), ld_uniform_f64(p.specZoneMaskEdge + eB));
+  const double invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
+  const size_t o1 = (size_t)c1 * K + 2 * lc, o2 = (size_t)c2 * K + 2 * lc;
+  const d2 rt1 = ld2(p.rtheta_pp + o1), rt2 = ld2(p.rtheta_pp + o2);
+  const d2 zz1 = ld2(p.zz + o1), zz2 = ld2(p.zz + o2), ex1 = ld2(p.exner + o1), ex2 = ld2(p.exner + o2);
+  const d2 rp1 = ld2(p.rho_pp + o1), rp2 = ld2(p.rho_pp + o2);
+  d2 ro1{}, ro2{}, th1{}, th2{};
+  if (DD) {
+    ro1 = ld2(p.rtheta_pp_old + o1);
+    ro2 = ld2(p.rtheta_pp_old + o2);
+    th1 = ld2(p.theta_m1 + o1);
+    th2 = ld2(p.theta_m1 + o2);
+  }
+  const double rcv = RGAS / (CP - RGAS);
+  const double c2v = CP * rcv;
+  auto level = [&](double r, double tu_, double cq, double zx, double a1, double a2, double z1, double z2,
+                   double x1, double x2, double p1, double p2, double o1_, double o2_, double t1, double t2) {
+    if (DD) {
+      const double dd1 = -(a1 - o1_);
+      const double dd2 = -(a2 - o2_);
+      r = r + coef_divdamp * (dd2 - dd1) * (1.0 - mask) / (t1 + t2);
+    }
+    double pgrad = ((a2 - a1) * invDc) / (.5 * (z2 + z1));
+    pgrad = cq * 0.5 * c2v * (x1 + x2) * pgrad;
+    pgrad = pgrad + 0.5 * zx * GRAVITY * (p1 + p2);
+    return r + dts * (tu_ - (1.0 - mask) * pgrad);
+  };
+  rup.x = level(rup.x, tu.x, cqu.x, zxu.x, rt1.x, rt2.x, zz1.x, zz2.x, ex1.x, ex2.x, rp1.x, rp2.x, ro1.x, ro2.x,
+                th1.x, th2.x);
+  rup.y = level(rup.y, tu.y, cqu.y, zxu.y, rt1.y, rt2.y, zz1.y, zz2.y, ex1.y, ex2.y, rp1.y, rp2.y, ro1.y, ro2.y,
+                th1.y, th2.y);
+  if (st) {
+    st2(p.ru_p + o, rup);
+    st2(p.ruAvg + o, d2{rua.x + rup.x, rua.y + rup.y});
   }
 }
 
@@ -2085,10 +2358,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells_b(Dims d, Ptrs p, 
 }
 
 template <int NE2>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges_b(Dims d, Ptrs p, const double* __restrict__ u,
+__global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_b(Dims d, Ptrs p, const double* __restrict__ u,
                                                                 const double* __restrict__ h, int reconstruct_v,
                                                                 double apvm, double dt) {
-  const int e = wave_elem(0);
+  const int e = wave_elem_e();
   if (e >= d.nEdges) return;
   const int k = lane_id(), K = d.K;
   if (k >= K) return;
