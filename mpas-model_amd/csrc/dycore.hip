@@ -746,6 +746,8 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     }
   }
   if (!batched(d)) LAUNCH(k_dyn_advflux, d.nEdges, d, p);
+  else if (pair_layout(d) && d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_p<10>, (d.nEdges + 1) / 2, d, p);
+  else if (pair_layout(d)) LAUNCH_E(k_dyn_advflux_p<12>, (d.nEdges + 1) / 2, d, p);
   else if (d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_b<10>, d.nEdges, d, p);
   else LAUNCH_E(k_dyn_advflux_b<12>, d.nEdges, d, p);
 #ifndef MPAS_NO_CELL_REC
@@ -811,7 +813,8 @@ void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
 
 void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase) {
   // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
-  LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase);
+  if (pair_layout(d)) LAUNCH_E(k_divdamp_p, (d.nEdges + 1) / 2, d, p, coef_divdamp(ctx, dts), phase);
+  else LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase);
 }
 
 void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt, int tl, int rk_step /*0 = absent*/) {
@@ -825,7 +828,13 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double d
     return;
   }
   LAUNCH(k_diag_vertices, d.nVertices, d, p, u);  // the batched variant measured slower
-  if (d.maxEdges == 6) {
+  if (pair_layout(d)) {
+    if (d.maxEdges == 6) LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
+    else LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
+    const int64_t nw = (d.nEdges + 1) / 2;
+    if (d.maxEdges == 6) LAUNCH_E(k_diag_edges_p<10>, nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
+    else LAUNCH_E(k_diag_edges_p<12>, nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
+  } else if (d.maxEdges == 6) {
     LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
     LAUNCH_E(k_diag_edges_b<10>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt);
   } else {

@@ -1724,6 +1724,187 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   if (RK1) del2(tue, dv1, dv2, vo1, vo2, kd1, kd2, invDv, msd2);
 }
 
+// k_dyn_advflux_b in the pair layout
+template <int NA>
+__global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  const size_t K1 = K + 1;
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const int naA = p.nAdvCellsForEdge[eA], naB = p.nAdvCellsForEdge[eB];
+  int ic[NA];
+  double a[NA], b[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
+    a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j));
+    b[j] = sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
+               ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
+  }
+  const d2 rue = ld2(p.ru + o);
+  const bool onA = ceA.x < d.nCellsSolve || ceA.y < d.nCellsSolve;
+  const bool onB = hasB && (ceB.x < d.nCellsSolve || ceB.y < d.nCellsSolve);
+  if (!onA && !onB) return;
+  const bool wide = naA > NA || naB > NA;  // not produced by meshes with maxEdges <= 7
+  d2 wv[NA], tv[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    wv[j] = ld2(p.w2 + (size_t)ic[j] * K1 + 2 * lw);
+    tv[j] = ld2(p.theta_m2 + (size_t)ic[j] * K + 2 * lc);
+  }
+  const d2 fzm = ld2(p.fzm + 2 * lc), fzp = ld2(p.fzp + 2 * lc);
+  const d2 rue_m = km1(rue, l);
+  const int kx = 2 * l, ky = 2 * l + 1;
+  const double rewx = kx < K ? fzm.x * rue.x + fzp.x * rue_m.x : 0.0;
+  const double rewy = ky < K ? fzm.y * rue.y + fzp.y * rue_m.y : 0.0;
+  const double swx = sgn1(rewx), swy = sgn1(rewy), stx_ = sgn1(rue.x), sty_ = sgn1(rue.y);
+  const int na = sel(h, naA, naB);
+  d2 fw{0.0, 0.0}, ft{0.0, 0.0};
+  if (wide) {  // general path: every coefficient and neighbour read in the loop
+    for (int j = 0; j < max(naA, naB); ++j) {
+      if (j < na) {
+        const int cj = p.advCellsForEdge[(size_t)e * 15 + j];
+        const double aj = p.adv_coefs[(size_t)e * 15 + j], bj = p.adv_coefs_3rd[(size_t)e * 15 + j];
+        const d2 w_ = ld2(p.w2 + (size_t)cj * K1 + 2 * lw), t_ = ld2(p.theta_m2 + (size_t)cj * K + 2 * lc);
+        fw.x = fw.x + (aj + swx * bj) * w_.x;
+        fw.y = fw.y + (aj + swy * bj) * w_.y;
+        ft.x = ft.x + (aj + stx_ * bj) * t_.x;
+        ft.y = ft.y + (aj + sty_ * bj) * t_.y;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    if (j < na && !wide) {
+      fw.x = fw.x + (a[j] + swx * b[j]) * wv[j].x;
+      fw.y = fw.y + (a[j] + swy * b[j]) * wv[j].y;
+      ft.x = ft.x + (a[j] + stx_ * b[j]) * tv[j].x;
+      ft.y = ft.y + (a[j] + sty_ * b[j]) * tv[j].y;
+    }
+  }
+  if ((h ? onB : onA) && 2 * l < K) {
+    st2(p.advflux_w + o, fw);
+    st2(p.advflux_th + o, ft);
+  }
+}
+
+// k_diag_edges_b in the pair layout
+template <int NE2>
+__global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, const double* __restrict__ u,
+                                                               const double* __restrict__ hh, int reconstruct_v,
+                                                               double apvm, double dt) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const int2 veA = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eA);
+  const int2 veB = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eB);
+  int neoe = 0;
+  int eoe[NE2];
+  double wgt[NE2];
+  if (reconstruct_v) {
+    neoe = sel(h, p.nEdgesOnEdge[eA], p.nEdgesOnEdge[eB]);
+#pragma unroll
+    for (int j = 0; j < NE2; ++j) {
+      eoe[j] = sel(h, p.edgesOnEdge[(size_t)eA * d.maxEdges2 + j], p.edgesOnEdge[(size_t)eB * d.maxEdges2 + j]);
+      wgt[j] = sel(h, ld_uniform_f64(p.weightsOnEdge + (size_t)eA * d.maxEdges2 + j),
+                   ld_uniform_f64(p.weightsOnEdge + (size_t)eB * d.maxEdges2 + j));
+    }
+  }
+  double invDv = 0.0, invDc = 0.0;
+  d2 ue{};
+  if (apvm > 0.0) {
+    invDv = sel(h, ld_uniform_f64(p.invDvEdge + eA), ld_uniform_f64(p.invDvEdge + eB));
+    invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
+    ue = ld2(u + o);
+  }
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y), v1 = sel(h, veA.x, veB.x), v2 = sel(h, veA.y, veB.y);
+  const d2 h1 = ld2(hh + (size_t)c1 * K + 2 * lc), h2 = ld2(hh + (size_t)c2 * K + 2 * lc);
+  const d2 pv1 = ld2(p.pv_vertex + (size_t)v1 * K + 2 * lc), pv2 = ld2(p.pv_vertex + (size_t)v2 * K + 2 * lc);
+  d2 pc1{}, pc2{};
+  if (apvm > 0.0) {
+    pc1 = ld2(p.pv_cell + (size_t)c1 * K + 2 * lc);
+    pc2 = ld2(p.pv_cell + (size_t)c2 * K + 2 * lc);
+  }
+  const bool st = (h == 0 || hasB) && 2 * l < K;
+  d2 vv;
+  if (reconstruct_v) {
+    d2 uu[NE2];
+#pragma unroll
+    for (int j = 0; j < NE2; ++j) uu[j] = ld2(u + (size_t)eoe[j] * K + 2 * lc);
+    vv = d2{0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < NE2; ++j) {
+      if (j < neoe) {
+        vv.x = vv.x + wgt[j] * uu[j].x;
+        vv.y = vv.y + wgt[j] * uu[j].y;
+      }
+    }
+    if (st) st2(p.v + o, vv);
+  } else {
+    vv = ld2(p.v + o);
+  }
+  if (st) st2(p.rho_edge + o, d2{0.5 * (h1.x + h2.x), 0.5 * (h1.y + h2.y)});
+  d2 pve{0.5 * (pv1.x + pv2.x), 0.5 * (pv1.y + pv2.y)};
+  if (apvm > 0.0) {
+    const double r = apvm * dt;
+    const double r1 = 1.0 * invDv;
+    const double r2 = 1.0 * invDc;
+    const d2 gt{(pv2.x - pv1.x) * r1, (pv2.y - pv1.y) * r1};
+    const d2 gn{(pc2.x - pc1.x) * r2, (pc2.y - pc1.y) * r2};
+    if (st) {
+      st2(p.gradPVt + o, gt);
+      st2(p.gradPVn + o, gn);
+    }
+    pve.x = pve.x - r * (vv.x * gt.x + ue.x * gn.x);
+    pve.y = pve.y - r * (vv.y * gt.y + ue.y * gn.y);
+  }
+  if (st) st2(p.pv_edge + o, pve);
+}
+
+// k_divdamp in the pair layout
+__global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const int bA = phase ? p.edge_bnd[eA] : 0, bB = phase ? p.edge_bnd[eB] : 0;
+  const d2 ru = ld2(p.ru_p + o);
+  const double mask = sel(h, ld_uniform_f64(p.specZoneMaskEdge + eA), ld_uniform_f64(p.specZoneMaskEdge + eB));
+  auto active = [&](int2 ce, int bnd) {
+    return (ce.x < d.nCellsSolve || ce.y < d.nCellsSolve) && (phase == 0 || ((bnd != 0) == (phase == 2)));
+  };
+  const bool onA = active(ceA, bA), onB = hasB && active(ceB, bB);
+  if (!onA && !onB) return;
+  const size_t o1 = (size_t)sel(h, ceA.x, ceB.x) * K + 2 * lc, o2 = (size_t)sel(h, ceA.y, ceB.y) * K + 2 * lc;
+  const d2 r1 = ld2(p.rtheta_pp + o1), r2 = ld2(p.rtheta_pp + o2);
+  const d2 q1 = ld2(p.rtheta_pp_old + o1), q2 = ld2(p.rtheta_pp_old + o2);
+  const d2 t1 = ld2(p.theta_m1 + o1), t2 = ld2(p.theta_m1 + o2);
+  d2 out;
+  out.x = ru.x + coef_divdamp * (-(r2.x - q2.x) - -(r1.x - q1.x)) * (1.0 - mask) / (t1.x + t2.x);
+  out.y = ru.y + coef_divdamp * (-(r2.y - q2.y) - -(r1.y - q1.y)) * (1.0 - mask) / (t1.y + t2.y);
+  if ((h ? onB : onA) && 2 * l < K) st2(p.ru_p + o, out);
+}
+
 // k_acoustic_edges in the pair layout (same expressions, per level)
 template <bool DD>
 __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,
