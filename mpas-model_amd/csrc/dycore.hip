@@ -851,7 +851,12 @@ void advance_scalars(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt,
     if (rk_step == 2) wt_new = 1. / 2;
     if (rk_step == 3) wt_new = 1.;
   }
-  LAUNCH(k_scalars_edges, d.nEdges, d, p);
+  if (batched(d) && pair_layout(d)) {
+    if (d.maxEdges == 6) LAUNCH_E(k_scalars_edges_p<10>, (d.nEdges + 1) / 2, d, p);
+    else LAUNCH_E(k_scalars_edges_p<12>, (d.nEdges + 1) / 2, d, p);
+  } else {
+    LAUNCH(k_scalars_edges, d.nEdges, d, p);
+  }
   LAUNCH(k_scalars_cells, d.nCellsSolve, d, p, dt, wt_new, ctx->cf.coef_3rd_order);
 }
 
@@ -870,7 +875,12 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
     for (int b = 0; b < nb; ++b) {
       const Dims& d = ctx->blk[b].d;
       LAUNCH(k_mono_bounds, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
-      LAUNCH(k_mono_edges1, d.nEdges, d, P[b], is, dt);
+      if (batched(d) && pair_layout(d)) {
+        if (d.maxEdges == 6) LAUNCH_E(k_mono_edges1_p<10>, (d.nEdges + 1) / 2, d, P[b], is, dt);
+        else LAUNCH_E(k_mono_edges1_p<12>, (d.nEdges + 1) / 2, d, P[b], is, dt);
+      } else {
+        LAUNCH(k_mono_edges1, d.nEdges, d, P[b], is, dt);
+      }
       LAUNCH(k_mono_cells1, d.nCellsSolve, d, P[b], is, dt, ad);
     }
     CHK(exchange(ctx, {{"scratch", "scale_arr", 1, 0x1u}}));

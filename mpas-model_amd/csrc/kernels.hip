@@ -1905,6 +1905,127 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   if ((h ? onB : onA) && 2 * l < K) st2(p.ru_p + o, out);
 }
 
+// k_scalars_edges in the pair layout (atm_advance_scalars_work, 3357-3426)
+template <int NA>
+__global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31, ns = d.ns;
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int na = sel(h, p.nAdvCellsForEdge[eA], p.nAdvCellsForEdge[eB]);
+  int ic[NA];
+  double a[NA], b[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
+    a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j));
+    b[j] = sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
+               ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
+  }
+  const d2 uh = ld2(p.ruAvg + o);
+  const double sgx = sgn1(uh.x), sgy = sgn1(uh.y);
+  const bool hex = na == 10;  // the reference's unrolled hexagon form (3363-3390)
+  const bool st = (h == 0 || hasB) && 2 * l < K;
+  for (int is = 0; is < ns; ++is) {
+    d2 sv[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) sv[j] = ld2(p.scalars2 + SIX(ic[j], 2 * lc, is));
+    d2 acc{0.0, 0.0};
+    if (hex) {
+      acc.x = (a[0] + sgx * b[0]) * sv[0].x;
+      acc.y = (a[0] + sgy * b[0]) * sv[0].y;
+#pragma unroll
+      for (int j = 1; j < 10 && j < NA; ++j) {
+        acc.x = acc.x + (a[j] + sgx * b[j]) * sv[j].x;
+        acc.y = acc.y + (a[j] + sgy * b[j]) * sv[j].y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        if (j < na) {
+          acc.x = acc.x + (a[j] + sgx * b[j]) * sv[j].x;
+          acc.y = acc.y + (a[j] + sgy * b[j]) * sv[j].y;
+        }
+      }
+    }
+    if (st) st2(p.horiz_flux_array + HIX(e, 2 * lc, is), acc);
+  }
+}
+
+// k_mono_edges1 in the pair layout (atm_advance_scalars_mono_work, 3916-3961, 4007-4022)
+template <int NA>
+__global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, int is, double dt) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31, ns = d.ns;
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const int na = sel(h, p.nAdvCellsForEdge[eA], p.nAdvCellsForEdge[eB]);
+  int ic[NA];
+  double a[NA], b[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
+    a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j));
+    b[j] = sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
+               ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
+  }
+  const double dv = sel(h, ld_uniform_f64(p.dvEdge + eA), ld_uniform_f64(p.dvEdge + eB));
+  const d2 uh = ld2(p.ruAvg + o);
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
+  const bool on = c1 < d.nCellsSolve || c2 < d.nCellsSolve;
+  // scalars outside the block (the garbage slot) read as 0, as the reference's halo loops see them
+  auto val = [&](const double* arr, int cc) {
+    const d2 v = ld2(arr + SIX(cc, 2 * lc, is));
+    return cc < d.nCells ? v : d2{0.0, 0.0};
+  };
+  d2 sv[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) sv[j] = val(p.scalars2, ic[j]);
+  const d2 so1 = val(p.scalars1, c1), so2 = val(p.scalars1, c2);
+  auto flux = [&](double u, int lev) {
+    double acc = 0.0;
+    if (na == 10) {
+      const bool up = u > 0;
+#pragma unroll
+      for (int j = 0; j < 10 && j < NA; ++j) {
+        const double swa = up ? (a[j] + b[j]) : (a[j] - b[j]);
+        const double term = swa * (lev ? sv[j].y : sv[j].x);
+        acc = (j == 0) ? term : acc + term;
+      }
+      return u * (acc);
+    }
+    double fa = 0.0;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      if (j < na) fa = fa + (u * (a[j] + sgn1(u) * b[j])) * (lev ? sv[j].y : sv[j].x);
+    }
+    return fa;
+  };
+  d2 fa{0.0, 0.0};
+  if (on) {
+    fa.x = flux(uh.x, 0);
+    fa.y = flux(uh.y, 1);
+  }
+  d2 fu;
+  fu.x = dv * dt * (fmax(0.0, uh.x) * so1.x + fmin(0.0, uh.x) * so2.x);
+  fu.y = dv * dt * (fmax(0.0, uh.y) * so1.y + fmin(0.0, uh.y) * so2.y);
+  if ((h == 0 || hasB) && 2 * l < K) {
+    st2(p.flux_arr + o, fa);
+    st2(p.flux_upwind_tmp + o, fu);
+    st2(p.flux_tmp + o, d2{dt * fa.x - fu.x, dt * fa.y - fu.y});
+  }
+}
+
 // k_acoustic_edges in the pair layout (same expressions, per level)
 template <bool DD>
 __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,

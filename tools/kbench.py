@@ -21,12 +21,14 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--moist", action="store_true", help="BASELINE configs[3]: ns=6 moist species")
     a = ap.parse_args()
     from mpas_dycore import Dycore
     from mpas_dycore.cases import jw_case
-    case = jw_case(a.ncells, K=a.levels)
+    ns = 6 if a.moist else 1
+    case = jw_case(a.ncells, K=a.levels, ns=ns, moist=a.moist)
     dt = case["dt"]
-    dy = Dycore(case, device=0)
+    dy = Dycore(case, device=0, moist_end=ns)
     dy.init_diagnostics(dt)
     dy.use_graph(not a.no_graph)
     for i in range(2):
