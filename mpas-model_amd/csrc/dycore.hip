@@ -857,7 +857,9 @@ void advance_scalars(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt,
   } else {
     LAUNCH(k_scalars_edges, d.nEdges, d, p);
   }
-  LAUNCH(k_scalars_cells, d.nCellsSolve, d, p, dt, wt_new, ctx->cf.coef_3rd_order);
+  if (!batched(d)) LAUNCH(k_scalars_cells, d.nCellsSolve, d, p, dt, wt_new, ctx->cf.coef_3rd_order);
+  else if (d.maxEdges == 6) LAUNCH(k_scalars_cells_b<6>, d.nCellsSolve, d, p, dt, wt_new, ctx->cf.coef_3rd_order);
+  else LAUNCH(k_scalars_cells_b<7>, d.nCellsSolve, d, p, dt, wt_new, ctx->cf.coef_3rd_order);
 }
 
 // atm_advance_scalars_mono (3548-4210) over all blocks: its two halo exchanges
@@ -874,20 +876,32 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
   for (int is = 0; is < ns; ++is) {
     for (int b = 0; b < nb; ++b) {
       const Dims& d = ctx->blk[b].d;
-      LAUNCH(k_mono_bounds, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
+      const bool bt = batched(d), m6 = d.maxEdges == 6;
+      if (!bt) LAUNCH(k_mono_bounds, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
+      else if (m6) LAUNCH(k_mono_bounds_b<6>, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
+      else LAUNCH(k_mono_bounds_b<7>, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
       if (batched(d) && pair_layout(d)) {
         if (d.maxEdges == 6) LAUNCH_E(k_mono_edges1_p<10>, (d.nEdges + 1) / 2, d, P[b], is, dt);
         else LAUNCH_E(k_mono_edges1_p<12>, (d.nEdges + 1) / 2, d, P[b], is, dt);
       } else {
         LAUNCH(k_mono_edges1, d.nEdges, d, P[b], is, dt);
       }
-      LAUNCH(k_mono_cells1, d.nCellsSolve, d, P[b], is, dt, ad);
+      if (!bt) LAUNCH(k_mono_cells1, d.nCellsSolve, d, P[b], is, dt, ad);
+      else if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, P[b], is, dt, ad);
+      else LAUNCH(k_mono_cells1_b<7>, d.nCellsSolve, d, P[b], is, dt, ad);
     }
     CHK(exchange(ctx, {{"scratch", "scale_arr", 1, 0x1u}}));
     for (int b = 0; b < nb; ++b) {
       const Dims& d = ctx->blk[b].d;
-      LAUNCH(k_mono_edges2, d.nEdges, d, P[b], dt);
-      LAUNCH(k_mono_cells2, d.nCells, d, P[b], is, ad);
+      if (!batched(d)) {
+        LAUNCH(k_mono_edges2, d.nEdges, d, P[b], dt);
+        LAUNCH(k_mono_cells2, d.nCells, d, P[b], is, ad);
+        continue;
+      }
+      if (pair_layout(d)) LAUNCH_E(k_mono_edges2_p, (d.nEdges + 1) / 2, d, P[b], dt);
+      else LAUNCH(k_mono_edges2, d.nEdges, d, P[b], dt);
+      if (d.maxEdges == 6) LAUNCH(k_mono_cells2_b<6>, d.nCells, d, P[b], is, ad);
+      else LAUNCH(k_mono_cells2_b<7>, d.nCells, d, P[b], is, ad);
     }
   }
   return MPAS_DYC_OK;

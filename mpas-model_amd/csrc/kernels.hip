@@ -3174,6 +3174,245 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2(Dims d, Ptrs p, i
   p.scalars2[SIX(c, k, is)] = fmax(0.0, snew);
 }
 
+// ---- batched-load variants of the transport cell kernels (maxEdges 6 / 7, per-cell records) and
+// the pair-layout flux correction; same expressions and order as the kernels above
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_cells_b(Dims d, Ptrs p, double dt, double wt_new,
+                                                                    double coef_3rd_order) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + kc;
+  const double wt_old = 1. - wt_new;
+  const CellSten<ME> st = load_sten<ME>(p, c);
+  const double invA = ld_uniform_f64(p.invAreaCell + c);
+  const double fnm = p.fzm[kc], fnp = p.fzp[kc], rdnw = p.rdzw[kc];
+  const double wwa = p.wwAvg[(size_t)c * K1 + kw];
+  const double rzo = p.rho_zz1[o], rzn = p.rho_zz2[o];
+  double ra[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) ra[i] = p.ruAvg[(size_t)st.e[i] * K + kc];
+  const double rho_zz_new_inv = act ? 1.0 / (wt_old * rzo + wt_new * rzn) : 0.0;
+  double sru[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) sru[i] = st.sg(i) * ra[i];  // edgesOnCell_sign * uhAvg
+  for (int is = 0; is < ns; ++is) {
+    double hf[ME];
+#pragma unroll
+    for (int i = 0; i < ME; ++i) hf[i] = p.horiz_flux_array[HIX(st.e[i], kc, is)];
+    double sn = p.scalars2[SIX(c, kc, is)];
+    const double so = p.scalars1[SIX(c, kc, is)];
+    if (!act) sn = 0.0;
+    double stc = 0.0;
+#pragma unroll
+    for (int i = 0; i < ME; ++i)
+      if (i < st.ne) stc = stc - sru[i] * hf[i];
+    if (act) {
+      p.scalars_tend[SIX(c, k, is)] = 0.0;  // no physics: scalar_tend_save zeroed (3437-3439)
+      stc = stc * invA + 0.0;
+    }
+    const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
+    double wdtn = 0.0;
+    if (k == 1 || k == K - 1) wdtn = wwa * (fnm * sn + fnp * snm1);
+    else if (k >= 2 && k <= K - 2) wdtn = flux3(snm2, snm1, sn, snp1, wwa, coef_3rd_order);
+    const double wdtn_p = dn1(wdtn);
+    if (act) p.scalars2[SIX(c, k, is)] = (so * rzo + dt * (stc - rdnw * (wdtn_p - wdtn))) * rho_zz_new_inv;
+  }
+}
+
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds_b(Dims d, Ptrs p, int is, double coef_3rd_order) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + kc;
+  const int ne = p.nEdgesOnCell[c];
+  int cc[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) cc[i] = p.cellsOnCell[(size_t)c * ME + i];
+  double so = p.scalars1[SIX(c, kc, is)], sn = p.scalars2[SIX(c, kc, is)];
+  const double wwa = p.wwAvg[(size_t)c * K1 + kw];
+  const double fnm = p.fzm[kc], fnp = p.fzp[kc];
+  double sv[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const double v = p.scalars1[SIX(cc[i], kc, is)];
+    sv[i] = cc[i] < d.nCells ? v : 0.0;  // sold() of the reference's halo loop
+  }
+  if (!act) {
+    so = 0.0;
+    sn = 0.0;
+  }
+  const double som = up1(so), sop = dn1(so);
+  const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
+  double wdtn = 0.0;
+  if (k == 1 || k == K - 1) wdtn = wwa * (fnm * sn + fnp * snm1);
+  else if (k >= 2 && k <= K - 2) wdtn = flux3(snm2, snm1, sn, snp1, wwa, coef_3rd_order);
+  if (k <= K) p.wdtn[(size_t)c * K1 + k] = wdtn;
+  if (!act) return;
+  double smax, smin;
+  if (k == 0) {
+    smax = fmax(so, sop);
+    smin = fmin(so, sop);
+  } else if (k == K - 1) {
+    smax = fmax(so, som);
+    smin = fmin(so, som);
+  } else {
+    smax = fmax(fmax(som, so), sop);
+    smin = fmin(fmin(som, so), sop);
+  }
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    if (i < ne) {
+      smax = fmax(smax, sv[i]);
+      smin = fmin(smin, sv[i]);
+    }
+  }
+  p.s_max[o] = smax;
+  p.s_min[o] = smin;
+}
+
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p, int is, double dt, int advance_density) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
+  const double eps = 1.e-20;
+  const CellSten<ME> st = load_sten<ME>(p, c);
+  const double invA = ld_uniform_f64(p.invAreaCell + c);
+  double so = p.scalars1[SIX(c, kc, is)];
+  double rzo = p.rho_zz1[o];
+  const double wwa = p.wwAvg[ow], rdnw = p.rdzw[kc];
+  double wd = p.wdtn[ow];
+  const double rhoref = advance_density ? p.rho_zz_int[o] : p.rho_zz2[o];
+  const double smx = p.s_max[o], smn = p.s_min[o];
+  double ft[ME], fu[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    ft[i] = p.flux_tmp[(size_t)st.e[i] * K + kc];
+    fu[i] = p.flux_upwind_tmp[(size_t)st.e[i] * K + kc];
+  }
+  if (!act) {
+    so = 0.0;
+    rzo = 0.0;
+  }
+  const double som = up1(so);
+  double snew = so * rzo;
+  double fua = 0.0;  // flux_upwind_arr(k), k >= 2
+  if (act && k >= 1) fua = dt * (fmax(0.0, wwa) * som + fmin(0.0, wwa) * so);
+  const double fua_p = dn1(fua);
+  if (act && k <= K - 2) snew = snew - fua_p * rdnw;
+  if (k > K) wd = 0.0;
+  if (act && k >= 1) {
+    snew = snew + fua * rdnw;
+    wd = dt * wd - fua;
+  }
+  if (k <= K) p.wdtn[ow] = wd;
+  const double wdp = dn1(wd);
+  double sin_ = 0.0, sout = 0.0;
+  if (act) {
+    sin_ = -rdnw * (fmin(0.0, wdp) - fmax(0.0, wd));
+    sout = -rdnw * (fmax(0.0, wdp) - fmin(0.0, wd));
+  }
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    if (i < st.ne && act) {
+      const double sg = st.sg(i);
+      snew = snew - sg * fu[i] * invA;
+      sout = sout - fmax(0.0, sg * ft[i]) * invA;
+      sin_ = sin_ - fmin(0.0, sg * ft[i]) * invA;
+    }
+  }
+  if (!act) return;
+  double scale_factor = (smx * rhoref - snew) / (sin_ + eps);
+  const double scale_in = fmin(1.0, fmax(0.0, scale_factor));
+  scale_factor = (smn * rhoref - snew) / (sout - eps);
+  const double scale_out = fmin(1.0, fmax(0.0, scale_factor));
+  p.scalar_old_copy[o] = snew;  // upwind solution (the reference's scratch scalar_new)
+  p.scale_arr[((size_t)c * 2 + 0) * K + k] = scale_in;
+  p.scale_arr[((size_t)c * 2 + 1) * K + k] = scale_out;
+}
+
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2_b(Dims d, Ptrs p, int is, int advance_density) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
+  if (c >= d.nCellsSolve) {  // halo cells: scalars_new = max(0, scalar_new) with scalar_new = input copy
+    if (act) p.scalars2[SIX(c, k, is)] = fmax(0.0, p.scalars2[SIX(c, k, is)]);
+    return;
+  }
+  const CellSten<ME> st = load_sten<ME>(p, c);
+  const double invA = ld_uniform_f64(p.invAreaCell + c);
+  double si = p.scale_arr[((size_t)c * 2 + 0) * K + kc], so_ = p.scale_arr[((size_t)c * 2 + 1) * K + kc];
+  double wd = p.wdtn[ow];
+  const double sold_copy = p.scalar_old_copy[o];
+  const double rhoref = advance_density ? p.rho_zz_int[o] : p.rho_zz2[o];
+  const double rdzw = p.rdzw[kc];
+  double fa[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) fa[i] = p.flux_arr[(size_t)st.e[i] * K + kc];
+  if (!act) {
+    si = 0.0;
+    so_ = 0.0;
+  }
+  if (k > K) wd = 0.0;
+  const double sim = up1(si), som = up1(so_);
+  if (act && k >= 1) {
+    const double f = wd;
+    wd = fmax(0.0, f) * fmin(som, si) + fmin(0.0, f) * fmin(so_, sim);
+  }
+  const double wdp = dn1(wd);
+  if (!act) return;
+  double snew = sold_copy;
+#pragma unroll
+  for (int i = 0; i < ME; ++i)
+    if (i < st.ne) snew = snew - st.sg(i) * fa[i] * invA;
+  snew = (snew + (-rdzw * (wdp - wd))) / rhoref;
+  p.scalars2[SIX(c, k, is)] = fmax(0.0, snew);
+}
+
+__global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges2_p(Dims d, Ptrs p, double dt) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const d2 fa = ld2(p.flux_arr + o), fu = ld2(p.flux_upwind_tmp + o);
+  const bool onA = ceA.x < d.nCellsSolve || ceA.y < d.nCellsSolve;
+  const bool onB = hasB && (ceB.x < d.nCellsSolve || ceB.y < d.nCellsSolve);
+  if (!onA && !onB) return;
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
+  auto sc = [&](int cc, int io) {
+    const d2 v = ld2(p.scale_arr + ((size_t)cc * 2 + io) * K + 2 * lc);
+    return cc < d.nCells ? v : d2{0.0, 0.0};
+  };
+  const d2 a10 = sc(c1, 0), a11 = sc(c1, 1), a20 = sc(c2, 0), a21 = sc(c2, 1);
+  d2 f{dt * fa.x - fu.x, dt * fa.y - fu.y};
+  f.x = fmax(0.0, f.x) * fmin(a11.x, a20.x) + fmin(0.0, f.x) * fmin(a10.x, a21.x);
+  f.y = fmax(0.0, f.y) * fmin(a11.y, a20.y) + fmin(0.0, f.y) * fmin(a10.y, a21.y);
+  if ((h ? onB : onA) && 2 * l < K) st2(p.flux_arr + o, f);
+}
+
 // ============================================================================
 // mpas_reconstruct_2d  (operators/mpas_vector_reconstruction.F:245-294), owned cells:
 // cell-centre velocity from the edge normals with the precomputed RBF weights
