@@ -715,9 +715,10 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
 #ifndef MPAS_NO_CELL_REC
   if (batched(d) && pair_layout(d)) {
     const int64_t nw = (d.nEdges + 1) / 2;
-    if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 10>), nw, d, p, cf, s, 0);
+    if (rk_step == 1) LAUNCH_E(k_dyn_edges_pgf_p, nw, d, p);
+    if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 10, true>), nw, d, p, cf, s, 0);
     if (d.maxEdges == 6 && rk_step != 1) LAUNCH_E((k_dyn_edges_p<false, 10>), nw, d, p, cf, s, 1);
-    if (d.maxEdges == 7 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 12>), nw, d, p, cf, s, 0);
+    if (d.maxEdges == 7 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 12, true>), nw, d, p, cf, s, 0);
     if (d.maxEdges == 7 && rk_step != 1) LAUNCH_E((k_dyn_edges_p<false, 12>), nw, d, p, cf, s, 1);
   } else if ((d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2) {
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_b<true, 10>), d.nEdges, d, p, cf, s, 0);

@@ -1578,10 +1578,13 @@ __device__ __forceinline__ d2 kp1(d2 v) {  // levels (k+1)
   return d2{v.y, lane_shl1(v.x)};
 }
 
-// k_dyn_edges_b in the pair layout (NE2 = 2*maxEdges-2 TRiSK neighbours)
-template <bool RK1, int NE2>
+// k_dyn_edges_b in the pair layout (NE2 = 2*maxEdges-2 TRiSK neighbours).  SPLIT (rk1 only): this
+// launch computes tend_u alone and k_dyn_edges_pgf_p the PGF part of tend_u_euler and del2 --
+// at rk1 the two are independent (no finalize), and together they need 244 VGPRs (2 waves/SIMD).
+template <bool RK1, int NE2, bool SPLIT = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Config cf, DynTendScal s,
                                                               int finalize) {
+  constexpr bool PGF = RK1 && !SPLIT;
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
@@ -1618,7 +1621,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
     store(p.tend_u_euler, out);
   };
   if (!solveA && !solveB) {  // halo pair: rk1 del2 only
-    if (!RK1) return;
+    if (!PGF) return;
     const int2 veA = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eA);
     const int2 veB = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eB);
     const double invDv = sel(h, ld_uniform_f64(p.invDvEdge + eA), ld_uniform_f64(p.invDvEdge + eB));
@@ -1642,7 +1645,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   int v1 = 0, v2 = 0;
   double invDv = 0.0, msd2 = 0.0;
   d2 cqu{}, zxu{};
-  if (RK1) {
+  if (PGF) {
     const int2 veA = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eA);
     const int2 veB = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eB);
     v1 = sel(h, veA.x, veB.x);
@@ -1654,7 +1657,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   }
   const d2 uk = ld2(p.u2 + o), pve = ld2(p.pv_edge + o);
   d2 tue = RK1 ? d2{0.0, 0.0} : ld2(p.tend_u_euler + o);
-  if (RK1 && !solve) tue = ld2(p.tend_u_euler + o);  // the halo edge of a mixed pair
+  if (PGF && !solve) tue = ld2(p.tend_u_euler + o);  // the halo edge of a mixed pair
   // ---- batch 2: gathers
   const d2 rw1 = ld2(p.rw + (size_t)c1 * K1 + 2 * lw), rw2 = ld2(p.rw + (size_t)c2 * K1 + 2 * lw);
   const d2 ke1 = ld2(p.ke + o1), ke2 = ld2(p.ke + o2), hd1 = ld2(p.h_divergence + o1), hd2 = ld2(p.h_divergence + o2);
@@ -1666,7 +1669,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
     uu[j] = ld2(p.u2 + oj);
   }
   d2 pp1{}, pp2{}, zz1{}, zz2{}, dpz1{}, dpz2{}, dv1{}, dv2{}, vo1{}, vo2{}, kd1{}, kd2{};
-  if (RK1) {
+  if (PGF) {
     pp1 = ld2(p.pressure_p + o1);
     pp2 = ld2(p.pressure_p + o2);
     zz1 = ld2(p.zz + o1);
@@ -1682,7 +1685,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   }
   const d2 fzm = ld2(p.fzm + 2 * lc), fzp = ld2(p.fzp + 2 * lc), rdzw = ld2(p.rdzw + 2 * lc);
   // ---- tend_u (PGF rk1 4781-4788, vertical transport 4792-4807, Coriolis/KE 4811-4838)
-  if (RK1 && solve) {
+  if (PGF && solve) {
     tue.x = -cqu.x * ((pp2.x - pp1.x) * invDc / (.5 * (zz2.x + zz1.x)) - 0.5 * zxu.x * (dpz1.x + dpz2.x));
     tue.y = -cqu.y * ((pp2.y - pp1.y) * invDc / (.5 * (zz2.y + zz1.y)) - 0.5 * zxu.y * (dpz1.y + dpz2.y));
   }
@@ -1721,7 +1724,51 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
     tu.y = tu.y + tue.y + PHYS_ZERO;
   }
   if (solve) store(p.tend_u, tu);
-  if (RK1) del2(tue, dv1, dv2, vo1, vo2, kd1, kd2, invDv, msd2);
+  if (PGF) del2(tue, dv1, dv2, vo1, vo2, kd1, kd2, invDv, msd2);
+}
+
+// rk1, all edges: the PGF part of tend_u_euler (4781-4788, edges 1..nEdgesSolve) and the del2 of u
+// (4856-4883) -- the half of k_dyn_edges_p<true> that SPLIT leaves out
+__global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_pgf_p(Dims d, Ptrs p) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const bool solve = h ? (hasB && eB < d.nEdgesSolve) : (eA < d.nEdgesSolve);
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const int2 veA = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eA);
+  const int2 veB = *reinterpret_cast<const int2*>(p.verticesOnEdge + 2 * eB);
+  const double invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
+  const double invDv = sel(h, ld_uniform_f64(p.invDvEdge + eA), ld_uniform_f64(p.invDvEdge + eB));
+  const double msd2 = sel(h, ld_uniform_f64(p.meshScalingDel2 + eA), ld_uniform_f64(p.meshScalingDel2 + eB));
+  const d2 re = ld2(p.rho_edge + o), cqu = ld2(p.cqu + o), zxu = ld2(p.zxu + o), tue0 = ld2(p.tend_u_euler + o);
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y), v1 = sel(h, veA.x, veB.x), v2 = sel(h, veA.y, veB.y);
+  const size_t o1 = (size_t)c1 * K + 2 * lc, o2 = (size_t)c2 * K + 2 * lc;
+  const d2 pp1 = ld2(p.pressure_p + o1), pp2 = ld2(p.pressure_p + o2), zz1 = ld2(p.zz + o1), zz2 = ld2(p.zz + o2);
+  const d2 dpz1 = ld2(p.dpdz + o1), dpz2 = ld2(p.dpdz + o2), dv1 = ld2(p.divergence + o1), dv2 = ld2(p.divergence + o2);
+  const d2 vo1 = ld2(p.vorticity + (size_t)v1 * K + 2 * lc), vo2 = ld2(p.vorticity + (size_t)v2 * K + 2 * lc);
+  const d2 kd1 = ld2(p.kdiff + o1), kd2 = ld2(p.kdiff + o2);
+  d2 tue = tue0;
+  if (solve) {
+    tue.x = -cqu.x * ((pp2.x - pp1.x) * invDc / (.5 * (zz2.x + zz1.x)) - 0.5 * zxu.x * (dpz1.x + dpz2.x));
+    tue.y = -cqu.y * ((pp2.y - pp1.y) * invDc / (.5 * (zz2.y + zz1.y)) - 0.5 * zxu.y * (dpz1.y + dpz2.y));
+  }
+  const double r_dc = invDc;
+  const double r_dv = fmin(invDv, 4 * invDc);
+  d2 ud, out;
+  ud.x = (dv2.x - dv1.x) * r_dc - (vo2.x - vo1.x) * r_dv;
+  ud.y = (dv2.y - dv1.y) * r_dc - (vo2.y - vo1.y) * r_dv;
+  out.x = tue.x + re.x * (0.5 * (kd1.x + kd2.x)) * ud.x * msd2;
+  out.y = tue.y + re.y * (0.5 * (kd1.y + kd2.y)) * ud.y * msd2;
+  if ((h == 0 || hasB) && 2 * l < K) {
+    st2(p.delsq_u + o, d2{0.0 + ud.x, 0.0 + ud.y});
+    st2(p.tend_u_euler + o, out);
+  }
 }
 
 // k_dyn_advflux_b in the pair layout
