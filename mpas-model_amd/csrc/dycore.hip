@@ -662,14 +662,15 @@ void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
   if (!ctx->planning) hipLaunchKernelGGL(k_copy_many, dim3(gx, 10), dim3(256), 0, ctx->stream, c);
 }
 
-// batched-load kernel variants (k_*_b / k_*_r) cover meshes with maxEdges 6 or 7; other meshes
-// take the general kernels
+// Kernel families: 0 "general" (one column per wave, loads where used -- any mesh), 1 "batched"
+// (k_*_b / k_*_r: per-cell records, every load issued up front; maxEdges 6 or 7), 2 "pair"
+// (k_*_p: two edges per wave, two levels per lane; even K).  All three give the same bits
+// (tests/test_gpu_kernels.py); the environment variable MPAS_DYCORE_KERNELS=general|batched|pair,
+// read when a context is created, caps the family (default pair).
+int g_kernel_tier = 2;
+
 inline bool batched(const Dims& d) {
-#ifdef MPAS_NO_CELL_REC
-  return false;
-#else
-  return (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
-#endif
+  return g_kernel_tier >= 1 && (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
 }
 
 void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
@@ -677,13 +678,7 @@ void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts)
 }
 
 // pair-layout edge kernels (k_*_p: two edges per wave, two levels per lane) need an even K
-inline bool pair_layout(const Dims& d) {
-#ifdef MPAS_NO_PAIR
-  return false;
-#else
-  return d.K % 2 == 0 && d.K <= 64;
-#endif
-}
+inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K % 2 == 0 && d.K <= 64; }
 
 // part: 0 = all kernels; 1 = only k_dyn_cells1, which reads nothing the exchange after the
 // diagnostics (1234-1249) or at the substep boundary (1282-1297) delivers; 2 = the rest
@@ -712,22 +707,19 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     else LAUNCH(k_dyn_cells1_b<7>, d.nCells, d, p, cf, s);
   }
   if (part == 1) return;
-#ifndef MPAS_NO_CELL_REC
-  if (batched(d) && pair_layout(d)) {
+  if (pair_layout(d)) {
     const int64_t nw = (d.nEdges + 1) / 2;
     if (rk_step == 1) LAUNCH_E(k_dyn_edges_pgf_p, nw, d, p);
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 10, true>), nw, d, p, cf, s, 0);
     if (d.maxEdges == 6 && rk_step != 1) LAUNCH_E((k_dyn_edges_p<false, 10>), nw, d, p, cf, s, 1);
     if (d.maxEdges == 7 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 12, true>), nw, d, p, cf, s, 0);
     if (d.maxEdges == 7 && rk_step != 1) LAUNCH_E((k_dyn_edges_p<false, 12>), nw, d, p, cf, s, 1);
-  } else if ((d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2) {
+  } else if (batched(d)) {
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_b<true, 10>), d.nEdges, d, p, cf, s, 0);
     if (d.maxEdges == 6 && rk_step != 1) LAUNCH_E((k_dyn_edges_b<false, 10>), d.nEdges, d, p, cf, s, 1);
     if (d.maxEdges == 7 && rk_step == 1) LAUNCH_E((k_dyn_edges_b<true, 12>), d.nEdges, d, p, cf, s, 0);
     if (d.maxEdges == 7 && rk_step != 1) LAUNCH_E((k_dyn_edges_b<false, 12>), d.nEdges, d, p, cf, s, 1);
-  } else
-#endif
-  if (rk_step == 1)
+  } else if (rk_step == 1)
     LAUNCH(k_dyn_edges<true>, d.nEdges, d, p, cf, s, 0);
   else
     LAUNCH(k_dyn_edges<false>, d.nEdges, d, p, cf, s, 1);
@@ -751,15 +743,13 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   else if (pair_layout(d)) LAUNCH_E(k_dyn_advflux_p<12>, (d.nEdges + 1) / 2, d, p);
   else if (d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_b<10>, d.nEdges, d, p);
   else LAUNCH_E(k_dyn_advflux_b<12>, d.nEdges, d, p);
-#ifndef MPAS_NO_CELL_REC
-  if (d.maxEdges == 6 || d.maxEdges == 7) {
+  if (batched(d)) {
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH((k_dyn_cells3_r<6, true>), d.nCellsSolve, d, p, cf, s);
     if (d.maxEdges == 6 && rk_step != 1) LAUNCH((k_dyn_cells3_r<6, false>), d.nCellsSolve, d, p, cf, s);
     if (d.maxEdges == 7 && rk_step == 1) LAUNCH((k_dyn_cells3_r<7, true>), d.nCellsSolve, d, p, cf, s);
     if (d.maxEdges == 7 && rk_step != 1) LAUNCH((k_dyn_cells3_r<7, false>), d.nCellsSolve, d, p, cf, s);
     return;
   }
-#endif
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
 }
 
@@ -799,16 +789,14 @@ void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
 }
 
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
-#ifndef MPAS_NO_CELL_REC
-  if (d.maxEdges == 6) {
+  if (batched(d) && d.maxEdges == 6) {
     LAUNCH(k_acoustic_cells_r<6>, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
     return;
   }
-  if (d.maxEdges == 7) {
+  if (batched(d) && d.maxEdges == 7) {
     LAUNCH(k_acoustic_cells_r<7>, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
     return;
   }
-#endif
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
 }
 
@@ -1258,6 +1246,12 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
       hipEventCreateWithFlags(&ctx->xjoin, hipEventDisableTiming) != hipSuccess) {
     mpas_dyc_destroy(ctx);
     return MPAS_DYC_EHIP;
+  }
+  if (const char* kt = getenv("MPAS_DYCORE_KERNELS")) {
+    const std::string t(kt);
+    g_kernel_tier = t == "general" ? 0 : t == "batched" ? 1 : 2;
+  } else {
+    g_kernel_tier = 2;
   }
   for (auto& b : ctx->blk) {
     build_registry(b);
