@@ -56,6 +56,42 @@ def cpu_baseline(case, dt, nthreads, steps, moist_end=1):
                        f"2..{steps} ({t:.2f} s/step)")
 
 
+def small_mesh_line(args, torch, device, ncells=10242, steps=20, warmup=3):
+    from mpas_dycore import Dycore
+    from mpas_dycore.cases import jw_case
+    ns = 6 if args.moist else 1
+    case = jw_case(ncells, K=args.levels, ns=ns, moist=args.moist)
+    dt = case["dt"]
+    dy = Dycore(case, device=device, moist_end=ns if args.moist else 1)
+    dy.init_diagnostics(dt)
+    if not args.no_graph:
+        dy.use_graph(True)
+    for i in range(warmup):
+        dy.atm_timestep(dt, i + 1)
+        dy.shift_time_levels()
+    dy.synchronize()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        dy.atm_timestep(dt, warmup + i + 1)
+        dy.shift_time_levels()
+    dy.synchronize()
+    torch.cuda.synchronize(device)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    nss = case["config"]["config_number_of_sub_steps"]
+    dts = dt / case["config"]["config_dynamics_split_steps"] / nss
+    _, ms_k = dy.time_acoustic_step(dts, small_step=2, reps=args.acoustic_reps)
+    b_ac = dy.acoustic_bytes()
+    dy.close()
+    achieved = b_ac / (sum(ms_k) / 1e3) / 1e9
+    return {"workload": f"x1.{ncells} {'moist (num_scalars=6)' if args.moist else 'dry'} dycore, "
+                        f"{case['nVertLevels']} levels, dt={dt:g}s, 1 GPU (BASELINE.json configs[1])",
+            "value": case["nCells"] * case["nVertLevels"] / (ms / 1e3), "unit": "cell-updates/s",
+            "ms_per_step": ms, "steps": steps, "warmup": warmup,
+            "acoustic_roofline": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": achieved / HBM_PEAK_GBS, "ms_per_substep": sum(ms_k)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -81,6 +117,8 @@ def main():
     ap.add_argument("--acoustic-reps", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=1, help="blocks per GPU (MPAS blocks with halos)")
     ap.add_argument("--rccl-local", action="store_true", help="route in-process block exchanges through RCCL")
+    ap.add_argument("--no-configs1", action="store_true",
+                    help="skip the secondary x1.10242 (BASELINE.json configs[1]) measurement")
     args = ap.parse_args()
 
     world, rank, local = _dist()
@@ -243,6 +281,10 @@ def main():
             out["cpu_baseline"] = {"error": str(e)[:200]}
     out["build_s"] = round(t_build, 1)
     dy.close()
+    # BASELINE.json configs[1] (x1.10242 x 56 on one MI355X) alongside the headline mesh: the same
+    # measurement on the small mesh (launch-bound), reported under "configs1"
+    if world == 1 and not (args.init or args.varres or args.no_configs1) and args.ncells != 10242:
+        out["configs1"] = small_mesh_line(args, torch, device)
     if dist:
         dist.destroy_process_group()
     if rank == 0:
