@@ -673,12 +673,16 @@ inline bool batched(const Dims& d) {
   return g_kernel_tier >= 1 && (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
 }
 
-void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
-  LAUNCH(k_vert_imp_coefs, std::max(d.nCellsSolve, 1), d, p, dts, ctx->cf.epssm);
-}
 
 // pair-layout edge kernels (k_*_p: two edges per wave, two levels per lane) need an even K
 inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K % 2 == 0 && d.K <= 64; }
+
+void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
+  if (pair_layout(d))
+    LAUNCH_E(k_vert_imp_coefs_p, std::max((d.nCellsSolve + 1) / 2, 1), d, p, dts, ctx->cf.epssm);
+  else
+    LAUNCH(k_vert_imp_coefs, std::max(d.nCellsSolve, 1), d, p, dts, ctx->cf.epssm);
+}
 
 // part: 0 = all kernels; 1 = only k_dyn_cells1, which reads nothing the exchange after the
 // diagnostics (1234-1249) or at the substep boundary (1282-1297) delivers; 2 = the rest

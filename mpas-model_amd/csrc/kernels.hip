@@ -2073,6 +2073,107 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
   }
 }
 
+// atm_compute_vert_imp_coefs_work (2064-2129) in the pair layout: two owned cells per wave, two
+// levels per lane.  The LU recurrence alpha(k) = 1/(b(k) - a(k) gamma(k-1)), gamma(k) = c(k) alpha(k)
+// runs as a lane-shift sweep: each iteration finalizes one more lane (two levels, the second from
+// the first in registers), K/2 iterations instead of K-1, each from exactly the operands of the
+// sequential recurrence -- and a wave now carries two columns, halving the DP work per column.
+__global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs p, double dts, double epssm) {
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const double dtseps = .5 * dts * (1. + epssm);
+  const double rcv = RGAS / (CP - RGAS);
+  const double c2 = CP * rcv;
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)K) p.cofrz[threadIdx.x] = dtseps * p.rdzw[threadIdx.x];
+  const int cA = 2 * pair_wave();
+  if (cA >= d.nCellsSolve) return;
+  const bool hasB = cA + 1 < d.nCellsSolve;
+  const int c = sel(h, cA, hasB ? cA + 1 : cA);
+  const bool mine = h == 0 || hasB;
+  const int lc = min(l, K / 2 - 1);
+  const int kx = 2 * l, ky = 2 * l + 1;
+  const bool ax = kx < K, ay = ky < K;  // "act" of the two levels
+  const size_t o = (size_t)c * K + 2 * lc;
+  auto LDP = [&](const double* a) {
+    d2 v = ld2(a + o);
+    return d2{ax ? v.x : 0.0, ay ? v.y : 0.0};
+  };
+  auto LD1 = [&](const double* a) {
+    d2 v = ld2(a + 2 * lc);
+    return d2{ax ? v.x : 0.0, ay ? v.y : 0.0};
+  };
+  const d2 zz = LDP(p.zz), pp = LDP(p.exner), t = LDP(p.theta_m2), rb = LDP(p.rho_base), rtb = LDP(p.rtheta_base);
+  const d2 pb = LDP(p.exner_base), rt = LDP(p.rtheta_p), cqw = LDP(p.cqw), qtot = LDP(p.qtot);
+  const d2 fzm = LD1(p.fzm), fzp = LD1(p.fzp), rdzu = LD1(p.rdzu), rdzw = LD1(p.rdzw);
+  const d2 zzm = km1(zz, l), pm = km1(pp, l), tm = km1(t, l);
+  d2 cofwr{0.0, 0.0}, cofwz{0.0, 0.0}, coftz{0.0, 0.0}, cofwt{0.0, 0.0};
+  auto lev1 = [&](bool act, int k, double zz_, double zzm_, double pp_, double pm_, double t_, double tm_,
+                  double fzm_, double fzp_, double rdzu_, double cqw_, double& wr, double& wz, double& tz) {
+    if (act && k >= 1) {
+      wr = .5 * dtseps * GRAVITY * (fzm_ * zz_ + fzp_ * zzm_);
+      wz = dtseps * c2 * (fzm_ * zz_ + fzp_ * zzm_) * rdzu_ * cqw_ * (fzm_ * pp_ + fzp_ * pm_);
+      tz = dtseps * (fzm_ * t_ + fzp_ * tm_);
+    }
+  };
+  lev1(ax, kx, zz.x, zzm.x, pp.x, pm.x, t.x, tm.x, fzm.x, fzp.x, rdzu.x, cqw.x, cofwr.x, cofwz.x, coftz.x);
+  lev1(ay, ky, zz.y, zzm.y, pp.y, pm.y, t.y, tm.y, fzm.y, fzp.y, rdzu.y, cqw.y, cofwr.y, cofwz.y, coftz.y);
+  if (ax) cofwt.x = .5 * dtseps * rcv * zz.x * GRAVITY * rb.x / (1. + qtot.x) * pp.x / ((rtb.x + rt.x) * pb.x);
+  if (ay) cofwt.y = .5 * dtseps * rcv * zz.y * GRAVITY * rb.y / (1. + qtot.y) * pp.y / ((rtb.y + rt.y) * pb.y);
+  const d2 coftz_p = kp1(coftz), coftz_m = km1(coftz, l), cofwt_m = km1(cofwt, l), rdzw_m = km1(rdzw, l);
+  const d2 cofrz{dtseps * rdzw.x, dtseps * rdzw.y};
+  const d2 cofrz_m = km1(cofrz, l);
+  d2 a{0.0, 0.0}, b{1.0, 1.0}, cc{0.0, 0.0};
+  auto lev2 = [&](bool act, int k, double& a_, double& b_, double& c_, double wz, double wr, double wt, double tz,
+                  double tzm, double tzp, double wtm, double rw, double rwm, double z, double zm, double rz,
+                  double rzm) {
+    if (act && k >= 1) {
+      a_ = -wz * tzm * rwm * zm + wr * rzm - wtm * tzm * rwm;
+      b_ = 1. + wz * (tz * rw * z + tz * rwm * zm) - tz * (wt * rw - wtm * rwm) + wr * (rz - rzm);
+      c_ = -wz * tzp * rw * z - wr * rz + wt * tzp * rw;
+    }
+  };
+  lev2(ax, kx, a.x, b.x, cc.x, cofwz.x, cofwr.x, cofwt.x, coftz.x, coftz_m.x, coftz_p.x, cofwt_m.x, rdzw.x,
+       rdzw_m.x, zz.x, zzm.x, cofrz.x, cofrz_m.x);
+  lev2(ay, ky, a.y, b.y, cc.y, cofwz.y, cofwr.y, cofwt.y, coftz.y, coftz_m.y, coftz_p.y, cofwt_m.y, rdzw.y,
+       rdzw_m.y, zz.y, zzm.y, cofrz.y, cofrz_m.y);
+  // sequential LU recurrence (2124-2127) as a lane-shift sweep
+  const bool fx = kx >= 1 && ax, fy = ay;
+  d2 alpha{0.0, 0.0}, gamma{0.0, 0.0};
+  for (int it = 0; it < K / 2; ++it) {
+    const double gpx = lane_shr1(gamma.y);
+    if (fx) {
+      alpha.x = 1. / (b.x - a.x * (l == 0 ? 0.0 : gpx));
+      gamma.x = cc.x * alpha.x;
+    }
+    if (fy) {
+      alpha.y = 1. / (b.y - a.y * gamma.x);
+      gamma.y = cc.y * alpha.y;
+    }
+  }
+  if (mine && ax) {
+    if (l == 0) {  // level 1 only: cofwr(1) / cofwz(1) are not written (2077-2081)
+      p.cofwr[o + 1] = cofwr.y;
+      p.cofwz[o + 1] = cofwz.y;
+    } else {
+      st2(p.cofwr + o, cofwr);
+      st2(p.cofwz + o, cofwz);
+    }
+    st2(p.cofwt + o, cofwt);
+    st2(p.a_tri + o, a);
+    st2(p.alpha_tri + o, alpha);
+    st2(p.gamma_tri + o, gamma);
+  }
+  // coftz(1) = coftz(K+1) = 0: levels 0..K, the lane holding level K stores that one level
+  if (mine && kx <= K) {
+    double* ct = p.coftz + (size_t)c * (K + 1) + kx;
+    if (ky <= K) {
+      ct[0] = coftz.x;
+      ct[1] = coftz.y;
+    } else {
+      ct[0] = coftz.x;
+    }
+  }
+}
+
 // k_acoustic_edges in the pair layout (same expressions, per level)
 template <bool DD>
 __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,
