@@ -96,6 +96,19 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep);
 int mpas_dyc_shift_time_levels(mpas_dyc_ctx* ctx);
 /* Block until all queued device work of the context is complete. */
 int mpas_dyc_synchronize(mpas_dyc_ctx* ctx);
+/* Physics coupling (the reference built with -DDO_PHYSICS, mpas_atm_time_integration.F:424-449,
+ * 1610-1648, 3437, 3743).  With MPAS_DYC_PHYSICS_TENDENCIES the host (the physics package's
+ * physics_get_tend, mpas_atmphys_todynamics.F:59) supplies, before each mpas_dyc_timestep,
+ *   tend_physics.tend_ru_physics (K, nEdges+1), tend_physics.tend_rtheta_physics and
+ *   tend_physics.tend_rho_physics (K, nCells+1), and tend.scalars_tend (ns, K, nCells+1);
+ * the step adds them where the reference does (tend_u, tend_theta, tend_rho; the scalar
+ * transport's scalar_tend_save / scalar_tend), and at its end sets negative scalars of time
+ * level 2 to zero (1645-1646).  MPAS_DYC_PHYSICS_RQVDYNTEN also computes tend_physics.rqvdynten
+ * (1629-1643; config_convection_scheme cu_grell_freitas, cu_tiedtke or cu_ntiedtke).  The
+ * microphysics driver (1650-1660) stays with the host, after the step. */
+#define MPAS_DYC_PHYSICS_TENDENCIES 1
+#define MPAS_DYC_PHYSICS_RQVDYNTEN 2
+int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags);
 /* atm_compute_output_diagnostics(state, time_level, diag, mesh) (mpas_atm_core.F:753, called
  * before history writes at :544 and :694): diag theta, rho and pressure from theta_m, rho_zz,
  * scalars(index_qv) of the time level, zz, pressure_base and pressure_p.  Asynchronous. */

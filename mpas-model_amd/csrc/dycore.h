@@ -30,6 +30,7 @@ struct Dims {
   int nCellsSolve, nEdgesSolve, nVerticesSolve;
   int moist_start, moist_end;  // 0-based inclusive range of moist scalars
   int diabatic;                // rt_diabatic_tend holds nonzero data (else it is read as 0)
+  int physics;                 // DO_PHYSICS coupling: tend_*_physics and scalars_tend come from the host
 };
 
 struct Config {
@@ -75,7 +76,7 @@ struct Ptrs {
   double *uReconstructX, *uReconstructY, *uReconstructZ, *uReconstructZonal, *uReconstructMeridional;
   // ---- tend / tend_physics
   double *tend_u, *tend_u_euler, *tend_w, *tend_w_euler, *tend_theta, *tend_theta_euler;
-  double *tend_rho, *rt_diabatic_tend, *scalars_tend, *rthdynten;
+  double *tend_rho, *rt_diabatic_tend, *scalars_tend, *rthdynten, *rqvdynten;
   // ---- module scratch (mpas_atm_time_integration.F:35-71)
   double *qtot, *tend_ru_physics, *tend_rtheta_physics, *tend_rho_physics;
   double *delsq_theta, *delsq_w, *delsq_divergence, *delsq_u, *delsq_vorticity, *dpdz;

@@ -110,6 +110,7 @@ struct mpas_dyc_ctx {
   hipEvent_t xfork = nullptr, xjoin = nullptr;
   int overlap = -1;                     // 1 on, 0 off, -1 auto: on when exchanges go through RCCL
   bool bnd_ready = false;
+  int physics = 0;                      // MPAS_DYC_PHYSICS_* flags (mpas_dyc_set_physics)
 };
 
 namespace {
@@ -245,10 +246,16 @@ void build_registry(Block& c) {
   c.fields.back().nsub = ns;
   add(c, "tend_physics", "rthdynten", L_CELL, K);
   // module scratch (mpas_atm_time_integration.F:35-71)
-  for (const char* n : {"qtot", "tend_rtheta_physics", "tend_rho_physics", "delsq_theta", "delsq_w",
+  // the physics tendencies of physics_get_tend (module scratch of the reference, 268-279), set by
+  // the host when physics coupling is on (mpas_dyc_set_physics)
+  add(c, "tend_physics", "rqvdynten", L_CELL, K);
+  add(c, "tend_physics", "tend_rtheta_physics", L_CELL, K);
+  add(c, "tend_physics", "tend_rho_physics", L_CELL, K);
+  add(c, "tend_physics", "tend_ru_physics", L_EDGE, K);
+  for (const char* n : {"qtot", "delsq_theta", "delsq_w",
                         "delsq_divergence", "dpdz", "s_max", "s_min", "rho_zz_int", "scalar_old_copy"})
     add(c, "scratch", n, L_CELL, K);
-  for (const char* n : {"tend_ru_physics", "delsq_u", "ke_edge", "flux_arr", "flux_upwind_tmp", "flux_tmp",
+  for (const char* n : {"delsq_u", "ke_edge", "flux_arr", "flux_upwind_tmp", "flux_tmp",
                         "advflux_w", "advflux_th"})
     add(c, "scratch", n, L_EDGE, K);
   for (const char* n : {"delsq_vorticity", "ke_vertex"}) add(c, "scratch", n, L_VERTEX, K);
@@ -316,7 +323,11 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   p.tend_theta = P<double>(c, b, "tend", "theta_m"); p.tend_theta_euler = P<double>(c, b, "tend", "theta_euler");
   p.tend_rho = P<double>(c, b, "tend", "rho_zz"); p.rt_diabatic_tend = P<double>(c, b, "tend", "rt_diabatic_tend");
   p.scalars_tend = P<double>(c, b, "tend", "scalars_tend"); p.rthdynten = P<double>(c, b, "tend_physics", "rthdynten");
-  SC(qtot); SC(tend_ru_physics); SC(tend_rtheta_physics); SC(tend_rho_physics);
+  SC(qtot);
+  p.tend_ru_physics = P<double>(c, b, "tend_physics", "tend_ru_physics");
+  p.tend_rtheta_physics = P<double>(c, b, "tend_physics", "tend_rtheta_physics");
+  p.tend_rho_physics = P<double>(c, b, "tend_physics", "tend_rho_physics");
+  p.rqvdynten = P<double>(c, b, "tend_physics", "rqvdynten");
   SC(delsq_theta); SC(delsq_w); SC(delsq_divergence); SC(delsq_u); SC(delsq_vorticity); SC(dpdz);
   SC(ke_vertex); SC(ke_edge); SC(horiz_flux_array);
   SC(s_max); SC(s_min); SC(scale_arr); SC(flux_arr); SC(flux_upwind_tmp); SC(flux_tmp); SC(wdtn); SC(rho_zz_int);
@@ -1100,6 +1111,18 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
     }
   }
   EACH(LAUNCH(k_reconstruct, d.nCellsSolve, d, p, p.u2));          // mpas_reconstruct (1581-1603)
+  if (ctx->physics & MPAS_DYC_PHYSICS_TENDENCIES) {                // DO_PHYSICS block, 1610-1648
+    // rqvdynten (1629-1643) for cu_grell_freitas / cu_tiedtke / cu_ntiedtke, from the scalars before
+    // the clip; the microphysics call itself (1650-1660) belongs to the host, after this step
+    if (ctx->physics & MPAS_DYC_PHYSICS_RQVDYNTEN)
+      EACH(LAUNCH(k_physics_rqvdynten, d.nCells + 1, d, p, ctx->index_qv, cf.monotonic, dt));
+    for (auto& b : ctx->blk) {
+      const int64_t n = (int64_t)b.d.ns * (b.d.nCells + 1) * b.d.K;
+      if (!ctx->planning)
+        hipLaunchKernelGGL(k_physics_clip_scalars, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)),
+                           dim3(256), 0, ctx->stream, ::P<double>(ctx, b, "state", "scalars", 2), n);
+    }
+  }
   // summarize_timestep (1794) only logs: outside the hot path.
   return MPAS_DYC_OK;
 }
@@ -1570,6 +1593,20 @@ int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
   int r = init_diagnostics(ctx, dt);
   HIPCHK(hipGetLastError());
   return r;
+}
+
+int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags) {
+  if (!ctx || (flags & ~(MPAS_DYC_PHYSICS_TENDENCIES | MPAS_DYC_PHYSICS_RQVDYNTEN))) return MPAS_DYC_EINVAL;
+  if ((flags & MPAS_DYC_PHYSICS_RQVDYNTEN) && !(flags & MPAS_DYC_PHYSICS_TENDENCIES)) return MPAS_DYC_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->physics = flags;
+  for (auto& b : ctx->blk) b.d.physics = (flags & MPAS_DYC_PHYSICS_TENDENCIES) ? 1 : 0;
+  for (int i = 0; i < 2; ++i) {  // captured steps bake the flags in
+    if (ctx->graph_exec[i]) (void)hipGraphExecDestroy(ctx->graph_exec[i]);
+    ctx->graph_exec[i] = nullptr;
+  }
+  return MPAS_DYC_OK;
 }
 
 int mpas_dyc_output_diagnostics(mpas_dyc_ctx* ctx, int32_t time_level) {

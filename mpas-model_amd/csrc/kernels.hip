@@ -144,6 +144,10 @@ __device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, 
 // by atm_srk3 when the model is built without DO_PHYSICS (mpas_atm_time_integration.F:
 // 268-279, 450-457): the kernels add the same +0.0 without streaming the zero arrays.
 #define PHYS_ZERO 0.0
+// With physics coupling on (mpas_dyc_set_physics, the reference built with DO_PHYSICS), the
+// tendencies physics_get_tend computed (mpas_atm_time_integration.F:424-449) are added in the
+// same places instead of the zeros of 450-457.
+#define PHYS(arr, i) (d.physics ? (arr)[(i)] : 0.0)
 #define LDW(p, i) (actw ? (p)[(i)] : 0.0)
 
 // Per-cell stencil records (dycore.h, Ptrs::cell_rec / cell_sdv), one thread per cell.  The
@@ -359,7 +363,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells1(Dims d, Ptrs p, Co
     const double rwk = (k <= K) ? p.rw[ow] : 0.0;
     const double rwp = dn1(rwk);
     if (act) {
-      p.tend_rho[o] = -hd - p.rdzw[k] * (rwp - rwk) + PHYS_ZERO;  // tend_rho_physics
+      p.tend_rho[o] = -hd - p.rdzw[k] * (rwp - rwk) + PHYS(p.tend_rho_physics, o);
       const double qt = p.qtot[o];
       p.dpdz[o] = -GRAVITY * (p.rho_base[o] * (qt) + p.rho_p_save[o] * (1. + qt));
     }
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells1_b(Dims d, Ptrs p, 
   if (rk1) {
     const double rwp = dn1(rwk);
     if (act) {
-      p.tend_rho[o] = -hd - p.rdzw[k] * (rwp - rwk) + PHYS_ZERO;  // tend_rho_physics
+      p.tend_rho[o] = -hd - p.rdzw[k] * (rwp - rwk) + PHYS(p.tend_rho_physics, o);
       p.dpdz[o] = -GRAVITY * (rb * (qt) + rps * (1. + qt));
     }
   }
@@ -539,7 +543,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges(Dims d, Ptrs p, Con
         const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
         tu = tu - re * uk * coef;
       }
-      tu = tu + tue + PHYS_ZERO;  // tend_ru_physics
+      tu = tu + tue + PHYS(p.tend_ru_physics, o);
     }
     if (act) p.tend_u[o] = tu;
   }
@@ -672,7 +676,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_b(Dims d, Ptrs p, Co
       const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
       tu = tu - re * uk * coef;
     }
-    tu = tu + tue + PHYS_ZERO;  // tend_ru_physics
+    tu = tu + tue + PHYS(p.tend_ru_physics, o);
   }
   if (act) p.tend_u[o] = tu;
   if (RK1) del2(tue, dv1, dv2, vo1, vo2, kd1, kd2, invDv, msd2);
@@ -757,7 +761,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_rk1b(Dims d, Ptrs p
     const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
     tu = tu - p.rho_edge[o] * uk * coef;
   }
-  p.tend_u[o] = tu + tue + PHYS_ZERO;  // tend_ru_physics
+  p.tend_u[o] = tu + tue + PHYS(p.tend_ru_physics, o);
 }
 
 // cells (all), rk1: del^2 for w (5107-5130) and theta (5278-5301)
@@ -915,7 +919,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_rk1b_b(Dims d, Ptrs
     const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
     tu = tu - re * uk * coef;
   }
-  p.tend_u[o] = tu + tue + PHYS_ZERO;  // tend_ru_physics
+  p.tend_u[o] = tu + tue + PHYS(p.tend_ru_physics, o);
 }
 
 template <int ME>
@@ -1205,7 +1209,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3_r(Dims d, Ptrs p, 
     p.rthdynten[o] = tt / rz;
     tt = tt + rz * rtd;
     if (RK1) p.tend_theta_euler[o] = tte;
-    p.tend_theta[o] = tt + tte + PHYS_ZERO;  // tend_rtheta_physics
+    p.tend_theta[o] = tt + tte + PHYS(p.tend_rtheta_physics, o);
   }
 }
 
@@ -1407,7 +1411,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Co
     p.rthdynten[o] = tt / rz;
     tt = tt + rz * (d.diabatic ? p.rt_diabatic_tend[o] : 0.0);
     if (rk1) p.tend_theta_euler[o] = tte;
-    p.tend_theta[o] = tt + tte + PHYS_ZERO;  // tend_rtheta_physics
+    p.tend_theta[o] = tt + tte + PHYS(p.tend_rtheta_physics, o);
   }
 }
 
@@ -1720,8 +1724,9 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
       if (kx >= k0) tu.x = tu.x - re.x * uk.x * ((double)(kx + 1 - k0) * s.rayleigh_coef_inverse);
       if (ky >= k0) tu.y = tu.y - re.y * uk.y * ((double)(ky + 1 - k0) * s.rayleigh_coef_inverse);
     }
-    tu.x = tu.x + tue.x + PHYS_ZERO;  // tend_ru_physics
-    tu.y = tu.y + tue.y + PHYS_ZERO;
+    const d2 tph = d.physics ? ld2(p.tend_ru_physics + o) : d2{0.0, 0.0};  // tend_ru_physics
+    tu.x = tu.x + tue.x + tph.x;
+    tu.y = tu.y + tue.y + tph.y;
   }
   if (solve) store(p.tend_u, tu);
   if (PGF) del2(tue, dv1, dv2, vo1, vo2, kd1, kd2, invDv, msd2);
@@ -2872,6 +2877,24 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_b(Dims d, Ptrs p, c
 }
 
 // ============================================================================
+// end of atm_srk3 with physics (DO_PHYSICS block, mpas_atm_time_integration.F:1610-1648):
+// rqvdynten for the convection schemes that need it, then negative mixing ratios set to zero
+// ============================================================================
+__global__ __launch_bounds__(BLOCK_THREADS) void k_physics_rqvdynten(Dims d, Ptrs p, int index_qv, int monotonic,
+                                                                      double config_dt) {
+  const int c = wave_elem(0);
+  if (c > d.nCells) return;
+  const int k = lane_id(), K = d.K;
+  if (k >= K) return;
+  p.rqvdynten[(size_t)c * K + k] =
+      monotonic ? (p.scalars2[SIX(c, k, index_qv)] - p.scalars1[SIX(c, k, index_qv)]) / config_dt : 0.0;
+}
+__global__ void k_physics_clip_scalars(double* s, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (s[i] < 0.0) s[i] = 0.0;  // where (scalars_2 < 0.0) scalars_2 = 0.0
+}
+
+// ============================================================================
 // atm_compute_output_diagnostics  (core_atmosphere/mpas_atm_core.F:753-800): theta, rho and
 // pressure of the history output from the prognostic state of time level `tl`
 // ============================================================================
@@ -3086,8 +3109,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_cells(Dims d, Ptrs p,
       }
     }
     if (act) {
-      p.scalars_tend[SIX(c, k, is)] = 0.0;  // no physics: scalar_tend_save zeroed (3437-3439)
-      stc = stc * invA + 0.0;
+      double sts = 0.0;
+      if (d.physics) sts = p.scalars_tend[SIX(c, k, is)];  // scalar_tend_save from physics
+      else p.scalars_tend[SIX(c, k, is)] = 0.0;           // no physics: zeroed (3437-3439)
+      stc = stc * invA + sts;
     }
     const double sn = LD(p.scalars2, SIX(c, k, is));
     const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
@@ -3121,7 +3146,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_prep(Dims d, Ptrs p, dou
     const double rzo = p.rho_zz1[o];
     for (int is = 0; is < ns; ++is) {
       const size_t so = SIX(c, k, is);
-      p.scalars_tend[so] = 0.0;
+      if (!d.physics) p.scalars_tend[so] = 0.0;  // 3743-3747: zeroed only without physics
       p.scalars1[so] = p.scalars1[so] + dt * p.scalars_tend[so] / rzo;
       p.scalars_tend[so] = 0.0;
     }
@@ -3359,8 +3384,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_cells_b(Dims d, Ptrs 
     for (int i = 0; i < ME; ++i)
       if (i < st.ne) stc = stc - sru[i] * hf[i];
     if (act) {
-      p.scalars_tend[SIX(c, k, is)] = 0.0;  // no physics: scalar_tend_save zeroed (3437-3439)
-      stc = stc * invA + 0.0;
+      double sts = 0.0;
+      if (d.physics) sts = p.scalars_tend[SIX(c, k, is)];  // scalar_tend_save from physics
+      else p.scalars_tend[SIX(c, k, is)] = 0.0;           // no physics: zeroed (3437-3439)
+      stc = stc * invA + sts;
     }
     const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
     double wdtn = 0.0;

@@ -20,6 +20,7 @@ EXPORTS = (
     "mpas_dyc_get_block_field", "mpas_dyc_block_field_bytes", "mpas_dyc_block_field_device_ptr",
     "mpas_dyc_set_exchange_list", "mpas_dyc_comm_unique_id_bytes", "mpas_dyc_comm_unique_id", "mpas_dyc_comm_init",
     "mpas_dyc_set_transport", "mpas_dyc_halo_exchange", "mpas_dyc_set_overlap", "mpas_dyc_output_diagnostics",
+    "mpas_dyc_set_physics",
 )
 CELL, EDGE, VERTEX = 0, 1, 2
 SEND, RECV = 0, 1
@@ -85,6 +86,7 @@ def load() -> C.CDLL:
     lib.mpas_dyc_shift_time_levels.argtypes = [vp]
     lib.mpas_dyc_synchronize.argtypes = [vp]
     lib.mpas_dyc_output_diagnostics.argtypes = [vp, i32]
+    lib.mpas_dyc_set_physics.argtypes = [vp, i32]
     lib.mpas_dyc_time_acoustic_step.argtypes = [vp, dbl, i32, i32, C.POINTER(dbl), C.POINTER(dbl)]
     lib.mpas_dyc_use_graph.argtypes = [vp, i32]
     lib.mpas_dyc_acoustic_bytes.argtypes = [vp]

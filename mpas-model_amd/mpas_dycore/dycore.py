@@ -175,6 +175,15 @@ class Dycore:
         """atm_timestep -> atm_srk3 (mpas_atm_time_integration.F:87-139); asynchronous."""
         self._check(self.lib.mpas_dyc_timestep(self.h, float(dt), int(itimestep)), "atm_timestep")
 
+    PHYSICS_TENDENCIES, PHYSICS_RQVDYNTEN = 1, 2
+
+    def set_physics(self, tendencies: bool = True, rqvdynten: bool = False):
+        """Physics coupling (the reference's DO_PHYSICS build): the host sets tend_physics.
+        tend_ru_physics / tend_rtheta_physics / tend_rho_physics and tend.scalars_tend before each
+        step (as physics_get_tend does, mpas_atm_time_integration.F:424-449)."""
+        flags = (self.PHYSICS_TENDENCIES if tendencies else 0) | (self.PHYSICS_RQVDYNTEN if rqvdynten else 0)
+        self._check(self.lib.mpas_dyc_set_physics(self.h, flags), "set_physics")
+
     def output_diagnostics(self, time_level: int = 1):
         """atm_compute_output_diagnostics (mpas_atm_core.F:753-800): diag theta, rho, pressure."""
         self._check(self.lib.mpas_dyc_output_diagnostics(self.h, int(time_level)), "output_diagnostics")
@@ -216,10 +225,11 @@ for _n in ("theta_m", "rho_zz", "rho_p", "rtheta_p", "exner", "pressure_p", "pre
            "wwAvg", "cqw", "h_divergence", "pv_cell", "rho_pp", "rtheta_pp", "rw_p", "exner_base", "pressure_base",
            "rtheta_base", "coftz", "cofwz", "cofwr", "cofwt", "a_tri", "alpha_tri", "gamma_tri", "rw_save",
            "tend_rtheta_adv", "rho_p_save", "rtheta_p_save", "rho_zz_old_split", "rtheta_pp_old", "wwAvg_split",
+           "tend_rtheta_physics", "tend_rho_physics", "rqvdynten",
            "scalars_tend", "rthdynten", "rt_diabatic_tend", "theta_euler", "w_euler", "uReconstructX",
            "uReconstructY", "uReconstructZ", "uReconstructZonal", "uReconstructMeridional"):
     _LOCS[_n] = "cell"
-for _n in ("ru", "ruAvg", "ru_p", "ru_save", "cqu", "rho_edge", "v", "pv_edge", "gradPVn", "gradPVt",
+for _n in ("ru", "ruAvg", "ru_p", "ru_save", "cqu", "rho_edge", "v", "pv_edge", "gradPVn", "gradPVt", "tend_ru_physics",
            "ruAvg_split", "u_euler"):
     _LOCS[_n] = "edge"
 for _n in ("vorticity", "pv_vertex"):

@@ -284,7 +284,7 @@ program mpas_ref_harness
    real(kind=RKIND) :: config_len_disp, config_visc4_2dsmag, config_del4u_div_factor, config_coef_3rd_order
    real(kind=RKIND) :: config_smagorinsky_coef, config_epssm, config_smdiv, config_apvm_upwinding
    real(kind=RKIND) :: config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days
-   character(len=64) :: config_horiz_mixing
+   character(len=64) :: config_horiz_mixing, config_convection_scheme
    character(len=32) :: mode
    integer :: kernel_small_step, kernel_rk_step
    real(kind=RKIND) :: kernel_dts
@@ -297,10 +297,10 @@ program mpas_ref_harness
       config_h_theta_eddy_visc2, config_h_theta_eddy_visc4, config_v_theta_eddy_visc2, &
       config_len_disp, config_visc4_2dsmag, config_del4u_div_factor, config_coef_3rd_order, &
       config_smagorinsky_coef, config_epssm, config_smdiv, config_apvm_upwinding, &
-      config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days, config_horiz_mixing
+      config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days, config_horiz_mixing, config_convection_scheme
 
    type (domain_type), pointer :: domain
-   type (mpas_pool_type), pointer :: configs, dimpool, mesh, state, diag, tend, tend_physics
+   type (mpas_pool_type), pointer :: configs, dimpool, mesh, state, diag, tend, tend_physics, diag_physics
    type (mpas_pool_type), pointer, dimension(:) :: plist
    integer :: K, nC1, nE1, nV1, ns, step, i, u, nthr, t
    integer, dimension(:), pointer :: cts, cte, csts, cste, ets, ete, ests, este, vts, vte, vsts, vste
@@ -316,6 +316,7 @@ program mpas_ref_harness
    nthreads_req = 0
    moist_end = 1
    config_horiz_mixing = '2d_smagorinsky'
+   config_convection_scheme = 'off'
    mode = 'run'
    kernel_small_step = 2
    kernel_rk_step = 1
@@ -399,7 +400,7 @@ program mpas_ref_harness
    call mpas_pool_add_config_logical(configs, 'config_apply_lbcs', .false.)
    call mpas_pool_add_config_char(configs, 'config_IAU_option', 'off')
    call mpas_pool_add_config_char(configs, 'config_microp_scheme', 'off')
-   call mpas_pool_add_config_char(configs, 'config_convection_scheme', 'off')
+   call mpas_pool_add_config_char(configs, 'config_convection_scheme', trim(config_convection_scheme))
    call mpas_pool_add_config_logical(configs, 'config_print_global_minmax_vel', .false.)
    call mpas_pool_add_config_logical(configs, 'config_print_detailed_minmax_vel', .false.)
    call mpas_pool_add_config_logical(configs, 'config_print_global_minmax_sca', .false.)
@@ -410,11 +411,14 @@ program mpas_ref_harness
    call mpas_pool_create_pool(diag)
    call mpas_pool_create_pool(tend)
    call mpas_pool_create_pool(tend_physics)
+   call mpas_pool_create_pool(diag_physics)
    call mpas_pool_add_subpool(hblock % structs, 'mesh', mesh)
    call mpas_pool_add_subpool(hblock % structs, 'state', state)
    call mpas_pool_add_subpool(hblock % structs, 'diag', diag)
    call mpas_pool_add_subpool(hblock % structs, 'tend', tend)
    call mpas_pool_add_subpool(hblock % structs, 'tend_physics', tend_physics)
+   ! empty: only the DO_PHYSICS build looks it up, for driver_microphysics (scheme 'off' -> unused)
+   call mpas_pool_add_subpool(hblock % structs, 'diag_physics', diag_physics)
 
    call add_dims(hblock % dimensions)
    call add_dims(mesh)
@@ -559,6 +563,14 @@ program mpas_ref_harness
    call add_r3(tend, 'tend', 'scalars_tend', ns, K, nC1, 1)
    call add_r2(tend_physics, 'tend_physics', 'rthdynten', K, nC1, 1)
    call add_r2(tend_physics, 'tend_physics', 'rqvdynten', K, nC1, 1)
+   ! prescribed physics tendencies, handed to the DO_PHYSICS dycore by the physics_get_tend test
+   ! double (shims/mpas_atmphys_todynamics_stub.F90); shapes as allocated in atm_srk3
+   if (file_exists('tend_ru_physics_in')) then
+      call add_r2(tend_physics, 'tend_physics', 'tend_ru_physics_in', K, nE1, 1)
+      call add_r2(tend_physics, 'tend_physics', 'tend_rtheta_physics_in', K, nC1, 1)
+      call add_r2(tend_physics, 'tend_physics', 'tend_rho_physics_in', K, nC1, 1)
+      call add_r3(tend_physics, 'tend_physics', 'scalars_tend_in', ns, K, nC1, 1)
+   end if
 
    allocate(plist(1))
 

@@ -19,6 +19,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HARNESS = os.path.join(HERE, "_ref", "mpas_ref_harness")
+# the reference dycore built with -DDO_PHYSICS, physics_get_tend replaced by a test double that
+# hands over prescribed tendencies (make -C oracle phys; shims/mpas_atmphys_todynamics_stub.F90)
+PHYS_HARNESS = os.path.join(HERE, "_ref", "mpas_ref_harness_phys")
 # the same harness driver linked against the Fortran drop-in module + libmpas_dycore.so
 # (make -C oracle dropin): the product behind the reference's own Fortran API, not an oracle
 DROPIN_HARNESS = os.path.join(HERE, "_ref", "mpas_dropin_harness")
@@ -46,8 +49,22 @@ def to_fortran(case: dict, name: str) -> np.ndarray:
     return tf(case, name)
 
 
+def write_physics_inputs(case: dict, d: str, physics: dict):
+    """Prescribed physics tendencies in the Fortran images the DO_PHYSICS harness reads:
+    element-major tend_ru_physics (nEdges, K), tend_rtheta_physics / tend_rho_physics (nCells, K),
+    scalars_tend (nCells, K, ns) -> (K, n+1) / (ns, K, nCells+1) with a zero garbage slot."""
+    K, ns = case["nVertLevels"], case["num_scalars"]
+    shapes = {"tend_ru_physics": (case["nEdges"], K), "tend_rtheta_physics": (case["nCells"], K),
+              "tend_rho_physics": (case["nCells"], K), "scalars_tend": (case["nCells"], K, ns)}
+    for n, shp in shapes.items():
+        a = np.asarray(physics[n], dtype=np.float64).reshape(shp)
+        img = np.zeros((shp[0] + 1,) + shp[1:])
+        img[:-1] = a
+        img.tofile(os.path.join(d, n + "_in.bin"))
+
+
 def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthreads: int = 0,
-                 moist_end: int = 1):
+                 moist_end: int = 1, convection_scheme: str = "off"):
     F = _fields()
     os.makedirs(d, exist_ok=True)
     names = [n for n in case if n in F.LOCATION or n in F.VERTICAL_1D or n in F.SCALARS_0D]
@@ -89,7 +106,7 @@ def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthr
  config_smdiv={cfg['config_smdiv']!r}, config_apvm_upwinding={cfg['config_apvm_upwinding']!r},
  config_mpas_cam_coef={cfg['config_mpas_cam_coef']!r},
  config_rayleigh_damp_u_timescale_days={cfg['config_rayleigh_damp_u_timescale_days']!r},
- config_horiz_mixing='{cfg['config_horiz_mixing']}'
+ config_horiz_mixing='{cfg['config_horiz_mixing']}', config_convection_scheme='{convection_scheme}'
 /
 """
     nml = nml.replace("e+", "d+").replace("e-", "d-")
@@ -127,9 +144,14 @@ def read_dump(case: dict, stepdir: str) -> dict:
 
 
 def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads: int = 0,
-                  workdir: str | None = None, moist_end: int = 1, timeout: int = 3000, binary: str = HARNESS):
+                  workdir: str | None = None, moist_end: int = 1, timeout: int = 3000, binary: str = HARNESS,
+                  physics: dict | None = None):
     """Run the reference dycore; returns ({step: {field: array}}, [step wall times]).
-    ``binary=DROPIN_HARNESS`` runs the same driver on the drop-in module instead."""
+    ``binary=DROPIN_HARNESS`` runs the same driver on the drop-in module instead.
+    ``physics`` (dict of write_physics_inputs' arrays, optional key "convection_scheme") runs the
+    DO_PHYSICS build with those tendencies handed over by physics_get_tend every step."""
+    if physics is not None:
+        binary = PHYS_HARNESS
     if not available(binary):
         raise RuntimeError(f"{binary} not built (make -C oracle)")
     if dump_steps is None:
@@ -137,7 +159,10 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     own = workdir is None
     tmp = tempfile.mkdtemp(prefix="mpasref_") if own else workdir
     ind, outd = os.path.join(tmp, "in"), os.path.join(tmp, "out")
-    write_inputs(case, ind, nsteps, dt, dump_steps, nthreads, moist_end)
+    write_inputs(case, ind, nsteps, dt, dump_steps, nthreads, moist_end,
+                 (physics or {}).get("convection_scheme", "off"))
+    if physics is not None:
+        write_physics_inputs(case, ind, physics)
     env = dict(os.environ)
     if nthreads:
         env["OMP_NUM_THREADS"] = str(nthreads)

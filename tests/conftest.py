@@ -44,3 +44,26 @@ def varres_case_small():
     """Variable-resolution SCVT (4x refinement, pentagons/hexagons/heptagons, maxEdges=7)."""
     from mpas_dycore.cases import varres_case
     return varres_case(2562, ratio=4.0, K=26, ns=3, moist=True, lloyd_iters=30, cache=False)
+
+
+def physics_forcing(case, scale: float = 1.0) -> dict:
+    """Smooth prescribed physics tendencies for the physics-coupling tests (what physics_get_tend
+    hands the dycore, mpas_atm_time_integration.F:424-449): coupled momentum / theta / density
+    tendencies and scalar tendencies of typical magnitude, element-major.  The water-vapour
+    tendency is negative aloft so that the clip of negative mixing ratios (1642-1644) is exercised."""
+    import numpy as np
+    K, ns = case["nVertLevels"], case["num_scalars"]
+    kk = (np.arange(K) + 0.5) / K
+    latc, lonc = case["latCell"][:, None], case["lonCell"][:, None]
+    late, lone = case["latEdge"][:, None], case["lonEdge"][:, None]
+    f = dict(
+        tend_ru_physics=scale * 2e-4 * np.cos(late) * np.sin(2 * lone) * (1 - kk),
+        tend_rtheta_physics=scale * 3e-4 * np.cos(latc) ** 2 * np.exp(-3 * kk) * (1 + 0.5 * np.sin(lonc)),
+        tend_rho_physics=scale * 1e-7 * np.sin(latc) * np.cos(lonc) * (1 - kk),
+    )
+    st = np.zeros((case["nCells"], K, ns))
+    for i in range(ns):
+        st[:, :, i] = scale * 1e-7 * np.cos((i + 1) * latc) * np.sin(lonc + i) * (1 - kk) ** (i + 1)
+    st[:, :, 0] -= scale * 5e-7 * kk ** 2  # drying aloft: drives some qv negative -> clipped
+    f["scalars_tend"] = st
+    return f

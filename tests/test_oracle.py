@@ -59,3 +59,34 @@ def test_reference_reproduces_trajectory_fixture():
             ref = z[f"step{s}_{key}"]
             got = res[s][key].reshape(ref.shape)
             assert rel_linf(got, ref) <= 1e-12, (s, key)
+
+
+def test_physics_oracle_build():
+    """The DO_PHYSICS reference build (prescribed tendencies through the physics_get_tend test
+    double) with zero tendencies reproduces the plain build bit for bit; nonzero tendencies move
+    u, theta_m, rho_zz and the scalars, and rqvdynten is (qv(n+1) - qv(n)) / dt before the clip."""
+    from conftest import physics_forcing
+    from oracle import ref_runner
+    from mpas_dycore.cases import jw_case
+    if not (ref_runner.available() and ref_runner.available(ref_runner.PHYS_HARNESS)):
+        pytest.skip("oracle/_ref not built")
+    case = jw_case(642, K=26, ns=3, moist=True, cache=False)
+    dt = float(case["dt"])
+    zero = {k: np.zeros_like(v) for k, v in physics_forcing(case).items()}
+    a, _ = ref_runner.run_reference(case, 2, dt, [2], nthreads=2)
+    b, _ = ref_runner.run_reference(case, 2, dt, [2], nthreads=2, physics=zero)
+    keys = ("state.u.tl1", "state.theta_m.tl1", "state.rho_zz.tl1", "state.w.tl1", "state.scalars.tl1")
+    for k in keys:
+        assert np.array_equal(a[2][k], b[2][k]), k
+    phys = dict(physics_forcing(case), convection_scheme="cu_tiedtke")
+    c, _ = ref_runner.run_reference(case, 2, dt, [1, 2], nthreads=2, physics=phys)
+    for k in keys[:3] + keys[4:]:
+        assert not np.array_equal(a[2][k], c[2][k]), k
+    assert c[2]["state.scalars.tl1"].min() >= 0.0
+    # the monotone transport adds dt * scalars_tend / rho_zz to time level 1 in place (3748), so
+    # rqvdynten differences against that updated level -- time level 2 of the dump after the shift
+    q1, q2 = c[2]["state.scalars.tl2"][..., 0], c[2]["state.scalars.tl1"][..., 0]
+    rqv = c[2]["tend_physics.rqvdynten"]
+    pos = q2 > 0  # where the clip did not act, rqvdynten is the exact difference quotient
+    assert (~pos).any() and pos.any()
+    assert np.array_equal(rqv[pos], ((q2 - q1) / dt)[pos])
