@@ -219,7 +219,7 @@ def main():
     achieved = b_ac / t_kern / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "acoustic_traffic.json")
-    if os.path.isfile(tf):
+    if os.path.isfile(tf) and nparts == 1:  # the PMC figures are for the whole mesh as one block
         try:
             with open(tf) as f:
                 tj = json.load(f)

@@ -786,21 +786,22 @@ double coef_divdamp(const mpas_dyc_ctx* ctx, double dts) {  // 2761-2763
 }
 
 // edge phase of acoustic sub-step `small_step`; damp = 1 also applies the divergence damping of
-// the previous sub-step (k_acoustic_edges<true>)
+// the previous sub-step (k_acoustic_edges<true>); fresh = 1 when that sub-step was sub-step 1,
+// whose edge phase is not launched (its ru_p = ruAvg = dts * tend_u are formed by the readers)
 void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int damp,
-                    int phase) {
+                    int phase, int fresh = 0) {
   if (pair_layout(d)) {
     const int64_t nw = (d.nEdges + 1) / 2;
     if (damp)
-      LAUNCH_E(k_acoustic_edges_p<true>, nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase);
+      LAUNCH_E(k_acoustic_edges_p<true>, nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh);
     else
-      LAUNCH_E(k_acoustic_edges_p<false>, nw, d, p, dts, small_step, 0.0, phase);
+      LAUNCH_E(k_acoustic_edges_p<false>, nw, d, p, dts, small_step, 0.0, phase, fresh);
     return;
   }
   if (damp)
-    LAUNCH_E(k_acoustic_edges<true>, d.nEdges, d, p, dts, small_step, coef_divdamp(ctx, dts), phase);
+    LAUNCH_E(k_acoustic_edges<true>, d.nEdges, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh);
   else
-    LAUNCH_E(k_acoustic_edges<false>, d.nEdges, d, p, dts, small_step, 0.0, phase);
+    LAUNCH_E(k_acoustic_edges<false>, d.nEdges, d, p, dts, small_step, 0.0, phase, fresh);
 }
 
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
@@ -815,10 +816,12 @@ void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
 }
 
-void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase) {
+// fresh = 1: the stage had a single sub-step (no edge phase launched), see k_divdamp_p
+void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase, int fresh = 0) {
   // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
-  if (pair_layout(d)) LAUNCH_E(k_divdamp_p, (d.nEdges + 1) / 2, d, p, coef_divdamp(ctx, dts), phase);
-  else LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase);
+  if (pair_layout(d)) LAUNCH_E(k_divdamp_p, (d.nEdges + 1) / 2, d, p, coef_divdamp(ctx, dts), phase, dts, fresh);
+  else LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase,
+              dts, fresh);
 }
 
 void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt, int tl, int rk_step /*0 = absent*/) {
@@ -1016,16 +1019,21 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       // * Damping.  The divergence damping of sub-step n (849-869) is fused into the edge phase
       //   of sub-step n+1 (k_acoustic_edges<true>).  Only the last sub-step's damping is a
       //   kernel of its own.
+      // * Sub-step 1's edge phase (794-837 with small_step = 1) only sets ru_p = ruAvg =
+      //   dts * tend_u on the edges with an owned cell.  It is not launched: its three readers
+      //   form that product themselves -- the cell phase of sub-step 1, then either the damped
+      //   edge phase of sub-step 2 or, for a one-sub-step stage, the damping, which also stores
+      //   ruAvg (on the same edges, so the 876 exchange and the recovery see the same values).
       const int nsub = number_sub_steps[rk_step - 1];
       for (int small_step = 1; small_step <= nsub; ++small_step) {
         if (small_step == 1) {
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 0, 0));   // 794-837
+          // 794-837: formed by the readers (above)
         } else if (split) {  // interior edges overlap the exchange issued after the last cell phase
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 1));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 1, small_step == 2));
           CHK(exchange_wait(ctx));
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 2));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 2, small_step == 2));
         } else {
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2));
         }
         EACH(acoustic_cells(ctx, d, p, dts, small_step));
         std::vector<XField> xf = {{"diag", "rtheta_pp", 0, 0x1u}};  // 845
@@ -1037,11 +1045,11 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         }
       }
       if (split) {  // the last sub-step's damping (849-869), interior edges overlapping the exchange
-        EACH(divergence_damping(ctx, d, p, dts, 1));
+        EACH(divergence_damping(ctx, d, p, dts, 1, nsub == 1));
         CHK(exchange_wait(ctx));
-        EACH(divergence_damping(ctx, d, p, dts, 2));
+        EACH(divergence_damping(ctx, d, p, dts, 2, nsub == 1));
       } else {
-        EACH(divergence_damping(ctx, d, p, dts, 0));
+        EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1));
       }
       const std::vector<XField> xrec = {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},  // 876-887
                                         {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};

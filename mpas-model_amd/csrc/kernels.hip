@@ -1489,9 +1489,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert_b(Dims d, Ptrs p
 // rho_pp halo exchange in between, so one pass over ru_p does both.  The sum is the same
 // double either way: the damped ru_p is rounded before the update adds to it.
 // phase: 0 = every edge; 1 / 2 = edges without / with a halo cell (split around that exchange).
+// fresh = 1: the previous sub-step was sub-step 1, whose edge phase srk3 no longer launches:
+// its ru_p and ruAvg are dts * tend_u (794-837 with small_step = 1), formed here from tend_u.
 template <bool DD>
 __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges(Dims d, Ptrs p, double dts, int small_step,
-                                                                  double coef_divdamp, int phase) {
+                                                                  double coef_divdamp, int phase, int fresh) {
   const int e = wave_elem_e();
   if (e >= d.nEdges) return;
   const int k = lane_id(), K = d.K;
@@ -1510,8 +1512,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges(Dims d, Ptrs p,
     }
     return;
   }
-  double rup = p.ru_p[o];
-  const double rua = p.ruAvg[o], cqu = p.cqu[o], zxu = p.zxu[o];
+  double rup = fresh ? dts * tu : p.ru_p[o];
+  const double rua = fresh ? rup : p.ruAvg[o], cqu = p.cqu[o], zxu = p.zxu[o];
   const double mask = p.specZoneMaskEdge[e], invDc = p.invDcEdge[e];
   if (!(ce.x < d.nCellsSolve || ce.y < d.nCellsSolve) || (phase && ((bnd != 0) != (phase == 2)))) return;
   const int c1 = uni(ce.x), c2 = uni(ce.y);
@@ -1928,7 +1930,10 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
 }
 
 // k_divdamp in the pair layout
-__global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase) {
+// fresh = 1: the stage has one sub-step, whose edge phase srk3 does not launch, so ru_p enters as
+// dts * tend_u and ruAvg (= the same value, 794-837 with small_step = 1) is stored here.
+__global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
+                                                            int fresh) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
@@ -1940,7 +1945,13 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
   const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
   const int bA = phase ? p.edge_bnd[eA] : 0, bB = phase ? p.edge_bnd[eB] : 0;
-  const d2 ru = ld2(p.ru_p + o);
+  d2 ru;
+  if (fresh) {
+    const d2 tu = ld2(p.tend_u + o);
+    ru = d2{dts * tu.x, dts * tu.y};
+  } else {
+    ru = ld2(p.ru_p + o);
+  }
   const double mask = sel(h, ld_uniform_f64(p.specZoneMaskEdge + eA), ld_uniform_f64(p.specZoneMaskEdge + eB));
   auto active = [&](int2 ce, int bnd) {
     return (ce.x < d.nCellsSolve || ce.y < d.nCellsSolve) && (phase == 0 || ((bnd != 0) == (phase == 2)));
@@ -1954,7 +1965,10 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   d2 out;
   out.x = ru.x + coef_divdamp * (-(r2.x - q2.x) - -(r1.x - q1.x)) * (1.0 - mask) / (t1.x + t2.x);
   out.y = ru.y + coef_divdamp * (-(r2.y - q2.y) - -(r1.y - q1.y)) * (1.0 - mask) / (t1.y + t2.y);
-  if ((h ? onB : onA) && 2 * l < K) st2(p.ru_p + o, out);
+  if ((h ? onB : onA) && 2 * l < K) {
+    st2(p.ru_p + o, out);
+    if (fresh) st2(p.ruAvg + o, ru);
+  }
 }
 
 // k_scalars_edges in the pair layout (atm_advance_scalars_work, 3357-3426)
@@ -2182,7 +2196,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs 
 // k_acoustic_edges in the pair layout (same expressions, per level)
 template <bool DD>
 __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,
-                                                                   double coef_divdamp, int phase) {
+                                                                   double coef_divdamp, int phase, int fresh) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const int eB = min(eA + 1, d.nEdges - 1);
@@ -2209,8 +2223,15 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
     }
     return;
   }
-  d2 rup = ld2(p.ru_p + o);
-  const d2 rua = ld2(p.ruAvg + o), cqu = ld2(p.cqu + o), zxu = ld2(p.zxu + o);
+  d2 rup, rua;
+  if (fresh) {  // sub-step 1 left ru_p = ruAvg = dts * tend_u (see k_acoustic_edges)
+    rup = d2{dts * tu.x, dts * tu.y};
+    rua = rup;
+  } else {
+    rup = ld2(p.ru_p + o);
+    rua = ld2(p.ruAvg + o);
+  }
+  const d2 cqu = ld2(p.cqu + o), zxu = ld2(p.zxu + o);
   const double mask = sel(h, ld_uniform_f64(p.specZoneMaskEdge + eA), ld_uniform_f64(p.specZoneMaskEdge + eB));
   const double invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
   const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
@@ -2281,10 +2302,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
   double rhopp = p.rho_pp[o], rwp = p.rw_p[ow], wwa = p.wwAvg[ow];
   const double thc = p.theta_m1[o], trho = p.tend_rho[o], tth = p.tend_theta[o], tw = p.tend_w[ow];
   double ru[ME], th[ME];
+  // sub-step 1: ru_p = dts * tend_u (794-837), formed here; srk3 launches no edge phase for it
+  const double* __restrict__ rusrc = small_step == 1 ? p.tend_u : p.ru_p;
 #pragma unroll
   for (int i = 0; i < ME; ++i) {
-    ru[i] = p.ru_p[(size_t)re[i] * K + kc];
+    ru[i] = rusrc[(size_t)re[i] * K + kc];
     th[i] = p.theta_m1[(size_t)rc[i] * K + kc];
+  }
+  if (small_step == 1) {
+#pragma unroll
+    for (int i = 0; i < ME; ++i) ru[i] = dts * ru[i];
   }
   const double coftz = p.coftz[ow], zz = p.zz[o], cofwt = p.cofwt[o], cofwz = p.cofwz[o], cofwr = p.cofwr[o];
   const double a_tri = p.a_tri[o], alpha_tri = p.alpha_tri[o], gamma_tri = p.gamma_tri[o];
@@ -2382,7 +2409,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p
       const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
       const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
       if (act) {
-        const double flux = p.edgesOnCell_sign[c * d.maxEdges + i] * dts * p.dvEdge[e] * p.ru_p[(size_t)e * K + k] * invA;
+        // sub-step 1: ru_p = dts * tend_u (794-837), formed here (no edge phase is launched for it)
+        const double rue = small_step == 1 ? dts * p.tend_u[(size_t)e * K + k] : p.ru_p[(size_t)e * K + k];
+        const double flux = p.edgesOnCell_sign[c * d.maxEdges + i] * dts * p.dvEdge[e] * rue * invA;
         rs = rs - flux;
         const double th1 = (c1 == c) ? thc : p.theta_m1[(size_t)c1 * K + k];
         const double th2 = (c2 == c) ? thc : p.theta_m1[(size_t)c2 * K + k];
@@ -2456,7 +2485,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p
 // EPW edges is issued before the first store, so each wave keeps EPW x 7 column loads
 // in flight (the kernel is latency x occupancy bound with one edge per wave).
 template <int EPW>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, double coef_divdamp, int phase) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
+                                                           int fresh) {  // fresh: see k_divdamp_p
   const int e0 = wave_elem(0) * EPW;
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
@@ -2472,7 +2502,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, doubl
               (phase == 0 || ((p.edge_bnd[e] != 0) == (phase == 2)));  // 1 / 2: edges without / with a halo cell
       if (on[j] && act) {
         const size_t o = (size_t)e * K + k, o1 = (size_t)c1 * K + k, o2 = (size_t)c2 * K + k;
-        ru[j] = p.ru_p[o];
+        ru[j] = fresh ? dts * p.tend_u[o] : p.ru_p[o];
         d1[j] = -(p.rtheta_pp[o1] - p.rtheta_pp_old[o1]);
         d2[j] = -(p.rtheta_pp[o2] - p.rtheta_pp_old[o2]);
         th[j] = p.theta_m1[o1] + p.theta_m1[o2];
@@ -2482,8 +2512,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, doubl
   }
 #pragma unroll
   for (int j = 0; j < EPW; ++j) {
-    if (on[j] && act)
+    if (on[j] && act) {
       p.ru_p[(size_t)(e0 + j) * K + k] = ru[j] + coef_divdamp * (d2[j] - d1[j]) * (1.0 - mask[j]) / th[j];
+      if (fresh) p.ruAvg[(size_t)(e0 + j) * K + k] = ru[j];
+    }
   }
 }
 
