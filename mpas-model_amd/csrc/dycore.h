@@ -60,6 +60,7 @@ struct Ptrs {
   const double *edgesOnCell_sign, *edgesOnVertex_sign, *kiteAreasOnVertex, *weightsOnEdge;
   const double *adv_coefs, *adv_coefs_3rd, *defc_a, *defc_b;
   const double *zgrid, *zz, *zxu, *dss, *zb_cell, *zb3_cell;
+  const double *zb_p, *zb_m;  // scratch: zb_cell + zb3_cell and zb_cell - zb3_cell (k_build_zb)
   const double *u_init, *v_init, *t_init, *angleEdge;
   const double *latCell, *lonCell, *coeffs_reconstruct;
   double cf1, cf2, cf3;

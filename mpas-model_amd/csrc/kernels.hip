@@ -150,6 +150,19 @@ __device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, 
 #define PHYS(arr, i) (d.physics ? (arr)[(i)] : 0.0)
 #define LDW(p, i) (actw ? (p)[(i)] : 0.0)
 
+// zb_p = zb_cell + zb3_cell, zb_m = zb_cell - zb3_cell.  The reference forms
+// zb_cell + sign(1,flux) * zb3_cell (2299, 3085) with sign(1,flux) = +-1, whose product is exact,
+// so the sum is one of these two doubles bit for bit.  The w-flux kernels then load only the one
+// their flux sign selects: the sign is mostly uniform down a column, so a wave touches the cache
+// lines of one array instead of both (8 B instead of 16 B per cell-edge-level).
+__global__ void k_build_zb(int64_t n, const double* __restrict__ zb, const double* __restrict__ zb3,
+                           double* __restrict__ zp, double* __restrict__ zm) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    zp[i] = zb[i] + 1.0 * zb3[i];
+    zm[i] = zb[i] + -1.0 * zb3[i];
+  }
+}
+
 // Per-cell stencil records (dycore.h, Ptrs::cell_rec / cell_sdv), one thread per cell.  The
 // cell across edge i is the other entry of cellsOnEdge, exactly the operand the reference
 // loops pick with their cellsOnEdge(1/2,iEdge) tests.  cell_sdv = edgesOnCell_sign * dvEdge:
@@ -1453,13 +1466,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert_b(Dims d, Ptrs p
   const size_t K1 = K + 1;
   const int bnd = phase ? p.cell_bnd[c] : 0;
   const CellSten<ME> st = load_sten<ME>(p, c);
-  double zb[ME], zb3[ME];
-#pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    const size_t zo = ((size_t)c * ME + i) * K1 + kw;
-    zb[i] = p.zb_cell[zo];
-    zb3[i] = p.zb3_cell[zo];
-  }
   double wt = p.tend_w[(size_t)c * K1 + kw];
   const double zz = p.zz[(size_t)c * K + kc];
   const double fzm = p.fzm[kc], fzp = p.fzp[kc];
@@ -1467,12 +1473,16 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert_b(Dims d, Ptrs p
   double ut[ME];
 #pragma unroll
   for (int i = 0; i < ME; ++i) ut[i] = p.tend_u[(size_t)uni(st.e[i]) * K + kc];
+  // zb_cell + sign(1,ut) * zb3_cell, loaded as the one of zb_p / zb_m the sign selects (k_build_zb)
+  double zs[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) zs[i] = (sgn1(ut[i]) > 0.0 ? p.zb_p : p.zb_m)[((size_t)c * ME + i) * K1 + kw];
 #pragma unroll
   for (int i = 0; i < ME; ++i) {
     const double utm = up1(ut[i]);
     if (i < st.ne && act && k >= 1) {
       const double flux = st.sg(i) * (fzm * ut[i] + fzp * utm);
-      wt = wt - (zb[i] + sgn1(ut[i]) * zb3[i]) * flux;
+      wt = wt - zs[i] * flux;
     }
   }
   const double zzm = up1(zz);
@@ -1853,7 +1863,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
 template <int NE2>
 __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, const double* __restrict__ u,
                                                                const double* __restrict__ hh, int reconstruct_v,
-                                                               double apvm, double dt) {
+                                                               double apvm, double dt, int store_grad) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
@@ -1919,7 +1929,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
     const double r2 = 1.0 * invDc;
     const d2 gt{(pv2.x - pv1.x) * r1, (pv2.y - pv1.y) * r1};
     const d2 gn{(pc2.x - pc1.x) * r2, (pc2.y - pc1.y) * r2};
-    if (st) {
+    if (st && store_grad) {
       st2(p.gradPVt + o, gt);
       st2(p.gradPVn + o, gn);
     }
@@ -2691,7 +2701,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells(Dims d, Ptrs p, co
 
 __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges(Dims d, Ptrs p, const double* __restrict__ u,
                                                                const double* __restrict__ h, int reconstruct_v,
-                                                               double apvm, double dt) {
+                                                               double apvm, double dt, int store_grad) {
   const int e = wave_elem(0);
   if (e >= d.nEdges) return;
   const int k = lane_id(), K = d.K;
@@ -2729,8 +2739,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges(Dims d, Ptrs p, co
     const double r2 = 1.0 * p.invDcEdge[e];
     const double gt = (pv2 - pv1) * r1;
     const double gn = (p.pv_cell[(size_t)c2 * K + k] - p.pv_cell[(size_t)c1 * K + k]) * r2;
-    p.gradPVt[o] = gt;
-    p.gradPVn[o] = gn;
+    if (store_grad) {  // see solve_diagnostics: only the last call of a dt stores them
+      p.gradPVt[o] = gt;
+      p.gradPVn[o] = gn;
+    }
     pve = pve - r * (vv * gt + u[o] * gn);
   }
   p.pv_edge[o] = pve;
@@ -2749,14 +2761,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs
   const int bnd = phase ? p.cell_bnd[c] : 0;
   const int ne = p.nEdgesOnCell[c];
   int ei[ME];
-  double sg[ME], zb[ME], zb3[ME];
+  double sg[ME];
 #pragma unroll
   for (int i = 0; i < ME; ++i) {
     ei[i] = p.edgesOnCell[(size_t)c * ME + i];
     sg[i] = ld_uniform_f64(p.edgesOnCell_sign + (size_t)c * ME + i);
-    const size_t zo = ((size_t)c * ME + i) * K1 + kw;
-    zb[i] = p.zb_cell[zo];
-    zb3[i] = p.zb3_cell[zo];
   }
   double w = p.w2[ow];
   const double rz = p.rho_zz2[o];
@@ -2766,20 +2775,21 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs
 #pragma unroll
   for (int i = 0; i < ME; ++i) ru[i] = p.ru[(size_t)uni(ei[i]) * K + kc];
   if (!act) w = 0.0;
+  // the vertical flux of each edge, then zb_cell + sign(1,flux) * zb3_cell as the one of
+  // zb_p / zb_m the sign selects (k_build_zb)
+  double fl[ME], zs[ME];
 #pragma unroll
   for (int i = 0; i < ME; ++i) {
     const double ruk = ru[i];
     const double rum = up1(ruk);
     const double ru1 = readlane_d(ruk, 0), ru2 = readlane_d(ruk, 1), ru3 = readlane_d(ruk, 2);
-    if (i < ne) {
-      if (k == 0) {
-        const double flux = (p.cf1 * ru1 + p.cf2 * ru2 + p.cf3 * ru3);
-        w = w + sg[i] * (zb[i] + sgn1(flux) * zb3[i]) * flux;
-      } else if (act) {
-        const double flux = (fzm * ruk + fzp * rum);
-        w = w + sg[i] * (zb[i] + sgn1(flux) * zb3[i]) * flux;
-      }
-    }
+    fl[i] = (k == 0) ? (p.cf1 * ru1 + p.cf2 * ru2 + p.cf3 * ru3) : (fzm * ruk + fzp * rum);
+  }
+#pragma unroll
+  for (int i = 0; i < ME; ++i) zs[i] = (sgn1(fl[i]) > 0.0 ? p.zb_p : p.zb_m)[((size_t)c * ME + i) * K1 + kw];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    if (i < ne && (k == 0 || act)) w = w + sg[i] * zs[i] * fl[i];
   }
   const double rzm = up1(rz);
   const double r1 = readlane_d(rz, 0), r2 = readlane_d(rz, 1), r3 = readlane_d(rz, 2);
@@ -2847,7 +2857,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells_b(Dims d, Ptrs p, 
 template <int NE2>
 __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_b(Dims d, Ptrs p, const double* __restrict__ u,
                                                                 const double* __restrict__ h, int reconstruct_v,
-                                                                double apvm, double dt) {
+                                                                double apvm, double dt, int store_grad) {
   const int e = wave_elem_e();
   if (e >= d.nEdges) return;
   const int k = lane_id(), K = d.K;
@@ -2901,8 +2911,10 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_b(Dims d, Ptrs p, c
     const double r2 = 1.0 * invDc;
     const double gt = (pv2 - pv1) * r1;
     const double gn = (pc2 - pc1) * r2;
-    p.gradPVt[o] = gt;
-    p.gradPVn[o] = gn;
+    if (store_grad) {  // see solve_diagnostics: only the last call of a dt stores them
+      p.gradPVt[o] = gt;
+      p.gradPVn[o] = gn;
+    }
     pve = pve - r * (vv * gt + ue * gn);
   }
   p.pv_edge[o] = pve;
