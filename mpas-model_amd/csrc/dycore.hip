@@ -816,13 +816,21 @@ void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
     LAUNCH_E(k_acoustic_edges<false>, d.nEdges, d, p, dts, small_step, 0.0, phase, fresh);
 }
 
-void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step) {
+// the record kernels fuse the owned cells' recover_cells1 into a stage's last sub-step
+bool fused_recover(const Dims& d) { return batched(d) && (d.maxEdges == 6 || d.maxEdges == 7); }
+
+// fin = 1: the stage's last sub-step, which also recovers the owned cells (k_acoustic_cells_r<ME,
+// true>) when fused_recover(d); rdt / invNs / rk_step are k_recover_cells1's arguments
+void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int fin = 0,
+                    double rdt = 0.0, double invNs = 0.0, int rk_step = 0) {
   if (batched(d) && d.maxEdges == 6) {
-    LAUNCH(k_acoustic_cells_r<6>, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
+    if (fin) LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step);
+    else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0);
     return;
   }
   if (batched(d) && d.maxEdges == 7) {
-    LAUNCH(k_acoustic_cells_r<7>, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
+    if (fin) LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step);
+    else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0);
     return;
   }
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
@@ -1052,7 +1060,8 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         } else {
           EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2));
         }
-        EACH(acoustic_cells(ctx, d, p, dts, small_step));
+        EACH(acoustic_cells(ctx, d, p, dts, small_step, small_step == nsub, rk_timestep[rk_step - 1],
+                            1 / (double)nsub, rk_step));
         std::vector<XField> xf = {{"diag", "rtheta_pp", 0, 0x1u}};  // 845
         if (small_step < nsub) xf.push_back({"diag", "rho_pp", 0, 0x1u});  // 792 of the next sub-step
         if (split) {
@@ -1076,17 +1085,21 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         // 889-1185: owned cells and interior edges overlap the 876-887 exchange; once every
         // owned u is final, the u exchange (988) overlaps the w recovery, which does not read u
         CHK(exchange_async(ctx, xrec));
-        EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 1));
+        // owned cells: recovered by the last sub-step's cell phase (fused_recover) or here
+        EACH(if (!fused_recover(d)) LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 1, 0));
         EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1));
         CHK(exchange_wait(ctx));
-        EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 2));
+        EACH(LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2, d.nCellsSolve));
         EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
         CHK(exchange_async(ctx, {{"state", "u", 2, ALL_LAYERS}}));
         EACH(recover_cells3(ctx, d, p, 0));
         CHK(exchange_wait(ctx));
       } else {
         CHK((exchange)(ctx, xrec));
-        EACH(LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0));  // 889-930
+        // 889-930: the owned cells were recovered by the last sub-step if fused_recover
+        EACH(if (fused_recover(d)) LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2,
+                                          d.nCellsSolve);
+             else LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0, 0));
         EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0));
         EACH(recover_cells3(ctx, d, p, 0));
         CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));      // 988

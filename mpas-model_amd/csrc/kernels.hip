@@ -2284,9 +2284,61 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
 // column needs -- the record, its own 22 columns, the ru_p of its edges and theta_m of the cells
 // across them -- is issued before the first use, so one wave waits for two memory round trips
 // (record, then gathers) instead of a chain per edge.  Same expressions, same order as below.
-template <int ME>
+// recover_cells1 (2998-3040) of owned cell c from the final sub-step's new rho_pp / rtheta_pp /
+// rw_p / wwAvg, still in registers (k_acoustic_cells_r<ME, true>): the same expressions as
+// k_recover_cells1, lane for lane (inactive lanes see zz = fzm = fzp = 0 there too).
+__device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p, int c, int k, double zz_k, double rws,
+                                                   double rhopp, double rtpp, double rwp, double wwa, double dt,
+                                                   double invNs, int rk_step) {
+  const int K = d.K;
+  const size_t K1 = K + 1;
+  const bool act = k < K;
+  const int kc = min(k, K - 1), kw = min(k, K);
+  const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
+  const double rcv = RGAS / (CP - RGAS);
+  const double rps = p.rho_p_save[o], rb = p.rho_base[o];
+  const double rtps = p.rtheta_p_save[o], rtb = p.rtheta_base[o];
+  const double fzm = act ? p.fzm[kc] : 0.0, fzp = act ? p.fzp[kc] : 0.0;
+  const double zz = act ? zz_k : 0.0, zzm = up1(zz);
+  double rz = 0.0;
+  if (act) {
+    const double rho_p = rps + rhopp;
+    p.rho_p[o] = rho_p;
+    rz = rho_p + rb;
+    p.rho_zz2[o] = rz;
+  }
+  double w = 0.0;  // w(1) = w(nVertLevels+1) = 0
+  if (act && k >= 1) {
+    p.wwAvg[ow] = rws + (wwa * invNs);
+    const double rw = rws + rwp;
+    p.rw[ow] = rw;
+    w = rw / (fzm * zz + fzp * zzm);  // divided by density in k_recover_cells3
+  }
+  if (k <= K) p.w2[ow] = w;
+  if (act) {
+    if (rk_step == 3) {
+      const double rtp = rtps + rtpp - dt * rz * (d.diabatic ? p.rt_diabatic_tend[o] : 0.0);
+      p.rtheta_p[o] = rtp;
+      p.theta_m2[o] = (rtp + rtb) / rz;
+      const double ex = pow(zz * (RGAS / P0) * (rtp + rtb), rcv);
+      p.exner[o] = ex;
+      p.pressure_p[o] = zz * RGAS * (ex * rtp + rtb * (ex - p.exner_base[o]));
+    } else {
+      const double rtp = rtps + rtpp;
+      p.rtheta_p[o] = rtp;
+      p.theta_m2[o] = (rtp + rtb) / rz;
+    }
+  }
+}
+
+// FIN: the stage's last sub-step also recovers its owned cells (recover_cell_fused): nothing
+// between this launch and k_recover_cells1 -- the Theta''/rho'' exchange, the damping (ru_p,
+// ruAvg) and the 876-887 exchange -- reads or writes what the recovery reads or writes for an
+// owned cell, so k_recover_cells1 then runs on the halo cells and the garbage slot only.
+template <int ME, bool FIN = false>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs p, double dts, int small_step,
-                                                                    double epssm) {
+                                                                    double epssm, double rdt = 0.0,
+                                                                    double invNs = 0.0, int rk_step = 0) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
   const int k = lane_id(), K = d.K;
@@ -2367,15 +2419,19 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       wwa = wwa + 0.5 * (1.0 + epssm) * rwp;
     }
     const double rwp_p2 = dn1(rwp);
+    const double rho_new = rs - cofrz * (rwp_p2 - rwp);
+    const double rt_new = ts - rdzw * (coftz_p * rwp_p2 - coftz * rwp);
     if (act) {
       p.rtheta_pp_old[o] = rtpp_old;  // stored last: no store precedes the loads above
-      p.rho_pp[o] = rs - cofrz * (rwp_p2 - rwp);
-      p.rtheta_pp[o] = ts - rdzw * (coftz_p * rwp_p2 - coftz * rwp);
+      p.rho_pp[o] = rho_new;
+      p.rtheta_pp[o] = rt_new;
     }
     if (actw) {
       p.rw_p[ow] = rwp;
-      p.wwAvg[ow] = wwa;
+      if (!FIN) p.wwAvg[ow] = wwa;
+      else if (k == 0 || k == K) p.wwAvg[ow] = wwa;  // levels 2..K: recover_cell_fused
     }
+    if (FIN) recover_cell_fused(d, p, c, k, zz, rws, rho_new, rt_new, rwp, wwa, rdt, invNs, rk_step);
   } else {
     // specified zone (2710-2719): regional only, masks are 0 for global meshes
     if (act) {
@@ -2389,8 +2445,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
     }
     if (actw) {
       p.rw_p[ow] = rwp;
-      p.wwAvg[ow] = wwa;
+      if (!FIN) p.wwAvg[ow] = wwa;
+      else if (k == 0 || k == K) p.wwAvg[ow] = wwa;
     }
+    if (FIN) recover_cell_fused(d, p, c, k, zz, rws, rhopp, rtpp, rwp, wwa, rdt, invNs, rk_step);
   }
 }
 
@@ -2537,8 +2595,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, doubl
 // ============================================================================
 // cells (all, and the garbage slot): 2998-3040
 __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p, double dt, double invNs, int rk_step,
-                                                                  int phase) {
-  const int c = wave_elem(0);
+                                                                  int phase, int c0) {
+  const int c = wave_elem(c0);
   if (phase && ((c >= d.nCellsSolve) != (phase == 2))) return;
   const int k = lane_id(), K = d.K;
   const size_t K1 = K + 1;

@@ -281,6 +281,11 @@ def _cells_vertices_ccw(p, f, width=None):
 
 
 def _topology_and_geometry(p, f, radius):
+    # vertex (triangle) order: by the sorted cell triple, like the edges' (first cell, second
+    # cell) order below, so vertices follow the cells' Hilbert order too -- the vertex gathers
+    # of the diagnostics (edgesOnVertex, verticesOnCell, verticesOnEdge) stay local in memory
+    fs = np.sort(f, axis=1)
+    f = f[np.lexsort((fs[:, 2], fs[:, 1], fs[:, 0]))]
     nC, nV = len(p), len(f)
     xv = _circumcenters(p, f)
     nEoC, voc = _cells_vertices_ccw(p, f)
