@@ -53,6 +53,7 @@ struct Block {
   std::map<std::string, int> by_name;  // "pool.name"
   std::vector<XList> xl;
   int64_t nEdges_act = -1;             // edges with an owned cell (from cellsOnEdge), for B_ac
+  int64_t n_bnd_edges = -1;            // edges with a halo (or garbage) cell, from compute_bnd
   std::vector<int32_t> h_coe, h_eoc, h_noc;  // host copies (0-based) for the halo-boundary flags
 };
 
@@ -600,8 +601,11 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
       return MPAS_DYC_ESTATE;
     }
     std::vector<int32_t> eb(d.nEdges + 1, 1), cb(d.nCells + 1, 1);
-    for (int e = 0; e < d.nEdges; ++e)
+    b.n_bnd_edges = 0;
+    for (int e = 0; e < d.nEdges; ++e) {
       eb[e] = (b.h_coe[2 * e] >= d.nCellsSolve || b.h_coe[2 * e + 1] >= d.nCellsSolve) ? 1 : 0;
+      b.n_bnd_edges += eb[e];
+    }
     for (int c = 0; c < d.nCells; ++c) {
       int bnd = c >= d.nCellsSolve ? CELL_HALO_EDGE | CELL_BND_EDGE : 0;
       for (int i = 0; i < b.h_noc[c]; ++i) {
@@ -836,10 +840,18 @@ void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
 }
 
-// fresh = 1: the stage had a single sub-step (no edge phase launched), see k_divdamp_p
-void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase, int fresh = 0) {
+// the last damping of a stage also recovers the edges with two owned cells (k_divdamp_p<true>);
+// needs the owned cells' rho_zz recovered by the last cell phase (fused_recover)
+bool fused_recover_edges(const Dims& d) { return pair_layout(d) && fused_recover(d); }
+
+// fresh = 1: the stage had a single sub-step (no edge phase launched), see k_divdamp_p;
+// invNs > 0: recover the edges with two owned cells too (fused_recover_edges)
+void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase, int fresh = 0,
+                        double invNs = 0.0) {
   // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
-  if (pair_layout(d)) LAUNCH_E(k_divdamp_p, (d.nEdges + 1) / 2, d, p, coef_divdamp(ctx, dts), phase, dts, fresh);
+  if (pair_layout(d) && invNs > 0.0 && fused_recover_edges(d))
+    LAUNCH_E(k_divdamp_p<true>, (d.nEdges + 1) / 2, d, p, coef_divdamp(ctx, dts), phase, dts, fresh, invNs);
+  else if (pair_layout(d)) LAUNCH_E(k_divdamp_p<false>, (d.nEdges + 1) / 2, d, p, coef_divdamp(ctx, dts), phase, dts, fresh, 0.0);
   else LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase,
               dts, fresh);
 }
@@ -1071,11 +1083,11 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         }
       }
       if (split) {  // the last sub-step's damping (849-869), interior edges overlapping the exchange
-        EACH(divergence_damping(ctx, d, p, dts, 1, nsub == 1));
+        EACH(divergence_damping(ctx, d, p, dts, 1, nsub == 1, 1 / (double)nsub));
         CHK(exchange_wait(ctx));
         EACH(divergence_damping(ctx, d, p, dts, 2, nsub == 1));
       } else {
-        EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1));
+        EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1, 1 / (double)nsub));
       }
       const std::vector<XField> xrec = {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},  // 876-887
                                         {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};
@@ -1087,10 +1099,12 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         CHK(exchange_async(ctx, xrec));
         // owned cells: recovered by the last sub-step's cell phase (fused_recover) or here
         EACH(if (!fused_recover(d)) LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 1, 0));
-        EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1));
+        // edges with two owned cells: recovered by the last damping (fused_recover_edges) or here
+        EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1));
         CHK(exchange_wait(ctx));
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2, d.nCellsSolve));
-        EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
+        EACH(if (!fused_recover_edges(d) || ctx->blk[ib_].n_bnd_edges != 0)
+               LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
         CHK(exchange_async(ctx, {{"state", "u", 2, ALL_LAYERS}}));
         EACH(recover_cells3(ctx, d, p, 0));
         CHK(exchange_wait(ctx));
@@ -1100,7 +1114,9 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         EACH(if (fused_recover(d)) LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2,
                                           d.nCellsSolve);
              else LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0, 0));
-        EACH(LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0));
+        // the edges with two owned cells were recovered by the last damping if fused_recover_edges
+        EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0);
+             else if (ctx->blk[ib_].n_bnd_edges != 0) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
         EACH(recover_cells3(ctx, d, p, 0));
         CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));      // 988
       }

@@ -1942,8 +1942,14 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
 // k_divdamp in the pair layout
 // fresh = 1: the stage has one sub-step, whose edge phase srk3 does not launch, so ru_p enters as
 // dts * tend_u and ruAvg (= the same value, 794-837 with small_step = 1) is stored here.
+// REC: the stage's last damping also recovers the edges with two owned cells (recover_edges,
+// 3048-3059): their rho_zz at both cells was recovered by the last cell phase
+// (k_acoustic_cells_r<ME, true>), and nothing between here and k_recover_edges -- the 876-887
+// exchange, k_recover_cells1 on halo cells -- touches ru_save, ruAvg, ru or u there.
+// k_recover_edges then runs on the other edges (phase 2).
+template <bool REC = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
-                                                            int fresh) {
+                                                            int fresh, double invNs = 0.0) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
@@ -1975,9 +1981,28 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   d2 out;
   out.x = ru.x + coef_divdamp * (-(r2.x - q2.x) - -(r1.x - q1.x)) * (1.0 - mask) / (t1.x + t2.x);
   out.y = ru.y + coef_divdamp * (-(r2.y - q2.y) - -(r1.y - q1.y)) * (1.0 - mask) / (t1.y + t2.y);
+  if (!REC) {
+    if ((h ? onB : onA) && 2 * l < K) {
+      st2(p.ru_p + o, out);
+      if (fresh) st2(p.ruAvg + o, ru);
+    }
+    return;
+  }
+  const bool rA = onA && (phase ? bA : p.edge_bnd[eA]) == 0;  // edges with two owned cells
+  const bool rB = onB && (phase ? bB : p.edge_bnd[eB]) == 0;
+  const d2 rs = ld2(p.ru_save + o);
+  const d2 ra = fresh ? ru : ld2(p.ruAvg + o);  // fresh: sub-step 1 left ruAvg = dts * tend_u
+  const d2 z1 = ld2(p.rho_zz2 + o1), z2 = ld2(p.rho_zz2 + o2);
   if ((h ? onB : onA) && 2 * l < K) {
     st2(p.ru_p + o, out);
-    if (fresh) st2(p.ruAvg + o, ru);
+    if (h ? rB : rA) {  // recover_edges (3048-3059), same expressions
+      st2(p.ruAvg + o, d2{rs.x + (ra.x * invNs), rs.y + (ra.y * invNs)});
+      const d2 rr{rs.x + out.x, rs.y + out.y};
+      st2(p.ru + o, rr);
+      st2(p.u2 + o, d2{2. * rr.x / (z1.x + z2.x), 2. * rr.y / (z1.y + z2.y)});
+    } else if (fresh) {
+      st2(p.ruAvg + o, ru);
+    }
   }
 }
 
