@@ -713,10 +713,14 @@ void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts)
 
 // part: 0 = all kernels; 1 = only k_dyn_cells1, which reads nothing the exchange after the
 // diagnostics (1234-1249) or at the substep boundary (1282-1297) delivers; 2 = the rest
-void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, double dt, int part = 0) {
+// hdiv_done: the previous stage's w recovery computed h_divergence (recover_cells3 with hdiv), so
+// at rk_step 2 / 3, where k_dyn_cells1 computes nothing else, it is not launched
+void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, double dt, int part = 0,
+              bool hdiv_done = false, bool last = true) {
   const Config& cf = ctx->cf;
   DynTendScal s{};
   s.rk_step = rk_step;
+  s.store_phys_diag = last ? 1 : 0;  // last: the dt's final dyn_tend
   s.dt = dt;
   s.invDt = 1.0 / dt;
   s.coef_3rd_order = cf.coef_3rd_order;
@@ -732,7 +736,7 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     s.rayleigh_coef_inverse = 1.0 / ((double)cf.number_rayleigh_damp_u_levels *
                                      (cf.rayleigh_damp_u_timescale_days * SECONDS_PER_DAY));
   const bool bt = batched(d), m6 = d.maxEdges == 6;
-  if (part != 2) {
+  if (part != 2 && !(hdiv_done && rk_step > 1)) {
     if (!bt) LAUNCH(k_dyn_cells1, d.nCells, d, p, cf, s);
     else if (m6) LAUNCH(k_dyn_cells1_b<6>, d.nCells, d, p, cf, s);
     else LAUNCH(k_dyn_cells1_b<7>, d.nCells, d, p, cf, s);
@@ -790,10 +794,11 @@ void smlstep_pert(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int phase) {
   else LAUNCH(k_smlstep_pert_b<7>, d.nCellsSolve, d, p, phase);
 }
 
-void recover_cells3(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int phase) {
+// hdiv = 1: the batched kernel also computes the next stage's h_divergence (k_recover_cells3_b)
+void recover_cells3(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int phase, int hdiv = 0) {
   if (!batched(d)) LAUNCH(k_recover_cells3, d.nCells, d, p, phase);
-  else if (d.maxEdges == 6) LAUNCH(k_recover_cells3_b<6>, d.nCells, d, p, phase);
-  else LAUNCH(k_recover_cells3_b<7>, d.nCells, d, p, phase);
+  else if (d.maxEdges == 6) LAUNCH(k_recover_cells3_b<6>, d.nCells, d, p, phase, hdiv);
+  else LAUNCH(k_recover_cells3_b<7>, d.nCells, d, p, phase, hdiv);
 }
 
 double coef_divdamp(const mpas_dyc_ctx* ctx, double dts) {  // 2761-2763
@@ -1027,13 +1032,14 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
     // 513 (exner): carried by the step-start exchange and by the 1282-1297 exchange below
     for (int rk_step = 1; rk_step <= 3; ++rk_step) {
       if (cf.time_integration_order == 3 && rk_step == 2) EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[1]));
+      const bool last_stage = dynamics_substep == dynamics_split && rk_step == 3;
       if (pending) {  // 561-630, k_dyn_cells1 overlapping the exchange
-        EACH(dyn_tend(ctx, d, p, rk_step, dt, 1));
+        EACH(dyn_tend(ctx, d, p, rk_step, dt, 1, !split && batched(d)));
         CHK(xwait());
         pending = false;
-        EACH(dyn_tend(ctx, d, p, rk_step, dt, 2));
+        EACH(dyn_tend(ctx, d, p, rk_step, dt, 2, false, last_stage));
       } else {
-        EACH(dyn_tend(ctx, d, p, rk_step, dt));                   // 561-630
+        EACH(dyn_tend(ctx, d, p, rk_step, dt, 0, !split && batched(d), last_stage));  // 561-630
       }
       const double dts = rk_sub_timestep[rk_step - 1];
       if (split) {  // 642 | 644-678: interior cells overlap the tend_u exchange
@@ -1117,7 +1123,8 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         // the edges with two owned cells were recovered by the last damping if fused_recover_edges
         EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0);
              else if (ctx->blk[ib_].n_bnd_edges != 0) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
-        EACH(recover_cells3(ctx, d, p, 0));
+        // stages 1 and 2: also the next stage's h_divergence (dyn_tend then skips k_dyn_cells1)
+        EACH(recover_cells3(ctx, d, p, 0, rk_step < 3));
         CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));      // 988
       }
       if (scalars_in_dynamics) {                                  // 993-1185

@@ -327,6 +327,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_vert_imp_coefs(Dims d, Ptrs p
 // ============================================================================
 struct DynTendScal {
   int rk_step;
+  // tend_rtheta_adv / rthdynten (5350-5351) are read only by the physics, after the step: every
+  // dyn_tend overwrites them, so only the last one of a dt stores them (store_phys_diag = 1)
+  int store_phys_diag;
   double dt, invDt, h_mom_eddy_visc4, h_theta_eddy_visc4, coef_3rd_order, c_s;
   double rayleigh_coef_inverse;
 };
@@ -1218,8 +1221,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3_r(Dims d, Ptrs p, 
   }
   if (act) {
     tt = tt * invA - rdzw_k * (wdtz_p - wdtz);
-    p.tend_rtheta_adv[o] = tt;
-    p.rthdynten[o] = tt / rz;
+    if (s.store_phys_diag) {
+      p.tend_rtheta_adv[o] = tt;
+      p.rthdynten[o] = tt / rz;
+    }
     tt = tt + rz * rtd;
     if (RK1) p.tend_theta_euler[o] = tte;
     p.tend_theta[o] = tt + tte + PHYS(p.tend_rtheta_physics, o);
@@ -1420,8 +1425,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3(Dims d, Ptrs p, Co
   if (act) {
     const double rz = p.rho_zz2[o];
     tt = tt * p.invAreaCell[c] - p.rdzw[k] * (wdtz_p - wdtz);
-    p.tend_rtheta_adv[o] = tt;
-    p.rthdynten[o] = tt / rz;
+    if (s.store_phys_diag) {
+      p.tend_rtheta_adv[o] = tt;
+      p.rthdynten[o] = tt / rz;
+    }
     tt = tt + rz * (d.diabatic ? p.rt_diabatic_tend[o] : 0.0);
     if (rk1) p.tend_theta_euler[o] = tte;
     p.tend_theta[o] = tt + tte + PHYS(p.tend_rtheta_physics, o);
@@ -2832,8 +2839,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_edges(Dims d, Ptrs p, co
 }
 
 // batched variants of the recover / diagnostics kernels (maxEdges <= 7, see k_acoustic_cells_r)
+// hdiv = 1: also the next stage's h_divergence (4729-4748) from the ru just recovered, which
+// this kernel already gathers -- k_dyn_cells1 at rk_step 2 / 3 computes nothing else, and no
+// kernel in between reads or writes ru or h_divergence; srk3 then skips that launch.
 template <int ME>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs p, int phase) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs p, int phase, int hdiv) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
   const int k = lane_id(), K = d.K;
@@ -2873,6 +2883,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs
 #pragma unroll
   for (int i = 0; i < ME; ++i) {
     if (i < ne && (k == 0 || act)) w = w + sg[i] * zs[i] * fl[i];
+  }
+  if (hdiv) {  // as k_dyn_cells1_b: edgesOnCell_sign * dvEdge * ru summed in edge order, times 1/area
+    double hd = 0.0;
+#pragma unroll
+    for (int i = 0; i < ME; ++i)
+      if (i < ne) hd = hd + ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i) * ru[i];
+    hd = hd * ld_uniform_f64(p.invAreaCell + c);
+    if (act) p.h_divergence[o] = hd;
   }
   const double rzm = up1(rz);
   const double r1 = readlane_d(rz, 0), r2 = readlane_d(rz, 1), r3 = readlane_d(rz, 2);

@@ -20,7 +20,8 @@ RECON = [("diag", n, "diag." + n) for n in ("uReconstructX", "uReconstructY", "u
 # diagnostics as the last atm_compute_solve_diagnostics of the step leaves them (gradPVt / gradPVn
 # are stored by that call only: nothing reads them in between)
 DIAG = [("diag", n, "diag." + n) for n in ("gradPVt", "gradPVn", "pv_edge", "pv_vertex", "pv_cell", "vorticity",
-                                           "divergence", "ke", "rho_edge", "v")]
+                                           "divergence", "ke", "rho_edge", "v", "h_divergence", "tend_rtheta_adv")] + \
+    [("tend_physics", "rthdynten", "tend_physics.rthdynten")]
 PROG = [("state", "u", "state.u.tl1"), ("state", "theta_m", "state.theta_m.tl1"),
         ("state", "rho_zz", "state.rho_zz.tl1"), ("state", "w", "state.w.tl1")]
 
