@@ -2319,18 +2319,32 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
 // recover_cells1 (2998-3040) of owned cell c from the final sub-step's new rho_pp / rtheta_pp /
 // rw_p / wwAvg, still in registers (k_acoustic_cells_r<ME, true>): the same expressions as
 // k_recover_cells1, lane for lane (inactive lanes see zz = fzm = fzp = 0 there too).
+// The recovery's own operands (RecIn) are loaded with the sub-step's, before the solve.
+struct RecIn {
+  double rps, rb, rtps, rtb, exb, rtd;
+};
+__device__ __forceinline__ RecIn load_rec_in(const Dims& d, const Ptrs& p, size_t o, int rk_step) {
+  RecIn r;
+  r.rps = p.rho_p_save[o];
+  r.rb = p.rho_base[o];
+  r.rtps = p.rtheta_p_save[o];
+  r.rtb = p.rtheta_base[o];
+  r.exb = rk_step == 3 ? p.exner_base[o] : 0.0;
+  r.rtd = (rk_step == 3 && d.diabatic) ? p.rt_diabatic_tend[o] : 0.0;
+  return r;
+}
 __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p, int c, int k, double zz_k, double rws,
-                                                   double rhopp, double rtpp, double rwp, double wwa, double dt,
-                                                   double invNs, int rk_step) {
+                                                   double fzm_k, double fzp_k, const RecIn& ri, double rhopp,
+                                                   double rtpp, double rwp, double wwa, double dt, double invNs,
+                                                   int rk_step) {
   const int K = d.K;
   const size_t K1 = K + 1;
   const bool act = k < K;
   const int kc = min(k, K - 1), kw = min(k, K);
   const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
   const double rcv = RGAS / (CP - RGAS);
-  const double rps = p.rho_p_save[o], rb = p.rho_base[o];
-  const double rtps = p.rtheta_p_save[o], rtb = p.rtheta_base[o];
-  const double fzm = act ? p.fzm[kc] : 0.0, fzp = act ? p.fzp[kc] : 0.0;
+  const double rps = ri.rps, rb = ri.rb, rtps = ri.rtps, rtb = ri.rtb;
+  const double fzm = act ? fzm_k : 0.0, fzp = act ? fzp_k : 0.0;
   const double zz = act ? zz_k : 0.0, zzm = up1(zz);
   double rz = 0.0;
   if (act) {
@@ -2349,12 +2363,12 @@ __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p,
   if (k <= K) p.w2[ow] = w;
   if (act) {
     if (rk_step == 3) {
-      const double rtp = rtps + rtpp - dt * rz * (d.diabatic ? p.rt_diabatic_tend[o] : 0.0);
+      const double rtp = rtps + rtpp - dt * rz * ri.rtd;  // rtd = 0.0 without diabatic forcing, as in k_recover_cells1
       p.rtheta_p[o] = rtp;
       p.theta_m2[o] = (rtp + rtb) / rz;
       const double ex = pow(zz * (RGAS / P0) * (rtp + rtb), rcv);
       p.exner[o] = ex;
-      p.pressure_p[o] = zz * RGAS * (ex * rtp + rtb * (ex - p.exner_base[o]));
+      p.pressure_p[o] = zz * RGAS * (ex * rtp + rtb * (ex - ri.exb));
     } else {
       const double rtp = rtps + rtpp;
       p.rtheta_p[o] = rtp;
@@ -2411,6 +2425,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
   const double a_tri = p.a_tri[o], alpha_tri = p.alpha_tri[o], gamma_tri = p.gamma_tri[o];
   const double rz = p.rho_zz2[o], dss = p.dss[o], rws = p.rw_save[ow], rw = p.rw[ow], w2 = p.w2[ow];
   const double cofrz = p.cofrz[kc], rdzw = p.rdzw[kc], fzm = p.fzm[kc], fzp = p.fzp[kc];
+  RecIn ri{};
+  if (FIN) ri = load_rec_in(d, p, o, rk_step);
   const double rtpp_old = (small_step == 1) ? 0.0 : rtpp;
   const double resm = (1.0 - epssm) / (1.0 + epssm);
   if (small_step == 1) { wwa = 0.0; rhopp = 0.0; rtpp = 0.0; rwp = 0.0; }
@@ -2463,7 +2479,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       if (!FIN) p.wwAvg[ow] = wwa;
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;  // levels 2..K: recover_cell_fused
     }
-    if (FIN) recover_cell_fused(d, p, c, k, zz, rws, rho_new, rt_new, rwp, wwa, rdt, invNs, rk_step);
+    if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rho_new, rt_new, rwp, wwa, rdt, invNs, rk_step);
   } else {
     // specified zone (2710-2719): regional only, masks are 0 for global meshes
     if (act) {
@@ -2480,7 +2496,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       if (!FIN) p.wwAvg[ow] = wwa;
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;
     }
-    if (FIN) recover_cell_fused(d, p, c, k, zz, rws, rhopp, rtpp, rwp, wwa, rdt, invNs, rk_step);
+    if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rhopp, rtpp, rwp, wwa, rdt, invNs, rk_step);
   }
 }
 
