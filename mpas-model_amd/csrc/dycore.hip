@@ -73,6 +73,7 @@ struct XPlan {
   double* sendbuf = nullptr;
   double* recvbuf = nullptr;
   std::vector<XMsg> rsend, rrecv;  // in matching order
+  bool warmed = false;              // its RCCL group has run once outside graph capture (warm_rccl)
 };
 
 // One field of an exchange point: mpas_dmpar_exch_halo_field(field[, haloLayers]).
@@ -1287,13 +1288,42 @@ void count_active_edges(Block& b, const int32_t* coe) {
 }
 
 // build the exchange plans of both time-level parities of a step outside graph capture
+// Run every plan's RCCL group once, eagerly, before the step is captured into a hipGraph: RCCL
+// sets up a peer connection the first time a send/recv to that peer is enqueued, and that
+// setup is kept out of stream capture.  Plans are visited in key order, which is the same on
+// every rank (same srk3 sequence, same keys), so the sends and receives of each rank pair
+// match.  The received bytes land in the receive buffers only (no unpack): they are scratch
+// until the real exchange overwrites them.
+int warm_rccl(mpas_dyc_ctx* ctx) {
+  if (!ctx->comm) return MPAS_DYC_OK;
+  bool any = false;
+  for (auto& kv : ctx->plans) {
+    XPlan& pl = kv.second;
+    if (pl.warmed) continue;
+    pl.warmed = true;
+    if (pl.rsend.empty() && pl.rrecv.empty()) continue;
+    NCCLCHK(ncclGroupStart());
+    for (const XMsg& m : pl.rsend)
+      NCCLCHK(ncclSend(pl.sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
+    for (const XMsg& m : pl.rrecv)
+      NCCLCHK(ncclRecv(pl.recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
+    NCCLCHK(ncclGroupEnd());
+    any = true;
+  }
+  if (any) HIPCHK(hipStreamSynchronize(ctx->stream));
+  return MPAS_DYC_OK;
+}
+
 int plan_all(mpas_dyc_ctx* ctx, double dt) {
   if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
   if (!needs_exchange(ctx) || ctx->planned[ctx->cur]) return MPAS_DYC_OK;
   ctx->planning = true;
   int r = srk3(ctx, dt);
   ctx->planning = false;
-  if (r == MPAS_DYC_OK) ctx->planned[ctx->cur] = true;
+  if (r == MPAS_DYC_OK) {
+    ctx->planned[ctx->cur] = true;
+    r = warm_rccl(ctx);
+  }
   return r;
 }
 
