@@ -1157,8 +1157,9 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         CHK((exchange)(ctx, xd));
       }
     }
-    EACH(LAUNCH(k_substep_finish, d.nEdges + d.nCells, d, p, dynamics_substep, dynamics_split,
-                1.0 / (double)dynamics_split));                   // 1304-1341
+    if (!ctx->planning)                                           // 1304-1341
+      EACH(hipLaunchKernelGGL(k_substep_finish_v, dim3(2048), dim3(BLOCK_THREADS), 0, ctx->stream, d, p,
+                              dynamics_substep, dynamics_split, 1.0 / (double)dynamics_split));
   }
 
   if (cf.scalar_advection && cf.split_dynamics_transport) {       // 1355-1576

@@ -1770,7 +1770,9 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_pgf_p(Dims d, Ptrs p
   const double invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
   const double invDv = sel(h, ld_uniform_f64(p.invDvEdge + eA), ld_uniform_f64(p.invDvEdge + eB));
   const double msd2 = sel(h, ld_uniform_f64(p.meshScalingDel2 + eA), ld_uniform_f64(p.meshScalingDel2 + eB));
-  const d2 re = ld2(p.rho_edge + o), cqu = ld2(p.cqu + o), zxu = ld2(p.zxu + o), tue0 = ld2(p.tend_u_euler + o);
+  const d2 re = ld2(p.rho_edge + o), cqu = ld2(p.cqu + o), zxu = ld2(p.zxu + o);
+  d2 tue0{};
+  if (!solve) tue0 = ld2(p.tend_u_euler + o);  // an owned edge overwrites it below: not read there
   const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y), v1 = sel(h, veA.x, veB.x), v2 = sel(h, veA.y, veB.y);
   const size_t o1 = (size_t)c1 * K + 2 * lc, o2 = (size_t)c2 * K + 2 * lc;
   const d2 pp1 = ld2(p.pressure_p + o1), pp2 = ld2(p.pressure_p + o2), zz1 = ld2(p.zz + o1), zz2 = ld2(p.zz + o2);
@@ -3179,6 +3181,90 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_substep_finish(Dims d, Ptrs p
         p.rho_zz1[o] = p.rho_zz2[o];
       }
       if (dynamics_substep == dynamics_split) p.rho_zz1[o] = p.rho_zz_old_split[o];
+    }
+  }
+}
+
+// k_substep_finish as flat 16-byte streams: each (K, n) / (K+1, n) array is contiguous over its
+// owned+halo columns, so the element-per-wave layout above (56 of 64 lanes, 8 B each) becomes
+// two doubles per lane on every lane.  Same ranges (garbage slot excluded), same expressions.
+__device__ __forceinline__ void fin_edge_pair(const Ptrs& p, int64_t j, int n, int cp, int first, int last, double inv) {
+  for (int q = 0; q < n; ++q) {  // n = 2, or 1 for an odd tail
+    const int64_t i = j + q;
+    if (cp) {
+      p.ru_save[i] = p.ru[i];
+      p.u1[i] = p.u2[i];
+    }
+    const double ras = first ? p.ruAvg[i] : p.ruAvg[i] + p.ruAvg_split[i];
+    p.ruAvg_split[i] = ras;
+    if (last) p.ruAvg[i] = ras * inv;
+  }
+}
+__global__ __launch_bounds__(BLOCK_THREADS) void k_substep_finish_v(Dims d, Ptrs p, int dynamics_substep,
+                                                                     int dynamics_split, double inv_dynamics_split) {
+  const int64_t nE = (int64_t)d.nEdges * d.K, nW = (int64_t)d.nCells * (d.K + 1), nC = (int64_t)d.nCells * d.K;
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+  const int cp = dynamics_substep < dynamics_split, first = dynamics_substep == 1, last = dynamics_substep == dynamics_split;
+  const double inv = inv_dynamics_split;
+  for (int64_t j = 2 * t0; j < nE; j += 2 * st) {
+    if (j + 1 < nE) {
+      if (cp) {
+        st2(p.ru_save + j, ld2(p.ru + j));
+        st2(p.u1 + j, ld2(p.u2 + j));
+      }
+      const d2 a = ld2(p.ruAvg + j);
+      d2 ras = a;
+      if (!first) {
+        const d2 b = ld2(p.ruAvg_split + j);
+        ras = d2{a.x + b.x, a.y + b.y};
+      }
+      st2(p.ruAvg_split + j, ras);
+      if (last) st2(p.ruAvg + j, d2{ras.x * inv, ras.y * inv});
+    } else {
+      fin_edge_pair(p, j, 1, cp, first, last, inv);
+    }
+  }
+  for (int64_t j = 2 * t0; j < nW; j += 2 * st) {
+    if (j + 1 < nW) {
+      if (cp) {
+        st2(p.rw_save + j, ld2(p.rw + j));
+        st2(p.w1 + j, ld2(p.w2 + j));
+      }
+      const d2 a = ld2(p.wwAvg + j);
+      d2 was = a;
+      if (!first) {
+        const d2 b = ld2(p.wwAvg_split + j);
+        was = d2{a.x + b.x, a.y + b.y};
+      }
+      st2(p.wwAvg_split + j, was);
+      if (last) st2(p.wwAvg + j, d2{was.x * inv, was.y * inv});
+    } else {
+      if (cp) {
+        p.rw_save[j] = p.rw[j];
+        p.w1[j] = p.w2[j];
+      }
+      const double was = first ? p.wwAvg[j] : p.wwAvg[j] + p.wwAvg_split[j];
+      p.wwAvg_split[j] = was;
+      if (last) p.wwAvg[j] = was * inv;
+    }
+  }
+  for (int64_t j = 2 * t0; j < nC; j += 2 * st) {
+    if (j + 1 < nC) {
+      if (cp) {
+        st2(p.rtheta_p_save + j, ld2(p.rtheta_p + j));
+        st2(p.rho_p_save + j, ld2(p.rho_p + j));
+        st2(p.theta_m1 + j, ld2(p.theta_m2 + j));
+        st2(p.rho_zz1 + j, ld2(p.rho_zz2 + j));
+      }
+      if (last) st2(p.rho_zz1 + j, ld2(p.rho_zz_old_split + j));
+    } else {
+      if (cp) {
+        p.rtheta_p_save[j] = p.rtheta_p[j];
+        p.rho_p_save[j] = p.rho_p[j];
+        p.theta_m1[j] = p.theta_m2[j];
+        p.rho_zz1[j] = p.rho_zz2[j];
+      }
+      if (last) p.rho_zz1[j] = p.rho_zz_old_split[j];
     }
   }
 }
