@@ -95,8 +95,14 @@ struct Ptrs {
   // edgesOnCell_sign * dvEdge (maxEdges doubles per cell).  A cell reads its whole stencil with
   // one scalar load.
   const int* cell_rec;
+  // LDS-staged advflux tiles (k_dyn_advflux_t): per tile of ADV_T edges, the number of distinct
+  // stencil cells, their indices (ADV_UMAX per tile), and per edge the local slot of each
+  // stencil cell (ADV_LOC bytes per edge)
+  const int *adv_tn, *adv_tcell;
+  const unsigned char* adv_loc;
   const double* cell_sdv;
 };
 constexpr int CELL_REC = 16, CELL_REC_ME = 7;
+constexpr int ADV_T = 8, ADV_UMAX = 32, ADV_LOC = 16;
 
 }  // namespace mpas

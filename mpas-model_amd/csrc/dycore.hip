@@ -54,6 +54,10 @@ struct Block {
   std::vector<XList> xl;
   int64_t nEdges_act = -1;             // edges with an owned cell (from cellsOnEdge), for B_ac
   int64_t n_bnd_edges = -1;            // edges with a halo (or garbage) cell, from compute_bnd
+  // LDS-staged advflux tiles (build_adv_tiles); null when the mesh does not qualify
+  int* d_adv_tn = nullptr;
+  int* d_adv_tcell = nullptr;
+  unsigned char* d_adv_loc = nullptr;
   std::vector<int32_t> h_coe, h_eoc, h_noc;  // host copies (0-based) for the halo-boundary flags
 };
 
@@ -342,6 +346,9 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   p.cell_rec = P<const int>(c, b, "scratch", "cell_rec");
   p.cell_sdv = P<const double>(c, b, "scratch", "cell_sdv");
   p.zb_p = P<const double>(c, b, "scratch", "zb_p");
+  p.adv_tn = b.d_adv_tn;
+  p.adv_tcell = b.d_adv_tcell;
+  p.adv_loc = b.d_adv_loc;
   p.zb_m = P<const double>(c, b, "scratch", "zb_m");
   // 0-d mesh fields are mirrored on the host
   p.cf1 = b.fields[b.by_name["mesh.cf1"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf1"]].buf[1] : 0.0;
@@ -590,6 +597,80 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   return MPAS_DYC_OK;
 }
 
+// Kernel families: 0 "general" (one column per wave, loads where used -- any mesh), 1 "batched"
+// (k_*_b / k_*_r: per-cell records, every load issued up front; maxEdges 6 or 7), 2 "pair"
+// (k_*_p: two edges per wave, two levels per lane; even K).  All three give the same bits
+// (tests/test_gpu_kernels.py); the environment variable MPAS_DYCORE_KERNELS=general|batched|pair,
+// read when a context is created, caps the family (default pair).
+int g_kernel_tier = 2;
+// MPAS_DYCORE_LDS=1 turns the LDS-staged advflux (k_dyn_advflux_t) on.  Off by default: measured
+// 572 us against 368 us for k_dyn_advflux_p at 163842x56 (rejected experiments)
+bool g_lds_advflux = false;
+
+inline bool batched(const Dims& d) {
+  return g_kernel_tier >= 1 && (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
+}
+
+
+// pair-layout edge kernels (k_*_p: two edges per wave, two levels per lane) need an even K
+inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K % 2 == 0 && d.K <= 64; }
+
+void free_adv_tiles(Block& b) {
+  if (b.d_adv_tn) (void)hipFree(b.d_adv_tn);
+  if (b.d_adv_tcell) (void)hipFree(b.d_adv_tcell);
+  if (b.d_adv_loc) (void)hipFree(b.d_adv_loc);
+  b.d_adv_tn = b.d_adv_tcell = nullptr;
+  b.d_adv_loc = nullptr;
+}
+
+// Tiles of k_dyn_advflux_t: ADV_T consecutive edges; the distinct advCellsForEdge cells of the
+// tile's edges with an owned cell (the ones k_dyn_advflux computes), and each edge's slot map.
+// Leaves the tiles off (k_dyn_advflux_p runs) unless the pair layout applies, maxEdges = 6
+// (NA = 10 stencil slots); a tile with more than ADV_UMAX distinct cells (tn = -1) gathers.
+int build_adv_tiles(mpas_dyc_ctx* ctx, Block& b) {
+  free_adv_tiles(b);
+  const Dims& d = b.d;
+  if (!g_lds_advflux || !pair_layout(d) || d.maxEdges != 6 || d.nEdges < 1) return MPAS_DYC_OK;
+  const int64_t nE = d.nEdges;
+  std::vector<int32_t> adv((size_t)(nE + 1) * 15), nadv(nE + 1);
+  HIPCHK(hipMemcpy(adv.data(), find(b, "mesh", "advCellsForEdge")->buf[0], adv.size() * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(nadv.data(), find(b, "mesh", "nAdvCellsForEdge")->buf[0], nadv.size() * 4, hipMemcpyDeviceToHost));
+  const int64_t nt = (nE + ADV_T - 1) / ADV_T;
+  std::vector<int32_t> tn(nt, 0), tcell((size_t)nt * ADV_UMAX, 0);
+  std::vector<unsigned char> loc((size_t)nE * ADV_LOC, 0);
+  for (int64_t t = 0; t < nt; ++t) {
+    int cnt = 0;
+    int32_t* u = &tcell[(size_t)t * ADV_UMAX];
+    for (int64_t e = t * ADV_T; e < std::min<int64_t>(nE, (t + 1) * ADV_T); ++e) {
+      const bool on = b.h_coe[2 * e] < d.nCellsSolve || b.h_coe[2 * e + 1] < d.nCellsSolve;
+      if (!on) continue;
+      if (nadv[e] > 10) return MPAS_DYC_OK;  // wider stencil: k_dyn_advflux_p
+      for (int j = 0; j < nadv[e]; ++j) {
+        const int32_t c = adv[(size_t)e * 15 + j];
+        int s = 0;
+        while (s < cnt && u[s] != c) ++s;
+        if (s == cnt) {
+          if (cnt == ADV_UMAX) {  // tile too wide for the LDS budget: its edges gather from memory
+            cnt = -1;
+            break;
+          }
+          u[cnt++] = c;
+        }
+        loc[(size_t)e * ADV_LOC + j] = (unsigned char)s;
+      }
+      if (cnt < 0) break;
+    }
+    tn[t] = cnt;
+  }
+  HIPCHK(hipMalloc(&b.d_adv_tn, tn.size() * 4));
+  HIPCHK(hipMalloc(&b.d_adv_tcell, tcell.size() * 4));
+  HIPCHK(hipMalloc(&b.d_adv_loc, loc.size()));
+  HIPCHK(hipMemcpy(b.d_adv_tn, tn.data(), tn.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(b.d_adv_tcell, tcell.data(), tcell.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(b.d_adv_loc, loc.data(), loc.size(), hipMemcpyHostToDevice));
+  return MPAS_DYC_OK;
+}
+
 // Halo-boundary flags of the split-phase exchanges: an edge is "boundary" when one of its
 // cells is a halo cell (it reads exchanged cell data); an owned cell is "boundary" when
 // one of its edges is a halo edge (it reads exchanged edge data).
@@ -618,6 +699,7 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
     }
     HIPCHK(hipMemcpy(find(b, "scratch", "edge_bnd")->buf[0], eb.data(), eb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(find(b, "scratch", "cell_bnd")->buf[0], cb.data(), cb.size() * 4, hipMemcpyHostToDevice));
+    CHK(build_adv_tiles(ctx, b));
     hipLaunchKernelGGL(k_build_cell_rec, dim3((d.nCells + 1 + 255) / 256), dim3(256), 0, ctx->stream, d,
                        P<const int>(ctx, b, "mesh", "nEdgesOnCell"), P<const int>(ctx, b, "mesh", "edgesOnCell"),
                        P<const int>(ctx, b, "mesh", "cellsOnEdge"), P<const double>(ctx, b, "mesh", "dvEdge"),
@@ -690,20 +772,6 @@ void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
   if (!ctx->planning) hipLaunchKernelGGL(k_copy_many, dim3(gx, 10), dim3(256), 0, ctx->stream, c);
 }
 
-// Kernel families: 0 "general" (one column per wave, loads where used -- any mesh), 1 "batched"
-// (k_*_b / k_*_r: per-cell records, every load issued up front; maxEdges 6 or 7), 2 "pair"
-// (k_*_p: two edges per wave, two levels per lane; even K).  All three give the same bits
-// (tests/test_gpu_kernels.py); the environment variable MPAS_DYCORE_KERNELS=general|batched|pair,
-// read when a context is created, caps the family (default pair).
-int g_kernel_tier = 2;
-
-inline bool batched(const Dims& d) {
-  return g_kernel_tier >= 1 && (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
-}
-
-
-// pair-layout edge kernels (k_*_p: two edges per wave, two levels per lane) need an even K
-inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K % 2 == 0 && d.K <= 64; }
 
 void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
   if (pair_layout(d))
@@ -775,7 +843,11 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     }
   }
   if (!batched(d)) LAUNCH(k_dyn_advflux, d.nEdges, d, p);
-  else if (pair_layout(d) && d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_p<10>, (d.nEdges + 1) / 2, d, p);
+  else if (pair_layout(d) && d.maxEdges == 6 && p.adv_tn) {
+    if (!ctx->planning)  // one workgroup per tile of ADV_T edges, LDS = ADV_UMAX (K+2 + K) doubles
+      hipLaunchKernelGGL(k_dyn_advflux_t<10>, dim3((unsigned)((d.nEdges + ADV_T - 1) / ADV_T)), dim3(BLOCK_THREADS),
+                         (size_t)ADV_UMAX * (((d.K + 2) & ~1) + d.K) * sizeof(double), ctx->stream, d, p);
+  } else if (pair_layout(d) && d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_p<10>, (d.nEdges + 1) / 2, d, p);
   else if (pair_layout(d)) LAUNCH_E(k_dyn_advflux_p<12>, (d.nEdges + 1) / 2, d, p);
   else if (d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_b<10>, d.nEdges, d, p);
   else LAUNCH_E(k_dyn_advflux_b<12>, d.nEdges, d, p);
@@ -1373,6 +1445,10 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   } else {
     g_kernel_tier = 2;
   }
+  {
+    const char* lv = getenv("MPAS_DYCORE_LDS");
+    g_lds_advflux = lv && std::string(lv) == "1";
+  }
   for (auto& b : ctx->blk) {
     build_registry(b);
     for (auto& f : b.fields) {
@@ -1408,6 +1484,7 @@ void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
     }
     for (auto& x : b.xl)
       if (x.d_idx) (void)hipFree(x.d_idx);
+    free_adv_tiles(b);
   }
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
@@ -1497,6 +1574,7 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
       b.h_eoc = tmp;
       ctx->bnd_ready = false;
     }
+    if (f->pool == "mesh" && f->name == "advCellsForEdge") ctx->bnd_ready = false;  // advflux tiles
     HIPCHK(hipMemcpyAsync(f->buf[slot], tmp.data(), nb, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   } else if (f->nsub > 1) {
@@ -1517,6 +1595,7 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
       ctx->bnd_ready = false;
     }
     if (f->pool == "mesh" && (f->name == "zb_cell" || f->name == "zb3_cell")) ctx->bnd_ready = false;  // zb_p / zb_m
+    if (f->pool == "mesh" && f->name == "nAdvCellsForEdge") ctx->bnd_ready = false;  // advflux tiles
     if (f->pool == "tend" && f->name == "rt_diabatic_tend") {
       const double* h = (const double*)host;
       int nz = 0;

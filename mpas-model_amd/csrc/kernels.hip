@@ -1868,6 +1868,112 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
   }
 }
 
+// k_dyn_advflux_p with the stencil columns staged through LDS.  One workgroup per tile of ADV_T
+// consecutive (SFC-ordered) edges: its waves first copy the w / theta_m columns of the tile's
+// distinct stencil cells (about 33 for 16 edges at x1.163842, instead of 160 gathered columns)
+// into LDS with coalesced column loads, then run the pair-layout edge computation with every
+// stencil operand read from LDS.  Same operands, same order of the sums: bit-identical to
+// k_dyn_advflux_p.  Only for NA = 10 (maxEdges 6) meshes; tile metadata built on the host
+// (checked on the host, build_adv_tiles); LDS = ADV_UMAX * (K+2 + K) doubles.  A tile with more
+// than ADV_UMAX cells (a jump of the space-filling curve, ~1 % of tiles) reads them from memory.
+template <int NA>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_advflux_t(Dims d, Ptrs p) {
+  static_assert(ADV_T == 2 * WAVES_PER_BLOCK, "one edge pair per wave");
+  extern __shared__ double lds[];
+  const int tile = xcd_block();
+  const int e0 = tile * ADV_T;
+  if (e0 >= d.nEdges) return;
+  const int n = __builtin_amdgcn_readfirstlane(p.adv_tn[tile]);
+  if (n == 0) return;  // no edge of this tile has an owned cell
+  const bool staged = n > 0;  // n < 0: more than ADV_UMAX cells (a jump of the curve): gathered from memory
+  const int K = d.K, K1 = K + 1, K1p = (K + 2) & ~1;
+  double* sw = lds;                              // [ADV_UMAX][K1p]
+  double* sth = lds + (size_t)ADV_UMAX * K1p;    // [ADV_UMAX][K]
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  // ---- this wave's edge pair: every operand that does not come from LDS, issued first
+  const int eA = min(e0 + 2 * wid, d.nEdges - 1);
+  const bool live = e0 + 2 * wid < d.nEdges;
+  const bool hasB = live && eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const int naA = p.nAdvCellsForEdge[eA], naB = p.nAdvCellsForEdge[eB];
+  double a[NA], b[NA];
+  int lA[4], lB[4];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j));
+    b[j] = sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
+               ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {  // slot bytes, four per int, through the scalar unit
+    lA[q] = reinterpret_cast<const int*>(p.adv_loc + (size_t)eA * ADV_LOC)[q];
+    lB[q] = reinterpret_cast<const int*>(p.adv_loc + (size_t)eB * ADV_LOC)[q];
+  }
+  const d2 rue = ld2(p.ru + o);
+  const d2 fzm = ld2(p.fzm + 2 * lc), fzp = ld2(p.fzp + 2 * lc);
+  // ---- stage the tile's distinct stencil columns: wave wid copies columns wid, wid+4, ...
+  if (staged) {
+    for (int u0 = wid; u0 < n; u0 += 4 * WAVES_PER_BLOCK) {
+      double wr[4], tr[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = u0 + q * WAVES_PER_BLOCK;
+        const int c = __builtin_amdgcn_readfirstlane(p.adv_tcell[(size_t)tile * ADV_UMAX + min(u, n - 1)]);
+        wr[q] = p.w2[(size_t)c * K1 + min(lane, K)];
+        tr[q] = p.theta_m2[(size_t)c * K + min(lane, K - 1)];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = u0 + q * WAVES_PER_BLOCK;
+        if (u < n) {
+          if (lane < K1) sw[u * K1p + lane] = wr[q];
+          if (lane < K) sth[u * K + lane] = tr[q];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const bool onA = live && (ceA.x < d.nCellsSolve || ceA.y < d.nCellsSolve);
+  const bool onB = hasB && (ceB.x < d.nCellsSolve || ceB.y < d.nCellsSolve);
+  if (!onA && !onB) return;
+  const int kx = 2 * l, ky = 2 * l + 1;
+  const d2 rue_m = km1(rue, l);
+  const double rewx = kx < K ? fzm.x * rue.x + fzp.x * rue_m.x : 0.0;
+  const double rewy = ky < K ? fzm.y * rue.y + fzp.y * rue_m.y : 0.0;
+  const double swx = sgn1(rewx), swy = sgn1(rewy), stx_ = sgn1(rue.x), sty_ = sgn1(rue.y);
+  const int na = sel(h, naA, naB);
+  d2 fw{0.0, 0.0}, ft{0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    d2 w_, t_;
+    if (staged) {
+      const int u = (sel(h, lA[j >> 2], lB[j >> 2]) >> (8 * (j & 3))) & 0xff;
+      w_ = ld2(sw + u * K1p + 2 * lw);
+      t_ = ld2(sth + u * K + 2 * lc);
+    } else {
+      const size_t cj = (size_t)p.advCellsForEdge[(size_t)e * 15 + j];
+      w_ = ld2(p.w2 + cj * K1 + 2 * lw);
+      t_ = ld2(p.theta_m2 + cj * K + 2 * lc);
+    }
+    if (j < na) {
+      fw.x = fw.x + (a[j] + swx * b[j]) * w_.x;
+      fw.y = fw.y + (a[j] + swy * b[j]) * w_.y;
+      ft.x = ft.x + (a[j] + stx_ * b[j]) * t_.x;
+      ft.y = ft.y + (a[j] + sty_ * b[j]) * t_.y;
+    }
+  }
+  if ((h ? onB : onA) && 2 * l < K) {
+    st2(p.advflux_w + o, fw);
+    st2(p.advflux_th + o, ft);
+  }
+}
+
 // k_diag_edges_b in the pair layout
 template <int NE2>
 __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, const double* __restrict__ u,
