@@ -86,17 +86,19 @@ def test_acoustic_substep_bitwise_vs_reference_fixture():
     dy.close()
 
 
-def _steps_with_kernels(case, family, nsteps=3, dt=None):
+def _steps_with_kernels(case, family, nsteps=3, dt=None, lds="0"):
     from mpas_dycore import Dycore
-    old = os.environ.get("MPAS_DYCORE_KERNELS")
+    saved = {k: os.environ.get(k) for k in ("MPAS_DYCORE_KERNELS", "MPAS_DYCORE_LDS")}
     os.environ["MPAS_DYCORE_KERNELS"] = family
+    os.environ["MPAS_DYCORE_LDS"] = lds
     try:
         dy = Dycore(case, device=0, moist_end=case["num_scalars"])
     finally:
-        if old is None:
-            os.environ.pop("MPAS_DYCORE_KERNELS")
-        else:
-            os.environ["MPAS_DYCORE_KERNELS"] = old
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
     dt = dt or 2880.0
     dy.init_diagnostics(dt)
     for i in range(nsteps):
@@ -122,6 +124,15 @@ def test_kernel_families_give_identical_bits(which, request):
         got = _steps_with_kernels(case, fam, dt=dt)
         for n in ref:
             assert np.array_equal(got[n], ref[n]), f"{fam}: {n}"
+
+
+def test_lds_staged_advflux_gives_identical_bits(moist_case):
+    """The opt-in LDS-staged advflux (MPAS_DYCORE_LDS=1, k_dyn_advflux_t) reads the same stencil
+    operands from LDS: three moist monotone steps agree to the bit with the pair kernel."""
+    ref = _steps_with_kernels(moist_case, "pair")
+    got = _steps_with_kernels(moist_case, "pair", lds="1")
+    for n in ref:
+        assert np.array_equal(got[n], ref[n]), n
 
 
 def test_odd_level_count_runs_the_single_column_kernels():
