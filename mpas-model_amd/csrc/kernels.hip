@@ -2500,9 +2500,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
   const int kc = min(k, K - 1), kw = min(k, K);  // clamped lanes load in bounds and store nothing
   const size_t K1 = K + 1;
   const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
-  double rtpp = p.rtheta_pp[o];
+  // sub-step 1 starts from zero perturbations (2617-2622): rtheta_pp, rho_pp, rw_p and wwAvg are
+  // not read then (the values would be replaced by 0 below), which saves four streams
+  const bool first = small_step == 1;
+  double rtpp = first ? 0.0 : p.rtheta_pp[o];
   if (c >= d.nCellsSolve) {
-    if (act) p.rtheta_pp_old[o] = (small_step == 1) ? 0.0 : rtpp;
+    if (act) p.rtheta_pp_old[o] = first ? 0.0 : rtpp;
     return;
   }
   int re[ME], rc[ME];
@@ -2515,7 +2518,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
   }
   const int ne = p.cell_rec[(size_t)c * CELL_REC + 14];
   const double invA = p.invAreaCell[c], spec = p.specZoneMaskCell[c];
-  double rhopp = p.rho_pp[o], rwp = p.rw_p[ow], wwa = p.wwAvg[ow];
+  double rhopp = first ? 0.0 : p.rho_pp[o], rwp = first ? 0.0 : p.rw_p[ow], wwa = first ? 0.0 : p.wwAvg[ow];
   const double thc = p.theta_m1[o], trho = p.tend_rho[o], tth = p.tend_theta[o], tw = p.tend_w[ow];
   double ru[ME], th[ME];
   // sub-step 1: ru_p = dts * tend_u (794-837), formed here; srk3 launches no edge phase for it
