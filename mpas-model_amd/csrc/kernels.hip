@@ -3252,51 +3252,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_init_coupled_c(Dims d, Ptrs p
 // ============================================================================
 // atm_rk_dynamics_substep_finish  (mpas_atm_time_integration.F:6051-6079)
 // ============================================================================
-__global__ __launch_bounds__(BLOCK_THREADS) void k_substep_finish(Dims d, Ptrs p, int dynamics_substep,
-                                                                   int dynamics_split, double inv_dynamics_split) {
-  const int idx = wave_elem(0);
-  const int k = lane_id(), K = d.K;
-  const size_t K1 = K + 1;
-  if (idx < d.nEdges) {
-    const int e = idx;
-    if (k >= K) return;
-    const size_t o = (size_t)e * K + k;
-    if (dynamics_substep < dynamics_split) {
-      p.ru_save[o] = p.ru[o];
-      p.u1[o] = p.u2[o];
-    }
-    double ras = (dynamics_substep == 1) ? p.ruAvg[o] : p.ruAvg[o] + p.ruAvg_split[o];
-    p.ruAvg_split[o] = ras;
-    if (dynamics_substep == dynamics_split) p.ruAvg[o] = ras * inv_dynamics_split;
-  } else {
-    const int c = idx - d.nEdges;
-    if (c >= d.nCells) return;
-    if (k <= K) {
-      const size_t ow = (size_t)c * K1 + k;
-      if (dynamics_substep < dynamics_split) {
-        p.rw_save[ow] = p.rw[ow];
-        p.w1[ow] = p.w2[ow];
-      }
-      double was = (dynamics_substep == 1) ? p.wwAvg[ow] : p.wwAvg[ow] + p.wwAvg_split[ow];
-      p.wwAvg_split[ow] = was;
-      if (dynamics_substep == dynamics_split) p.wwAvg[ow] = was * inv_dynamics_split;
-    }
-    if (k < K) {
-      const size_t o = (size_t)c * K + k;
-      if (dynamics_substep < dynamics_split) {
-        p.rtheta_p_save[o] = p.rtheta_p[o];
-        p.rho_p_save[o] = p.rho_p[o];
-        p.theta_m1[o] = p.theta_m2[o];
-        p.rho_zz1[o] = p.rho_zz2[o];
-      }
-      if (dynamics_substep == dynamics_split) p.rho_zz1[o] = p.rho_zz_old_split[o];
-    }
-  }
-}
-
-// k_substep_finish as flat 16-byte streams: each (K, n) / (K+1, n) array is contiguous over its
-// owned+halo columns, so the element-per-wave layout above (56 of 64 lanes, 8 B each) becomes
-// two doubles per lane on every lane.  Same ranges (garbage slot excluded), same expressions.
+// Called at 1304-1341; flat 16-byte streams: each (K, n) /
+// (K+1, n) array is contiguous over its owned+halo columns, so instead of one column per wave
+// (56 of 64 lanes, 8 B each) every lane moves two doubles.  Same ranges (garbage slot excluded),
+// same expressions.
 __device__ __forceinline__ void fin_edge_pair(const Ptrs& p, int64_t j, int n, int cp, int first, int last, double inv) {
   for (int q = 0; q < n; ++q) {  // n = 2, or 1 for an odd tail
     const int64_t i = j + q;
