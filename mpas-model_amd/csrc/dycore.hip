@@ -903,16 +903,19 @@ bool fused_recover(const Dims& d) { return batched(d) && (d.maxEdges == 6 || d.m
 
 // fin = 1: the stage's last sub-step, which also recovers the owned cells (k_acoustic_cells_r<ME,
 // true>) when fused_recover(d); rdt / invNs / rk_step are k_recover_cells1's arguments
+// keep_pp = 0: a fin launch need not store rho_pp / rw_p (see k_acoustic_cells_r)
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int fin = 0,
-                    double rdt = 0.0, double invNs = 0.0, int rk_step = 0) {
+                    double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1) {
   if (batched(d) && d.maxEdges == 6) {
-    if (fin) LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step);
-    else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0);
+    if (fin)
+      LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp);
+    else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1);
     return;
   }
   if (batched(d) && d.maxEdges == 7) {
-    if (fin) LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step);
-    else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0);
+    if (fin)
+      LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp);
+    else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1);
     return;
   }
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
@@ -1152,7 +1155,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
           EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2));
         }
         EACH(acoustic_cells(ctx, d, p, dts, small_step, small_step == nsub, rk_timestep[rk_step - 1],
-                            1 / (double)nsub, rk_step));
+                            1 / (double)nsub, rk_step, needs_exchange(ctx) || last_stage));
         std::vector<XField> xf = {{"diag", "rtheta_pp", 0, 0x1u}};  // 845
         if (small_step < nsub) xf.push_back({"diag", "rho_pp", 0, 0x1u});  // 792 of the next sub-step
         if (split) {

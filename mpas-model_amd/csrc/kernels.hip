@@ -2489,10 +2489,14 @@ __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p,
 // between this launch and k_recover_cells1 -- the Theta''/rho'' exchange, the damping (ru_p,
 // ruAvg) and the 876-887 exchange -- reads or writes what the recovery reads or writes for an
 // owned cell, so k_recover_cells1 then runs on the halo cells and the garbage slot only.
+// keep_pp = 0 (FIN only): rho_pp and rw_p are not stored.  After a stage's last sub-step nothing
+// reads them but the 876-887 exchange and the halo-cell recovery; srk3 passes 0 only for a block
+// without exchanges and a stage that is not the dt's last (whose values the pool keeps).
 template <int ME, bool FIN = false>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs p, double dts, int small_step,
                                                                     double epssm, double rdt = 0.0,
-                                                                    double invNs = 0.0, int rk_step = 0) {
+                                                                    double invNs = 0.0, int rk_step = 0,
+                                                                    int keep_pp = 1) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
   const int k = lane_id(), K = d.K;
@@ -2582,11 +2586,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
     const double rt_new = ts - rdzw * (coftz_p * rwp_p2 - coftz * rwp);
     if (act) {
       p.rtheta_pp_old[o] = rtpp_old;  // stored last: no store precedes the loads above
-      p.rho_pp[o] = rho_new;
+      if (!FIN || keep_pp) p.rho_pp[o] = rho_new;
       p.rtheta_pp[o] = rt_new;
     }
     if (actw) {
-      p.rw_p[ow] = rwp;
+      if (!FIN || keep_pp) p.rw_p[ow] = rwp;
       if (!FIN) p.wwAvg[ow] = wwa;
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;  // levels 2..K: recover_cell_fused
     }
