@@ -989,14 +989,24 @@ void advance_scalars(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt,
 
 // atm_advance_scalars_mono (3548-4210) over all blocks: its two halo exchanges
 // (scalars_old at 3757, the limiter factors at 4098) sit between the block loops.
-int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt, bool advance_density) {
+// the preparation (3737-3777: scalars_old += dt * tend / rho_zz_old, rho_zz_int) and its
+// scalars_old exchange (3757); split out so srk3 can merge that exchange with the one before it
+void mono_prep(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt, bool advance_density) {
+  for (size_t b = 0; b < ctx->blk.size(); ++b) {
+    const Dims& d = ctx->blk[b].d;
+    LAUNCH(k_mono_prep, d.nCells, d, P[b], dt, advance_density ? 1 : 0);
+  }
+}
+
+// prepared = true: mono_prep ran and its exchange was merged into the caller's
+int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt, bool advance_density,
+                         bool prepared = false) {
   const int ad = advance_density ? 1 : 0;
   const int nb = (int)ctx->blk.size();
-  for (int b = 0; b < nb; ++b) {
-    const Dims& d = ctx->blk[b].d;
-    LAUNCH(k_mono_prep, d.nCells, d, P[b], dt, ad);
+  if (!prepared) {
+    mono_prep(ctx, P, dt, advance_density);
+    CHK(exchange(ctx, {{"state", "scalars", 1, ALL_LAYERS}}));
   }
-  CHK(exchange(ctx, {{"state", "scalars", 1, ALL_LAYERS}}));
   const int ns = ctx->blk[0].d.ns;
   for (int is = 0; is < ns; ++is) {
     for (int b = 0; b < nb; ++b) {
@@ -1240,13 +1250,22 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   if (cf.scalar_advection && cf.split_dynamics_transport) {       // 1355-1576
     double rk_ts[3] = {dt / 3., dt / 2., dt};
     if (cf.time_integration_order == 2) rk_ts[0] = dt / 2.;
+    const bool mono3 = cf.monotonic || cf.positive_definite;
     for (int rk_step = 1; rk_step <= 3; ++rk_step) {
-      if (rk_step < 3 || (!cf.monotonic && !cf.positive_definite)) {
+      if (rk_step < 3 || !mono3) {
         EACH(advance_scalars(ctx, d, p, rk_ts[rk_step - 1], rk_step, true));
       } else {
-        CHK(advance_scalars_mono(ctx, P, rk_ts[rk_step - 1], true));
+        CHK(advance_scalars_mono(ctx, P, rk_ts[rk_step - 1], true, true));
       }
-      if (rk_step < 3) CHK(exchange(ctx, {{"state", "scalars", 2, ALL_LAYERS}}));  // 1569-1572
+      if (rk_step == 2 && mono3) {
+        // the rk3 limiter's preparation (3737-3777) reads scalars(tl1), scalars_tend, rho_zz(tl1),
+        // ruAvg and wwAvg, none of which this exchange touches, and writes none of the scalars(tl2)
+        // it moves: so it runs first and its scalars_old exchange (3757) rides with 1569-1572
+        mono_prep(ctx, P, rk_ts[2], true);
+        CHK(exchange(ctx, {{"state", "scalars", 2, ALL_LAYERS}, {"state", "scalars", 1, ALL_LAYERS}}));
+      } else if (rk_step < 3) {
+        CHK(exchange(ctx, {{"state", "scalars", 2, ALL_LAYERS}}));  // 1569-1572
+      }
     }
   }
   EACH(LAUNCH(k_reconstruct, d.nCellsSolve, d, p, p.u2));          // mpas_reconstruct (1581-1603)
