@@ -1113,6 +1113,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   auto xchg = [&](const std::vector<XField>& fs) { return split ? exchange_async(ctx, fs) : (exchange)(ctx, fs); };
   auto xwait = [&]() { return split ? exchange_wait(ctx) : MPAS_DYC_OK; };
   bool pending = false;  // an xchg whose xwait is still due
+  bool final_pending = false;  // the last substep's 1234-1249 exchange, waited for after substep_finish
   EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));           // 476-510 of dynamics substep 1
   for (int dynamics_substep = 1; dynamics_substep <= dynamics_split; ++dynamics_substep) {
     // 513 (exner): carried by the step-start exchange and by the 1282-1297 exchange below
@@ -1238,6 +1239,11 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         CHK(xchg(xd));
         EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));     // 476-510 of the next substep
         CHK(xwait());
+      } else if (split) {
+        // the dt's last 1234-1249: overlaps substep_finish, which reads and writes none of its
+        // fields (w, pv_edge, rho_edge, scalars)
+        CHK(exchange_async(ctx, xd));
+        final_pending = true;
       } else {
         CHK((exchange)(ctx, xd));
       }
@@ -1245,6 +1251,10 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
     if (!ctx->planning)                                           // 1304-1341
       EACH(hipLaunchKernelGGL(k_substep_finish_v, dim3(2048), dim3(BLOCK_THREADS), 0, ctx->stream, d, p,
                               dynamics_substep, dynamics_split, 1.0 / (double)dynamics_split));
+    if (final_pending) {
+      CHK(exchange_wait(ctx));
+      final_pending = false;
+    }
   }
 
   if (cf.scalar_advection && cf.split_dynamics_transport) {       // 1355-1576
