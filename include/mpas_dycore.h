@@ -114,6 +114,38 @@ int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags);
  * scalars(index_qv) of the time level, zz, pressure_base and pressure_p.  Asynchronous. */
 int mpas_dyc_output_diagnostics(mpas_dyc_ctx* ctx, int32_t time_level);
 
+/* ---- summarize_timestep (mpas_atm_time_integration.F:6675-7018, called at the end of atm_srk3, 1794) ----
+ * The modes are the namelist switches of the reference; each step reduces the enabled ones on
+ * the device (part of mpas_dyc_timestep, captured with the step), and mpas_dyc_get_summary
+ * folds the blocks of this process and, over RCCL, all ranks. */
+#define MPAS_DYC_PRINT_GLOBAL_MINMAX_VEL 1   /* config_print_global_minmax_vel (default .true.), 6945-6983 */
+#define MPAS_DYC_PRINT_DETAILED_MINMAX_VEL 2 /* config_print_detailed_minmax_vel, 6721-6943 */
+#define MPAS_DYC_PRINT_GLOBAL_MINMAX_SCA 4   /* config_print_global_minmax_sca, 6986-7016 */
+
+/* One located extreme of the detailed mode: the value, the level and the lat/lon in degrees of
+ * the first owned element (cell-major, level-minor) holding it, as the reference's loops find it,
+ * reduced over ranks as mpas_dmpar_min/maxattributes_real does (MPI_MINLOC / MPI_MAXLOC per
+ * attribute, mpas_dmpar.F:1090-1160).  lon is shifted to (-180, 180] as at 6771-6773. */
+typedef struct {
+  double value, lat, lon;
+  int32_t k;      /* 1-based level (kMax_global); -1 if no element */
+  int32_t index;  /* 1-based local index on its block (indexMax); -1 if no element */
+} mpas_dyc_extreme;
+
+typedef struct {
+  int32_t flags;                     /* the modes the values below were reduced for */
+  double w_min, w_max, u_min, u_max; /* global_minmax_vel: min/max over owned w, u starting from 0.0 */
+  mpas_dyc_extreme w_min_at, w_max_at, u_min_at, u_max_at, wsp_max_at; /* detailed_minmax_vel */
+  int64_t nan_w, nan_u;              /* NaNs in the owned w, u (the detailed mode aborts on any, 6926-6940) */
+} mpas_dyc_summary;
+
+/* Modes reduced by every following step (default MPAS_DYC_PRINT_GLOBAL_MINMAX_VEL; 0 = none). */
+int mpas_dyc_set_summary(mpas_dyc_ctx* ctx, int32_t flags);
+/* The last step's summary over all blocks and ranks (collective when ranks share a communicator:
+ * every rank calls it after the same step).  Waits for the step.  scalar_minmax (may be NULL)
+ * receives num_scalars (min, max) pairs of the global_minmax_sca mode; n = its length in doubles. */
+int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scalar_minmax, int32_t n);
+
 /* ---- domain decomposition: several blocks per process, halo exchange ----
  *
  * A context holds the blocks this process owns (MPAS domain%blocklist; one per

@@ -18,6 +18,7 @@
 #include "../../include/mpas_dycore.h"
 #include "kernels.hip"
 #include "halo.hip"
+#include "summary.hip"
 
 using namespace mpas;
 
@@ -59,6 +60,9 @@ struct Block {
   int* d_adv_tcell = nullptr;
   unsigned char* d_adv_loc = nullptr;
   std::vector<int32_t> h_coe, h_eoc, h_noc;  // host copies (0-based) for the halo-boundary flags
+  // summarize_timestep records (summary.hip): partials and one SUM_REC record per field
+  double* sum_part = nullptr;
+  double* sum_out = nullptr;
 };
 
 // One RCCL message of an exchange point: a contiguous range of the process-wide send or receive buffer.
@@ -117,6 +121,11 @@ struct mpas_dyc_ctx {
   int overlap = -1;                     // 1 on, 0 off, -1 auto: on when exchanges go through RCCL
   bool bnd_ready = false;
   int physics = 0;                      // MPAS_DYC_PHYSICS_* flags (mpas_dyc_set_physics)
+  // summarize_timestep: MPAS_DYC_PRINT_* modes reduced at the end of every step (the namelist
+  // default is config_print_global_minmax_vel = true, Registry.xml:339)
+  int summary_flags = MPAS_DYC_PRINT_GLOBAL_MINMAX_VEL;
+  int summary_tl = 0;                   // time level the records describe (0: none yet)
+  double* sum_gather = nullptr;         // RCCL all-gather buffer of the per-rank records
 };
 
 namespace {
@@ -193,7 +202,7 @@ void build_registry(Block& c) {
   add(c, "mesh", "edgesOnVertex", L_VERTEX, 3, 1, true, T_EDGE);
   // mesh: geometry
   for (const char* n : {"dcEdge", "dvEdge", "invDcEdge", "invDvEdge", "fEdge", "meshScalingDel2",
-                        "meshScalingDel4", "specZoneMaskEdge", "angleEdge"})
+                        "meshScalingDel4", "specZoneMaskEdge", "angleEdge", "latEdge", "lonEdge"})
     add(c, "mesh", n, L_EDGE, 1);
   for (const char* n : {"invAreaCell", "specZoneMaskCell", "latCell", "lonCell"}) add(c, "mesh", n, L_CELL, 1);
   add(c, "mesh", "coeffs_reconstruct", L_CELL, 3 * (int64_t)ME);
@@ -1048,6 +1057,63 @@ std::vector<Ptrs> block_ptrs(mpas_dyc_ctx* ctx) {
   return P;
 }
 
+// summarize_timestep (1794 -> 6675-7018): the fields its enabled modes reduce, on time level
+// `tl` of block b.  0 = w, 1 = u (with v for the wind speed in detailed mode), 2.. = scalars.
+std::vector<SumField> summary_fields(mpas_dyc_ctx* ctx, Block& b, int tl) {
+  const Dims& d = b.d;
+  const int fl = ctx->summary_flags;
+  std::vector<SumField> fs;
+  const bool vel = fl & (MPAS_DYC_PRINT_GLOBAL_MINMAX_VEL | MPAS_DYC_PRINT_DETAILED_MINMAX_VEL);
+  const bool det = fl & MPAS_DYC_PRINT_DETAILED_MINMAX_VEL;
+  SumField w{}, u{};
+  w.a = P<const double>(ctx, b, "state", "w", tl);
+  w.ncol = vel ? d.nCellsSolve : 0;
+  w.K = d.K;
+  w.stride = d.K + 1;
+  u.a = P<const double>(ctx, b, "state", "u", tl);
+  u.ncol = vel ? d.nEdgesSolve : 0;
+  u.K = d.K;
+  u.stride = d.K;
+  if (det) {
+    w.lat = P<const double>(ctx, b, "mesh", "latCell");
+    w.lon = P<const double>(ctx, b, "mesh", "lonCell");
+    u.v = P<const double>(ctx, b, "diag", "v");
+    u.lat = P<const double>(ctx, b, "mesh", "latEdge");
+    u.lon = P<const double>(ctx, b, "mesh", "lonEdge");
+  }
+  fs.push_back(w);
+  fs.push_back(u);
+  const double* sc = P<const double>(ctx, b, "state", "scalars", tl);
+  for (int is = 0; is < d.ns; ++is) {
+    SumField s{};
+    s.a = sc + (size_t)is * (d.nCells + 1) * d.K;  // scalar-major [ns][nCells+1][K]
+    s.ncol = (fl & MPAS_DYC_PRINT_GLOBAL_MINMAX_SCA) ? d.nCellsSolve : 0;
+    s.K = d.K;
+    s.stride = d.K;
+    fs.push_back(s);
+  }
+  return fs;
+}
+
+// the device half of summarize_timestep: per-block records in Block::sum_out (mpas_dyc_get_summary
+// folds blocks and ranks)
+int summary_launch(mpas_dyc_ctx* ctx, int tl) {
+  if (!ctx->summary_flags || ctx->planning) return MPAS_DYC_OK;
+  for (auto& b : ctx->blk) {
+    const std::vector<SumField> fs = summary_fields(ctx, b, tl);
+    for (size_t f0 = 0; f0 < fs.size(); f0 += SUM_MAX_FIELDS) {
+      const int nf = (int)std::min<size_t>(SUM_MAX_FIELDS, fs.size() - f0);
+      SumFields sf{};
+      for (int i = 0; i < nf; ++i) sf.f[i] = fs[f0 + i];
+      hipLaunchKernelGGL(k_summary_partial, dim3(SUM_PARTS, nf), dim3(256), 0, ctx->stream, sf, b.sum_part);
+      hipLaunchKernelGGL(k_summary_final, dim3(nf), dim3(256), 0, ctx->stream, sf, b.sum_part, SUM_PARTS,
+                         b.sum_out + f0 * SUM_REC);
+    }
+  }
+  ctx->summary_tl = tl;
+  return MPAS_DYC_OK;
+}
+
 // run `body(d, p)` for every block (the reference's `block => domain % blocklist` loops)
 #define EACH(...)                                       \
   for (size_t ib_ = 0; ib_ < ctx->blk.size(); ++ib_) {  \
@@ -1291,7 +1357,8 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
                            dim3(256), 0, ctx->stream, ::P<double>(ctx, b, "state", "scalars", 2), n);
     }
   }
-  // summarize_timestep (1794) only logs: outside the hot path.
+  // summarize_timestep (1794): the reductions on the device, the log lines on the host
+  CHK(summary_launch(ctx, 2));
   return MPAS_DYC_OK;
 }
 
@@ -1494,6 +1561,12 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
       }
       if (is_host_0d(f)) f.buf[1] = new double(0.0);  // host mirror of the 0-d field
     }
+    const size_t nf = 2 + (size_t)b.d.ns;
+    if (hipMalloc(&b.sum_part, (size_t)SUM_MAX_FIELDS * SUM_PARTS * SUM_REC * sizeof(double)) != hipSuccess ||
+        hipMalloc(&b.sum_out, nf * SUM_REC * sizeof(double)) != hipSuccess) {
+      mpas_dyc_destroy(ctx);
+      return MPAS_DYC_EHIP;
+    }
   }
   *out = ctx;
   return MPAS_DYC_OK;
@@ -1517,7 +1590,10 @@ void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
     for (auto& x : b.xl)
       if (x.d_idx) (void)hipFree(x.d_idx);
     free_adv_tiles(b);
+    if (b.sum_part) (void)hipFree(b.sum_part);
+    if (b.sum_out) (void)hipFree(b.sum_out);
   }
+  if (ctx->sum_gather) (void)hipFree(ctx->sum_gather);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1788,6 +1864,122 @@ int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name
   int r = exchange(ctx, {{sp.c_str(), sn.c_str(), time_level, (unsigned)layer_mask}});
   if (r) return r;
   HIPCHK(hipGetLastError());
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_set_summary(mpas_dyc_ctx* ctx, int32_t flags) {
+  const int all = MPAS_DYC_PRINT_GLOBAL_MINMAX_VEL | MPAS_DYC_PRINT_DETAILED_MINMAX_VEL | MPAS_DYC_PRINT_GLOBAL_MINMAX_SCA;
+  if (!ctx || (flags & ~all)) return MPAS_DYC_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->summary_flags = flags;
+  ctx->summary_tl = 0;
+  for (int i = 0; i < 2; ++i) {  // captured steps bake the modes in
+    if (ctx->graph_exec[i]) (void)hipGraphExecDestroy(ctx->graph_exec[i]);
+    ctx->graph_exec[i] = nullptr;
+  }
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scalar_minmax, int32_t n) {
+  if (!ctx || !out) return MPAS_DYC_EINVAL;
+  const int ns = ctx->blk[0].d.ns;
+  if (scalar_minmax && n < 2 * ns) return MPAS_DYC_EINVAL;
+  if (!ctx->summary_flags || !ctx->summary_tl) {
+    ctx->err = "no summary: no step has run with summary modes on (mpas_dyc_set_summary)";
+    return MPAS_DYC_ESTATE;
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  // Per field a payload of three located extremes (min, max, wind-speed max), each
+  // (value, index, k, lat, lon) as the reference's localVals, then min0, max0, NaN count.
+  const int nf = 2 + ns, PL = 18;
+  std::vector<double> pay((size_t)nf * PL);
+  auto fold = [&](double* acc, const double* x) {
+    for (int e = 0; e < 3; ++e) {  // MPI_MINLOC / MPI_MAXLOC per attribute (mpas_dmpar.F:1106, 1154)
+      double* a = acc + 5 * e;
+      const double* b = x + 5 * e;
+      const bool is_min = e == 0;
+      if (is_min ? b[0] < a[0] : b[0] > a[0]) {
+        for (int i = 0; i < 5; ++i) a[i] = b[i];
+      } else if (b[0] == a[0]) {
+        for (int i = 1; i < 5; ++i) a[i] = std::min(a[i], b[i]);
+      }
+    }
+    acc[15] = std::min(acc[15], x[15]);
+    acc[16] = std::max(acc[16], x[16]);
+    acc[17] += x[17];
+  };
+  for (size_t ib = 0; ib < ctx->blk.size(); ++ib) {
+    Block& b = ctx->blk[ib];
+    std::vector<double> rec((size_t)nf * SUM_REC);
+    HIPCHK(hipMemcpy(rec.data(), b.sum_out, rec.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int f = 0; f < nf; ++f) {
+      const double* r = &rec[(size_t)f * SUM_REC];
+      double x[PL];
+      auto ext = [&](double* o, double v, double idx, double lat, double lon) {
+        const long long i = (long long)idx;
+        o[0] = v;
+        o[1] = i >= 0 ? (double)(i / b.d.K + 1) : -1.0;  // indexMax
+        o[2] = i >= 0 ? (double)(i % b.d.K + 1) : -1.0;  // kMax
+        o[3] = lat;
+        o[4] = lon;
+      };
+      ext(x, r[SR_MIN], r[SR_IMIN], r[SR_LAT_MIN], r[SR_LON_MIN]);
+      ext(x + 5, r[SR_MAX], r[SR_IMAX], r[SR_LAT_MAX], r[SR_LON_MAX]);
+      ext(x + 10, r[SR_SPD], r[SR_ISPD], r[SR_LAT_SPD], r[SR_LON_SPD]);
+      x[15] = r[SR_MIN0];
+      x[16] = r[SR_MAX0];
+      x[17] = r[SR_NAN];
+      double* acc = &pay[(size_t)f * PL];
+      if (ib == 0) std::copy(x, x + PL, acc);
+      else fold(acc, x);
+    }
+  }
+  if (ctx->comm && ctx->nranks > 1) {
+    // all ranks' payloads to every rank (RCCL all-gather, in place), folded in rank order
+    const size_t cnt = pay.size();
+    if (!ctx->sum_gather) HIPCHK(hipMalloc(&ctx->sum_gather, cnt * ctx->nranks * sizeof(double)));
+    HIPCHK(hipMemcpy(ctx->sum_gather + cnt * ctx->rank, pay.data(), cnt * sizeof(double), hipMemcpyHostToDevice));
+    NCCLCHK(ncclAllGather(ctx->sum_gather + cnt * ctx->rank, ctx->sum_gather, cnt, ncclFloat64, ctx->comm, ctx->stream));
+    std::vector<double> all(cnt * ctx->nranks);
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(all.data(), ctx->sum_gather, all.size() * sizeof(double), hipMemcpyDeviceToHost));
+    std::copy(all.begin(), all.begin() + cnt, pay.begin());
+    for (int r = 1; r < ctx->nranks; ++r)
+      for (int f = 0; f < nf; ++f) fold(&pay[(size_t)f * PL], &all[cnt * r + (size_t)f * PL]);
+  }
+  const double pi_const = 2.0 * asin(1.0);
+  auto located = [&](const double* x) {
+    mpas_dyc_extreme e;
+    e.value = x[0];
+    e.index = (int32_t)x[1];
+    e.k = (int32_t)x[2];
+    e.lat = x[3] * 180.0 / pi_const;  // 6769-6773
+    e.lon = x[4] * 180.0 / pi_const;
+    if (e.lon > 180.0) e.lon = e.lon - 360.0;
+    return e;
+  };
+  *out = mpas_dyc_summary{};
+  out->flags = ctx->summary_flags;
+  const double* w = &pay[0];
+  const double* u = &pay[PL];
+  out->w_min = w[15];
+  out->w_max = w[16];
+  out->u_min = u[15];
+  out->u_max = u[16];
+  out->w_min_at = located(w);
+  out->w_max_at = located(w + 5);
+  out->u_min_at = located(u);
+  out->u_max_at = located(u + 5);
+  out->wsp_max_at = located(u + 10);
+  out->nan_w = (int64_t)w[17];
+  out->nan_u = (int64_t)u[17];
+  if (scalar_minmax)
+    for (int is = 0; is < ns; ++is) {
+      scalar_minmax[2 * is] = pay[(size_t)(2 + is) * PL + 15];
+      scalar_minmax[2 * is + 1] = pay[(size_t)(2 + is) * PL + 16];
+    }
   return MPAS_DYC_OK;
 }
 

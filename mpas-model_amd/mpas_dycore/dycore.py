@@ -24,7 +24,7 @@ from .layout import LOC_N, to_fortran
 STATE_INPUTS = ("u", "w", "scalars")
 DIAG_INPUTS = ("theta", "rho", "rho_base", "theta_base")
 _SKIP = set(STATE_INPUTS) | set(DIAG_INPUTS) | {"xCell", "yCell", "zCell", "xEdge", "yEdge", "zEdge", "xVertex",
-                                                "yVertex", "zVertex", "latEdge", "lonEdge",
+                                                "yVertex", "zVertex",
                                                 "latVertex", "lonVertex", "areaCell", "areaTriangle",
                                                 "meshDensity", "indexToCellID", "deriv_two", "zb", "zb3"}
 
@@ -187,6 +187,48 @@ class Dycore:
     def output_diagnostics(self, time_level: int = 1):
         """atm_compute_output_diagnostics (mpas_atm_core.F:753-800): diag theta, rho, pressure."""
         self._check(self.lib.mpas_dyc_output_diagnostics(self.h, int(time_level)), "output_diagnostics")
+
+    def set_summary(self, global_minmax_vel: bool = True, detailed_minmax_vel: bool = False,
+                    global_minmax_sca: bool = False):
+        """The namelist switches of summarize_timestep (Registry.xml:339-349): which reductions
+        every following step performs at its end (mpas_atm_time_integration.F:1794)."""
+        flags = ((_lib.PRINT_GLOBAL_MINMAX_VEL if global_minmax_vel else 0)
+                 | (_lib.PRINT_DETAILED_MINMAX_VEL if detailed_minmax_vel else 0)
+                 | (_lib.PRINT_GLOBAL_MINMAX_SCA if global_minmax_sca else 0))
+        self._check(self.lib.mpas_dyc_set_summary(self.h, flags), "set_summary")
+
+    def summarize_timestep(self, log=None) -> dict:
+        """summarize_timestep (mpas_atm_time_integration.F:6675-7018) of the last step: the global
+        extrema over all blocks and ranks, and the reference's log lines (passed to ``log`` if given).
+        In detailed mode a NaN in w or u raises DycoreError, as the reference aborts (6926-6940)."""
+        s = _lib.Summary()
+        mm = (C.c_double * (2 * self.ns))()
+        self._check(self.lib.mpas_dyc_get_summary(self.h, C.byref(s), mm, 2 * self.ns), "summarize_timestep")
+        out = {"flags": s.flags, "w_min": s.w_min, "w_max": s.w_max, "u_min": s.u_min, "u_max": s.u_max,
+               "nan_w": s.nan_w, "nan_u": s.nan_u, "scalars": [(mm[2 * i], mm[2 * i + 1]) for i in range(self.ns)]}
+        for n in ("w_min_at", "w_max_at", "u_min_at", "u_max_at", "wsp_max_at"):
+            e = getattr(s, n)
+            out[n] = {"value": e.value, "k": e.k, "index": e.index, "lat": e.lat, "lon": e.lon}
+        lines = []
+        if s.flags & _lib.PRINT_DETAILED_MINMAX_VEL:
+            lines.append("")
+            for n, tag in (("w_min_at", "min w"), ("w_max_at", "max w"), ("u_min_at", "min u"),
+                           ("u_max_at", "max u"), ("wsp_max_at", "max wsp")):
+                e = out[n]
+                lines.append(f" global {tag}: {e['value']} k={e['k']}, {e['lat']} lat, {e['lon']} lon")
+        elif s.flags & _lib.PRINT_GLOBAL_MINMAX_VEL:
+            lines += ["", f"global min, max w {s.w_min} {s.w_max}", f"global min, max u {s.u_min} {s.u_max}"]
+        if s.flags & _lib.PRINT_GLOBAL_MINMAX_SCA:
+            if not s.flags & (_lib.PRINT_GLOBAL_MINMAX_VEL | _lib.PRINT_DETAILED_MINMAX_VEL):
+                lines.append("")
+            lines += [f" global min, max scalar {i + 1} {a} {b}" for i, (a, b) in enumerate(out["scalars"])]
+        out["log"] = lines
+        if log is not None:
+            for ln in lines:
+                log(ln)
+        if s.flags & _lib.PRINT_DETAILED_MINMAX_VEL and (s.nan_w or s.nan_u):
+            raise DycoreError("NaN detected in '" + ("w" if s.nan_w else "u") + "' field.")
+        return out
 
     def shift_time_levels(self):
         self._check(self.lib.mpas_dyc_shift_time_levels(self.h), "shift_time_levels")

@@ -288,7 +288,8 @@ program mpas_ref_harness
    character(len=32) :: mode
    integer :: kernel_small_step, kernel_rk_step
    real(kind=RKIND) :: kernel_dts
-   namelist /harness/ mode, kernel_small_step, kernel_rk_step, kernel_dts, nCells, nEdges, nVertices, nVertLevels_in, maxEdges_in, maxEdges2_in, num_scalars_in, &
+   integer :: print_minmax   ! summarize_timestep switches: 1 global_minmax_vel, 2 detailed_minmax_vel, 4 global_minmax_sca
+   namelist /harness/ mode, print_minmax, kernel_small_step, kernel_rk_step, kernel_dts, nCells, nEdges, nVertices, nVertLevels_in, maxEdges_in, maxEdges2_in, num_scalars_in, &
       nsteps, moist_end, nthreads_req, dump_steps, dt, sphere_radius, &
       config_time_integration_order, config_number_of_sub_steps, config_dynamics_split_steps, &
       config_number_rayleigh_damp_u_levels, config_split_dynamics_transport, config_scalar_advection, &
@@ -321,6 +322,7 @@ program mpas_ref_harness
    kernel_small_step = 2
    kernel_rk_step = 1
    kernel_dts = 0.0_RKIND
+   print_minmax = 0
    open(newunit=u, file=trim(indir)//'/harness.nml', status='old')
    read(u, nml=harness)
    close(u)
@@ -401,9 +403,9 @@ program mpas_ref_harness
    call mpas_pool_add_config_char(configs, 'config_IAU_option', 'off')
    call mpas_pool_add_config_char(configs, 'config_microp_scheme', 'off')
    call mpas_pool_add_config_char(configs, 'config_convection_scheme', trim(config_convection_scheme))
-   call mpas_pool_add_config_logical(configs, 'config_print_global_minmax_vel', .false.)
-   call mpas_pool_add_config_logical(configs, 'config_print_detailed_minmax_vel', .false.)
-   call mpas_pool_add_config_logical(configs, 'config_print_global_minmax_sca', .false.)
+   call mpas_pool_add_config_logical(configs, 'config_print_global_minmax_vel', iand(print_minmax, 1) /= 0)
+   call mpas_pool_add_config_logical(configs, 'config_print_detailed_minmax_vel', iand(print_minmax, 2) /= 0)
+   call mpas_pool_add_config_logical(configs, 'config_print_global_minmax_sca', iand(print_minmax, 4) /= 0)
 
    ! ---- subpools ----
    call mpas_pool_create_pool(mesh)

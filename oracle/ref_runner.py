@@ -64,7 +64,7 @@ def write_physics_inputs(case: dict, d: str, physics: dict):
 
 
 def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthreads: int = 0,
-                 moist_end: int = 1, convection_scheme: str = "off"):
+                 moist_end: int = 1, convection_scheme: str = "off", print_minmax: int = 0):
     F = _fields()
     os.makedirs(d, exist_ok=True)
     names = [n for n in case if n in F.LOCATION or n in F.VERTICAL_1D or n in F.SCALARS_0D]
@@ -109,6 +109,8 @@ def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthr
  config_horiz_mixing='{cfg['config_horiz_mixing']}', config_convection_scheme='{convection_scheme}'
 /
 """
+    if print_minmax:
+        nml = nml.replace("&harness\n", f"&harness\n print_minmax={print_minmax},\n")
     nml = nml.replace("e+", "d+").replace("e-", "d-")
     with open(os.path.join(d, "harness.nml"), "w") as f:
         f.write(nml)
@@ -145,11 +147,13 @@ def read_dump(case: dict, stepdir: str) -> dict:
 
 def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads: int = 0,
                   workdir: str | None = None, moist_end: int = 1, timeout: int = 3000, binary: str = HARNESS,
-                  physics: dict | None = None):
+                  physics: dict | None = None, print_minmax: int = 0):
     """Run the reference dycore; returns ({step: {field: array}}, [step wall times]).
     ``binary=DROPIN_HARNESS`` runs the same driver on the drop-in module instead.
     ``physics`` (dict of write_physics_inputs' arrays, optional key "convection_scheme") runs the
-    DO_PHYSICS build with those tendencies handed over by physics_get_tend every step."""
+    DO_PHYSICS build with those tendencies handed over by physics_get_tend every step.
+    ``print_minmax`` turns on summarize_timestep's namelist switches (1 global_minmax_vel,
+    2 detailed_minmax_vel, 4 global_minmax_sca); the reference's log text is then res["log"]."""
     if physics is not None:
         binary = PHYS_HARNESS
     if not available(binary):
@@ -160,7 +164,7 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     tmp = tempfile.mkdtemp(prefix="mpasref_") if own else workdir
     ind, outd = os.path.join(tmp, "in"), os.path.join(tmp, "out")
     write_inputs(case, ind, nsteps, dt, dump_steps, nthreads, moist_end,
-                 (physics or {}).get("convection_scheme", "off"))
+                 (physics or {}).get("convection_scheme", "off"), print_minmax)
     if physics is not None:
         write_physics_inputs(case, ind, physics)
     env = dict(os.environ)
@@ -173,6 +177,9 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     for s in dump_steps:
         sd = os.path.join(outd, f"step_{s:04d}")
         res[s] = read_dump(case, sd)
+    if print_minmax:
+        logs = sorted(fn for fn in os.listdir(tmp) if fn.startswith("log.") and fn.endswith(".out"))
+        res["log"] = "".join(open(os.path.join(tmp, fn)).read() for fn in logs)
     times = []
     with open(os.path.join(outd, "timing.txt")) as f:
         for line in f:
