@@ -50,17 +50,28 @@ def cpu_baseline(case, dt, nthreads, steps, moist_end=1):
     use = times[1:] if len(times) > 1 else times  # first step pays allocation / first-touch
     t = sum(use) / len(use)
     return dict(value=case["nCells"] * case["nVertLevels"] / t, unit="cell-updates/s", cores=nthreads,
-                kind="reference",
+                kind="reference", cpu_model=_cpu_model(),
                 sample=f"unmodified reference atm_srk3 (amdflang -O2, OpenMP {nthreads} threads) on the same "
-                       f"x1.{case['nCells']} x {case['nVertLevels']} JW case: {steps} dt steps, mean of steps "
-                       f"2..{steps} ({t:.2f} s/step)")
+                       f"{case['nCells']}-cell x {case['nVertLevels']} JW case: {steps} dt steps, mean of the "
+                       f"{len(use)} timed steps 2..{steps} ({t:.2f} s/step)")
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def small_mesh_line(args, torch, device, ncells=10242, steps=20, warmup=3):
     from mpas_dycore import Dycore
     from mpas_dycore.cases import jw_case
     ns = 6 if args.moist else 1
-    case = jw_case(ncells, K=args.levels, ns=ns, moist=args.moist)
+    case = jw_case(ncells, K=args.levels, ns=ns, moist=args.moist, order=args.order)
     dt = case["dt"]
     dy = Dycore(case, device=device, moist_end=ns if args.moist else 1)
     dy.init_diagnostics(dt)
@@ -112,7 +123,9 @@ def main():
                     help="BASELINE.json configs[3]: moist JW (qv) + tracer blobs, num_scalars=6, monotone transport")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=4, help="reference steps; the first is untimed")
+    ap.add_argument("--order", type=int, default=3, choices=(2, 3),
+                    help="config_time_integration_order of the synthetic cases (SURVEY.md §8d: 3)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--acoustic-reps", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=1, help="blocks per GPU (MPAS blocks with halos)")
@@ -146,7 +159,7 @@ def main():
         if args.varres:
             from mpas_dycore.cases import varres_case
             return varres_case(args.varres, ratio=20.0, K=args.levels, ns=args.num_scalars, moist=args.moist)
-        return jw_case(args.ncells, K=args.levels, ns=args.num_scalars, moist=args.moist)
+        return jw_case(args.ncells, K=args.levels, ns=args.num_scalars, moist=args.moist, order=args.order)
 
     t_build = time.time()
     if rank == 0:
@@ -202,10 +215,17 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    graph = dy.graph_active()
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # every rank replays its captured step, or none does (the library refuses a per-rank
+        # eager fallback with more than one rank; this checks the outcome)
+        g = torch.tensor([int(graph), -int(graph)], dtype=torch.int64)
+        dist.all_reduce(g, op=dist.ReduceOp.MAX)
+        if int(g[0]) != -int(g[1]):
+            raise SystemExit("hipGraph replay differs between ranks")
     ms_per_step = elapsed / args.steps * 1e3
     # strong scaling: the whole x1.N mesh is advanced once per step, whatever the rank count
     value = case["nCells"] * case["nVertLevels"] / (ms_per_step / 1e3)
@@ -261,7 +281,7 @@ def main():
             "parallelism": (f"domain decomposition: {nparts} SFC blocks with 2-layer halos, "
                             f"{args.blocks} per GPU, halo exchange over RCCL" if nparts > 1 else "single block"),
             "owned_cells_rank0": owned, "halo_cells_rank0": halo,
-            "hip_graph": not args.no_graph,
+            "hip_graph": graph,
         },
         "roofline": {
             "kernel": "acoustic sub-step (k_acoustic_edges<damped> + k_acoustic_cells; per sub-step of an "

@@ -69,7 +69,8 @@ typedef struct {
 } mpas_dyc_config;
 
 /* Create a dycore context on HIP device `device` (-1 = current); allocates all
- * device fields (mesh, state x2 time levels, diag, tend, module scratch). */
+ * device fields (mesh, state x2 time levels, diag, tend, module scratch).
+ * device = MPAS_DYC_HOST_ONLY: a planner-only context (see mpas_dyc_plan_exchanges). */
 int mpas_dyc_create(const mpas_dyc_dims* dims, const mpas_dyc_config* cfg, int device, mpas_dyc_ctx** out);
 void mpas_dyc_destroy(mpas_dyc_ctx* ctx);
 const char* mpas_dyc_last_error(const mpas_dyc_ctx* ctx);
@@ -194,6 +195,40 @@ int mpas_dyc_set_overlap(mpas_dyc_ctx* ctx, int32_t on);
 /* mpas_dmpar_exch_halo_field(field, haloLayers) for one field; layer_mask bit l-1 = layer l. */
 int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level,
                            int32_t layer_mask);
+
+/* ---- exchange-plan dry run (no device) ----
+ * `device` = MPAS_DYC_HOST_ONLY in mpas_dyc_create(_blocks) makes a context that holds dims,
+ * config and exchange lists but no device memory, stream or communicator.  Only
+ * mpas_dyc_set_exchange_list, mpas_dyc_set_overlap / _set_transport and
+ * mpas_dyc_plan_exchanges work on it (field calls return MPAS_DYC_ESTATE).  It lets a host
+ * check, before any GPU is touched, that the RCCL messages every rank will post match: rank r's
+ * sends to rank p at an exchange point must be rank p's receives from r there, in the same
+ * order and of the same sizes (what ncclGroupStart/End requires, mpas_dmpar.F:5386-5552). */
+#define MPAS_DYC_HOST_ONLY (-2)
+
+/* One RCCL message of an exchange point, as the step posts it. */
+typedef struct {
+  int32_t point;      /* 0-based index of the exchange call in issue order (see below) */
+  int32_t direction;  /* MPAS_DYC_SEND (ncclSend) / MPAS_DYC_RECV (ncclRecv) */
+  int32_t block;      /* local block that packs / unpacks it */
+  int32_t peer_rank, peer_block;
+  int64_t count;      /* doubles */
+} mpas_dyc_plan_msg;
+
+/* Run the exchange planner as rank `rank` of `nranks` over the calls one model run issues, in
+ * order: the model-init exchanges (mpas_dyc_init_diagnostics), then one atm_srk3 on each
+ * time-level parity (a step, mpas_dyc_shift_time_levels, a step).  Writes up to `cap` messages
+ * (each point's sends, then its receives, in posting order) and sets *n_msgs to the number
+ * needed; writes the calls' plan keys, one per line in issue order, into keys[keys_bytes]
+ * (NUL-terminated) and sets *keys_len to the bytes needed.  Returns MPAS_DYC_EINVAL when
+ * either buffer was too small (the counts are still set). */
+int mpas_dyc_plan_exchanges(mpas_dyc_ctx* ctx, int32_t nranks, int32_t rank, double dt, mpas_dyc_plan_msg* msgs,
+                            int64_t cap, int64_t* n_msgs, char* keys, int64_t keys_bytes, int64_t* keys_len);
+
+/* 1 if the last mpas_dyc_timestep replayed a captured hipGraph, 0 if it ran eagerly.  With more
+ * than one rank a failed capture is an error (MPAS_DYC_EHIP), never a per-rank eager fallback:
+ * one eager rank would add ~280 launches per dt to every exchange wait of the others. */
+int mpas_dyc_graph_active(const mpas_dyc_ctx* ctx);
 
 /* ---- measurement hooks (bench.py / tests) ---- */
 /* A `reps`-sub-step acoustic loop (atm_advance_acoustic_step + atm_divergence_damping_3d per

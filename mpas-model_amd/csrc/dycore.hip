@@ -99,12 +99,14 @@ struct mpas_dyc_ctx {
   Config cf{};
   int index_qv = 0;
   int device = 0;
+  bool host_only = false;               // MPAS_DYC_HOST_ONLY: planner only, no device state
   hipStream_t stream = nullptr;
   std::vector<Block> blk;
   int cur = 0;                          // time level 1 -> buf[cur], 2 -> buf[1-cur]
   std::string err;
   hipEvent_t ev[8] = {};
   bool use_graph = false;
+  bool graph_ran = false;               // the last step replayed a captured graph
   hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
   double graph_dt[2] = {0, 0};
   // halo exchange
@@ -114,6 +116,7 @@ struct mpas_dyc_ctx {
   bool planning = false;                // dry run: build exchange plans, launch nothing
   bool planned[2] = {false, false};
   std::map<std::string, XPlan> plans;
+  std::vector<std::string>* record = nullptr;  // mpas_dyc_plan_exchanges: keys of the calls, in order
   // split-phase exchanges: packs, RCCL and unpacks run on the exchange stream while the
   // compute stream works on elements that read no halo data
   hipStream_t xstream = nullptr;
@@ -412,7 +415,7 @@ void free_plan(XPlan& pl) {
 }
 
 void invalidate_plans(mpas_dyc_ctx* ctx) {
-  (void)hipStreamSynchronize(ctx->stream);
+  if (!ctx->host_only) (void)hipStreamSynchronize(ctx->stream);
   for (auto& kv : ctx->plans) free_plan(kv.second);
   ctx->plans.clear();
   ctx->planned[0] = ctx->planned[1] = false;
@@ -540,10 +543,19 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
       if (!local && rtotal > start) pl.rrecv.push_back(XMsg{bi, pr.first, pr.second, start, rtotal - start});
     }
   }
-  if ((!pl.rsend.empty() || !pl.rrecv.empty()) && !ctx->comm) {
+  if ((!pl.rsend.empty() || !pl.rrecv.empty()) && !ctx->comm && !ctx->host_only) {
     ctx->err = "exchange lists name other processes but no communicator was set (mpas_dyc_comm_init)";
     return MPAS_DYC_ECOMM;
   }
+  // point-to-point messages between two ranks match in issue order: order both sides by
+  // (source block, destination block)
+  std::sort(pl.rsend.begin(), pl.rsend.end(), [](const XMsg& a, const XMsg& b) {
+    return std::make_tuple(a.peer_rank, a.block, a.peer_block) < std::make_tuple(b.peer_rank, b.block, b.peer_block);
+  });
+  std::sort(pl.rrecv.begin(), pl.rrecv.end(), [](const XMsg& a, const XMsg& b) {
+    return std::make_tuple(a.peer_rank, a.peer_block, a.block) < std::make_tuple(b.peer_rank, b.peer_block, b.block);
+  });
+  if (ctx->host_only) return MPAS_DYC_OK;  // the dry run keeps the message lists only
   if (stotal) HIPCHK(hipMalloc(&pl.sendbuf, stotal * sizeof(double)));
   if (rtotal) HIPCHK(hipMalloc(&pl.recvbuf, rtotal * sizeof(double)));
   for (size_t i = 0; i < pre.size(); ++i)
@@ -559,24 +571,17 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
     HIPCHK(hipMalloc(&pl.d_post, post.size() * sizeof(XSeg)));
     HIPCHK(hipMemcpy(pl.d_post, post.data(), post.size() * sizeof(XSeg), hipMemcpyHostToDevice));
   }
-  // point-to-point messages between two ranks match in issue order: order both sides by
-  // (source block, destination block)
-  std::sort(pl.rsend.begin(), pl.rsend.end(), [](const XMsg& a, const XMsg& b) {
-    return std::make_tuple(a.peer_rank, a.block, a.peer_block) < std::make_tuple(b.peer_rank, b.block, b.peer_block);
-  });
-  std::sort(pl.rrecv.begin(), pl.rrecv.end(), [](const XMsg& a, const XMsg& b) {
-    return std::make_tuple(a.peer_rank, a.peer_block, a.block) < std::make_tuple(b.peer_rank, b.peer_block, b.block);
-  });
   return MPAS_DYC_OK;
 }
 
 int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   if (!needs_exchange(ctx)) return MPAS_DYC_OK;
   const std::string key = plan_key(ctx, fs);
+  if (ctx->record) ctx->record->push_back(key);
   auto it = ctx->plans.find(key);
   if (it == ctx->plans.end()) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(ctx->stream, &cs);
+    if (!ctx->host_only) (void)hipStreamIsCapturing(ctx->stream, &cs);
     if (cs != hipStreamCaptureStatusNone) {
       ctx->err = "internal: exchange plan missing during graph capture";
       return MPAS_DYC_ESTATE;
@@ -1522,6 +1527,12 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
     delete ctx;
     return MPAS_DYC_EINVAL;
   }
+  if (device == MPAS_DYC_HOST_ONLY) {  // planner only: registry and dims, nothing on a device
+    ctx->host_only = true;
+    for (auto& b : ctx->blk) build_registry(b);
+    *out = ctx;
+    return MPAS_DYC_OK;
+  }
   if (device >= 0 && hipSetDevice(device) != hipSuccess) {
     delete ctx;
     return MPAS_DYC_EHIP;
@@ -1578,6 +1589,10 @@ int mpas_dyc_create(const mpas_dyc_dims* dims, const mpas_dyc_config* cfg, int d
 
 void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
   if (!ctx) return;
+  if (ctx->host_only) {
+    delete ctx;
+    return;
+  }
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   invalidate_plans(ctx);
@@ -1636,6 +1651,10 @@ void* mpas_dyc_field_device_ptr(mpas_dyc_ctx* ctx, const char* pool, const char*
 int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name,
                              int32_t time_level, const void* host, int64_t nbytes) {
   if (!ctx || !pool || !name || !host) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) {
+    ctx->err = "host-only context holds no fields";
+    return MPAS_DYC_ESTATE;
+  }
   Block* bp = get_block(ctx, block);
   if (!bp) {
     ctx->err = "no block " + std::to_string(block);
@@ -1722,6 +1741,10 @@ int mpas_dyc_set_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, in
 int mpas_dyc_get_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool, const char* name,
                              int32_t time_level, void* host, int64_t nbytes) {
   if (!ctx || !pool || !name || !host) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) {
+    ctx->err = "host-only context holds no fields";
+    return MPAS_DYC_ESTATE;
+  }
   Block* bp = get_block(ctx, block);
   if (!bp) {
     ctx->err = "no block " + std::to_string(block);
@@ -1809,12 +1832,12 @@ int mpas_dyc_set_exchange_list(mpas_dyc_ctx* ctx, int32_t block, int32_t locatio
     b.xl.push_back(XList{location, halo_layer, direction, peer_rank, peer_block});
     x = &b.xl.back();
   }
-  if (x->d_idx) {
+  if (x->d_idx && !ctx->host_only) {
     HIPCHK(hipFree(x->d_idx));
     x->d_idx = nullptr;
   }
   x->n = n;
-  if (n > 0) {
+  if (n > 0 && !ctx->host_only) {
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipMalloc(&x->d_idx, n * sizeof(int32_t)));
     HIPCHK(hipMemcpy(x->d_idx, idx.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -1835,6 +1858,7 @@ int64_t mpas_dyc_comm_unique_id_bytes(void) { return (int64_t)sizeof(ncclUniqueI
 int mpas_dyc_comm_init(mpas_dyc_ctx* ctx, const void* id, int64_t nbytes, int32_t nranks, int32_t rank) {
   if (!ctx || !id || nbytes < (int64_t)sizeof(ncclUniqueId) || nranks < 1 || rank < 0 || rank >= nranks)
     return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   invalidate_plans(ctx);
   if (ctx->comm) {
@@ -1859,6 +1883,7 @@ int mpas_dyc_set_transport(mpas_dyc_ctx* ctx, int32_t rccl_for_local_blocks) {
 int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level,
                            int32_t layer_mask) {
   if (!ctx || !pool || !name || layer_mask <= 0 || layer_mask > 7) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   std::string sp(pool), sn(name);
   int r = exchange(ctx, {{sp.c_str(), sn.c_str(), time_level, (unsigned)layer_mask}});
@@ -1870,6 +1895,7 @@ int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name
 int mpas_dyc_set_summary(mpas_dyc_ctx* ctx, int32_t flags) {
   const int all = MPAS_DYC_PRINT_GLOBAL_MINMAX_VEL | MPAS_DYC_PRINT_DETAILED_MINMAX_VEL | MPAS_DYC_PRINT_GLOBAL_MINMAX_SCA;
   if (!ctx || (flags & ~all)) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   ctx->summary_flags = flags;
@@ -1883,6 +1909,7 @@ int mpas_dyc_set_summary(mpas_dyc_ctx* ctx, int32_t flags) {
 
 int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scalar_minmax, int32_t n) {
   if (!ctx || !out) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   const int ns = ctx->blk[0].d.ns;
   if (scalar_minmax && n < 2 * ns) return MPAS_DYC_EINVAL;
   if (!ctx->summary_flags || !ctx->summary_tl) {
@@ -1985,6 +2012,7 @@ int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scala
 
 int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
   if (!ctx) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
   int r = init_diagnostics(ctx, dt);
@@ -1994,6 +2022,7 @@ int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
 
 int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags) {
   if (!ctx || (flags & ~(MPAS_DYC_PHYSICS_TENDENCIES | MPAS_DYC_PHYSICS_RQVDYNTEN))) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   if ((flags & MPAS_DYC_PHYSICS_RQVDYNTEN) && !(flags & MPAS_DYC_PHYSICS_TENDENCIES)) return MPAS_DYC_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -2008,6 +2037,7 @@ int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags) {
 
 int mpas_dyc_output_diagnostics(mpas_dyc_ctx* ctx, int32_t time_level) {
   if (!ctx || (time_level != 1 && time_level != 2)) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   for (auto& b : ctx->blk) {
     const Ptrs p = make_ptrs(ctx, b);
@@ -2021,6 +2051,7 @@ int mpas_dyc_output_diagnostics(mpas_dyc_ctx* ctx, int32_t time_level) {
 int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
   (void)itimestep;
   if (!ctx || !(dt > 0.0)) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   CHK(plan_all(ctx, dt));
   if (ctx->use_graph) {
@@ -2037,10 +2068,16 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
       if (e == hipSuccess) e = hipGraphInstantiate(&ctx->graph_exec[parity], g, nullptr, nullptr, 0);
       if (g) (void)hipGraphDestroy(g);
       if (e != hipSuccess) {
-        // a runtime that cannot capture this step (e.g. its RCCL calls) runs it eagerly
         (void)hipGetLastError();
         ctx->graph_exec[parity] = nullptr;
+        if (ctx->nranks > 1) {  // every rank captures or the job fails: no rank goes eager alone
+          ctx->err = std::string("hipGraph capture of the step failed on rank ") + std::to_string(ctx->rank) + ": " +
+                     hipGetErrorString(e);
+          return MPAS_DYC_EHIP;
+        }
+        // one process: a runtime that cannot capture this step runs it eagerly, and says so
         ctx->use_graph = false;
+        ctx->graph_ran = false;
         fprintf(stderr, "mpas_dycore: hipGraph capture failed (%s); running the step eagerly\n",
                 hipGetErrorString(e));
         r = srk3(ctx, dt);
@@ -2050,11 +2087,66 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
       ctx->graph_dt[parity] = dt;
     }
     HIPCHK(hipGraphLaunch(ctx->graph_exec[parity], ctx->stream));
+    ctx->graph_ran = true;
     return MPAS_DYC_OK;
   }
+  ctx->graph_ran = false;
   int r = srk3(ctx, dt);
   HIPCHK(hipGetLastError());
   return r;
+}
+
+int mpas_dyc_graph_active(const mpas_dyc_ctx* ctx) { return ctx && ctx->graph_ran ? 1 : 0; }
+
+int mpas_dyc_plan_exchanges(mpas_dyc_ctx* ctx, int32_t nranks, int32_t rank, double dt, mpas_dyc_plan_msg* msgs,
+                            int64_t cap, int64_t* n_msgs, char* keys, int64_t keys_bytes, int64_t* keys_len) {
+  if (!ctx || !n_msgs || !keys_len || nranks < 1 || rank < 0 || rank >= nranks || !(dt > 0.0) || cap < 0 ||
+      keys_bytes < 0)
+    return MPAS_DYC_EINVAL;
+  if (!ctx->host_only) {
+    ctx->err = "mpas_dyc_plan_exchanges needs a MPAS_DYC_HOST_ONLY context";
+    return MPAS_DYC_ESTATE;
+  }
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  invalidate_plans(ctx);
+  std::vector<std::string> seq;
+  ctx->record = &seq;
+  ctx->planning = true;
+  const int cur0 = ctx->cur;
+  int r = init_diagnostics(ctx, dt);
+  for (int step = 0; step < 2 && r == MPAS_DYC_OK; ++step) {
+    r = srk3(ctx, dt);
+    ctx->cur ^= 1;  // mpas_dyc_shift_time_levels
+  }
+  ctx->cur = cur0;
+  ctx->planning = false;
+  ctx->record = nullptr;
+  if (r) return r;
+  int64_t nm = 0, kl = 1;
+  for (size_t i = 0; i < seq.size(); ++i) {
+    const XPlan& pl = ctx->plans.at(seq[i]);
+    for (int dir = 0; dir < 2; ++dir)
+      for (const XMsg& m : dir == 0 ? pl.rsend : pl.rrecv) {
+        if (msgs && nm < cap)
+          msgs[nm] = mpas_dyc_plan_msg{(int32_t)i, dir == 0 ? MPAS_DYC_SEND : MPAS_DYC_RECV, m.block, m.peer_rank,
+                                       m.peer_block, m.count};
+        ++nm;
+      }
+    kl += (int64_t)seq[i].size() + 1;
+  }
+  *n_msgs = nm;
+  *keys_len = kl;
+  if (keys && kl <= keys_bytes) {
+    char* q = keys;
+    for (const auto& k : seq) {
+      memcpy(q, k.data(), k.size());
+      q += k.size();
+      *q++ = '\n';
+    }
+    *q = '\0';
+  }
+  return (nm > cap || kl > keys_bytes) ? MPAS_DYC_EINVAL : MPAS_DYC_OK;
 }
 
 int mpas_dyc_shift_time_levels(mpas_dyc_ctx* ctx) {
@@ -2065,6 +2157,7 @@ int mpas_dyc_shift_time_levels(mpas_dyc_ctx* ctx) {
 
 int mpas_dyc_synchronize(mpas_dyc_ctx* ctx) {
   if (!ctx) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->xstream));
@@ -2097,6 +2190,7 @@ double mpas_dyc_acoustic_bytes(const mpas_dyc_ctx* ctx) {
 int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_step, int32_t reps, double* ms_out,
                                 double* ms_kernels) {
   if (!ctx || reps < 1) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
   Block& b = ctx->blk[0];

@@ -20,8 +20,10 @@ EXPORTS = (
     "mpas_dyc_get_block_field", "mpas_dyc_block_field_bytes", "mpas_dyc_block_field_device_ptr",
     "mpas_dyc_set_exchange_list", "mpas_dyc_comm_unique_id_bytes", "mpas_dyc_comm_unique_id", "mpas_dyc_comm_init",
     "mpas_dyc_set_transport", "mpas_dyc_halo_exchange", "mpas_dyc_set_overlap", "mpas_dyc_output_diagnostics",
-    "mpas_dyc_set_physics", "mpas_dyc_set_summary", "mpas_dyc_get_summary",
+    "mpas_dyc_set_physics", "mpas_dyc_set_summary", "mpas_dyc_get_summary", "mpas_dyc_plan_exchanges",
+    "mpas_dyc_graph_active",
 )
+HOST_ONLY = -2  # MPAS_DYC_HOST_ONLY: planner-only context
 PRINT_GLOBAL_MINMAX_VEL, PRINT_DETAILED_MINMAX_VEL, PRINT_GLOBAL_MINMAX_SCA = 1, 2, 4
 CELL, EDGE, VERTEX = 0, 1, 2
 SEND, RECV = 0, 1
@@ -57,6 +59,11 @@ class Summary(C.Structure):
     _fields_ = ([("flags", C.c_int32)] + [(n, C.c_double) for n in ("w_min", "w_max", "u_min", "u_max")]
                 + [(n, Extreme) for n in ("w_min_at", "w_max_at", "u_min_at", "u_max_at", "wsp_max_at")]
                 + [("nan_w", C.c_int64), ("nan_u", C.c_int64)])
+
+
+class PlanMsg(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("point", "direction", "block", "peer_rank", "peer_block")] + [
+        ("count", C.c_int64)]
 
 
 def make_config(cfg: dict) -> Config:
@@ -122,5 +129,8 @@ def load() -> C.CDLL:
     lib.mpas_dyc_set_overlap.argtypes = [vp, i32]
     lib.mpas_dyc_set_summary.argtypes = [vp, i32]
     lib.mpas_dyc_get_summary.argtypes = [vp, C.POINTER(Summary), C.POINTER(dbl), i32]
+    lib.mpas_dyc_plan_exchanges.argtypes = [vp, i32, i32, dbl, C.POINTER(PlanMsg), i64, C.POINTER(i64), C.c_char_p,
+                                            i64, C.POINTER(i64)]
+    lib.mpas_dyc_graph_active.argtypes = [vp]
     _lib = lib
     return lib

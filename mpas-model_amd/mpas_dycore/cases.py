@@ -20,6 +20,17 @@ CACHE = os.environ.get("MPAS_DYCORE_CACHE", "/tmp/mpas_dycore_cache")
 
 LEVEL_OF = {162: 2, 642: 3, 2562: 4, 10242: 5, 40962: 6, 163842: 7, 655362: 8}
 
+# the last mesh built in this process: the dry and moist cases of one resolution share it
+_MESH_MEMO: dict = {}
+
+
+def _mesh(level: int, lloyd_iters: int) -> dict:
+    key = (level, lloyd_iters)
+    if key not in _MESH_MEMO:
+        _MESH_MEMO.clear()
+        _MESH_MEMO[key] = build_mesh(level, lloyd_iters=lloyd_iters)
+    return _MESH_MEMO[key]
+
 
 def level_for(ncells: int) -> int:
     return LEVEL_OF[ncells]
@@ -41,7 +52,7 @@ def jw_case(ncells: int, K: int = 56, ns: int = 1, moist: bool = False, order: i
     if cache and os.path.isfile(path):
         with open(path, "rb") as f:  # our own cache file, written below
             return pickle.load(f)
-    m = build_mesh(level, lloyd_iters=lloyd_iters)
+    m = _mesh(level, lloyd_iters)
     cfg = dict(config_len_disp=jw_len_disp(level), config_dt=jw_dt(level), config_time_integration_order=order)
     case = build_case(m, K=K, ns=ns, moist=moist, config=cfg)
     case["dt"] = jw_dt(level)

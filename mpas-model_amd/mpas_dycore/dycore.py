@@ -33,6 +33,69 @@ class DycoreError(RuntimeError):
     pass
 
 
+def _make_dims(cases, solves, moist_end):
+    dims = (_lib.Dims * len(cases))()
+    for d, c, sv in zip(dims, cases, solves):
+        d.nCells, d.nEdges, d.nVertices = c["nCells"], c["nEdges"], c["nVertices"]
+        d.nVertLevels, d.maxEdges, d.maxEdges2 = c["nVertLevels"], c["maxEdges"], c["maxEdges2"]
+        d.num_scalars = c["num_scalars"]
+        if sv is None:
+            sv = (c["nCells"], c["nEdges"], c["nVertices"])
+        d.nCellsSolve, d.nEdgesSolve, d.nVerticesSolve = (int(x) for x in sv)
+        d.moist_start, d.moist_end, d.index_qv = 1, moist_end, 1
+    return dims
+
+
+def _install_lists(lib, h, blocks, placement, check):
+    """Every block's send / receive lists (mpas_multihalo_exchange_list) into the context."""
+    code = {"cell": _lib.CELL, "edge": _lib.EDGE, "vertex": _lib.VERTEX}
+    for ib, b in enumerate(blocks):
+        for direction, lists in ((_lib.SEND, b.send), (_lib.RECV, b.recv)):
+            for loc, layer, peer, idx in lists:
+                pr, pb = placement[peer]
+                a = np.ascontiguousarray(np.asarray(idx, dtype=np.int32) + 1)
+                check(lib.mpas_dyc_set_exchange_list(h, ib, code[loc], int(layer), direction, int(pr), int(pb),
+                                                     a.ctypes.data_as(C.c_void_p), int(a.size)), "set_exchange_list")
+
+
+def plan_exchanges(blocks: list, placement: dict, rank: int, nranks: int, dt: float, moist_end: int = 1,
+                   overlap: bool | None = None) -> tuple[np.ndarray, list[str]]:
+    """Dry run of the exchange planner for one rank, on the host (no GPU): the RCCL messages
+    this rank posts over model init and one step on each time-level parity, and the plan key of
+    every exchange call in issue order (mpas_dyc_plan_exchanges).  Messages are a structured array
+    with fields point, direction (_lib.SEND / _lib.RECV), block, peer_rank, peer_block, count."""
+    lib = _lib.load()
+    cases = [b.case for b in blocks]
+    dims = _make_dims(cases, [b.solve for b in blocks], moist_end)
+    cfg = _lib.make_config(cases[0]["config"])
+    h = C.c_void_p()
+    rc = lib.mpas_dyc_create_blocks(len(cases), dims, C.byref(cfg), _lib.HOST_ONLY, C.byref(h))
+    if rc != 0 or not h.value:
+        raise DycoreError(f"mpas_dyc_create_blocks(HOST_ONLY) failed ({rc})")
+
+    def check(r, what):
+        if r != 0:
+            msg = lib.mpas_dyc_last_error(h)
+            raise DycoreError(f"{what} failed ({r}): {msg.decode() if msg else ''}")
+    try:
+        _install_lists(lib, h, blocks, placement, check)
+        check(lib.mpas_dyc_set_overlap(h, -1 if overlap is None else int(bool(overlap))), "set_overlap")
+        nm, kl = C.c_int64(), C.c_int64()
+        lib.mpas_dyc_plan_exchanges(h, int(nranks), int(rank), float(dt), None, 0, C.byref(nm), None, 0,
+                                    C.byref(kl))
+        msgs = (_lib.PlanMsg * max(1, nm.value))()
+        keys = C.create_string_buffer(kl.value)
+        check(lib.mpas_dyc_plan_exchanges(h, int(nranks), int(rank), float(dt), msgs, nm.value, C.byref(nm), keys,
+                                          kl.value, C.byref(kl)), "plan_exchanges")
+        dt_msg = np.dtype([("point", "<i4"), ("direction", "<i4"), ("block", "<i4"), ("peer_rank", "<i4"),
+                           ("peer_block", "<i4"), ("count", "<i8")], align=True)
+        assert dt_msg.itemsize == C.sizeof(_lib.PlanMsg)
+        arr = np.frombuffer(bytes(msgs), dtype=dt_msg)[:nm.value].copy()
+        return arr, keys.value.decode().splitlines()
+    finally:
+        lib.mpas_dyc_destroy(h)
+
+
 class Dycore:
     """The blocks of this process on one GPU (MPAS domain%blocklist).
 
@@ -52,15 +115,7 @@ class Dycore:
         self.nblocks = len(cases)
         self.nb = [{"cell": c["nCells"], "edge": c["nEdges"], "vertex": c["nVertices"]} for c in cases]
         self.n = self.nb[0]
-        dims = (_lib.Dims * len(cases))()
-        for d, c, sv in zip(dims, cases, solves):
-            d.nCells, d.nEdges, d.nVertices = c["nCells"], c["nEdges"], c["nVertices"]
-            d.nVertLevels, d.maxEdges, d.maxEdges2 = self.K, c["maxEdges"], c["maxEdges2"]
-            d.num_scalars = self.ns
-            if sv is None:
-                sv = (c["nCells"], c["nEdges"], c["nVertices"])
-            d.nCellsSolve, d.nEdgesSolve, d.nVerticesSolve = (int(x) for x in sv)
-            d.moist_start, d.moist_end, d.index_qv = 1, moist_end, 1
+        dims = _make_dims(cases, solves, moist_end)
         cfg = _lib.make_config(self.case["config"])
         h = C.c_void_p()
         rc = self.lib.mpas_dyc_create_blocks(len(cases), dims, C.byref(cfg), int(device), C.byref(h))
@@ -86,16 +141,12 @@ class Dycore:
             self._check(self.lib.mpas_dyc_comm_init(self.h, idb, len(comm_id), int(nranks), int(rank)), "comm_init")
         if rccl_local:
             self._check(self.lib.mpas_dyc_set_transport(self.h, 1), "set_transport")
-        code = {"cell": _lib.CELL, "edge": _lib.EDGE, "vertex": _lib.VERTEX}
-        for ib, b in enumerate(blocks):
-            for direction, lists in ((_lib.SEND, b.send), (_lib.RECV, b.recv)):
-                for loc, layer, peer, idx in lists:
-                    pr, pb = placement[peer]
-                    a = np.ascontiguousarray(np.asarray(idx, dtype=np.int32) + 1)
-                    self._check(self.lib.mpas_dyc_set_exchange_list(self.h, ib, code[loc], int(layer), direction,
-                                                                    int(pr), int(pb), a.ctypes.data_as(C.c_void_p),
-                                                                    int(a.size)), "set_exchange_list")
+        _install_lists(self.lib, self.h, blocks, placement, self._check)
         return self
+
+    def graph_active(self) -> bool:
+        """True if the last step replayed its captured hipGraph (False: it ran eagerly)."""
+        return bool(self.lib.mpas_dyc_graph_active(self.h))
 
     @staticmethod
     def comm_unique_id() -> bytes:

@@ -29,6 +29,8 @@ module harness_fields
    implicit none
 
    character(len=256) :: indir, outdir
+   ! comma-separated 'pool.name' list; when not blank only these fields are dumped (full-size runs)
+   character(len=1024) :: dump_only = ''
    type (block_type), pointer :: hblock => null()
 
    integer, parameter :: MAXF = 400
@@ -228,6 +230,9 @@ contains
       call execute_command_line('mkdir -p '//trim(dir))
       do i = 1, nf
          if (fisint(i)) cycle
+         if (len_trim(dump_only) > 0) then
+            if (index(','//trim(dump_only)//',', ','//trim(fpool(i))//'.'//trim(fname(i))//',') == 0) cycle
+         end if
          call mpas_pool_get_subpool(hblock % structs, trim(fpool(i)), p)
          do t = 1, fntl(i)
             tl = ''
@@ -289,7 +294,7 @@ program mpas_ref_harness
    integer :: kernel_small_step, kernel_rk_step
    real(kind=RKIND) :: kernel_dts
    integer :: print_minmax   ! summarize_timestep switches: 1 global_minmax_vel, 2 detailed_minmax_vel, 4 global_minmax_sca
-   namelist /harness/ mode, print_minmax, kernel_small_step, kernel_rk_step, kernel_dts, nCells, nEdges, nVertices, nVertLevels_in, maxEdges_in, maxEdges2_in, num_scalars_in, &
+   namelist /harness/ mode, print_minmax, dump_only, kernel_small_step, kernel_rk_step, kernel_dts, nCells, nEdges, nVertices, nVertLevels_in, maxEdges_in, maxEdges2_in, num_scalars_in, &
       nsteps, moist_end, nthreads_req, dump_steps, dt, sphere_radius, &
       config_time_integration_order, config_number_of_sub_steps, config_dynamics_split_steps, &
       config_number_rayleigh_damp_u_levels, config_split_dynamics_transport, config_scalar_advection, &

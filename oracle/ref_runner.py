@@ -29,6 +29,15 @@ DROPIN_HARNESS = os.path.join(HERE, "_ref", "mpas_dropin_harness")
 _LOC_N = {"cell": "nCells", "edge": "nEdges", "vertex": "nVertices"}
 
 
+def _big_stack():
+    import resource
+    _, hard = resource.getrlimit(resource.RLIMIT_STACK)
+    try:
+        resource.setrlimit(resource.RLIMIT_STACK, (hard, hard))
+    except (ValueError, OSError):
+        pass
+
+
 def available(binary: str = HARNESS) -> bool:
     return os.path.isfile(binary) and os.access(binary, os.X_OK)
 
@@ -64,7 +73,8 @@ def write_physics_inputs(case: dict, d: str, physics: dict):
 
 
 def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthreads: int = 0,
-                 moist_end: int = 1, convection_scheme: str = "off", print_minmax: int = 0):
+                 moist_end: int = 1, convection_scheme: str = "off", print_minmax: int = 0,
+                 dump_only=()):
     F = _fields()
     os.makedirs(d, exist_ok=True)
     names = [n for n in case if n in F.LOCATION or n in F.VERTICAL_1D or n in F.SCALARS_0D]
@@ -111,6 +121,8 @@ def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthr
 """
     if print_minmax:
         nml = nml.replace("&harness\n", f"&harness\n print_minmax={print_minmax},\n")
+    if dump_only:
+        nml = nml.replace("&harness\n", f"&harness\n dump_only='{','.join(dump_only)}',\n")
     nml = nml.replace("e+", "d+").replace("e-", "d-")
     with open(os.path.join(d, "harness.nml"), "w") as f:
         f.write(nml)
@@ -147,11 +159,12 @@ def read_dump(case: dict, stepdir: str) -> dict:
 
 def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads: int = 0,
                   workdir: str | None = None, moist_end: int = 1, timeout: int = 3000, binary: str = HARNESS,
-                  physics: dict | None = None, print_minmax: int = 0):
+                  physics: dict | None = None, print_minmax: int = 0, dump_only=()):
     """Run the reference dycore; returns ({step: {field: array}}, [step wall times]).
     ``binary=DROPIN_HARNESS`` runs the same driver on the drop-in module instead.
     ``physics`` (dict of write_physics_inputs' arrays, optional key "convection_scheme") runs the
     DO_PHYSICS build with those tendencies handed over by physics_get_tend every step.
+    ``dump_only`` (e.g. ["state.u", "state.w"]) limits the dumps to those fields (full-size runs).
     ``print_minmax`` turns on summarize_timestep's namelist switches (1 global_minmax_vel,
     2 detailed_minmax_vel, 4 global_minmax_sca); the reference's log text is then res["log"]."""
     if physics is not None:
@@ -164,13 +177,17 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     tmp = tempfile.mkdtemp(prefix="mpasref_") if own else workdir
     ind, outd = os.path.join(tmp, "in"), os.path.join(tmp, "out")
     write_inputs(case, ind, nsteps, dt, dump_steps, nthreads, moist_end,
-                 (physics or {}).get("convection_scheme", "off"), print_minmax)
+                 (physics or {}).get("convection_scheme", "off"), print_minmax, dump_only)
     if physics is not None:
         write_physics_inputs(case, ind, physics)
     env = dict(os.environ)
     if nthreads:
         env["OMP_NUM_THREADS"] = str(nthreads)
-    r = subprocess.run([binary, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout)
+    # the reference's automatic arrays (nCells-sized locals in the *_work routines) live on the
+    # stack: large meshes need the main thread's stack unlimited and big OpenMP thread stacks
+    env.setdefault("OMP_STACKSIZE", "1G")
+    r = subprocess.run([binary, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout,
+                       preexec_fn=_big_stack)
     if r.returncode != 0:
         raise RuntimeError(f"{os.path.basename(binary)} failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
     res = {}

@@ -1,0 +1,152 @@
+"""GPU parity at BASELINE.json's full sizes: configs[2], [3] and [4] at their own meshes.
+
+north_star bar: relative L-infinity <= 1e-10 on u / theta_m / rho_zz after 10 RK3 steps vs the
+reference Fortran dycore on the same mesh and initial state (w and the mixing ratios <= 1e-9,
+relative to their own maximum).  The oracle is the unmodified reference atm_srk3
+(oracle/_ref/mpas_ref_harness, built from /root/reference by oracle/Makefile; it travels to the
+box as a binary) run on the GPU box's host cores, 16 OpenMP threads.
+
+  * configs[2]: x1.163842 x 56, dry JW, dt = 360 s, config_time_integration_order = 3:
+    10 steps vs the reference; the same mesh as 8 MPAS blocks exchanging through RCCL
+    (send/recv to self, split-phase) -- the 8-GPU decomposition on one device -- bitwise equal
+    to the one-block run;
+  * configs[3]: the same mesh, num_scalars = 6 (all moist species), monotone split transport,
+    10 steps vs the reference;
+  * configs[4]: variable-resolution SCVT, 835586 cells, 20x refinement, 56 levels: 2 steps vs the
+    reference, and 8 RCCL blocks (irregular halos) bitwise equal to one block.
+
+Cases are built on the box (about a minute at 163842, a few at 835586) and cached under
+$MPAS_DYCORE_CACHE (default /tmp/mpas_dycore_cache), where bench.py finds them too.
+Progress lines go to the real stderr so a long run shows it is alive.
+"""
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from conftest import rel_linf
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+PROG = [("state", "u", "state.u.tl1", "edge"), ("state", "theta_m", "state.theta_m.tl1", "cell"),
+        ("state", "rho_zz", "state.rho_zz.tl1", "cell"), ("state", "w", "state.w.tl1", "cell"),
+        ("state", "scalars", "state.scalars.tl1", "cell")]
+DUMP = ["state.u", "state.theta_m", "state.rho_zz", "state.w", "state.scalars"]
+TOL = 1e-10          # u, theta_m, rho_zz (north_star)
+TOL_LOOSE = 1e-9     # w and the mixing ratios
+_T0 = time.time()
+
+
+def progress(msg):
+    print(f"[full-configs {time.time() - _T0:7.1f}s] {msg}", file=sys.__stderr__, flush=True)
+
+
+def _reference(case, nsteps, moist_end=1):
+    from oracle import ref_runner
+    if not ref_runner.available():
+        pytest.skip("oracle/_ref not built")
+    progress(f"reference: {nsteps} steps on {case['nCells']} cells")
+    res, times = ref_runner.run_reference(case, nsteps=nsteps, dt=float(case["dt"]), dump_steps=[nsteps],
+                                          nthreads=16, moist_end=moist_end, dump_only=DUMP)
+    progress(f"reference done, s/step {np.round(times, 2).tolist()}")
+    return res[nsteps]
+
+
+def _check(got, ref):
+    errs = {key: rel_linf(got[key].reshape(ref[key].shape), ref[key]) for key in got}
+    bad = {k: v for k, v in errs.items()
+           if not v <= (TOL if k in ("state.u.tl1", "state.theta_m.tl1", "state.rho_zz.tl1") else TOL_LOOSE)}
+    assert not bad, f"rel Linf above tolerance: {bad} (all: {errs})"
+    progress(f"rel Linf vs reference {errs}")
+    return errs
+
+
+def _run(dy, dt, nsteps):
+    dy.init_diagnostics(dt)
+    dy.use_graph(True)
+    for it in range(nsteps):
+        dy.atm_timestep(dt, it + 1)
+        dy.shift_time_levels()
+    dy.synchronize()
+
+
+def _single(case, nsteps, moist_end=1):
+    from mpas_dycore import Dycore
+    dy = Dycore(case, device=0, moist_end=moist_end)
+    _run(dy, float(case["dt"]), nsteps)
+    out = {key: dy.get(pool, name, 1) for pool, name, key, _ in PROG}
+    dy.close()
+    progress(f"GPU one block: {nsteps} steps")
+    return out
+
+
+def _blocks_rccl(case, nblocks, nsteps, single, moist_end=1):
+    """nblocks MPAS blocks on one device, every block-to-block halo message through RCCL (send to
+    self), split-phase exchanges on: bitwise equal to the one-block run."""
+    from mpas_dycore import Dycore, decomp
+    blocks = decomp.decompose(case, decomp.partition_sfc(case["nCells"], nblocks))
+    dy = Dycore.from_blocks(blocks, device=0, comm_id=Dycore.comm_unique_id(), nranks=1, rank=0,
+                            rccl_local=True, moist_end=moist_end)
+    dy.set_overlap(True)
+    _run(dy, float(case["dt"]), nsteps)
+    n_glob = {"cell": case["nCells"], "edge": case["nEdges"]}
+    for pool, name, key, loc in PROG:
+        per = [dy.get(pool, name, 1, block=i) for i in range(len(blocks))]
+        got = decomp.gather_owned(blocks, per, loc, n_glob[loc])
+        assert np.array_equal(got, single[key]), f"{key}: {nblocks} RCCL blocks differ from one block"
+    dy.close()
+    progress(f"{nblocks} RCCL blocks bitwise equal to one block")
+
+
+# ---------------------------------------------------------------- configs[2]: x1.163842 x 56 dry
+
+@pytest.fixture(scope="module")
+def dry163842():
+    from mpas_dycore.cases import jw_case
+    progress("building x1.163842 x 56 dry case (order 3)")
+    c = jw_case(163842, K=56, ns=1, order=3)
+    assert c["config"]["config_time_integration_order"] == 3
+    return c
+
+
+@pytest.fixture(scope="module")
+def dry163842_gpu(dry163842):
+    return _single(dry163842, 10)
+
+
+def test_configs2_x1_163842_L56_dry_10_steps_matches_reference(dry163842, dry163842_gpu):
+    _check(dry163842_gpu, _reference(dry163842, 10))
+
+
+def test_configs2_x1_163842_L56_eight_rccl_blocks_bitwise(dry163842, dry163842_gpu):
+    _blocks_rccl(dry163842, 8, 10, dry163842_gpu)
+
+
+# ---------------------------------------------------------------- configs[3]: moist ns=6, monotone
+
+def test_configs3_x1_163842_L56_moist_ns6_mono_10_steps_matches_reference():
+    from mpas_dycore.cases import jw_case
+    progress("building x1.163842 x 56 moist ns=6 case (order 3)")
+    c = jw_case(163842, K=56, ns=6, moist=True, order=3)
+    assert c["config"]["config_monotonic"] and c["num_scalars"] == 6
+    got = _single(c, 10, moist_end=6)
+    _check(got, _reference(c, 10, moist_end=6))
+
+
+# ---------------------------------------------------------------- configs[4]: var-res ~835586
+
+@pytest.fixture(scope="module")
+def varres835586():
+    from mpas_dycore.cases import varres_case
+    progress("building the 835586-cell variable-resolution case (20x)")
+    c = varres_case(835586, ratio=20.0, K=56, ns=1)
+    assert c["maxEdges"] == 7
+    return c
+
+
+def test_configs4_varres_835586_L56_2_steps_matches_reference_and_8_blocks(varres835586):
+    c = varres835586
+    got = _single(c, 2)
+    _check(got, _reference(c, 2))
+    _blocks_rccl(c, 8, 2, got)

@@ -1,0 +1,109 @@
+"""The multi-process RCCL path, checked on the host before any GPU runs it.
+
+Every rank of an N-GPU run (bench.py --gpus N: one block per rank, SFC partition) builds its
+exchange plans with the library's own planner in a host-only context (MPAS_DYC_HOST_ONLY,
+mpas_dyc_plan_exchanges) over what a run issues: the model-init exchanges and one atm_srk3 on
+each time-level parity.  For N = 2, 4, 8 on the x1.163842 mesh this asserts what ncclGroupStart /
+ncclGroupEnd needs across ranks (the reference's MPI_Isend/MPI_Irecv pairs, mpas_dmpar.F:5386-5552):
+
+  * every rank issues the same exchange calls in the same order (same plan keys), so the
+    captured graphs and warm_rccl (plans in key order) line up;
+  * at every call, rank r's ncclSend list to rank p equals rank p's ncclRecv list from r:
+    same messages (source block -> destination block), same order, same element counts;
+  * the counts are the sizes of the exchange lists decomp.py built for that pair.
+"""
+import numpy as np
+import pytest
+
+from mpas_dycore import _lib, decomp
+from mpas_dycore.dycore import plan_exchanges
+
+
+@pytest.fixture(scope="module")
+def case163842():
+    from mpas_dycore.cases import jw_case
+    return jw_case(163842, K=56, ns=1, order=3)
+
+
+def _plans(case, nranks, overlap=None):
+    cell_part = decomp.partition_sfc(case["nCells"], nranks)
+    out = []
+    for r in range(nranks):
+        blocks, placement = decomp.rank_blocks(case, nranks, r, 1, cell_part=cell_part)
+        out.append(plan_exchanges(blocks, placement, r, nranks, float(case["dt"]), overlap=overlap))
+    return out
+
+
+def _check_matching(plans, nranks):
+    keys0 = plans[0][1]
+    assert len(keys0) > 40
+    for r in range(nranks):
+        assert plans[r][1] == keys0, f"rank {r} issues a different exchange sequence"
+    npts = len(keys0)
+    nmsg = 0
+    for r in range(nranks):
+        sends = plans[r][0][plans[r][0]["direction"] == _lib.SEND]
+        for p in range(nranks):
+            recvs = plans[p][0][plans[p][0]["direction"] == _lib.RECV]
+            for i in range(npts):
+                s = sends[(sends["point"] == i) & (sends["peer_rank"] == p)]
+                v = recvs[(recvs["point"] == i) & (recvs["peer_rank"] == r)]
+                # the RCCL pairing: the k-th send r->p matches the k-th receive at p from r
+                assert len(s) == len(v), f"point {i} ({keys0[i]}): {len(s)} sends {r}->{p}, {len(v)} receives"
+                assert np.array_equal(s["count"], v["count"]), f"point {i}: message sizes {r}->{p} differ"
+                assert np.array_equal(s["peer_block"], v["block"]) and np.array_equal(s["block"], v["peer_block"])
+                nmsg += len(s)
+    return nmsg
+
+
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_rank_plans_match_x1_163842(case163842, nranks):
+    plans = _plans(case163842, nranks)
+    nmsg = _check_matching(plans, nranks)
+    assert nmsg > 0
+    # a rank never messages itself with one block per rank
+    for r in range(nranks):
+        assert not np.any(plans[r][0]["peer_rank"] == r)
+
+
+def test_message_sizes_are_the_exchange_lists(case163842):
+    """The step-start exchange (theta_m, scalars, pressure_p, rtheta_p, exner over all layers,
+    mpas_atm_time_integration.F:329-338 + 513) of rank 0 sends, per peer, 5 cell fields of K
+    levels over every cell this rank lists for that peer."""
+    nranks = 4
+    case = case163842
+    cell_part = decomp.partition_sfc(case["nCells"], nranks)
+    blocks, placement = decomp.rank_blocks(case, nranks, 0, 1, cell_part=cell_part)
+    msgs, keys = plan_exchanges(blocks, placement, 0, nranks, float(case["dt"]))
+    i = next(j for j, k in enumerate(keys) if "state.theta_m" in k and "diag.exner" in k and "diag.pv_edge" not in k)
+    K = case["nVertLevels"]
+    send = decomp.messages(blocks[0], "send", layers=(1, 2), locs=("cell",))
+    got = msgs[(msgs["point"] == i) & (msgs["direction"] == _lib.SEND)]
+    assert sorted(got["peer_rank"].tolist()) == sorted(placement[p][0] for p in send)
+    for part, idx in send.items():
+        pr, pb = placement[part]
+        m = got[(got["peer_rank"] == pr) & (got["peer_block"] == pb)]
+        assert len(m) == 1 and m["count"][0] == 5 * K * idx.size
+
+
+def test_plans_match_without_split_phase(case163842):
+    plans = _plans(case163842, 2, overlap=False)
+    assert _check_matching(plans, 2) > 0
+
+
+def test_host_only_context_refuses_device_calls(case163842):
+    import ctypes as C
+    lib = _lib.load()
+    c = case163842
+    from mpas_dycore.dycore import _make_dims
+    dims = _make_dims([c], [None], 1)
+    cfg = _lib.make_config(c["config"])
+    h = C.c_void_p()
+    assert lib.mpas_dyc_create_blocks(1, dims, C.byref(cfg), _lib.HOST_ONLY, C.byref(h)) == 0
+    try:
+        assert lib.mpas_dyc_timestep(h, 1.0, 1) == -3
+        assert lib.mpas_dyc_init_diagnostics(h, 1.0) == -3
+        buf = np.zeros(8)
+        assert lib.mpas_dyc_set_field(h, b"mesh", b"cf1", 1, buf.ctypes.data_as(C.c_void_p), 8) == -3
+    finally:
+        lib.mpas_dyc_destroy(h)
