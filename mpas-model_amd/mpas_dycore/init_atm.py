@@ -26,6 +26,8 @@ from __future__ import annotations
 
 import os
 
+import math
+
 import numpy as np
 
 from .reconstruct import init_reconstruct
@@ -94,91 +96,236 @@ def _jw_hx(phi, r_earth):
                + (1.6 * np.cos(phi) ** 3 * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * r_earth * OMEGA))
 
 
-def _local_frame(c):
-    ez = np.array([0.0, 0.0, 1.0])
-    e1 = np.cross(ez, c)
-    bad = np.linalg.norm(e1, axis=-1) < 1e-8
-    if np.any(bad):
-        e1[bad] = np.cross(np.array([1.0, 0.0, 0.0]), c[bad])
-    e1 = _normalize(e1)
-    e2 = np.cross(c, e1)
-    return e1, e2
+# ---- the reference's spherical geometry (core_init_atmosphere/mpas_atm_advection.F:397-537),
+# elementwise over arrays of points (..., 3); same expressions, same evaluation order.
+# asin / acos go through the C library (math.asin / math.acos), as the compiled Fortran does:
+# numpy's own arcsin / arccos differ from it in the last bit for ~8 % of arguments, which the
+# ill-conditioned least-squares fits of deriv_two amplify to ~1e-8.
+_LIBM_ASIN = np.frompyfunc(math.asin, 1, 1)
+_LIBM_ACOS = np.frompyfunc(math.acos, 1, 1)
 
 
-def _azimuth(c, p, e1, e2):
-    d = p - c
-    return np.arctan2(np.sum(d * e2, -1), np.sum(d * e1, -1))
+_LIBM_POW = np.frompyfunc(math.pow, 2, 1)
+
+
+def _pow(x, y):
+    """Fortran x**y with a real constant exponent, as the compiled reference evaluates it: the
+    compiler turns **0.75 into sqrt(x) * sqrt(sqrt(x)); **0.25 and the other exponents call the C
+    library's pow (each checked bit for bit against the reference build: meshScalingDel4 / Del2,
+    dss on the variable-resolution mesh)."""
+    x = np.asarray(x, dtype=np.float64)
+    if y == 0.75:
+        return np.sqrt(x) * np.sqrt(np.sqrt(x))
+    return np.asarray(_LIBM_POW(x, float(y)), dtype=np.float64)
+
+
+def _asin(x):
+    return np.asarray(_LIBM_ASIN(np.asarray(x, dtype=np.float64)), dtype=np.float64)
+
+
+def _acos(x):
+    return np.asarray(_LIBM_ACOS(np.asarray(x, dtype=np.float64)), dtype=np.float64)
+
+def _ref_arc_length(a, b):
+    """arc_length (490-510)."""
+    cx, cy, cz = b[..., 0] - a[..., 0], b[..., 1] - a[..., 1], b[..., 2] - a[..., 2]
+    r = np.sqrt(a[..., 0] * a[..., 0] + a[..., 1] * a[..., 1] + a[..., 2] * a[..., 2])
+    c = np.sqrt(cx * cx + cy * cy + cz * cz)
+    return r * 2.0 * _asin(c / (2.0 * r))
+
+
+def _ref_sphere_angle(a, b, c):
+    """sphere_angle (403-447): the angle between arcs AB and AC."""
+    la = _ref_arc_length(b, c)
+    lb = _ref_arc_length(a, c)
+    lc = _ref_arc_length(a, b)
+    abx, aby, abz = b[..., 0] - a[..., 0], b[..., 1] - a[..., 1], b[..., 2] - a[..., 2]
+    acx, acy, acz = c[..., 0] - a[..., 0], c[..., 1] - a[..., 1], c[..., 2] - a[..., 2]
+    dx = (aby * acz) - (abz * acy)
+    dy = -((abx * acz) - (abz * acx))
+    dz = (abx * acy) - (aby * acx)
+    sp = 0.5 * (la + lb + lc)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        q = (np.sin(sp - lb) * np.sin(sp - lc)) / (np.sin(lb) * np.sin(lc))
+    sin_angle = np.sqrt(np.minimum(1.0, np.maximum(0.0, np.nan_to_num(q, nan=0.0))))
+    ang = 2.0 * _asin(np.maximum(np.minimum(sin_angle, 1.0), -1.0))
+    return np.where((dx * a[..., 0] + dy * a[..., 1] + dz * a[..., 2]) >= 0.0, ang, -ang)
+
+
+def _ref_plane_angle_z(bx, by, cx, cy):
+    """plane_angle (457-485) with A = 0, B = (bx, by, 0), C = (cx, cy, 0), normal (0, 0, 1)."""
+    mab = np.sqrt(bx * bx + by * by + 0.0 * 0.0)
+    mac = np.sqrt(cx * cx + cy * cy + 0.0 * 0.0)
+    dz = (bx * cy) - (by * cx)
+    cos_angle = (bx * cx + by * cy + 0.0 * 0.0) / (mab * mac)
+    ang = _acos(np.maximum(np.minimum(cos_angle, 1.0), -1.0))
+    return np.where(dz >= 0.0, ang, -ang)
+
+
+def _ref_arc_bisect(a, b):
+    """arc_bisect (520-537)."""
+    r = np.sqrt(a[..., 0] * a[..., 0] + a[..., 1] * a[..., 1] + a[..., 2] * a[..., 2])
+    c = 0.5 * (a + b)
+    d = np.sqrt(c[..., 0] * c[..., 0] + c[..., 1] * c[..., 1] + c[..., 2] * c[..., 2])
+    return r[..., None] * c / d[..., None]
+
+
+def _ref_migs(a):
+    """MIGS / ELGS (642-740): inverse by partial-pivoting Gaussian elimination, batched over the
+    leading axis; same pivot choice (first largest scaled element) and update order."""
+    a = a.copy()
+    nb, n, _ = a.shape
+    rows = np.arange(nb)
+    indx = np.tile(np.arange(n), (nb, 1))
+    cs = np.max(np.abs(a), axis=2)                     # rescaling factor of every row
+    for j in range(n - 1):
+        pi1 = np.zeros(nb)
+        k = np.full(nb, j)
+        for i in range(j, n):
+            pv = np.abs(a[rows, indx[:, i], j]) / cs[rows, indx[:, i]]
+            take = pv > pi1
+            pi1 = np.where(take, pv, pi1)
+            k = np.where(take, i, k)
+        tj = indx[:, j].copy()
+        indx[:, j] = indx[rows, k]
+        indx[rows, k] = tj
+        for i in range(j + 1, n):
+            ri, rj = indx[:, i], indx[:, j]
+            pj = a[rows, ri, j] / a[rows, rj, j]
+            a[rows, ri, j] = pj
+            for kk in range(j + 1, n):
+                a[rows, ri, kk] = a[rows, ri, kk] - pj * a[rows, rj, kk]
+    b = np.zeros((nb, n, n))
+    b[:, np.arange(n), np.arange(n)] = 1.0
+    for i in range(n - 1):
+        for j in range(i + 1, n):
+            rj, ri = indx[:, j], indx[:, i]
+            for kk in range(n):
+                b[rows, rj, kk] = b[rows, rj, kk] - a[rows, rj, i] * b[rows, ri, kk]
+    x = np.zeros((nb, n, n))
+    for i in range(n):
+        rn = indx[:, n - 1]
+        x[:, n - 1, i] = b[rows, rn, i] / a[rows, rn, n - 1]
+        for j in range(n - 2, -1, -1):
+            rj = indx[:, j]
+            v = b[rows, rj, i]
+            for kk in range(j + 1, n):
+                v = v - a[rows, rj, kk] * x[:, kk, i]
+            x[:, j, i] = v / a[rows, rj, j]
+    return x
+
+
+def _matmul_seq(x, y):
+    """Fortran matmul with the sum over the inner index taken in order from zero (batched)."""
+    out = np.zeros((x.shape[0], x.shape[1], y.shape[2]))
+    for k in range(x.shape[2]):
+        out = out + x[:, :, k:k + 1] * y[:, k:k + 1, :]
+    return out
+
+
+def _ref_local_polygon(c, pts, R):
+    """The tangent-plane coordinates both initialisations build (mpas_atm_advection.F:132-179,
+    823-874): theta_abs, the angles between consecutive points seen from the centre (thetav),
+    and the points' great-circle distances; pts (nc, n-1, 3) around centres c (nc, 3), unit sphere."""
+    nc, m = pts.shape[0], pts.shape[1]
+    pole = np.broadcast_to(np.array([0.0, 0.0, 1.0]), c.shape)
+    theta_abs = np.where(c[:, 2] == 1.0, PII / 2.0, PII / 2.0 - _ref_sphere_angle(c, pts[:, 0], pole))
+    nxt = pts[:, (np.arange(m) + 1) % m]               # ip2 wraps to the first point
+    cb = np.broadcast_to(c[:, None, :], pts.shape)
+    thetav = _ref_sphere_angle(cb, pts, nxt)
+    dl = R * _ref_arc_length(cb, pts)
+    return theta_abs, thetav, dl
 
 
 def compute_deriv_two(m):
-    """Quadratic least-squares second derivative along each edge normal
-    (mpas_atm_advection.F:92-392, polynomial_order = 2).  deriv_two[e, side, j]:
-    j=0 the cell itself, j=i+1 its neighbour cellsOnCell(i)."""
-    nC, nE, R = m["nCells"], m["nEdges"], m["sphere_radius"]
+    """deriv_two, as atm_initialize_advection_rk computes it (mpas_atm_advection.F:21-394,
+    polynomial_order = 2, on a sphere): per cell a weighted least-squares quadratic through the
+    cell and its neighbours (poly_fit_2 with MIGS), the fit's second derivative along each edge's
+    normal direction.  deriv_two[e, side, j]: side 0 when the cell is cellsOnEdge(1, e); j = 0 the
+    cell itself, j = i + 1 its neighbour cellsOnCell(i)."""
+    nE, R = m["nEdges"], m["sphere_radius"]
     xc = np.stack([m["xCell"], m["yCell"], m["zCell"]], 1) / R
     xv = np.stack([m["xVertex"], m["yVertex"], m["zVertex"]], 1) / R
     nEoC, coc, eoc, coe, voe = m["nEdgesOnCell"], m["cellsOnCell"], m["edgesOnCell"], m["cellsOnEdge"], m["verticesOnEdge"]
     d2 = np.zeros((nE, 2, 15))
-    e1, e2 = _local_frame(xc)
-    for n in np.unique(nEoC):
-        cells = np.nonzero(nEoC == n)[0]
+    for ne in np.unique(nEoC):
+        cells = np.nonzero(nEoC == ne)[0]
+        n = ne + 1
         c = xc[cells]
-        nb = xc[coc[cells, :n]]                                  # (nc, n, 3)
-        th = _azimuth(c[:, None, :], nb, e1[cells][:, None, :], e2[cells][:, None, :])
-        dl = R * arc_length(c[:, None, :], nb)
-        xp, yp = np.cos(th) * dl, np.sin(th) * dl
-        A = np.zeros((len(cells), n + 1, 6))
-        A[:, 0, 0] = 1.0
-        A[:, 1:, 0] = 1.0
-        A[:, 1:, 1] = xp
-        A[:, 1:, 2] = yp
-        A[:, 1:, 3] = xp ** 2
-        A[:, 1:, 4] = xp * yp
-        A[:, 1:, 5] = yp ** 2
-        B = np.linalg.pinv(A)                                     # (nc, 6, n+1)
-        for i in range(n):
+        nb = xc[coc[cells, :ne]]
+        theta_abs, thetav, dl = _ref_local_polygon(c, nb, R)
+        thetat = np.empty((len(cells), ne))
+        thetat[:, 0] = theta_abs                      # x direction along the longitude line (176)
+        for i in range(1, ne):
+            thetat[:, i] = thetat[:, i - 1] + thetav[:, i - 1]
+        xp, yp = np.cos(thetat) * dl, np.sin(thetat) * dl
+        a = np.zeros((len(cells), n, 6))
+        a[:, 0, 0] = 1.0
+        a[:, 1:, 0] = 1.0
+        a[:, 1:, 1] = xp
+        a[:, 1:, 2] = yp
+        a[:, 1:, 3] = xp * xp
+        a[:, 1:, 4] = xp * yp
+        a[:, 1:, 5] = yp * yp
+        at = np.transpose(a, (0, 2, 1))               # poly_fit_2 (567-614) with unit weights
+        ath = _matmul_seq(at, np.broadcast_to(np.eye(n), (len(cells), n, n)))
+        b = _matmul_seq(_ref_migs(_matmul_seq(ath, a)), ath)   # (nc, 6, n)
+        for i in range(ne):
             e = eoc[cells, i]
-            mid = _normalize(xv[voe[e, 0]] + xv[voe[e, 1]])       # arc_bisect of the edge's vertices
-            the = _azimuth(c, mid, e1[cells], e2[cells])
-            cs, sn = np.cos(the), np.sin(the)
-            val = 2.0 * cs[:, None] ** 2 * B[:, 3, :] + 2.0 * cs[:, None] * sn[:, None] * B[:, 4, :] \
-                + 2.0 * sn[:, None] ** 2 * B[:, 5, :]
+            mid = _ref_arc_bisect(xv[voe[e, 0]], xv[voe[e, 1]])
+            the = _ref_sphere_angle(c, nb[:, i], mid) + thetat[:, i]
+            cos2t, sin2t = np.cos(the), np.sin(the)
+            costsint = cos2t * sin2t
+            cos2t, sin2t = cos2t * cos2t, sin2t * sin2t
+            val = 2. * cos2t[:, None] * b[:, 3, :] + 2. * costsint[:, None] * b[:, 4, :] \
+                + 2. * sin2t[:, None] * b[:, 5, :]
             side = np.where(coe[e, 0] == cells, 0, 1)
-            d2[e, side, :n + 1] = val
+            d2[e, side, :n] = val
     return d2
 
 
 def compute_defc(m):
-    """Deformation weights defc_a/defc_b (mpas_atm_advection.F:802-946)."""
+    """Deformation weights defc_a / defc_b as atm_initialize_deformation_weights computes them
+    (mpas_atm_advection.F:744-937, on a sphere): the cell polygon in the tangent plane, each side's
+    direction from theta_abs plus the turning angles (plane_angle), side length over cell area."""
     nC, R = m["nCells"], m["sphere_radius"]
     xc = np.stack([m["xCell"], m["yCell"], m["zCell"]], 1) / R
     xv = np.stack([m["xVertex"], m["yVertex"], m["zVertex"]], 1) / R
     nEoC, voc, eoc, coe = m["nEdgesOnCell"], m["verticesOnCell"], m["edgesOnCell"], m["cellsOnEdge"]
-    maxE = m["maxEdges"]
-    defc_a = np.zeros((nC, maxE))
-    defc_b = np.zeros((nC, maxE))
-    e1, e2 = _local_frame(xc)
-    for n in np.unique(nEoC):
-        cells = np.nonzero(nEoC == n)[0]
+    defc_a = np.zeros((nC, m["maxEdges"]))
+    defc_b = np.zeros((nC, m["maxEdges"]))
+    for ne in np.unique(nEoC):
+        cells = np.nonzero(nEoC == ne)[0]
         c = xc[cells]
-        vv = xv[voc[cells, :n]]
-        th = _azimuth(c[:, None, :], vv, e1[cells][:, None, :], e2[cells][:, None, :])
-        dl = R * arc_length(c[:, None, :], vv)
+        vv = xv[voc[cells, :ne]]
+        theta_abs, thetav, dl = _ref_local_polygon(c, vv, R)
+        th = np.empty((len(cells), ne))
+        th[:, 0] = 0.0                                # 872: x direction towards the first vertex
+        for i in range(1, ne):
+            th[:, i] = th[:, i - 1] + thetav[:, i - 1]
         xp, yp = np.cos(th) * dl, np.sin(th) * dl
-        ip1 = (np.arange(n) + 1) % n
-        dx = xp[:, ip1] - xp
-        dy = yp[:, ip1] - yp
-        thetat = np.arctan2(dy, dx)                               # direction of segment i -> i+1
-        dls = np.sqrt(dx ** 2 + dy ** 2)
-        area = np.sum(0.25 * (xp + xp[:, ip1]) * dy - 0.25 * (yp + yp[:, ip1]) * dx, axis=1)
-        s2, c2, sc = np.sin(thetat) ** 2, np.cos(thetat) ** 2, np.sin(thetat) * np.cos(thetat)
-        a = dls * (c2 - s2) / area[:, None]
-        b = dls * 2.0 * sc / area[:, None]
-        flip = coe[eoc[cells, :n], 0] != cells[:, None]
-        a[flip] *= -1.0
-        b[flip] *= -1.0
-        defc_a[cells, :n] = a
-        defc_b[cells, :n] = b
+        ip1 = (np.arange(ne) + 1) % ne
+        thetat = np.empty((len(cells), ne))
+        thetat[:, 0] = theta_abs                      # 894
+        for i in range(1, ne):
+            j = ip1[i]
+            thetat[:, i] = _ref_plane_angle_z(xp[:, i] - xp[:, i - 1], yp[:, i] - yp[:, i - 1],
+                                              xp[:, j] - xp[:, i], yp[:, j] - yp[:, i]) + thetat[:, i - 1]
+        area = np.zeros(len(cells))
+        for i in range(ne):                           # 907-914, summed in order
+            j = ip1[i]
+            area = area + 0.25 * (xp[:, i] + xp[:, j]) * (yp[:, j] - yp[:, i]) \
+                - 0.25 * (yp[:, i] + yp[:, j]) * (xp[:, j] - xp[:, i])
+        for i in range(ne):
+            j = ip1[i]
+            dls = np.sqrt((xp[:, j] - xp[:, i]) ** 2 + (yp[:, j] - yp[:, i]) ** 2)
+            st, ct = np.sin(thetat[:, i]), np.cos(thetat[:, i])
+            sint2, cost2, sint_cost = st * st, ct * ct, st * ct
+            a = dls * (cost2 - sint2) / area
+            b = dls * 2. * sint_cost / area
+            flip = coe[eoc[cells, i], 0] != cells
+            defc_a[cells, i] = np.where(flip, -a, a)
+            defc_b[cells, i] = np.where(flip, -b, b)
     return defc_a, defc_b
 
 
@@ -420,12 +567,13 @@ def model_init(out: dict, cfg: dict) -> dict:
     zt_c = zgrid[:, nz1]
     zmid = 0.5 * (zgrid[:, :-1] + zgrid[:, 1:])
     zd, xnutr = cfg["config_zd"], cfg["config_xnutr"]
-    dss = np.where(zmid > zd, xnutr * np.sin(0.5 * PII * (zmid - zd) / (zt_c[:, None] - zd)) ** 2.0, 0.0)
-    dss = dss / m["meshDensity"][:, None] ** 0.25
+    sn = np.sin(0.5 * PII * (zmid - zd) / (zt_c[:, None] - zd))
+    dss = np.where(zmid > zd, xnutr * (sn * sn), 0.0)
+    dss = np.where(zmid > zd, dss / _pow(m["meshDensity"], 0.25 * 1.0)[:, None], 0.0)
     md = m["meshDensity"]
-    if cfg["config_h_ScaleWithMesh"]:
-        msd2 = 1.0 / ((md[c1] + md[c2]) / 2.0) ** 0.25
-        msd4 = 1.0 / ((md[c1] + md[c2]) / 2.0) ** 0.75
+    if cfg["config_h_ScaleWithMesh"]:   # mesh scaling (927-984)
+        msd2 = 1.0 / _pow((md[c1] + md[c2]) / 2.0, 0.25)
+        msd4 = 1.0 / _pow((md[c1] + md[c2]) / 2.0, 0.75)
     else:
         msd2 = np.ones(nE)
         msd4 = np.ones(nE)

@@ -277,7 +277,35 @@ def _cells_vertices_ccw(p, f, width=None):
     pos = np.arange(len(cell_s)) - start[cell_s]
     vof = -np.ones((nC, int(cnt.max()) if width is None else width), dtype=np.int64)
     vof[cell_s, pos] = face_s
-    return cnt, vof
+    return cnt, _walk_fans(f, cnt, vof, nC)
+
+
+def _walk_fans(f, cnt, vof, nC):
+    """Re-derive every cell's CCW face order by walking its triangle fan from the first face of
+    the angle sort: the face after (a, b, c) around a is the one holding the directed edge a -> c.
+    Where the angle sort is right this reproduces it; where two circumcentres nearly coincide
+    (co-circular generators: a near-zero Voronoi edge) the sort can swap them, and consecutive
+    faces then share no edge -- cellsOnCell / edgesOnCell would be broken for that cell."""
+    nF = len(f)
+    src = f.reshape(-1)
+    dst = f[:, [1, 2, 0]].reshape(-1)
+    keys = src * nC + dst
+    order = np.argsort(keys)
+    keys_s, face_of = keys[order], np.repeat(np.arange(nF), 3)[order]
+    out = vof.copy()
+    cells = np.arange(nC)
+    cur = vof[:, 0]
+    for j in range(1, vof.shape[1]):
+        live = j < cnt
+        fc = f[np.where(live, cur, 0)]
+        # c: the vertex before `cell` in face cur (CCW), i.e. f[(pos + 2) % 3]
+        pos = np.argmax(fc == cells[:, None], axis=1)
+        c = fc[np.arange(nC), (pos + 2) % 3]
+        k = np.searchsorted(keys_s, cells * nC + c)
+        nxt = face_of[np.minimum(k, len(keys_s) - 1)]
+        cur = np.where(live, nxt, cur)
+        out[:, j] = np.where(live, cur, out[:, j])
+    return out
 
 
 def _topology_and_geometry(p, f, radius):
@@ -342,6 +370,14 @@ def _topology_and_geometry(p, f, radius):
         eid = edge_of(cc, np.where(other >= 0, other, 0))
         edgesOnCell[:, i] = np.where(has, eid, -1)
         cellsOnCell[:, i] = np.where(has, other, -1)
+
+    # a closed mesh: every edge of a cell joins it to the neighbour listed beside it
+    slot = np.arange(maxEdges)[None, :] < nEoC[:, None]
+    ce = cellsOnEdge[np.where(slot, edgesOnCell, 0)]
+    own = np.arange(nC)[:, None]
+    ok = (cellsOnCell >= 0) & (((ce[..., 0] == own) & (ce[..., 1] == cellsOnCell))
+                               | ((ce[..., 1] == own) & (ce[..., 0] == cellsOnCell)))
+    assert np.all(ok | ~slot), f"inconsistent cell connectivity in {int((~ok & slot).sum())} slots"
 
     # vertex connectivity: cells of the (CCW) Delaunay face, edge j between cell j and j+1
     cellsOnVertex = f.copy()

@@ -31,6 +31,7 @@ module harness_fields
    character(len=256) :: indir, outdir
    ! comma-separated 'pool.name' list; when not blank only these fields are dumped (full-size runs)
    character(len=1024) :: dump_only = ''
+   logical :: dump_ints = .false.   ! mode 'init' also dumps integer fields (index arrays it builds)
    type (block_type), pointer :: hblock => null()
 
    integer, parameter :: MAXF = 400
@@ -227,9 +228,25 @@ contains
       type (field1DReal), pointer :: f1
       type (field2DReal), pointer :: f2
       type (field3DReal), pointer :: f3
+      type (field1DInteger), pointer :: i1
+      type (field2DInteger), pointer :: i2
       call execute_command_line('mkdir -p '//trim(dir))
       do i = 1, nf
-         if (fisint(i)) cycle
+         if (fisint(i)) then
+            if (.not. dump_ints) cycle
+            call mpas_pool_get_subpool(hblock % structs, trim(fpool(i)), p)
+            open(newunit=u, file=trim(dir)//'/'//trim(fpool(i))//'.'//trim(fname(i))//'.bin', &
+                 access='stream', form='unformatted', status='replace')
+            if (frank(i) == 1) then
+               call mpas_pool_get_field(p, trim(fname(i)), i1)
+               write(u) i1 % array
+            else
+               call mpas_pool_get_field(p, trim(fname(i)), i2)
+               write(u) i2 % array
+            end if
+            close(u)
+            cycle
+         end if
          if (len_trim(dump_only) > 0) then
             if (index(','//trim(dump_only)//',', ','//trim(fpool(i))//'.'//trim(fname(i))//',') == 0) cycle
          end if
@@ -272,6 +289,11 @@ program mpas_ref_harness
    use mpas_rbf_interpolation
    use mpas_vector_reconstruction
    use harness_fields
+#ifdef HARNESS_INIT
+   use atm_advection, only : atm_initialize_advection_rk, atm_initialize_deformation_weights
+   use atm_core_init_ref, only : atm_compute_mesh_scaling, atm_compute_signs, atm_compute_damping_coefs, &
+                                 atm_adv_coef_compression, atm_couple_coef_3rd_order
+#endif
    use omp_lib
    implicit none
 
@@ -290,6 +312,8 @@ program mpas_ref_harness
    real(kind=RKIND) :: config_smagorinsky_coef, config_epssm, config_smdiv, config_apvm_upwinding
    real(kind=RKIND) :: config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days
    character(len=64) :: config_horiz_mixing, config_convection_scheme
+   real(kind=RKIND) :: config_zd, config_xnutr
+   logical :: config_h_ScaleWithMesh
    character(len=32) :: mode
    integer :: kernel_small_step, kernel_rk_step
    real(kind=RKIND) :: kernel_dts
@@ -303,7 +327,8 @@ program mpas_ref_harness
       config_h_theta_eddy_visc2, config_h_theta_eddy_visc4, config_v_theta_eddy_visc2, &
       config_len_disp, config_visc4_2dsmag, config_del4u_div_factor, config_coef_3rd_order, &
       config_smagorinsky_coef, config_epssm, config_smdiv, config_apvm_upwinding, &
-      config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days, config_horiz_mixing, config_convection_scheme
+      config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days, config_horiz_mixing, config_convection_scheme, &
+      config_zd, config_xnutr, config_h_ScaleWithMesh
 
    type (domain_type), pointer :: domain
    type (mpas_pool_type), pointer :: configs, dimpool, mesh, state, diag, tend, tend_physics, diag_physics
@@ -328,6 +353,9 @@ program mpas_ref_harness
    kernel_rk_step = 1
    kernel_dts = 0.0_RKIND
    print_minmax = 0
+   config_zd = 22000.0_RKIND       ! Registry.xml defaults
+   config_xnutr = 0.2_RKIND
+   config_h_ScaleWithMesh = .true.
    open(newunit=u, file=trim(indir)//'/harness.nml', status='old')
    read(u, nml=harness)
    close(u)
@@ -411,6 +439,9 @@ program mpas_ref_harness
    call mpas_pool_add_config_logical(configs, 'config_print_global_minmax_vel', iand(print_minmax, 1) /= 0)
    call mpas_pool_add_config_logical(configs, 'config_print_detailed_minmax_vel', iand(print_minmax, 2) /= 0)
    call mpas_pool_add_config_logical(configs, 'config_print_global_minmax_sca', iand(print_minmax, 4) /= 0)
+   call mpas_pool_add_config_real(configs, 'config_zd', config_zd)
+   call mpas_pool_add_config_real(configs, 'config_xnutr', config_xnutr)
+   call mpas_pool_add_config_logical(configs, 'config_h_ScaleWithMesh', config_h_ScaleWithMesh)
 
    ! ---- subpools ----
    call mpas_pool_create_pool(mesh)
@@ -522,7 +553,9 @@ program mpas_ref_harness
    call add_r3(mesh, 'mesh', 'zb3', K+1, 2, nE1, 1)
    call add_r3(mesh, 'mesh', 'zb_cell', K+1, maxEdges_in, nC1, 1)
    call add_r3(mesh, 'mesh', 'zb3_cell', K+1, maxEdges_in, nC1, 1)
+   call add_i2(mesh, 'mesh', 'advCells', 21, nC1)   ! core_init_atmosphere Registry (TWENTYONE nCells)
 
+   write(0, '(a)') 'harness: mesh pool read'
    ! ---- state pool: 2 time levels (Registry.xml var_struct "state" time_levs="2") ----
    call add_r2(state, 'state', 'u', K, nE1, 2)
    call add_r2(state, 'state', 'w', K+1, nC1, 2)
@@ -580,6 +613,26 @@ program mpas_ref_harness
    end if
 
    allocate(plist(1))
+   write(0, '(a)') 'harness: pools built'
+
+#ifdef HARNESS_INIT
+   if (trim(mode) == 'init') then
+      ! the reference's mesh-dependent precompute, in model order: deriv_two / defc_a / defc_b as
+      ! init_atmosphere computes them for the init file (mpas_init_atm_cases.F:190-191 via
+      ! mpas_atm_advection.F), then atm_mpas_init_block's own (mpas_atm_core.F:311, 358, 360, 456, 458)
+      dump_ints = .true.
+      call atm_initialize_advection_rk(mesh, nCells, nEdges, maxEdges_in, .true., sphere_radius)
+      call atm_initialize_deformation_weights(mesh, nCells, .true., sphere_radius)
+      call atm_compute_signs(mesh)
+      call atm_adv_coef_compression(mesh)
+      call atm_couple_coef_3rd_order(mesh, configs)
+      call atm_compute_mesh_scaling(mesh, configs)
+      call atm_compute_damping_coefs(mesh, configs)
+      call dump_all(trim(outdir)//'/step_0000', plist)
+      call mpas_dmpar_finalize(domain % dminfo)
+      stop
+   end if
+#endif
 
    if (trim(mode) == 'acoustic') then
       ! kernel mode: one acoustic sub-step on a state restored from a dump
@@ -616,8 +669,11 @@ program mpas_ref_harness
 !$OMP END PARALLEL DO
    deallocate(ke_vertex)
    deallocate(ke_edge)
+   write(0, '(a)') 'harness: init diagnostics done'
    call mpas_rbf_interp_initialize(mesh)
+   write(0, '(a)') 'harness: rbf init done'
    call mpas_init_reconstruct(mesh)
+   write(0, '(a)') 'harness: reconstruct init done'
    call mpas_pool_get_array(state, 'u', uu, 1)
    call mpas_pool_get_array(diag, 'uReconstructX', uReconstructX)
    call mpas_pool_get_array(diag, 'uReconstructY', uReconstructY)
@@ -626,6 +682,7 @@ program mpas_ref_harness
    call mpas_pool_get_array(diag, 'uReconstructMeridional', uReconstructMeridional)
    call mpas_reconstruct(mesh, uu, uReconstructX, uReconstructY, uReconstructZ, uReconstructZonal, uReconstructMeridional)
 
+   write(0, '(a)') 'harness: reconstruct done'
    if (any(dump_steps == 0)) call dump_all(trim(outdir)//'/step_0000', plist)
 
    ! atm_timestep (mpas_atm_time_integration.F:117-118) binds this module pointer before
@@ -639,6 +696,7 @@ program mpas_ref_harness
       call atm_srk3(domain, dt, step)
       t1 = omp_get_wtime()
       steptime(step) = t1 - t0
+      write(0, '(a,i6,f10.3)') 'harness: step', step, steptime(step)
       call mpas_pool_shift_time_levels(state)
       if (any(dump_steps == step)) then
          write(sdir, '(a,i4.4)') 'step_', step

@@ -208,6 +208,51 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     return res, times
 
 
+# mode 'init': the reference's mesh-dependent precompute (mpas_atm_advection.F deriv_two / defc_a /
+# defc_b; mpas_atm_core.F:927-1288 signs, adv_coef compression, 3rd-order coupling, mesh scaling,
+# damping coefficients).  Outputs: name -> (location, Fortran leading dims, is_int).
+INIT_OUTPUTS = {
+    "deriv_two": ("edge", (15, 2), False), "defc_a": ("cell", ("ME",), False), "defc_b": ("cell", ("ME",), False),
+    "edgesOnCell_sign": ("cell", ("ME",), False), "edgesOnVertex_sign": ("vertex", (3,), False),
+    "kiteForCell": ("cell", ("ME",), True), "zb_cell": ("cell", ("K1", "ME"), False),
+    "zb3_cell": ("cell", ("K1", "ME"), False), "adv_coefs": ("edge", (15,), False),
+    "adv_coefs_3rd": ("edge", (15,), False), "advCellsForEdge": ("edge", (15,), True),
+    "nAdvCellsForEdge": ("edge", (), True), "meshScalingDel2": ("edge", (), False),
+    "meshScalingDel4": ("edge", (), False), "dss": ("cell", ("K",), False), "advCells": ("cell", (21,), True),
+}
+
+
+def run_reference_init(case: dict, nthreads: int = 1, timeout: int = 600) -> dict:
+    """Run the reference's model-init precompute on the case's mesh (harness mode 'init') and return
+    its outputs as element-major arrays (index arrays 0-based, a missing entry -1).  The inputs are
+    the mesh geometry and connectivity, zgrid, meshDensity, zb / zb3; every output above is
+    withheld from the harness, so it starts from zeros as the reference does."""
+    import shutil
+    tmp = tempfile.mkdtemp(prefix="mpasrefi_")
+    try:
+        ind, outd = os.path.join(tmp, "in"), os.path.join(tmp, "out")
+        write_inputs({k: v for k, v in case.items() if k not in INIT_OUTPUTS}, ind, 0, 1.0, [], nthreads)
+        with open(os.path.join(ind, "harness.nml")) as f:
+            nml = f.read()
+        with open(os.path.join(ind, "harness.nml"), "w") as f:
+            f.write(nml.replace("&harness\n", "&harness\n mode='init',\n"))
+        env = dict(os.environ, OMP_NUM_THREADS=str(nthreads))
+        r = subprocess.run([HARNESS, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout,
+                           preexec_fn=_big_stack)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference init run failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
+        dims = {"ME": case["maxEdges"], "K": case["nVertLevels"], "K1": case["nVertLevels"] + 1}
+        out = {}
+        for name, (loc, lead, is_int) in INIT_OUTPUTS.items():
+            a = np.fromfile(os.path.join(outd, "step_0000", f"mesh.{name}.bin"), dtype=np.int32 if is_int else np.float64)
+            inner = tuple(dims.get(x, x) for x in lead)
+            a = a.reshape((case[_LOC_N[loc]] + 1,) + inner[::-1])[:-1]
+            out[name] = a.astype(np.int64) - 1 if is_int and name != "nAdvCellsForEdge" else a
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def run_reference_kernel(case: dict, restore_dir: str, mode: str, dts: float = 0.0, small_step: int = 2,
                          rk_step: int = 1, nthreads: int = 1, timeout: int = 600) -> dict:
     """Run one reference routine ('acoustic' = atm_advance_acoustic_step + atm_divergence_damping_3d)

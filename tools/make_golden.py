@@ -16,8 +16,13 @@ inputs/outputs as compressed npz (data only -- no reference source).
   tests/golden/reconstruct_x1.642.npz
       mpas_rbf_interp_initialize + mpas_init_reconstruct outputs (edgeNormalVectors,
       cellTangentPlane, coeffs_reconstruct) on x1.642.
+  tests/golden/init_x1.642_K8.npz, tests/golden/init_varres2562_K8.npz
+      the reference's mesh-dependent precompute (harness mode 'init': deriv_two, defc_a/b from
+      core_init_atmosphere/mpas_atm_advection.F; signs, kiteForCell, adv_coefs compression,
+      3rd-order coupling, mesh scaling, dss from mpas_atm_core.F:927-1288) on the quasi-uniform
+      and the variable-resolution test meshes, with a checksum of the mesh it ran on.
 
-Usage: python tools/make_golden.py [acoustic|srk3|reconstruct ...]   (needs oracle/_ref built)
+Usage: python tools/make_golden.py [acoustic|srk3|reconstruct|init ...]   (needs oracle/_ref built)
 """
 from __future__ import annotations
 
@@ -104,6 +109,32 @@ def reconstruct_fixture():
                         cellTangentPlane=r0["mesh.cellTangentPlane"].reshape(nC + 1, 2, 3)[:-1])
 
 
+INIT_CASES = {
+    "init_x1.642_K8.npz": lambda: jw_case(642, K=8, ns=1, cache=False),
+    "init_varres2562_K8.npz": lambda: __import__("mpas_dycore.cases", fromlist=["varres_case"]).varres_case(
+        2562, ratio=4.0, K=8, ns=1, lloyd_iters=30, cache=False),
+}
+# the model-init outputs' inputs: the mesh the routines read (their checksum pins the fixture's mesh)
+INIT_INPUTS = ["xCell", "yCell", "zCell", "xVertex", "yVertex", "zVertex", "cellsOnCell", "edgesOnCell",
+               "verticesOnCell", "cellsOnEdge", "verticesOnEdge", "cellsOnVertex", "edgesOnVertex", "nEdgesOnCell",
+               "dcEdge", "dvEdge", "meshDensity", "zgrid", "zb", "zb3"]
+
+
+def init_inputs_checksum(case: dict) -> str:
+    return case_checksum({k: np.asarray(case[k]) for k in INIT_INPUTS})
+
+
+def init_fixture():
+    for fn, make in INIT_CASES.items():
+        case = make()
+        ref = ref_runner.run_reference_init(case)
+        out = {"checksum": init_inputs_checksum(case)}
+        for k, v in ref.items():
+            if k not in ("zb_cell", "zb3_cell"):  # copies of zb / zb3, checked live (and large)
+                out[k] = v
+        np.savez_compressed(os.path.join(GOLD, fn), **out)
+
+
 if __name__ == "__main__":
     if not ref_runner.available():
         sys.exit("build the oracle first: make -C oracle")
@@ -114,5 +145,7 @@ if __name__ == "__main__":
         srk3_fixture()
     if not only or "reconstruct" in only:
         reconstruct_fixture()
+    if not only or "init" in only:
+        init_fixture()
     for f in sorted(os.listdir(GOLD)):
         print(f, os.path.getsize(os.path.join(GOLD, f)))
