@@ -101,8 +101,20 @@ struct Ptrs {
   const int *adv_tn, *adv_tcell;
   const unsigned char* adv_loc;
   const double* cell_sdv;
+  // fused acoustic sub-step tiles (k_acoustic_fused, host-built): per tile of AC_T owned cells the
+  // number of distinct edges of its cells and the edges (2 e + 1 when the tile stores that edge),
+  // whether any of them touches a halo cell; per owned cell the LDS slot of each of its edges
+  const int *ac_tedge, *ac_tne, *ac_tbnd;
+  const unsigned char* ac_cslot;
 };
 constexpr int CELL_REC = 16, CELL_REC_ME = 7;
 constexpr int ADV_T = 8, ADV_UMAX = 32, ADV_LOC = 16;
+#ifndef AC_T_CELLS
+#define AC_T_CELLS 16
+#endif
+#ifndef AC_T_WAVES
+#define AC_T_WAVES 8
+#endif
+constexpr int AC_T = AC_T_CELLS, AC_WAVES = AC_T_WAVES, AC_THREADS = 64 * AC_WAVES;
 
 }  // namespace mpas

@@ -83,7 +83,7 @@ def varres_case(ncells: int, ratio: float = 20.0, K: int = 56, ns: int = 1, mois
     dt = float(max(1.0, round(5.0 * dx_min / 1000.0)))
     cfg = dict(config_len_disp=dx_min, config_dt=dt)
     if ncells > 200000:
-        print(f"varres case: mesh done ({m['nCells']} cells), building the JW state", file=sys.stderr, flush=True)
+        print(f"varres case: mesh done ({m['nCells']} cells), building the JW state", file=sys.__stderr__, flush=True)
     case = build_case(m, K=K, ns=ns, moist=moist, config=cfg)
     case["dt"] = dt
     if cache and ncells <= 400000:  # larger cases are rebuilt rather than pickled to /tmp

@@ -240,7 +240,7 @@ def build_varres_mesh(ncells: int, ratio: float = 20.0, lloyd_iters: int = 10, s
     for it in range(lloyd_iters):
         p = _lloyd_step(p, _delaunay(p), rho)
         if ncells > 200000:  # long builds report progress (a silent GPU-box job looks hung)
-            print(f"varres mesh: Lloyd iteration {it + 1}/{lloyd_iters}", file=sys.stderr, flush=True)
+            print(f"varres mesh: Lloyd iteration {it + 1}/{lloyd_iters}", file=sys.__stderr__, flush=True)
     f = _delaunay(p)
     if sfc:
         order = np.argsort(_hilbert3d_keys(p), kind="stable")

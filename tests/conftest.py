@@ -15,6 +15,59 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+_CAPMAN = None
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _capture_manager(request):
+    global _CAPMAN
+    _CAPMAN = request.config.pluginmanager.getplugin("capturemanager")
+    yield
+
+
+def progress(msg: str):
+    """A progress line that bypasses pytest's output capture (and, on a GPU box, is appended to
+    gpurun_out/progress.log): long full-size tests stay visibly alive."""
+    import time
+    line = f"[{time.strftime('%H:%M:%S')}] {msg}"
+    if _CAPMAN is not None:
+        with _CAPMAN.global_and_fixture_disabled():
+            print(line, file=sys.stderr, flush=True)
+    else:
+        print(line, file=sys.stderr, flush=True)
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        with open(os.path.join(ROOT, "gpurun_out", "progress.log"), "a") as f:
+            f.write(line + "\n")
+
+
+class heartbeat:
+    """``with heartbeat("what"):`` -- a progress line every ``every`` seconds until the block ends."""
+
+    def __init__(self, what: str, every: float = 30.0):
+        self.what, self.every = what, every
+
+    def __enter__(self):
+        import threading
+        import time
+        self.t0 = time.time()
+        self.stop = threading.Event()
+
+        def run():
+            while not self.stop.wait(self.every):
+                progress(f"{self.what}: {time.time() - self.t0:.0f} s")
+        self.th = threading.Thread(target=run, daemon=True)
+        self.th.start()
+        progress(f"{self.what} ...")
+        return self
+
+    def __exit__(self, *exc):
+        import time
+        self.stop.set()
+        self.th.join()
+        progress(f"{self.what}: done in {time.time() - self.t0:.0f} s")
+        return False
+
+
 def rel_linf(a, b):
     import numpy as np
     a = np.asarray(a, dtype=np.float64)

@@ -19,13 +19,10 @@ Cases are built on the box (about a minute at 163842, a few at 835586) and cache
 $MPAS_DYCORE_CACHE (default /tmp/mpas_dycore_cache), where bench.py finds them too.
 Progress lines go to the real stderr so a long run shows it is alive.
 """
-import sys
-import time
-
 import numpy as np
 import pytest
 
-from conftest import rel_linf
+from conftest import heartbeat, progress, rel_linf
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
@@ -35,20 +32,15 @@ PROG = [("state", "u", "state.u.tl1", "edge"), ("state", "theta_m", "state.theta
 DUMP = ["state.u", "state.theta_m", "state.rho_zz", "state.w", "state.scalars"]
 TOL = 1e-10          # u, theta_m, rho_zz (north_star)
 TOL_LOOSE = 1e-9     # w and the mixing ratios
-_T0 = time.time()
-
-
-def progress(msg):
-    print(f"[full-configs {time.time() - _T0:7.1f}s] {msg}", file=sys.__stderr__, flush=True)
 
 
 def _reference(case, nsteps, moist_end=1):
     from oracle import ref_runner
     if not ref_runner.available():
         pytest.skip("oracle/_ref not built")
-    progress(f"reference: {nsteps} steps on {case['nCells']} cells")
-    res, times = ref_runner.run_reference(case, nsteps=nsteps, dt=float(case["dt"]), dump_steps=[nsteps],
-                                          nthreads=16, moist_end=moist_end, dump_only=DUMP)
+    with heartbeat(f"reference: {nsteps} steps on {case['nCells']} cells"):
+        res, times = ref_runner.run_reference(case, nsteps=nsteps, dt=float(case["dt"]), dump_steps=[nsteps],
+                                              nthreads=16, moist_end=moist_end, dump_only=DUMP)
     progress(f"reference done, s/step {np.round(times, 2).tolist()}")
     return res[nsteps]
 
@@ -73,11 +65,11 @@ def _run(dy, dt, nsteps):
 
 def _single(case, nsteps, moist_end=1):
     from mpas_dycore import Dycore
-    dy = Dycore(case, device=0, moist_end=moist_end)
-    _run(dy, float(case["dt"]), nsteps)
-    out = {key: dy.get(pool, name, 1) for pool, name, key, _ in PROG}
-    dy.close()
-    progress(f"GPU one block: {nsteps} steps")
+    with heartbeat(f"GPU one block: {nsteps} steps"):
+        dy = Dycore(case, device=0, moist_end=moist_end)
+        _run(dy, float(case["dt"]), nsteps)
+        out = {key: dy.get(pool, name, 1) for pool, name, key, _ in PROG}
+        dy.close()
     return out
 
 
@@ -85,7 +77,8 @@ def _blocks_rccl(case, nblocks, nsteps, single, moist_end=1):
     """nblocks MPAS blocks on one device, every block-to-block halo message through RCCL (send to
     self), split-phase exchanges on: bitwise equal to the one-block run."""
     from mpas_dycore import Dycore, decomp
-    blocks = decomp.decompose(case, decomp.partition_sfc(case["nCells"], nblocks))
+    with heartbeat(f"{nblocks}-block decomposition"):
+        blocks = decomp.decompose(case, decomp.partition_sfc(case["nCells"], nblocks))
     dy = Dycore.from_blocks(blocks, device=0, comm_id=Dycore.comm_unique_id(), nranks=1, rank=0,
                             rccl_local=True, moist_end=moist_end)
     dy.set_overlap(True)
@@ -104,8 +97,8 @@ def _blocks_rccl(case, nblocks, nsteps, single, moist_end=1):
 @pytest.fixture(scope="module")
 def dry163842():
     from mpas_dycore.cases import jw_case
-    progress("building x1.163842 x 56 dry case (order 3)")
-    c = jw_case(163842, K=56, ns=1, order=3)
+    with heartbeat("building x1.163842 x 56 dry case (order 3)"):
+        c = jw_case(163842, K=56, ns=1, order=3)
     assert c["config"]["config_time_integration_order"] == 3
     return c
 
@@ -127,8 +120,8 @@ def test_configs2_x1_163842_L56_eight_rccl_blocks_bitwise(dry163842, dry163842_g
 
 def test_configs3_x1_163842_L56_moist_ns6_mono_10_steps_matches_reference():
     from mpas_dycore.cases import jw_case
-    progress("building x1.163842 x 56 moist ns=6 case (order 3)")
-    c = jw_case(163842, K=56, ns=6, moist=True, order=3)
+    with heartbeat("building x1.163842 x 56 moist ns=6 case (order 3)"):
+        c = jw_case(163842, K=56, ns=6, moist=True, order=3)
     assert c["config"]["config_monotonic"] and c["num_scalars"] == 6
     got = _single(c, 10, moist_end=6)
     _check(got, _reference(c, 10, moist_end=6))
@@ -139,8 +132,8 @@ def test_configs3_x1_163842_L56_moist_ns6_mono_10_steps_matches_reference():
 @pytest.fixture(scope="module")
 def varres835586():
     from mpas_dycore.cases import varres_case
-    progress("building the 835586-cell variable-resolution case (20x)")
-    c = varres_case(835586, ratio=20.0, K=56, ns=1)
+    with heartbeat("building the 835586-cell variable-resolution case (20x)"):
+        c = varres_case(835586, ratio=20.0, K=56, ns=1)
     assert c["maxEdges"] == 7
     return c
 
