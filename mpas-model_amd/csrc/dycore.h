@@ -95,26 +95,8 @@ struct Ptrs {
   // edgesOnCell_sign * dvEdge (maxEdges doubles per cell).  A cell reads its whole stencil with
   // one scalar load.
   const int* cell_rec;
-  // LDS-staged advflux tiles (k_dyn_advflux_t): per tile of ADV_T edges, the number of distinct
-  // stencil cells, their indices (ADV_UMAX per tile), and per edge the local slot of each
-  // stencil cell (ADV_LOC bytes per edge)
-  const int *adv_tn, *adv_tcell;
-  const unsigned char* adv_loc;
   const double* cell_sdv;
-  // fused acoustic sub-step tiles (k_acoustic_fused, host-built): per tile of AC_T owned cells the
-  // number of distinct edges of its cells and the edges (2 e + 1 when the tile stores that edge),
-  // whether any of them touches a halo cell; per owned cell the LDS slot of each of its edges
-  const int *ac_tedge, *ac_tne, *ac_tbnd;
-  const unsigned char* ac_cslot;
 };
 constexpr int CELL_REC = 16, CELL_REC_ME = 7;
-constexpr int ADV_T = 8, ADV_UMAX = 32, ADV_LOC = 16;
-#ifndef AC_T_CELLS
-#define AC_T_CELLS 16
-#endif
-#ifndef AC_T_WAVES
-#define AC_T_WAVES 8
-#endif
-constexpr int AC_T = AC_T_CELLS, AC_WAVES = AC_T_WAVES, AC_THREADS = 64 * AC_WAVES;
 
 }  // namespace mpas

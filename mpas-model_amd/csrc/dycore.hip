@@ -55,17 +55,7 @@ struct Block {
   std::vector<XList> xl;
   int64_t nEdges_act = -1;             // edges with an owned cell (from cellsOnEdge), for B_ac
   int64_t n_bnd_edges = -1;            // edges with a halo (or garbage) cell, from compute_bnd
-  // LDS-staged advflux tiles (build_adv_tiles); null when the mesh does not qualify
-  int* d_adv_tn = nullptr;
-  int* d_adv_tcell = nullptr;
-  unsigned char* d_adv_loc = nullptr;
   std::vector<int32_t> h_coe, h_eoc, h_noc;  // host copies (0-based) for the halo-boundary flags
-  // fused acoustic sub-step tiles (k_acoustic_fused, build_ac_tiles); ac_nt = 0: not available
-  int* d_ac_tedge = nullptr;
-  int* d_ac_tne = nullptr;
-  int* d_ac_tbnd = nullptr;
-  unsigned char* d_ac_cslot = nullptr;
-  int ac_nt = 0, ac_emax = 0;
   // summarize_timestep records (summary.hip): partials and one SUM_REC record per field
   double* sum_part = nullptr;
   double* sum_out = nullptr;
@@ -293,10 +283,6 @@ void build_registry(Block& c) {
   add(c, "scratch", "cell_sdv", L_CELL, ME);
   add(c, "scratch", "zb_p", L_CELL, (int64_t)ME * (K + 1));
   add(c, "scratch", "zb_m", L_CELL, (int64_t)ME * (K + 1));
-  // the rotating perturbation buffers of the fused acoustic sub-steps (srk3): with the canonical
-  // diag.rtheta_pp / rho_pp / ru_p they hold the sub-steps' values without copies
-  for (const char* n : {"rtheta_pp_b", "rtheta_pp_c", "rho_pp_b"}) add(c, "scratch", n, L_CELL, K);
-  add(c, "scratch", "ru_p_b", L_EDGE, K);
 }
 
 Field* find(Block& b, const char* pool, const char* name) {
@@ -368,13 +354,6 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   p.cell_rec = P<const int>(c, b, "scratch", "cell_rec");
   p.cell_sdv = P<const double>(c, b, "scratch", "cell_sdv");
   p.zb_p = P<const double>(c, b, "scratch", "zb_p");
-  p.adv_tn = b.d_adv_tn;
-  p.adv_tcell = b.d_adv_tcell;
-  p.adv_loc = b.d_adv_loc;
-  p.ac_tedge = b.d_ac_tedge;
-  p.ac_tne = b.d_ac_tne;
-  p.ac_tbnd = b.d_ac_tbnd;
-  p.ac_cslot = b.d_ac_cslot;
   p.zb_m = P<const double>(c, b, "scratch", "zb_m");
   // 0-d mesh fields are mirrored on the host
   p.cf1 = b.fields[b.by_name["mesh.cf1"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf1"]].buf[1] : 0.0;
@@ -631,13 +610,6 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
 // (tests/test_gpu_kernels.py); the environment variable MPAS_DYCORE_KERNELS=general|batched|pair,
 // read when a context is created, caps the family (default pair).
 int g_kernel_tier = 2;
-// MPAS_DYCORE_LDS=1 turns the LDS-staged advflux (k_dyn_advflux_t) on.  Off by default: measured
-// 572 us against 368 us for k_dyn_advflux_p at 163842x56 (rejected experiments)
-bool g_lds_advflux = false;
-// MPAS_DYCORE_FUSED=1 turns the fused acoustic sub-step (k_acoustic_fused) on; measured slower
-// than the two kernels (0.90-0.96 against 0.79 ms per sub-step), so off by default
-bool g_fused_ac = false;
-
 inline bool batched(const Dims& d) {
   return g_kernel_tier >= 1 && (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
 }
@@ -645,130 +617,6 @@ inline bool batched(const Dims& d) {
 
 // pair-layout edge kernels (k_*_p: two edges per wave, two levels per lane) need an even K
 inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K % 2 == 0 && d.K <= 64; }
-
-void free_adv_tiles(Block& b) {
-  if (b.d_adv_tn) (void)hipFree(b.d_adv_tn);
-  if (b.d_adv_tcell) (void)hipFree(b.d_adv_tcell);
-  if (b.d_adv_loc) (void)hipFree(b.d_adv_loc);
-  b.d_adv_tn = b.d_adv_tcell = nullptr;
-  b.d_adv_loc = nullptr;
-}
-
-// Tiles of k_dyn_advflux_t: ADV_T consecutive edges; the distinct advCellsForEdge cells of the
-// tile's edges with an owned cell (the ones k_dyn_advflux computes), and each edge's slot map.
-// Leaves the tiles off (k_dyn_advflux_p runs) unless the pair layout applies, maxEdges = 6
-// (NA = 10 stencil slots); a tile with more than ADV_UMAX distinct cells (tn = -1) gathers.
-int build_adv_tiles(mpas_dyc_ctx* ctx, Block& b) {
-  free_adv_tiles(b);
-  const Dims& d = b.d;
-  if (!g_lds_advflux || !pair_layout(d) || d.maxEdges != 6 || d.nEdges < 1) return MPAS_DYC_OK;
-  const int64_t nE = d.nEdges;
-  std::vector<int32_t> adv((size_t)(nE + 1) * 15), nadv(nE + 1);
-  HIPCHK(hipMemcpy(adv.data(), find(b, "mesh", "advCellsForEdge")->buf[0], adv.size() * 4, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(nadv.data(), find(b, "mesh", "nAdvCellsForEdge")->buf[0], nadv.size() * 4, hipMemcpyDeviceToHost));
-  const int64_t nt = (nE + ADV_T - 1) / ADV_T;
-  std::vector<int32_t> tn(nt, 0), tcell((size_t)nt * ADV_UMAX, 0);
-  std::vector<unsigned char> loc((size_t)nE * ADV_LOC, 0);
-  for (int64_t t = 0; t < nt; ++t) {
-    int cnt = 0;
-    int32_t* u = &tcell[(size_t)t * ADV_UMAX];
-    for (int64_t e = t * ADV_T; e < std::min<int64_t>(nE, (t + 1) * ADV_T); ++e) {
-      const bool on = b.h_coe[2 * e] < d.nCellsSolve || b.h_coe[2 * e + 1] < d.nCellsSolve;
-      if (!on) continue;
-      if (nadv[e] > 10) return MPAS_DYC_OK;  // wider stencil: k_dyn_advflux_p
-      for (int j = 0; j < nadv[e]; ++j) {
-        const int32_t c = adv[(size_t)e * 15 + j];
-        int s = 0;
-        while (s < cnt && u[s] != c) ++s;
-        if (s == cnt) {
-          if (cnt == ADV_UMAX) {  // tile too wide for the LDS budget: its edges gather from memory
-            cnt = -1;
-            break;
-          }
-          u[cnt++] = c;
-        }
-        loc[(size_t)e * ADV_LOC + j] = (unsigned char)s;
-      }
-      if (cnt < 0) break;
-    }
-    tn[t] = cnt;
-  }
-  HIPCHK(hipMalloc(&b.d_adv_tn, tn.size() * 4));
-  HIPCHK(hipMalloc(&b.d_adv_tcell, tcell.size() * 4));
-  HIPCHK(hipMalloc(&b.d_adv_loc, loc.size()));
-  HIPCHK(hipMemcpy(b.d_adv_tn, tn.data(), tn.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(b.d_adv_tcell, tcell.data(), tcell.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(b.d_adv_loc, loc.data(), loc.size(), hipMemcpyHostToDevice));
-  return MPAS_DYC_OK;
-}
-
-void free_ac_tiles(Block& b) {
-  for (void* q : {(void*)b.d_ac_tedge, (void*)b.d_ac_tne, (void*)b.d_ac_tbnd, (void*)b.d_ac_cslot})
-    if (q) (void)hipFree(q);
-  b.d_ac_tedge = b.d_ac_tne = b.d_ac_tbnd = nullptr;
-  b.d_ac_cslot = nullptr;
-  b.ac_nt = b.ac_emax = 0;
-}
-
-// Tiles of k_acoustic_fused: AC_T consecutive owned cells (SFC order); per tile the distinct
-// edges of its cells in first-seen order, each tagged with whether this tile stores it (the tile
-// of the edge's lowest-numbered owned cell), and per owned cell the slot of each of its edges.
-// Leaves the fused sub-step off unless the pair layout and the cell records apply and a tile's
-// edges fit the LDS (ac_emax K-columns, at most 64 KiB).
-int build_ac_tiles(mpas_dyc_ctx* ctx, Block& b) {
-  free_ac_tiles(b);
-  const Dims& d = b.d;
-  if (!g_fused_ac || !pair_layout(d) || (d.maxEdges != 6 && d.maxEdges != 7) || d.nCellsSolve < 1) return MPAS_DYC_OK;
-  const int nt = (d.nCellsSolve + AC_T - 1) / AC_T, ME = d.maxEdges, nS = d.nCellsSolve;
-  std::vector<std::vector<int>> tedge(nt);
-  std::vector<int32_t> tne(nt), tbnd(nt, 0);
-  std::vector<unsigned char> cslot((size_t)nS * 8, 0);
-  int emax = 1;
-  for (int t = 0; t < nt; ++t) {
-    std::vector<int>& es = tedge[t];
-    for (int c = t * AC_T; c < std::min(nS, (t + 1) * AC_T); ++c) {
-      for (int i = 0; i < b.h_noc[c] && i < ME; ++i) {
-        const int e = b.h_eoc[(size_t)c * ME + i];
-        if (e < 0 || e >= d.nEdges) return MPAS_DYC_OK;  // an owned cell with a missing edge: two kernels
-        size_t s = 0;
-        while (s < es.size() && es[s] != e) ++s;
-        if (s == es.size()) es.push_back(e);
-        if (s > 255) return MPAS_DYC_OK;
-        cslot[(size_t)c * 8 + i] = (unsigned char)s;
-      }
-    }
-    for (int& e : es) {
-      const int c1 = b.h_coe[2 * (size_t)e], c2 = b.h_coe[2 * (size_t)e + 1];
-      const int own = std::min(c1 < nS ? c1 : INT32_MAX, c2 < nS ? c2 : INT32_MAX);
-      if (c1 >= nS || c2 >= nS) tbnd[t] = 1;
-      e = 2 * e + ((own / AC_T) == t ? 1 : 0);
-    }
-    tne[t] = (int)es.size();
-    emax = std::max(emax, tne[t]);
-  }
-  if ((int64_t)emax * d.K * 8 > 65536) return MPAS_DYC_OK;
-  std::vector<int32_t> flat((size_t)nt * emax, 0);
-  for (int t = 0; t < nt; ++t)
-    for (int j = 0; j < emax; ++j) flat[(size_t)t * emax + j] = j < tne[t] ? tedge[t][j] : 2 * (tedge[t][0] >> 1);
-  HIPCHK(hipMalloc(&b.d_ac_tedge, flat.size() * 4));
-  HIPCHK(hipMalloc(&b.d_ac_tne, tne.size() * 4));
-  HIPCHK(hipMalloc(&b.d_ac_tbnd, tbnd.size() * 4));
-  HIPCHK(hipMalloc(&b.d_ac_cslot, cslot.size()));
-  HIPCHK(hipMemcpy(b.d_ac_tedge, flat.data(), flat.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(b.d_ac_tne, tne.data(), tne.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(b.d_ac_tbnd, tbnd.data(), tbnd.size() * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(b.d_ac_cslot, cslot.data(), cslot.size(), hipMemcpyHostToDevice));
-  b.ac_nt = nt;
-  b.ac_emax = emax;
-  return MPAS_DYC_OK;
-}
-
-// every block of the context runs its small_step >= 2 sub-steps as k_acoustic_fused
-bool fused_acoustic(const mpas_dyc_ctx* ctx) {
-  for (const auto& b : ctx->blk)
-    if (b.ac_nt == 0) return false;
-  return !ctx->blk.empty();
-}
 
 // Halo-boundary flags of the split-phase exchanges: an edge is "boundary" when one of its
 // cells is a halo cell (it reads exchanged cell data); an owned cell is "boundary" when
@@ -798,8 +646,6 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
     }
     HIPCHK(hipMemcpy(find(b, "scratch", "edge_bnd")->buf[0], eb.data(), eb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(find(b, "scratch", "cell_bnd")->buf[0], cb.data(), cb.size() * 4, hipMemcpyHostToDevice));
-    CHK(build_adv_tiles(ctx, b));
-    CHK(build_ac_tiles(ctx, b));
     hipLaunchKernelGGL(k_build_cell_rec, dim3((d.nCells + 1 + 255) / 256), dim3(256), 0, ctx->stream, d,
                        P<const int>(ctx, b, "mesh", "nEdgesOnCell"), P<const int>(ctx, b, "mesh", "edgesOnCell"),
                        P<const int>(ctx, b, "mesh", "cellsOnEdge"), P<const double>(ctx, b, "mesh", "dvEdge"),
@@ -943,11 +789,7 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     }
   }
   if (!batched(d)) LAUNCH(k_dyn_advflux, d.nEdges, d, p);
-  else if (pair_layout(d) && d.maxEdges == 6 && p.adv_tn) {
-    if (!ctx->planning)  // one workgroup per tile of ADV_T edges, LDS = ADV_UMAX (K+2 + K) doubles
-      hipLaunchKernelGGL(k_dyn_advflux_t<10>, dim3((unsigned)((d.nEdges + ADV_T - 1) / ADV_T)), dim3(BLOCK_THREADS),
-                         (size_t)ADV_UMAX * (((d.K + 2) & ~1) + d.K) * sizeof(double), ctx->stream, d, p);
-  } else if (pair_layout(d) && d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_p<10>, (d.nEdges + 1) / 2, d, p);
+  else if (pair_layout(d) && d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_p<10>, (d.nEdges + 1) / 2, d, p);
   else if (pair_layout(d)) LAUNCH_E(k_dyn_advflux_p<12>, (d.nEdges + 1) / 2, d, p);
   else if (d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_b<10>, d.nEdges, d, p);
   else LAUNCH_E(k_dyn_advflux_b<12>, d.nEdges, d, p);
@@ -1004,56 +846,22 @@ bool fused_recover(const Dims& d) { return batched(d) && (d.maxEdges == 6 || d.m
 // fin = 1: the stage's last sub-step, which also recovers the owned cells (k_acoustic_cells_r<ME,
 // true>) when fused_recover(d); rdt / invNs / rk_step are k_recover_cells1's arguments
 // keep_pp = 0: a fin launch need not store rho_pp / rw_p (see k_acoustic_cells_r)
-// keep_old = 0 (record kernels): rtheta_pp_old is not stored (rotating buffers, see srk3)
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int fin = 0,
-                    double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1, int keep_old = 1) {
+                    double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1) {
   if (batched(d) && d.maxEdges == 6) {
     if (fin)
-      LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
-             keep_old);
-    else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, keep_old);
+      LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp);
+    else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1);
     return;
   }
   if (batched(d) && d.maxEdges == 7) {
     if (fin)
-      LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
-             keep_old);
-    else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, keep_old);
+      LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp);
+    else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1);
     return;
   }
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
 }
-
-// One fused sub-step (k_acoustic_fused, small_step >= 2) of block b: one workgroup per tile.
-void acoustic_fused(mpas_dyc_ctx* ctx, const Block& b, const Ptrs& p, const AcBufs& ab, double dts, int fresh,
-                    int phase, int fin = 0, double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1,
-                    int damp = 1) {
-  if (ctx->planning || b.ac_nt == 0) return;
-  const Dims& d = b.d;
-  const size_t lds = (size_t)b.ac_emax * d.K * sizeof(double);
-  const double cd = coef_divdamp(ctx, dts);
-#define AF_LAUNCH(ME, FIN)                                                                                        \
-  hipLaunchKernelGGL((k_acoustic_fused<ME, FIN>), dim3(b.ac_nt), dim3(AC_THREADS), lds, ctx->stream, d, p, ab, dts, \
-                     cd, fresh, ctx->cf.epssm, phase, b.ac_emax, rdt, invNs, rk_step, keep_pp, damp)
-  if (d.maxEdges == 6) {
-    if (fin) AF_LAUNCH(6, true);
-    else AF_LAUNCH(6, false);
-  } else {
-    if (fin) AF_LAUNCH(7, true);
-    else AF_LAUNCH(7, false);
-  }
-#undef AF_LAUNCH
-}
-
-// The rotating perturbation buffers of a stage's fused sub-steps (srk3).  Sub-step s of nsub
-// writes rtheta_pp to RT_NAMES[(nsub - s) % 3] and rho_pp / ru_p to the [(nsub - s) % 2] entries,
-// so the stage's last sub-step lands in the canonical diag fields; rtheta_pp_old of sub-step s is
-// the buffer of s - 2 (zero for s = 2), never a copy.
-const char* const RT_NAMES[3][2] = {{"diag", "rtheta_pp"}, {"scratch", "rtheta_pp_b"}, {"scratch", "rtheta_pp_c"}};
-const char* const RP_NAMES[2][2] = {{"diag", "rho_pp"}, {"scratch", "rho_pp_b"}};
-const char* const RU_NAMES[2][2] = {{"diag", "ru_p"}, {"scratch", "ru_p_b"}};
-int rt_slot(int nsub, int s) { return (nsub - s) % 3; }
-int pr_slot(int nsub, int s) { return (nsub - s) % 2; }
 
 // the last damping of a stage also recovers the edges with two owned cells (k_divdamp_p<true>);
 // needs the owned cells' rho_zz recovered by the last cell phase (fused_recover)
@@ -1346,88 +1154,32 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       //   edge phase of sub-step 2 or, for a one-sub-step stage, the damping, which also stores
       //   ruAvg (on the same edges, so the 876 exchange and the recovery see the same values).
       const int nsub = number_sub_steps[rk_step - 1];
-      // fused sub-steps (k_acoustic_fused): sub-steps 2..nsub run as one kernel each, on
-      // rotating perturbation buffers (RT_NAMES); sub-step 1 writes its results into the
-      // buffers of sub-step 1 (the stage's only sub-step lands in the canonical fields)
-      const bool rot = nsub >= 2 && fused_acoustic(ctx);
-      auto bufs = [&](Block& b, const Ptrs& p, int s2) {  // sub-step s2 >= 2 of block b
-        AcBufs ab;
-        ab.rt_cur = ::P<double>(ctx, b, RT_NAMES[rt_slot(nsub, s2 - 1)][0], RT_NAMES[rt_slot(nsub, s2 - 1)][1]);
-        ab.rt_old = s2 >= 3 ? ::P<double>(ctx, b, RT_NAMES[rt_slot(nsub, s2 - 2)][0], RT_NAMES[rt_slot(nsub, s2 - 2)][1])
-                            : nullptr;
-        ab.rt_out = ::P<double>(ctx, b, RT_NAMES[rt_slot(nsub, s2)][0], RT_NAMES[rt_slot(nsub, s2)][1]);
-        ab.rp_cur = ::P<double>(ctx, b, RP_NAMES[pr_slot(nsub, s2 - 1)][0], RP_NAMES[pr_slot(nsub, s2 - 1)][1]);
-        ab.rp_out = ::P<double>(ctx, b, RP_NAMES[pr_slot(nsub, s2)][0], RP_NAMES[pr_slot(nsub, s2)][1]);
-        ab.ru_cur = ::P<double>(ctx, b, RU_NAMES[pr_slot(nsub, s2 - 1)][0], RU_NAMES[pr_slot(nsub, s2 - 1)][1]);
-        ab.ru_out = ::P<double>(ctx, b, RU_NAMES[pr_slot(nsub, s2)][0], RU_NAMES[pr_slot(nsub, s2)][1]);
-        (void)p;
-        return ab;
-      };
-      const double rdt_s = rk_timestep[rk_step - 1];
-      const int keep_pp_s = needs_exchange(ctx) || last_stage;
       for (int small_step = 1; small_step <= nsub; ++small_step) {
-        const bool fin = small_step == nsub;
-        if (rot && small_step == 1) {
-          for (size_t ib = 0; ib < ctx->blk.size(); ++ib) {
-            Ptrs q = P[ib];
-            q.rtheta_pp = ::P<double>(ctx, ctx->blk[ib], RT_NAMES[rt_slot(nsub, 1)][0], RT_NAMES[rt_slot(nsub, 1)][1]);
-            q.rho_pp = ::P<double>(ctx, ctx->blk[ib], RP_NAMES[pr_slot(nsub, 1)][0], RP_NAMES[pr_slot(nsub, 1)][1]);
-            acoustic_cells(ctx, ctx->blk[ib].d, q, dts, 1, 0, 0.0, 0.0, 0, 1, 0);
-          }
-        } else if (rot) {  // damping of sub-step s-1 and sub-step s in one kernel per tile
-          const int fresh = small_step == 2;
-          if (split) {
-            for (size_t ib = 0; ib < ctx->blk.size(); ++ib)
-              acoustic_fused(ctx, ctx->blk[ib], P[ib], bufs(ctx->blk[ib], P[ib], small_step), dts, fresh, 1, fin, rdt_s,
-                             1 / (double)nsub, rk_step, keep_pp_s);
-            CHK(exchange_wait(ctx));
-            for (size_t ib = 0; ib < ctx->blk.size(); ++ib)
-              acoustic_fused(ctx, ctx->blk[ib], P[ib], bufs(ctx->blk[ib], P[ib], small_step), dts, fresh, 2, fin, rdt_s,
-                             1 / (double)nsub, rk_step, keep_pp_s);
-          } else {
-            for (size_t ib = 0; ib < ctx->blk.size(); ++ib)
-              acoustic_fused(ctx, ctx->blk[ib], P[ib], bufs(ctx->blk[ib], P[ib], small_step), dts, fresh, 0, fin, rdt_s,
-                             1 / (double)nsub, rk_step, keep_pp_s);
-          }
-          // exner / pressure_p of the recovered owned cells (see k_recover_exner)
-          if (fin && rk_step == 3) EACH(LAUNCH(k_recover_exner, d.nCellsSolve, d, p));
+        if (small_step == 1) {
+          // 794-837: formed by the readers (above)
+        } else if (split) {  // interior edges overlap the exchange issued after the last cell phase
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 1, small_step == 2));
+          CHK(exchange_wait(ctx));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 2, small_step == 2));
         } else {
-          if (small_step == 1) {
-            // 794-837: formed by the readers (above)
-          } else if (split) {  // interior edges overlap the exchange issued after the last cell phase
-            EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 1, small_step == 2));
-            CHK(exchange_wait(ctx));
-            EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 2, small_step == 2));
-          } else {
-            EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2));
-          }
-          EACH(acoustic_cells(ctx, d, p, dts, small_step, fin, rdt_s, 1 / (double)nsub, rk_step, keep_pp_s));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2));
         }
-        const int rs = rot ? rt_slot(nsub, small_step) : 0, ps = rot ? pr_slot(nsub, small_step) : 0;
-        std::vector<XField> xf = {{RT_NAMES[rs][0], RT_NAMES[rs][1], 0, 0x1u}};  // 845
-        if (small_step < nsub) xf.push_back({RP_NAMES[ps][0], RP_NAMES[ps][1], 0, 0x1u});  // 792 of the next sub-step
+        EACH(acoustic_cells(ctx, d, p, dts, small_step, small_step == nsub, rk_timestep[rk_step - 1],
+                            1 / (double)nsub, rk_step, needs_exchange(ctx) || last_stage));
+        std::vector<XField> xf = {{"diag", "rtheta_pp", 0, 0x1u}};  // 845
+        if (small_step < nsub) xf.push_back({"diag", "rho_pp", 0, 0x1u});  // 792 of the next sub-step
         if (split) {
           CHK(exchange_async(ctx, xf));
         } else {
           CHK((exchange)(ctx, xf));  // parenthesised: no ADL lookup of std::exchange
         }
       }
-      // the last sub-step's damping (849-869); with rotating buffers rtheta_pp_old is the
-      // buffer of sub-step nsub - 1
-      std::vector<Ptrs> PD = P;
-      if (rot)
-        for (size_t ib = 0; ib < ctx->blk.size(); ++ib)
-          PD[ib].rtheta_pp_old = ::P<double>(ctx, ctx->blk[ib], RT_NAMES[rt_slot(nsub, nsub - 1)][0],
-                                             RT_NAMES[rt_slot(nsub, nsub - 1)][1]);
-      if (split) {  // interior edges overlapping the exchange
-        for (size_t ib = 0; ib < ctx->blk.size(); ++ib)
-          divergence_damping(ctx, ctx->blk[ib].d, PD[ib], dts, 1, nsub == 1, 1 / (double)nsub);
+      if (split) {  // the last sub-step's damping (849-869), interior edges overlapping the exchange
+        EACH(divergence_damping(ctx, d, p, dts, 1, nsub == 1, 1 / (double)nsub));
         CHK(exchange_wait(ctx));
-        for (size_t ib = 0; ib < ctx->blk.size(); ++ib)
-          divergence_damping(ctx, ctx->blk[ib].d, PD[ib], dts, 2, nsub == 1);
+        EACH(divergence_damping(ctx, d, p, dts, 2, nsub == 1));
       } else {
-        for (size_t ib = 0; ib < ctx->blk.size(); ++ib)
-          divergence_damping(ctx, ctx->blk[ib].d, PD[ib], dts, 0, nsub == 1, 1 / (double)nsub);
+        EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1, 1 / (double)nsub));
       }
       const std::vector<XField> xrec = {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},  // 876-887
                                         {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};
@@ -1731,12 +1483,6 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   } else {
     g_kernel_tier = 2;
   }
-  {
-    const char* lv = getenv("MPAS_DYCORE_LDS");
-    g_lds_advflux = lv && std::string(lv) == "1";
-    const char* fv = getenv("MPAS_DYCORE_FUSED");
-    g_fused_ac = fv && std::string(fv) == "1";
-  }
   for (auto& b : ctx->blk) {
     build_registry(b);
     for (auto& f : b.fields) {
@@ -1782,8 +1528,6 @@ void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
     }
     for (auto& x : b.xl)
       if (x.d_idx) (void)hipFree(x.d_idx);
-    free_adv_tiles(b);
-    free_ac_tiles(b);
     if (b.sum_part) (void)hipFree(b.sum_part);
     if (b.sum_out) (void)hipFree(b.sum_out);
   }
@@ -1880,7 +1624,6 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
       b.h_eoc = tmp;
       ctx->bnd_ready = false;
     }
-    if (f->pool == "mesh" && f->name == "advCellsForEdge") ctx->bnd_ready = false;  // advflux tiles
     HIPCHK(hipMemcpyAsync(f->buf[slot], tmp.data(), nb, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
   } else if (f->nsub > 1) {
@@ -1901,7 +1644,6 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
       ctx->bnd_ready = false;
     }
     if (f->pool == "mesh" && (f->name == "zb_cell" || f->name == "zb3_cell")) ctx->bnd_ready = false;  // zb_p / zb_m
-    if (f->pool == "mesh" && f->name == "nAdvCellsForEdge") ctx->bnd_ready = false;  // advflux tiles
     if (f->pool == "tend" && f->name == "rt_diabatic_tend") {
       const double* h = (const double*)host;
       int nz = 0;
@@ -2376,28 +2118,15 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
   const Ptrs p = make_ptrs(ctx, b);
   const Dims& d = b.d;
   // the sequence srk3 runs for a `reps`-sub-step acoustic loop: edges, cells, then per further
-  // sub-step the damped edge phase and cells, and the last sub-step's damping on its own.  With
-  // the fused sub-step each rep is one k_acoustic_fused (undamped for the first) on rotating
-  // buffers: rtheta_pp through {rtheta_pp_old, rtheta_pp, rtheta_pp_c}, rho_pp / ru_p through
-  // {canonical, *_b}; the canonical fields get the final values afterwards (untimed).
-  const bool fz = fused_acoustic(ctx);
-  double* X[3] = {P<double>(ctx, b, "diag", "rtheta_pp_old"), P<double>(ctx, b, "diag", "rtheta_pp"),
-                  P<double>(ctx, b, "scratch", "rtheta_pp_c")};
-  double* PP[2] = {P<double>(ctx, b, "diag", "rho_pp"), P<double>(ctx, b, "scratch", "rho_pp_b")};
-  double* U[2] = {P<double>(ctx, b, "diag", "ru_p"), P<double>(ctx, b, "scratch", "ru_p_b")};
+  // sub-step the damped edge phase and cells, and the last sub-step's damping on its own
   double acc[3] = {0, 0, 0};
   float t;
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
   for (int r = 0; r < reps; ++r) {
     HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
-    if (fz) {
-      AcBufs ab{X[(r + 1) % 3], X[r % 3], PP[r % 2], U[r % 2], X[(r + 2) % 3], PP[(r + 1) % 2], U[(r + 1) % 2]};
-      acoustic_fused(ctx, b, p, ab, dts, 0, 0, 0, 0.0, 0.0, 0, 1, r > 0 ? 1 : 0);
-    } else {
-      acoustic_edges(ctx, d, p, dts, small_step, r > 0 ? 1 : 0, 0);
-    }
+    acoustic_edges(ctx, d, p, dts, small_step, r > 0 ? 1 : 0, 0);
     HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
-    if (!fz) acoustic_cells(ctx, d, p, dts, small_step);
+    acoustic_cells(ctx, d, p, dts, small_step);
     HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
     if (ms_kernels) {
       HIPCHK(hipEventSynchronize(ctx->ev[3]));
@@ -2408,41 +2137,11 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
     }
   }
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-  if (fz) {
-    Ptrs q = p;
-    q.rtheta_pp = X[(reps + 1) % 3];
-    q.rtheta_pp_old = X[reps % 3];
-    q.ru_p = U[reps % 2];
-    divergence_damping(ctx, d, q, dts, 0);
-  } else {
-    divergence_damping(ctx, d, p, dts, 0);
-  }
+  divergence_damping(ctx, d, p, dts, 0);
   HIPCHK(hipEventRecord(ctx->ev[4], ctx->stream));
   HIPCHK(hipEventSynchronize(ctx->ev[4]));
   (void)hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]);
   acc[2] += t;
-  if (fz) {  // canonical rtheta_pp = the final values, rtheta_pp_old = the previous sub-step's
-    const size_t nbK = (size_t)(d.nCells + 1) * d.K * sizeof(double), neK = (size_t)(d.nEdges + 1) * d.K * sizeof(double);
-    double* F = X[(reps + 1) % 3];
-    double* Q = X[reps % 3];
-    auto cp = [&](double* dst, double* src, size_t n) {
-      return dst == src ? hipSuccess : hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, ctx->stream);
-    };
-    if (F == X[0] && Q == X[1]) {  // swapped: through the scratch buffer
-      HIPCHK(cp(X[2], X[0], nbK));
-      HIPCHK(cp(X[0], X[1], nbK));
-      HIPCHK(cp(X[1], X[2], nbK));
-    } else if (Q == X[1]) {
-      HIPCHK(cp(X[0], Q, nbK));
-      HIPCHK(cp(X[1], F, nbK));
-    } else {
-      HIPCHK(cp(X[1], F, nbK));
-      HIPCHK(cp(X[0], Q, nbK));
-    }
-    HIPCHK(cp(PP[0], PP[reps % 2], nbK));
-    HIPCHK(cp(U[0], U[reps % 2], neK));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-  }
   float tot;
   HIPCHK(hipEventElapsedTime(&tot, ctx->ev[0], ctx->ev[4]));
   if (ms_out) *ms_out = tot / reps;

@@ -1868,112 +1868,6 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
   }
 }
 
-// k_dyn_advflux_p with the stencil columns staged through LDS.  One workgroup per tile of ADV_T
-// consecutive (SFC-ordered) edges: its waves first copy the w / theta_m columns of the tile's
-// distinct stencil cells (about 33 for 16 edges at x1.163842, instead of 160 gathered columns)
-// into LDS with coalesced column loads, then run the pair-layout edge computation with every
-// stencil operand read from LDS.  Same operands, same order of the sums: bit-identical to
-// k_dyn_advflux_p.  Only for NA = 10 (maxEdges 6) meshes; tile metadata built on the host
-// (checked on the host, build_adv_tiles); LDS = ADV_UMAX * (K+2 + K) doubles.  A tile with more
-// than ADV_UMAX cells (a jump of the space-filling curve, ~1 % of tiles) reads them from memory.
-template <int NA>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_advflux_t(Dims d, Ptrs p) {
-  static_assert(ADV_T == 2 * WAVES_PER_BLOCK, "one edge pair per wave");
-  extern __shared__ double lds[];
-  const int tile = xcd_block();
-  const int e0 = tile * ADV_T;
-  if (e0 >= d.nEdges) return;
-  const int n = __builtin_amdgcn_readfirstlane(p.adv_tn[tile]);
-  if (n == 0) return;  // no edge of this tile has an owned cell
-  const bool staged = n > 0;  // n < 0: more than ADV_UMAX cells (a jump of the curve): gathered from memory
-  const int K = d.K, K1 = K + 1, K1p = (K + 2) & ~1;
-  double* sw = lds;                              // [ADV_UMAX][K1p]
-  double* sth = lds + (size_t)ADV_UMAX * K1p;    // [ADV_UMAX][K]
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
-  // ---- this wave's edge pair: every operand that does not come from LDS, issued first
-  const int eA = min(e0 + 2 * wid, d.nEdges - 1);
-  const bool live = e0 + 2 * wid < d.nEdges;
-  const bool hasB = live && eA + 1 < d.nEdges;
-  const int eB = hasB ? eA + 1 : eA;
-  const int e = sel(h, eA, eB);
-  const size_t o = (size_t)e * K + 2 * lc;
-  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
-  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
-  const int naA = p.nAdvCellsForEdge[eA], naB = p.nAdvCellsForEdge[eB];
-  double a[NA], b[NA];
-  int lA[4], lB[4];
-#pragma unroll
-  for (int j = 0; j < NA; ++j) {
-    a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j));
-    b[j] = sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
-               ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {  // slot bytes, four per int, through the scalar unit
-    lA[q] = reinterpret_cast<const int*>(p.adv_loc + (size_t)eA * ADV_LOC)[q];
-    lB[q] = reinterpret_cast<const int*>(p.adv_loc + (size_t)eB * ADV_LOC)[q];
-  }
-  const d2 rue = ld2(p.ru + o);
-  const d2 fzm = ld2(p.fzm + 2 * lc), fzp = ld2(p.fzp + 2 * lc);
-  // ---- stage the tile's distinct stencil columns: wave wid copies columns wid, wid+4, ...
-  if (staged) {
-    for (int u0 = wid; u0 < n; u0 += 4 * WAVES_PER_BLOCK) {
-      double wr[4], tr[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int u = u0 + q * WAVES_PER_BLOCK;
-        const int c = __builtin_amdgcn_readfirstlane(p.adv_tcell[(size_t)tile * ADV_UMAX + min(u, n - 1)]);
-        wr[q] = p.w2[(size_t)c * K1 + min(lane, K)];
-        tr[q] = p.theta_m2[(size_t)c * K + min(lane, K - 1)];
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int u = u0 + q * WAVES_PER_BLOCK;
-        if (u < n) {
-          if (lane < K1) sw[u * K1p + lane] = wr[q];
-          if (lane < K) sth[u * K + lane] = tr[q];
-        }
-      }
-    }
-  }
-  __syncthreads();
-  const bool onA = live && (ceA.x < d.nCellsSolve || ceA.y < d.nCellsSolve);
-  const bool onB = hasB && (ceB.x < d.nCellsSolve || ceB.y < d.nCellsSolve);
-  if (!onA && !onB) return;
-  const int kx = 2 * l, ky = 2 * l + 1;
-  const d2 rue_m = km1(rue, l);
-  const double rewx = kx < K ? fzm.x * rue.x + fzp.x * rue_m.x : 0.0;
-  const double rewy = ky < K ? fzm.y * rue.y + fzp.y * rue_m.y : 0.0;
-  const double swx = sgn1(rewx), swy = sgn1(rewy), stx_ = sgn1(rue.x), sty_ = sgn1(rue.y);
-  const int na = sel(h, naA, naB);
-  d2 fw{0.0, 0.0}, ft{0.0, 0.0};
-#pragma unroll
-  for (int j = 0; j < NA; ++j) {
-    d2 w_, t_;
-    if (staged) {
-      const int u = (sel(h, lA[j >> 2], lB[j >> 2]) >> (8 * (j & 3))) & 0xff;
-      w_ = ld2(sw + u * K1p + 2 * lw);
-      t_ = ld2(sth + u * K + 2 * lc);
-    } else {
-      const size_t cj = (size_t)p.advCellsForEdge[(size_t)e * 15 + j];
-      w_ = ld2(p.w2 + cj * K1 + 2 * lw);
-      t_ = ld2(p.theta_m2 + cj * K + 2 * lc);
-    }
-    if (j < na) {
-      fw.x = fw.x + (a[j] + swx * b[j]) * w_.x;
-      fw.y = fw.y + (a[j] + swy * b[j]) * w_.y;
-      ft.x = ft.x + (a[j] + stx_ * b[j]) * t_.x;
-      ft.y = ft.y + (a[j] + sty_ * b[j]) * t_.y;
-    }
-  }
-  if ((h ? onB : onA) && 2 * l < K) {
-    st2(p.advflux_w + o, fw);
-    st2(p.advflux_th + o, ft);
-  }
-}
-
 // k_diag_edges_b in the pair layout
 template <int NE2>
 __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, const double* __restrict__ u,
@@ -2441,12 +2335,10 @@ __device__ __forceinline__ RecIn load_rec_in(const Dims& d, const Ptrs& p, size_
   r.rtd = (rk_step == 3 && d.diabatic) ? p.rt_diabatic_tend[o] : 0.0;
   return r;
 }
-// exner_now = 0: exner and pressure_p (rk_step 3) are left to k_recover_exner, which computes
-// them from the stored rtheta_p -- the same operands, so the same bits.
 __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p, int c, int k, double zz_k, double rws,
                                                    double fzm_k, double fzp_k, const RecIn& ri, double rhopp,
                                                    double rtpp, double rwp, double wwa, double dt, double invNs,
-                                                   int rk_step, bool exner_now = true) {
+                                                   int rk_step) {
   const int K = d.K;
   const size_t K1 = K + 1;
   const bool act = k < K;
@@ -2476,11 +2368,9 @@ __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p,
       const double rtp = rtps + rtpp - dt * rz * ri.rtd;  // rtd = 0.0 without diabatic forcing, as in k_recover_cells1
       p.rtheta_p[o] = rtp;
       p.theta_m2[o] = (rtp + rtb) / rz;
-      if (exner_now) {
-        const double ex = pow(zz * (RGAS / P0) * (rtp + rtb), rcv);
-        p.exner[o] = ex;
-        p.pressure_p[o] = zz * RGAS * (ex * rtp + rtb * (ex - ri.exb));
-      }
+      const double ex = pow(zz * (RGAS / P0) * (rtp + rtb), rcv);
+      p.exner[o] = ex;
+      p.pressure_p[o] = zz * RGAS * (ex * rtp + rtb * (ex - ri.exb));
     } else {
       const double rtp = rtps + rtpp;
       p.rtheta_p[o] = rtp;
@@ -2489,12 +2379,6 @@ __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p,
   }
 }
 
-// The owned-cell column solve of the cell phase (2603-2721) for cell c, lane = level k, from the
-// ru_p of its edges (ru[], formed by the caller) and theta_m of the cells across them (th[]).
-// Shared by the record kernel (k_acoustic_cells_r: ru_p gathered from HBM) and the fused sub-step
-// (k_acoustic_fused: ru_p from LDS), so both evaluate the same expressions in the same order.
-// rtpp / rhopp / rwp / wwa: this sub-step's perturbations at (c, k) (zero on sub-step 1, 2617-2622).
-// rt_out / rp_out receive rtheta_pp / rho_pp; rt_old (nullptr: not kept) receives rtheta_pp_old.
 // FIN: the stage's last sub-step also recovers its owned cells (recover_cell_fused): nothing
 // between this launch and k_recover_cells1 -- the Theta''/rho'' exchange, the damping (ru_p,
 // ruAvg) and the 876-887 exchange -- reads or writes what the recovery reads or writes for an
@@ -2502,29 +2386,59 @@ __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p,
 // keep_pp = 0 (FIN only): rho_pp and rw_p are not stored.  After a stage's last sub-step nothing
 // reads them but the 876-887 exchange and the halo-cell recovery; srk3 passes 0 only for a block
 // without exchanges and a stage that is not the dt's last (whose values the pool keeps).
-template <int ME, bool FIN>
-__device__ __forceinline__ void acoustic_column(const Dims& d, const Ptrs& p, int c, int k, double dts, bool first,
-                                                double epssm, double rdt, double invNs, int rk_step, int keep_pp,
-                                                const double (&ru)[ME], const double (&th)[ME],
-                                                const double (&sdv)[ME], int ne, double rtpp, double rhopp,
-                                                double rwp, double wwa, double* rt_out, double* rp_out,
-                                                double* rt_old, bool exner_now = true) {
-  const int K = d.K;
+template <int ME, bool FIN = false>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs p, double dts, int small_step,
+                                                                    double epssm, double rdt = 0.0,
+                                                                    double invNs = 0.0, int rk_step = 0,
+                                                                    int keep_pp = 1) {
+  const int c = wave_elem(0);
+  if (c >= d.nCells) return;
+  const int k = lane_id(), K = d.K;
   const bool act = k < K, actw = k <= K;
   const int kc = min(k, K - 1), kw = min(k, K);  // clamped lanes load in bounds and store nothing
   const size_t K1 = K + 1;
   const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
+  // sub-step 1 starts from zero perturbations (2617-2622): rtheta_pp, rho_pp, rw_p and wwAvg are
+  // not read then (the values would be replaced by 0 below), which saves four streams
+  const bool first = small_step == 1;
+  double rtpp = first ? 0.0 : p.rtheta_pp[o];
+  if (c >= d.nCellsSolve) {
+    if (act) p.rtheta_pp_old[o] = first ? 0.0 : rtpp;
+    return;
+  }
+  int re[ME], rc[ME];
+  double sdv[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    re[i] = p.cell_rec[(size_t)c * CELL_REC + i];
+    rc[i] = p.cell_rec[(size_t)c * CELL_REC + CELL_REC_ME + i];
+    sdv[i] = ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i);
+  }
+  const int ne = p.cell_rec[(size_t)c * CELL_REC + 14];
   const double invA = p.invAreaCell[c], spec = p.specZoneMaskCell[c];
+  double rhopp = first ? 0.0 : p.rho_pp[o], rwp = first ? 0.0 : p.rw_p[ow], wwa = first ? 0.0 : p.wwAvg[ow];
   const double thc = p.theta_m1[o], trho = p.tend_rho[o], tth = p.tend_theta[o], tw = p.tend_w[ow];
+  double ru[ME], th[ME];
+  // sub-step 1: ru_p = dts * tend_u (794-837), formed here; srk3 launches no edge phase for it
+  const double* __restrict__ rusrc = small_step == 1 ? p.tend_u : p.ru_p;
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    ru[i] = rusrc[(size_t)re[i] * K + kc];
+    th[i] = p.theta_m1[(size_t)rc[i] * K + kc];
+  }
+  if (small_step == 1) {
+#pragma unroll
+    for (int i = 0; i < ME; ++i) ru[i] = dts * ru[i];
+  }
   const double coftz = p.coftz[ow], zz = p.zz[o], cofwt = p.cofwt[o], cofwz = p.cofwz[o], cofwr = p.cofwr[o];
   const double a_tri = p.a_tri[o], alpha_tri = p.alpha_tri[o], gamma_tri = p.gamma_tri[o];
   const double rz = p.rho_zz2[o], dss = p.dss[o], rws = p.rw_save[ow], rw = p.rw[ow], w2 = p.w2[ow];
   const double cofrz = p.cofrz[kc], rdzw = p.rdzw[kc], fzm = p.fzm[kc], fzp = p.fzp[kc];
   RecIn ri{};
   if (FIN) ri = load_rec_in(d, p, o, rk_step);
-  const double rtpp_old = first ? 0.0 : rtpp;
+  const double rtpp_old = (small_step == 1) ? 0.0 : rtpp;
   const double resm = (1.0 - epssm) / (1.0 + epssm);
-  if (first) { wwa = 0.0; rhopp = 0.0; rtpp = 0.0; rwp = 0.0; }
+  if (small_step == 1) { wwa = 0.0; rhopp = 0.0; rtpp = 0.0; rwp = 0.0; }
   if (!act) { rhopp = 0.0; rtpp = 0.0; }  // the column's k = K+1 lane: zero, as a masked load gives
   if (spec == 0.0) {
     double ts = 0.0, rs = 0.0;
@@ -2565,17 +2479,16 @@ __device__ __forceinline__ void acoustic_column(const Dims& d, const Ptrs& p, in
     const double rho_new = rs - cofrz * (rwp_p2 - rwp);
     const double rt_new = ts - rdzw * (coftz_p * rwp_p2 - coftz * rwp);
     if (act) {
-      if (rt_old) rt_old[o] = rtpp_old;  // stored last: no store precedes the loads above
-      if (!FIN || keep_pp) rp_out[o] = rho_new;
-      rt_out[o] = rt_new;
+      p.rtheta_pp_old[o] = rtpp_old;  // stored last: no store precedes the loads above
+      if (!FIN || keep_pp) p.rho_pp[o] = rho_new;
+      p.rtheta_pp[o] = rt_new;
     }
     if (actw) {
       if (!FIN || keep_pp) p.rw_p[ow] = rwp;
       if (!FIN) p.wwAvg[ow] = wwa;
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;  // levels 2..K: recover_cell_fused
     }
-    if (FIN)
-      recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rho_new, rt_new, rwp, wwa, rdt, invNs, rk_step, exner_now);
+    if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rho_new, rt_new, rwp, wwa, rdt, invNs, rk_step);
   } else {
     // specified zone (2710-2719): regional only, masks are 0 for global meshes
     if (act) {
@@ -2583,201 +2496,16 @@ __device__ __forceinline__ void acoustic_column(const Dims& d, const Ptrs& p, in
       rtpp = rtpp + dts * tth;
       rwp = rwp + dts * tw;
       wwa = wwa + 0.5 * (1.0 + epssm) * rwp;
-      if (rt_old) rt_old[o] = rtpp_old;
-      rp_out[o] = rhopp;
-      rt_out[o] = rtpp;
+      p.rtheta_pp_old[o] = rtpp_old;
+      p.rho_pp[o] = rhopp;
+      p.rtheta_pp[o] = rtpp;
     }
     if (actw) {
       p.rw_p[ow] = rwp;
       if (!FIN) p.wwAvg[ow] = wwa;
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;
     }
-    if (FIN)
-      recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rhopp, rtpp, rwp, wwa, rdt, invNs, rk_step, exner_now);
-  }
-}
-
-// exner and pressure_p of the owned cells at the end of rk_step 3 (3023-3031), after a fused
-// sub-step that recovered everything else: another tile's edge phase reads exner of the cells a
-// tile recovers, so the fused kernel leaves these two to this launch.
-__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_exner(Dims d, Ptrs p) {
-  const int c = wave_elem(0);
-  if (c >= d.nCellsSolve) return;
-  const int k = lane_id(), K = d.K;
-  if (k >= K) return;
-  const size_t o = (size_t)c * K + k;
-  const double rcv = RGAS / (CP - RGAS);
-  const double zz = p.zz[o], rtp = p.rtheta_p[o], rtb = p.rtheta_base[o], exb = p.exner_base[o];
-  const double ex = pow(zz * (RGAS / P0) * (rtp + rtb), rcv);
-  p.exner[o] = ex;
-  p.pressure_p[o] = zz * RGAS * (ex * rtp + rtb * (ex - exb));
-}
-
-// cell phase on the per-cell stencil record (ME = maxEdges <= 7): every load the column needs --
-// the record, its own columns, the ru_p of its edges and theta_m of the cells across them -- is
-// issued before the first use.  keep_old = 0: rtheta_pp_old is not stored (the rotating
-// perturbation buffers of the fused sub-steps make it a buffer of its own, see srk3).
-template <int ME, bool FIN = false>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs p, double dts, int small_step,
-                                                                    double epssm, double rdt = 0.0,
-                                                                    double invNs = 0.0, int rk_step = 0,
-                                                                    int keep_pp = 1, int keep_old = 1) {
-  const int c = wave_elem(0);
-  if (c >= d.nCells) return;
-  const int k = lane_id(), K = d.K;
-  const bool act = k < K;
-  const int kc = min(k, K - 1), kw = min(k, K);
-  const size_t o = (size_t)c * K + kc, ow = (size_t)c * (K + 1) + kw;
-  // sub-step 1 starts from zero perturbations (2617-2622): rtheta_pp, rho_pp, rw_p and wwAvg are
-  // not read then (the values would be replaced by 0), which saves four streams
-  const bool first = small_step == 1;
-  const double rtpp = first ? 0.0 : p.rtheta_pp[o];
-  if (c >= d.nCellsSolve) {
-    if (act && keep_old) p.rtheta_pp_old[o] = first ? 0.0 : rtpp;
-    return;
-  }
-  int re[ME], rc[ME];
-  double sdv[ME];
-#pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    re[i] = p.cell_rec[(size_t)c * CELL_REC + i];
-    rc[i] = p.cell_rec[(size_t)c * CELL_REC + CELL_REC_ME + i];
-    sdv[i] = ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i);
-  }
-  const int ne = p.cell_rec[(size_t)c * CELL_REC + 14];
-  const double rhopp = first ? 0.0 : p.rho_pp[o], rwp = first ? 0.0 : p.rw_p[ow], wwa = first ? 0.0 : p.wwAvg[ow];
-  double ru[ME], th[ME];
-  // sub-step 1: ru_p = dts * tend_u (794-837), formed here; srk3 launches no edge phase for it
-  const double* __restrict__ rusrc = first ? p.tend_u : p.ru_p;
-#pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    ru[i] = rusrc[(size_t)re[i] * K + kc];
-    th[i] = p.theta_m1[(size_t)rc[i] * K + kc];
-  }
-  if (first) {
-#pragma unroll
-    for (int i = 0; i < ME; ++i) ru[i] = dts * ru[i];
-  }
-  acoustic_column<ME, FIN>(d, p, c, k, dts, first, epssm, rdt, invNs, rk_step, keep_pp, ru, th, sdv, ne, rtpp, rhopp,
-                           rwp, wwa, p.rtheta_pp, p.rho_pp, keep_old ? p.rtheta_pp_old : nullptr);
-}
-
-// One fused acoustic sub-step, small_step >= 2 (atm_divergence_damping_3d of the previous sub-step
-// 2765-2793, then atm_advance_acoustic_step 2540-2721), per tile of AC_T consecutive owned cells:
-//   A. every edge of the tile's cells (ac_tedge: distinct, host-built) gets its damped, updated
-//      ru_p in the pair layout, into LDS; the tile that owns the edge (the lowest-numbered owned
-//      cell of the edge lies in it) also stores ru_p and ruAvg.  Edges between two tiles are
-//      computed by both -- from the same operands, so to the same bits.
-//   B. each owned cell's column solve reads its edges' ru_p from LDS (ac_cslot).
-// The edge and cell phases no longer meet in HBM: ru_p is not re-read, and the cells' own
-// columns the edge phase gathers are reused from the cache.  Phase A of one tile reads the
-// perturbations of cells another tile updates in phase B, so the sub-step reads rtheta_pp /
-// rho_pp / ru_p from one buffer and writes another (AcBufs; srk3 rotates them, with rtheta_pp_old
-// being the buffer two sub-steps back -- no copy).  old == nullptr: that buffer is all zero
-// (the stage's first sub-step set rtheta_pp_old = 0, 2610-2612); fresh: the previous sub-step was
-// sub-step 1, whose ru_p = ruAvg = dts * tend_u (794-837) are formed here.
-// phase 1 / 2: tiles without / with an edge touching a halo cell (split-phase exchanges), 0 all.
-// damp = 0: no damping precedes the sub-step (the first of mpas_dyc_time_acoustic_step's loop).
-struct AcBufs {
-  const double *rt_cur, *rt_old, *rp_cur, *ru_cur;
-  double *rt_out, *rp_out, *ru_out;
-};
-template <int ME, bool FIN>
-__global__ __launch_bounds__(AC_THREADS) void k_acoustic_fused(Dims d, Ptrs p, AcBufs b, double dts,
-                                                               double coef_divdamp, int fresh, double epssm,
-                                                               int phase, int emax, double rdt, double invNs,
-                                                               int rk_step, int keep_pp, int damp) {
-  extern __shared__ double lds[];  // emax columns of K doubles: the tile's new ru_p
-  const int t = xcd_block();
-  if (phase && ((p.ac_tbnd[t] != 0) != (phase == 2))) return;
-  const int ne_t = p.ac_tne[t];
-  const int K = d.K, wv = threadIdx.x >> 6;
-  // ---- A: the tile's edges, two per wave (pair layout: half h, lane l holds levels 2l, 2l+1)
-  {
-    const int h = pair_half(), l = threadIdx.x & 31;
-    const bool lev = 2 * l < K;
-    const int lc = min(l, K / 2 - 1);
-    const double rcv = RGAS / (CP - RGAS);
-    const double c2v = CP * rcv;
-    for (int j0 = 2 * wv; j0 < ne_t; j0 += 2 * AC_WAVES) {
-      const int jA = j0, jB = min(j0 + 1, ne_t - 1);
-      const int tA = p.ac_tedge[(size_t)t * emax + jA], tB = p.ac_tedge[(size_t)t * emax + jB];
-      const int eA = tA >> 1, eB = tB >> 1;
-      const int e = sel(h, eA, eB), j = sel(h, jA, jB);
-      const bool wr = (sel(h, tA, tB) & 1) && (h == 0 || j0 + 1 < ne_t);
-      const size_t o = (size_t)e * K + 2 * lc;
-      const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
-      const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
-      const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
-      const size_t o1 = (size_t)c1 * K + 2 * lc, o2 = (size_t)c2 * K + 2 * lc;
-      const d2 tu = ld2(p.tend_u + o);
-      d2 rup, rua{0.0, 0.0};
-      if (fresh) {
-        rup = d2{dts * tu.x, dts * tu.y};
-        rua = rup;
-      } else {
-        rup = ld2(b.ru_cur + o);
-        if (wr) rua = ld2(p.ruAvg + o);
-      }
-      const d2 cqu = ld2(p.cqu + o), zxu = ld2(p.zxu + o);
-      const double mask = sel(h, ld_uniform_f64(p.specZoneMaskEdge + eA), ld_uniform_f64(p.specZoneMaskEdge + eB));
-      const double invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
-      const d2 rt1 = ld2(b.rt_cur + o1), rt2 = ld2(b.rt_cur + o2);
-      const d2 zz1 = ld2(p.zz + o1), zz2 = ld2(p.zz + o2), ex1 = ld2(p.exner + o1), ex2 = ld2(p.exner + o2);
-      const d2 rp1 = ld2(b.rp_cur + o1), rp2 = ld2(b.rp_cur + o2);
-      const d2 ro1 = b.rt_old ? ld2(b.rt_old + o1) : d2{0.0, 0.0}, ro2 = b.rt_old ? ld2(b.rt_old + o2) : d2{0.0, 0.0};
-      const d2 th1 = ld2(p.theta_m1 + o1), th2 = ld2(p.theta_m1 + o2);
-      // the expressions of k_acoustic_edges_p<true>
-      auto level = [&](double r, double tu_, double cq, double zx, double a1, double a2, double z1, double z2,
-                       double x1, double x2, double p1, double p2, double o1_, double o2_, double t1, double t2) {
-        if (damp) {
-          const double dd1 = -(a1 - o1_);
-          const double dd2 = -(a2 - o2_);
-          r = r + coef_divdamp * (dd2 - dd1) * (1.0 - mask) / (t1 + t2);
-        }
-        double pgrad = ((a2 - a1) * invDc) / (.5 * (z2 + z1));
-        pgrad = cq * 0.5 * c2v * (x1 + x2) * pgrad;
-        pgrad = pgrad + 0.5 * zx * GRAVITY * (p1 + p2);
-        return r + dts * (tu_ - (1.0 - mask) * pgrad);
-      };
-      rup.x = level(rup.x, tu.x, cqu.x, zxu.x, rt1.x, rt2.x, zz1.x, zz2.x, ex1.x, ex2.x, rp1.x, rp2.x, ro1.x, ro2.x,
-                    th1.x, th2.x);
-      rup.y = level(rup.y, tu.y, cqu.y, zxu.y, rt1.y, rt2.y, zz1.y, zz2.y, ex1.y, ex2.y, rp1.y, rp2.y, ro1.y, ro2.y,
-                    th1.y, th2.y);
-      if (lev) {
-        st2(lds + (size_t)j * K + 2 * l, rup);
-        if (wr) {
-          st2(b.ru_out + o, rup);
-          st2(p.ruAvg + o, d2{rua.x + rup.x, rua.y + rup.y});
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // ---- B: the tile's owned cells, one per wave (lane = level)
-  const int k = lane_id();
-  const int kc = min(k, K - 1), kw = min(k, K);
-  const int c_end = min(d.nCellsSolve, (t + 1) * AC_T);
-  for (int c = __builtin_amdgcn_readfirstlane(t * AC_T + wv); c < c_end; c += AC_WAVES) {
-    const size_t o = (size_t)c * K + kc, ow = (size_t)c * (K + 1) + kw;
-    const unsigned long long slots = *reinterpret_cast<const unsigned long long*>(p.ac_cslot + (size_t)c * 8);
-    int rc[ME];
-    double sdv[ME], ru[ME], th[ME];
-#pragma unroll
-    for (int i = 0; i < ME; ++i) {
-      rc[i] = p.cell_rec[(size_t)c * CELL_REC + CELL_REC_ME + i];
-      sdv[i] = ld_uniform_f64(p.cell_sdv + (size_t)c * ME + i);
-    }
-    const int ne = p.cell_rec[(size_t)c * CELL_REC + 14];
-    const double rtpp = b.rt_cur[o], rhopp = b.rp_cur[o], rwp = p.rw_p[ow], wwa = p.wwAvg[ow];
-#pragma unroll
-    for (int i = 0; i < ME; ++i) {
-      const int s = (int)((slots >> (8 * i)) & 0xff);
-      ru[i] = lds[(size_t)s * K + kc];
-      th[i] = p.theta_m1[(size_t)rc[i] * K + kc];
-    }
-    acoustic_column<ME, FIN>(d, p, c, k, dts, false, epssm, rdt, invNs, rk_step, keep_pp, ru, th, sdv, ne, rtpp,
-                             rhopp, rwp, wwa, b.rt_out, b.rp_out, nullptr, false);
+    if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rhopp, rtpp, rwp, wwa, rdt, invNs, rk_step);
   }
 }
 

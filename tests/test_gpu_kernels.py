@@ -86,12 +86,10 @@ def test_acoustic_substep_bitwise_vs_reference_fixture():
     dy.close()
 
 
-def _steps_with_kernels(case, family, nsteps=3, dt=None, lds="0", fused="0"):
+def _steps_with_kernels(case, family, nsteps=3, dt=None):
     from mpas_dycore import Dycore
-    saved = {k: os.environ.get(k) for k in ("MPAS_DYCORE_KERNELS", "MPAS_DYCORE_LDS", "MPAS_DYCORE_FUSED")}
+    saved = {k: os.environ.get(k) for k in ("MPAS_DYCORE_KERNELS",)}
     os.environ["MPAS_DYCORE_KERNELS"] = family
-    os.environ["MPAS_DYCORE_LDS"] = lds
-    os.environ["MPAS_DYCORE_FUSED"] = fused
     try:
         dy = Dycore(case, device=0, moist_end=case["num_scalars"])
     finally:
@@ -125,42 +123,6 @@ def test_kernel_families_give_identical_bits(which, request):
         got = _steps_with_kernels(case, fam, dt=dt)
         for n in ref:
             assert np.array_equal(got[n], ref[n]), f"{fam}: {n}"
-
-
-@pytest.mark.parametrize("which", ["moist_case", "varres_case_small"])
-def test_fused_acoustic_substep_gives_identical_bits(which, request):
-    """The fused sub-step (k_acoustic_fused: damping + edge phase into LDS + cell phase per tile of
-    cells, on rotating rtheta_pp / rho_pp / ru_p buffers) against the two-kernel sub-step
-    (MPAS_DYCORE_FUSED=0): three moist monotone steps agree to the bit.  order 3 makes the last
-    stage's 2 sub-steps run it, with the stage's recovery fused in (FIN)."""
-    case = dict(request.getfixturevalue(which))
-    case["config"] = dict(case["config"], config_time_integration_order=3)
-    dt = float(case["dt"]) if which == "varres_case_small" else 2880.0
-    ref = _steps_with_kernels(case, "pair", dt=dt, fused="0")
-    got = _steps_with_kernels(case, "pair", dt=dt, fused="1")
-    for n in ref:
-        assert np.array_equal(got[n], ref[n]), n
-
-
-def test_fused_acoustic_loop_bitwise_with_many_substeps():
-    """config_number_of_sub_steps = 6 (stages of 1, 3 and 6 sub-steps): all three rotating rtheta_pp
-    buffers are in flight; 2 steps agree to the bit with the two-kernel path."""
-    from mpas_dycore.cases import jw_case
-    case = jw_case(642, K=26, ns=1, cache=False)
-    case["config"] = dict(case["config"], config_number_of_sub_steps=6, config_time_integration_order=3)
-    ref = _steps_with_kernels(case, "pair", nsteps=2, fused="0")
-    got = _steps_with_kernels(case, "pair", nsteps=2, fused="1")
-    for n in ref:
-        assert np.array_equal(got[n], ref[n]), n
-
-
-def test_lds_staged_advflux_gives_identical_bits(moist_case):
-    """The opt-in LDS-staged advflux (MPAS_DYCORE_LDS=1, k_dyn_advflux_t) reads the same stencil
-    operands from LDS: three moist monotone steps agree to the bit with the pair kernel."""
-    ref = _steps_with_kernels(moist_case, "pair")
-    got = _steps_with_kernels(moist_case, "pair", lds="1")
-    for n in ref:
-        assert np.array_equal(got[n], ref[n]), n
 
 
 def test_odd_level_count_runs_the_single_column_kernels():
