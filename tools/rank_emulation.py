@@ -21,10 +21,12 @@ def main():
     ap.add_argument("--ncells", type=int, default=163842)
     ap.add_argument("--parts", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--order", type=int, default=3)
+    ap.add_argument("--no-graph", action="store_true", help="eager launches (what a rank without hipGraph costs)")
     a = ap.parse_args()
     from mpas_dycore import Dycore, decomp
     from mpas_dycore.cases import jw_case
-    case = jw_case(a.ncells, K=56)
+    case = jw_case(a.ncells, K=56, order=a.order)
     dt = case["dt"]
     res = {}
     for n in a.parts:
@@ -34,7 +36,7 @@ def main():
             (b,) = decomp.decompose(case, decomp.partition_sfc(case["nCells"], n), parts=[0])
             dy = Dycore(b.case, device=0, solve=b.solve)
         dy.init_diagnostics(dt)
-        dy.use_graph(True)
+        dy.use_graph(not a.no_graph)
         for i in range(2):
             dy.atm_timestep(dt, i + 1)
             dy.shift_time_levels()
@@ -46,7 +48,8 @@ def main():
         dy.synchronize()
         res[n] = (time.perf_counter() - t0) / a.steps * 1e3
         dy.close()
-        print(json.dumps(dict(parts=n, ms_per_dt=res[n], compute_speedup=res[a.parts[0]] / res[n])), flush=True)
+        print(json.dumps(dict(parts=n, graph=not a.no_graph, ms_per_dt=res[n], compute_speedup=res[a.parts[0]] / res[n])),
+              flush=True)
 
 
 if __name__ == "__main__":
