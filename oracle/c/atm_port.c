@@ -5,7 +5,7 @@
  * Compiled with -ffp-contract=off: every expression keeps the Fortran
  * left-to-right evaluation order, so results are bit-identical to the
  * reference's x86 build (which has no FMA).  Pinned against the compiled
- * reference by tests/test_oracle_port.py.
+ * reference's fixture by tests/test_oracle.py.
  */
 #include "atm_port.h"
 
