@@ -32,6 +32,11 @@ module harness_fields
    ! comma-separated 'pool.name' list; when not blank only these fields are dumped (full-size runs)
    character(len=1024) :: dump_only = ''
    logical :: dump_ints = .false.   ! mode 'init' also dumps integer fields (index arrays it builds)
+   ! multi-block runs: fields are registered (for dumping) from the first block only, are active
+   ! (so mpas_dmpar exchanges them), and carry their decomposed dimension's name (for
+   ! mpas_pool_link_parinfo), inferred from the current block's element counts
+   logical :: registering = .true., fields_active = .false.
+   integer :: cur_nC1 = -1, cur_nE1 = -1, cur_nV1 = -1
    type (block_type), pointer :: hblock => null()
 
    integer, parameter :: MAXF = 400
@@ -47,10 +52,19 @@ contains
       inquire(file=trim(indir)//'/'//trim(name)//'.bin', exist=file_exists)
    end function file_exists
 
+   character(len=StrKIND) function dimname_of(n)
+      integer, intent(in) :: n
+      dimname_of = 'nVertLevels'
+      if (n == cur_nC1) dimname_of = 'nCells'
+      if (n == cur_nE1) dimname_of = 'nEdges'
+      if (n == cur_nV1) dimname_of = 'nVertices'
+   end function dimname_of
+
    subroutine register(pname, name, rnk, ntl, isint)
       character(len=*), intent(in) :: pname, name
       integer, intent(in) :: rnk, ntl
       logical, intent(in) :: isint
+      if (.not. registering) return
       nf = nf + 1
       fname(nf) = name
       fpool(nf) = pname
@@ -126,6 +140,8 @@ contains
       f % fieldName = name
       f % isActive = .false.
       f % dimSizes(1) = d1
+      f % isActive = fields_active
+      f % dimNames(1) = dimname_of(d1)
       allocate(f % array(d1))
       f % array = 0.0_RKIND
       call read_r(name, f % array, d1)
@@ -147,6 +163,8 @@ contains
          fa(t) % isActive = .false.
          fa(t) % dimSizes(1) = d1
          fa(t) % dimSizes(2) = d2
+         fa(t) % isActive = fields_active
+         fa(t) % dimNames(2) = dimname_of(d2)
          allocate(fa(t) % array(d1, d2))
          fa(t) % array = 0.0_RKIND
       end do
@@ -172,6 +190,8 @@ contains
          fa(t) % dimSizes(1) = d1
          fa(t) % dimSizes(2) = d2
          fa(t) % dimSizes(3) = d3
+         fa(t) % isActive = fields_active
+         fa(t) % dimNames(3) = dimname_of(d3)
          allocate(fa(t) % array(d1, d2, d3))
          fa(t) % array = 0.0_RKIND
       end do
@@ -318,7 +338,13 @@ program mpas_ref_harness
    integer :: kernel_small_step, kernel_rk_step
    real(kind=RKIND) :: kernel_dts
    integer :: print_minmax   ! summarize_timestep switches: 1 global_minmax_vel, 2 detailed_minmax_vel, 4 global_minmax_sca
-   namelist /harness/ mode, print_minmax, dump_only, kernel_small_step, kernel_rk_step, kernel_dts, nCells, nEdges, nVertices, nVertLevels_in, maxEdges_in, maxEdges2_in, num_scalars_in, &
+   integer :: nblocks, ib, nhalo_ev
+   integer :: nCellsSolve_in, nEdgesSolve_in, nVerticesSolve_in
+   character(len=256) :: rootdir
+   type (block_type), pointer :: blk
+   type (field2DReal), pointer :: f2_u, f2_pv, f2_ru, f2_rw
+   namelist /block/ nCells, nEdges, nVertices, nCellsSolve_in, nEdgesSolve_in, nVerticesSolve_in
+   namelist /harness/ mode, nblocks, print_minmax, dump_only, kernel_small_step, kernel_rk_step, kernel_dts, nCells, nEdges, nVertices, nVertLevels_in, maxEdges_in, maxEdges2_in, num_scalars_in, &
       nsteps, moist_end, nthreads_req, dump_steps, dt, sphere_radius, &
       config_time_integration_order, config_number_of_sub_steps, config_dynamics_split_steps, &
       config_number_rayleigh_damp_u_levels, config_split_dynamics_transport, config_scalar_advection, &
@@ -353,6 +379,7 @@ program mpas_ref_harness
    kernel_rk_step = 1
    kernel_dts = 0.0_RKIND
    print_minmax = 0
+   nblocks = 1
    config_zd = 22000.0_RKIND       ! Registry.xml defaults
    config_xnutr = 0.2_RKIND
    config_h_ScaleWithMesh = .true.
@@ -361,6 +388,14 @@ program mpas_ref_harness
    close(u)
    if (nthreads_req > 0) call omp_set_num_threads(nthreads_req)
    nthr = omp_get_max_threads()
+   nCellsSolve_in = nCells
+   nEdgesSolve_in = nEdges
+   nVerticesSolve_in = nVertices
+   ! halo layers of the exchange lists: cells 2, edges / vertices 3 (mpas_block_creator.F:734);
+   ! a single block keeps 2 everywhere (its lists are empty and its fields inactive)
+   nhalo_ev = 2
+   if (nblocks > 1) nhalo_ev = 3
+   fields_active = nblocks > 1
 
    K = nVertLevels_in
    ns = num_scalars_in
@@ -376,28 +411,7 @@ program mpas_ref_harness
    domain % core % coreName = 'atmosphere'
    call mpas_log_init(domain % logInfo, domain)
    call mpas_log_open()
-   allocate(hblock)
-   hblock % blockID = 0
-   hblock % localBlockID = 0
-   hblock % domain => domain
-   ! single block on one rank: every exchange list is empty (2 halo layers, no neighbours),
-   ! so mpas_dmpar exchanges (incl. the explicit scale_arr exchange of
-   ! atm_advance_scalars_mono_work, mpas_atm_time_integration.F:4084-4098) are no-ops.
-   allocate(hblock % parinfo)
-   call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % cellsToSend, 2)
-   call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % cellsToRecv, 2)
-   call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % cellsToCopy, 2)
-   call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % edgesToSend, 2)
-   call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % edgesToRecv, 2)
-   call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % edgesToCopy, 2)
-   call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % verticesToSend, 2)
-   call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % verticesToRecv, 2)
-   call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % verticesToCopy, 2)
-   domain % blocklist => hblock
-   call mpas_pool_create_pool(hblock % structs)
-   call mpas_pool_create_pool(hblock % dimensions)
    call mpas_pool_create_pool(configs)
-   hblock % configs => configs
    domain % configs => configs
 
    call mpas_atm_set_dims(K, maxEdges_in, maxEdges2_in, ns)
@@ -443,177 +457,64 @@ program mpas_ref_harness
    call mpas_pool_add_config_real(configs, 'config_xnutr', config_xnutr)
    call mpas_pool_add_config_logical(configs, 'config_h_ScaleWithMesh', config_h_ScaleWithMesh)
 
-   ! ---- subpools ----
-   call mpas_pool_create_pool(mesh)
-   call mpas_pool_create_pool(state)
-   call mpas_pool_create_pool(diag)
-   call mpas_pool_create_pool(tend)
-   call mpas_pool_create_pool(tend_physics)
-   call mpas_pool_create_pool(diag_physics)
-   call mpas_pool_add_subpool(hblock % structs, 'mesh', mesh)
-   call mpas_pool_add_subpool(hblock % structs, 'state', state)
-   call mpas_pool_add_subpool(hblock % structs, 'diag', diag)
-   call mpas_pool_add_subpool(hblock % structs, 'tend', tend)
-   call mpas_pool_add_subpool(hblock % structs, 'tend_physics', tend_physics)
-   ! empty: only the DO_PHYSICS build looks it up, for driver_microphysics (scheme 'off' -> unused)
-   call mpas_pool_add_subpool(hblock % structs, 'diag_physics', diag_physics)
 
-   call add_dims(hblock % dimensions)
-   call add_dims(mesh)
-   call add_dims(state)
-   call add_dims(diag)
-   call add_dims(tend)
-   call add_dims(tend_physics)
-   call mpas_pool_add_dimension(state, 'moist_start', 1)
-   call mpas_pool_add_dimension(state, 'moist_end', moist_end)
-   call mpas_pool_add_dimension(state, 'index_qv', 1)
-   call mpas_pool_add_config_real(mesh, 'sphere_radius', sphere_radius)
-   call mpas_pool_add_config_logical(mesh, 'on_a_sphere', .true.)
-   call mpas_pool_add_config_logical(mesh, 'is_periodic', .false.)
-   call mpas_pool_add_config_real(mesh, 'x_period', 0.0_RKIND)
-   call mpas_pool_add_config_real(mesh, 'y_period', 0.0_RKIND)
-
-   ! ---- thread ranges (replaces mpas_atm_threading.F; static contiguous blocks) ----
-   call thread_ranges(nCells, cts, cte)
-   call thread_ranges(nCells, csts, cste)
-   call thread_ranges(nEdges, ets, ete)
-   call thread_ranges(nEdges, ests, este)
-   call thread_ranges(nVertices, vts, vte)
-   call thread_ranges(nVertices, vsts, vste)
-   call mpas_pool_add_dimension(hblock % dimensions, 'nThreads', nthr)
-   call mpas_pool_add_dimension(hblock % dimensions, 'cellThreadStart', cts)
-   call mpas_pool_add_dimension(hblock % dimensions, 'cellThreadEnd', cte)
-   call mpas_pool_add_dimension(hblock % dimensions, 'cellSolveThreadStart', csts)
-   call mpas_pool_add_dimension(hblock % dimensions, 'cellSolveThreadEnd', cste)
-   call mpas_pool_add_dimension(hblock % dimensions, 'edgeThreadStart', ets)
-   call mpas_pool_add_dimension(hblock % dimensions, 'edgeThreadEnd', ete)
-   call mpas_pool_add_dimension(hblock % dimensions, 'edgeSolveThreadStart', ests)
-   call mpas_pool_add_dimension(hblock % dimensions, 'edgeSolveThreadEnd', este)
-   call mpas_pool_add_dimension(hblock % dimensions, 'vertexThreadStart', vts)
-   call mpas_pool_add_dimension(hblock % dimensions, 'vertexThreadEnd', vte)
-   call mpas_pool_add_dimension(hblock % dimensions, 'vertexSolveThreadStart', vsts)
-   call mpas_pool_add_dimension(hblock % dimensions, 'vertexSolveThreadEnd', vste)
-
-   ! ---- mesh pool (Registry.xml var_struct "mesh") ----
-   call add_r1(mesh, 'mesh', 'latCell', nC1);  call add_r1(mesh, 'mesh', 'lonCell', nC1)
-   call add_r1(mesh, 'mesh', 'xCell', nC1);    call add_r1(mesh, 'mesh', 'yCell', nC1)
-   call add_r1(mesh, 'mesh', 'zCell', nC1);    call add_r1(mesh, 'mesh', 'areaCell', nC1)
-   call add_r1(mesh, 'mesh', 'invAreaCell', nC1); call add_r1(mesh, 'mesh', 'meshDensity', nC1)
-   call add_r1(mesh, 'mesh', 'meshScalingRegionalCell', nC1); call add_r1(mesh, 'mesh', 'specZoneMaskCell', nC1)
-   call add_r1(mesh, 'mesh', 'latEdge', nE1);  call add_r1(mesh, 'mesh', 'lonEdge', nE1)
-   call add_r1(mesh, 'mesh', 'xEdge', nE1);    call add_r1(mesh, 'mesh', 'yEdge', nE1)
-   call add_r1(mesh, 'mesh', 'zEdge', nE1);    call add_r1(mesh, 'mesh', 'dcEdge', nE1)
-   call add_r1(mesh, 'mesh', 'dvEdge', nE1);   call add_r1(mesh, 'mesh', 'invDcEdge', nE1)
-   call add_r1(mesh, 'mesh', 'invDvEdge', nE1); call add_r1(mesh, 'mesh', 'angleEdge', nE1)
-   call add_r1(mesh, 'mesh', 'fEdge', nE1);    call add_r1(mesh, 'mesh', 'meshScalingDel2', nE1)
-   call add_r1(mesh, 'mesh', 'meshScalingDel4', nE1); call add_r1(mesh, 'mesh', 'meshScalingRegionalEdge', nE1)
-   call add_r1(mesh, 'mesh', 'specZoneMaskEdge', nE1)
-   call add_r1(mesh, 'mesh', 'latVertex', nV1); call add_r1(mesh, 'mesh', 'lonVertex', nV1)
-   call add_r1(mesh, 'mesh', 'xVertex', nV1);  call add_r1(mesh, 'mesh', 'yVertex', nV1)
-   call add_r1(mesh, 'mesh', 'zVertex', nV1);  call add_r1(mesh, 'mesh', 'areaTriangle', nV1)
-   call add_r1(mesh, 'mesh', 'invAreaTriangle', nV1); call add_r1(mesh, 'mesh', 'fVertex', nV1)
-   call add_r1(mesh, 'mesh', 'fzm', K);  call add_r1(mesh, 'mesh', 'fzp', K)
-   call add_r1(mesh, 'mesh', 'rdzw', K); call add_r1(mesh, 'mesh', 'rdzu', K)
-   call add_r1(mesh, 'mesh', 'u_init', K); call add_r1(mesh, 'mesh', 'v_init', K)
-   call add_r1(mesh, 'mesh', 'qv_init', K)
-   call add_r0(mesh, 'mesh', 'cf1'); call add_r0(mesh, 'mesh', 'cf2'); call add_r0(mesh, 'mesh', 'cf3')
-   call add_i1(mesh, 'mesh', 'nEdgesOnCell', nC1); call add_i1(mesh, 'mesh', 'indexToCellID', nC1)
-   call add_i1(mesh, 'mesh', 'bdyMaskCell', nC1);  call add_i1(mesh, 'mesh', 'nearestRelaxationCell', nC1)
-   call add_i1(mesh, 'mesh', 'nEdgesOnEdge', nE1); call add_i1(mesh, 'mesh', 'nAdvCellsForEdge', nE1)
-   call add_i1(mesh, 'mesh', 'bdyMaskEdge', nE1)
-   call add_i2(mesh, 'mesh', 'edgesOnCell', maxEdges_in, nC1)
-   call add_i2(mesh, 'mesh', 'cellsOnCell', maxEdges_in, nC1)
-   call add_i2(mesh, 'mesh', 'verticesOnCell', maxEdges_in, nC1)
-   call add_i2(mesh, 'mesh', 'kiteForCell', maxEdges_in, nC1)
-   call add_i2(mesh, 'mesh', 'cellsOnEdge', 2, nE1)
-   call add_i2(mesh, 'mesh', 'verticesOnEdge', 2, nE1)
-   call add_i2(mesh, 'mesh', 'edgesOnEdge', maxEdges2_in, nE1)
-   call add_i2(mesh, 'mesh', 'advCellsForEdge', 15, nE1)
-   call add_i2(mesh, 'mesh', 'cellsOnVertex', 3, nV1)
-   call add_i2(mesh, 'mesh', 'edgesOnVertex', 3, nV1)
-   call add_r2(mesh, 'mesh', 'edgesOnCell_sign', maxEdges_in, nC1, 1)
-   call add_r2(mesh, 'mesh', 'edgesOnVertex_sign', 3, nV1, 1)
-   call add_r2(mesh, 'mesh', 'kiteAreasOnVertex', 3, nV1, 1)
-   call add_r2(mesh, 'mesh', 'weightsOnEdge', maxEdges2_in, nE1, 1)
-   call add_r2(mesh, 'mesh', 'adv_coefs', 15, nE1, 1)
-   call add_r2(mesh, 'mesh', 'adv_coefs_3rd', 15, nE1, 1)
-   call add_r2(mesh, 'mesh', 'defc_a', maxEdges_in, nC1, 1)
-   call add_r2(mesh, 'mesh', 'defc_b', maxEdges_in, nC1, 1)
-   call add_r2(mesh, 'mesh', 'zgrid', K+1, nC1, 1)
-   call add_r2(mesh, 'mesh', 'zz', K, nC1, 1)
-   call add_r2(mesh, 'mesh', 'zxu', K, nE1, 1)
-   call add_r2(mesh, 'mesh', 'dss', K, nC1, 1)
-   call add_r2(mesh, 'mesh', 't_init', K, nC1, 1)
-   call add_r2(mesh, 'mesh', 'localVerticalUnitVectors', 3, nC1, 1)
-   call add_r2(mesh, 'mesh', 'edgeNormalVectors', 3, nE1, 1)
-   call add_r3(mesh, 'mesh', 'cellTangentPlane', 3, 2, nC1, 1)
-   call add_r3(mesh, 'mesh', 'coeffs_reconstruct', 3, maxEdges_in, nC1, 1)
-   call add_r3(mesh, 'mesh', 'deriv_two', 15, 2, nE1, 1)
-   call add_r3(mesh, 'mesh', 'zb', K+1, 2, nE1, 1)
-   call add_r3(mesh, 'mesh', 'zb3', K+1, 2, nE1, 1)
-   call add_r3(mesh, 'mesh', 'zb_cell', K+1, maxEdges_in, nC1, 1)
-   call add_r3(mesh, 'mesh', 'zb3_cell', K+1, maxEdges_in, nC1, 1)
-   call add_i2(mesh, 'mesh', 'advCells', 21, nC1)   ! core_init_atmosphere Registry (TWENTYONE nCells)
-
-   write(0, '(a)') 'harness: mesh pool read'
-   ! ---- state pool: 2 time levels (Registry.xml var_struct "state" time_levs="2") ----
-   call add_r2(state, 'state', 'u', K, nE1, 2)
-   call add_r2(state, 'state', 'w', K+1, nC1, 2)
-   call add_r2(state, 'state', 'theta_m', K, nC1, 2)
-   call add_r2(state, 'state', 'rho_zz', K, nC1, 2)
-   call add_r3(state, 'state', 'scalars', ns, K, nC1, 2)
-
-   ! ---- diag pool ----
-   call add_r2(diag, 'diag', 'theta', K, nC1, 1);        call add_r2(diag, 'diag', 'rho', K, nC1, 1)
-   call add_r2(diag, 'diag', 'rho_base', K, nC1, 1);     call add_r2(diag, 'diag', 'theta_base', K, nC1, 1)
-   call add_r2(diag, 'diag', 'rho_p', K, nC1, 1);        call add_r2(diag, 'diag', 'rho_p_save', K, nC1, 1)
-   call add_r2(diag, 'diag', 'rho_pp', K, nC1, 1);       call add_r2(diag, 'diag', 'rho_zz_old_split', K, nC1, 1)
-   call add_r2(diag, 'diag', 'rtheta_base', K, nC1, 1);  call add_r2(diag, 'diag', 'rtheta_p', K, nC1, 1)
-   call add_r2(diag, 'diag', 'rtheta_p_save', K, nC1, 1); call add_r2(diag, 'diag', 'rtheta_pp', K, nC1, 1)
-   call add_r2(diag, 'diag', 'rtheta_pp_old', K, nC1, 1); call add_r2(diag, 'diag', 'exner', K, nC1, 1)
-   call add_r2(diag, 'diag', 'exner_base', K, nC1, 1);   call add_r2(diag, 'diag', 'pressure_base', K, nC1, 1)
-   call add_r2(diag, 'diag', 'pressure_p', K, nC1, 1);   call add_r2(diag, 'diag', 'h_divergence', K, nC1, 1)
-   call add_r2(diag, 'diag', 'kdiff', K, nC1, 1);        call add_r2(diag, 'diag', 'ke', K, nC1, 1)
-   call add_r2(diag, 'diag', 'divergence', K, nC1, 1);   call add_r2(diag, 'diag', 'pv_cell', K, nC1, 1)
-   call add_r2(diag, 'diag', 'tend_rtheta_adv', K, nC1, 1); call add_r2(diag, 'diag', 'cqw', K, nC1, 1)
-   call add_r2(diag, 'diag', 'cofwr', K, nC1, 1);        call add_r2(diag, 'diag', 'cofwz', K, nC1, 1)
-   call add_r2(diag, 'diag', 'cofwt', K, nC1, 1);        call add_r2(diag, 'diag', 'coftz', K+1, nC1, 1)
-   call add_r2(diag, 'diag', 'a_tri', K, nC1, 1);        call add_r2(diag, 'diag', 'alpha_tri', K, nC1, 1)
-   call add_r2(diag, 'diag', 'gamma_tri', K, nC1, 1);    call add_r1(diag, 'diag', 'cofrz', K)
-   call add_r2(diag, 'diag', 'uReconstructX', K, nC1, 1); call add_r2(diag, 'diag', 'uReconstructY', K, nC1, 1)
-   call add_r2(diag, 'diag', 'uReconstructZ', K, nC1, 1); call add_r2(diag, 'diag', 'uReconstructZonal', K, nC1, 1)
-   call add_r2(diag, 'diag', 'uReconstructMeridional', K, nC1, 1)
-   call add_r2(diag, 'diag', 'rw', K+1, nC1, 1);         call add_r2(diag, 'diag', 'rw_p', K+1, nC1, 1)
-   call add_r2(diag, 'diag', 'rw_save', K+1, nC1, 1);    call add_r2(diag, 'diag', 'wwAvg', K+1, nC1, 1)
-   call add_r2(diag, 'diag', 'wwAvg_split', K+1, nC1, 1)
-   call add_r2(diag, 'diag', 'ru', K, nE1, 1);           call add_r2(diag, 'diag', 'ruAvg', K, nE1, 1)
-   call add_r2(diag, 'diag', 'ruAvg_split', K, nE1, 1);  call add_r2(diag, 'diag', 'ru_p', K, nE1, 1)
-   call add_r2(diag, 'diag', 'ru_save', K, nE1, 1);      call add_r2(diag, 'diag', 'cqu', K, nE1, 1)
-   call add_r2(diag, 'diag', 'rho_edge', K, nE1, 1);     call add_r2(diag, 'diag', 'v', K, nE1, 1)
-   call add_r2(diag, 'diag', 'pv_edge', K, nE1, 1);      call add_r2(diag, 'diag', 'gradPVn', K, nE1, 1)
-   call add_r2(diag, 'diag', 'gradPVt', K, nE1, 1)
-   call add_r2(diag, 'diag', 'vorticity', K, nV1, 1);    call add_r2(diag, 'diag', 'pv_vertex', K, nV1, 1)
-
-   ! ---- tend / tend_physics pools ----
-   call add_r2(tend, 'tend', 'u', K, nE1, 1);            call add_r2(tend, 'tend', 'u_euler', K, nE1, 1)
-   call add_r2(tend, 'tend', 'w', K+1, nC1, 1);          call add_r2(tend, 'tend', 'w_euler', K+1, nC1, 1)
-   call add_r2(tend, 'tend', 'w_pgf', K+1, nC1, 1);      call add_r2(tend, 'tend', 'w_buoy', K+1, nC1, 1)
-   call add_r2(tend, 'tend', 'theta_m', K, nC1, 1);      call add_r2(tend, 'tend', 'theta_euler', K, nC1, 1)
-   call add_r2(tend, 'tend', 'rho_zz', K, nC1, 1);       call add_r2(tend, 'tend', 'rt_diabatic_tend', K, nC1, 1)
-   call add_r3(tend, 'tend', 'scalars_tend', ns, K, nC1, 1)
-   call add_r2(tend_physics, 'tend_physics', 'rthdynten', K, nC1, 1)
-   call add_r2(tend_physics, 'tend_physics', 'rqvdynten', K, nC1, 1)
-   ! prescribed physics tendencies, handed to the DO_PHYSICS dycore by the physics_get_tend test
-   ! double (shims/mpas_atmphys_todynamics_stub.F90); shapes as allocated in atm_srk3
-   if (file_exists('tend_ru_physics_in')) then
-      call add_r2(tend_physics, 'tend_physics', 'tend_ru_physics_in', K, nE1, 1)
-      call add_r2(tend_physics, 'tend_physics', 'tend_rtheta_physics_in', K, nC1, 1)
-      call add_r2(tend_physics, 'tend_physics', 'tend_rho_physics_in', K, nC1, 1)
-      call add_r3(tend_physics, 'tend_physics', 'scalars_tend_in', ns, K, nC1, 1)
-   end if
+   ! ---- blocks (one, or nblocks with local-copy halo exchanges between them) ----
+   rootdir = indir
+   nullify(hblock)
+   do ib = 0, nblocks - 1
+      call build_block(ib)
+   end do
+   if (nblocks > 1) call link_blocks()
 
    allocate(plist(1))
    write(0, '(a)') 'harness: pools built'
+
+   if (nblocks > 1) then
+      ! model init (mpas_atm_core.F:143-186): u exchange, per-block diagnostics, then the
+      ! pv_edge / ru / rw exchanges; then the time loop (atm_srk3 exchanges between the blocks)
+      call mpas_pool_get_subpool(domain % blocklist % structs, 'state', state)
+      call mpas_pool_get_field(state, 'u', f2_u, 1)
+      call mpas_dmpar_exch_halo_field(f2_u)
+      blk => domain % blocklist
+      do while (associated(blk))
+         call init_block(blk)
+         blk => blk % next
+      end do
+      call mpas_pool_get_subpool(domain % blocklist % structs, 'diag', diag)
+      call mpas_pool_get_field(diag, 'pv_edge', f2_pv)
+      call mpas_dmpar_exch_halo_field(f2_pv)
+      call mpas_pool_get_field(diag, 'ru', f2_ru)
+      call mpas_dmpar_exch_halo_field(f2_ru)
+      call mpas_pool_get_field(diag, 'rw', f2_rw)
+      call mpas_dmpar_exch_halo_field(f2_rw)
+      write(0, '(a)') 'harness: init diagnostics done'
+      if (any(dump_steps == 0)) call dump_blocks(trim(outdir)//'/step_0000')
+      call mpas_pool_get_config(configs, 'config_apply_lbcs', config_apply_lbcs)
+      allocate(steptime(max(nsteps,1)))
+      do step = 1, nsteps
+         t0 = omp_get_wtime()
+         call atm_srk3(domain, dt, step)
+         t1 = omp_get_wtime()
+         steptime(step) = t1 - t0
+         write(0, '(a,i6,f10.3)') 'harness: step', step, steptime(step)
+         ! once, on the first block: the state fields of all blocks are linked (mpas_atm_core.F:670-671)
+         call mpas_pool_get_subpool(domain % blocklist % structs, 'state', state)
+         call mpas_pool_shift_time_levels(state)
+         if (any(dump_steps == step)) then
+            write(sdir, '(a,i4.4)') 'step_', step
+            call dump_blocks(trim(outdir)//'/'//trim(sdir))
+         end if
+      end do
+      call execute_command_line('mkdir -p '//trim(outdir))
+      open(newunit=u, file=trim(outdir)//'/timing.txt', status='replace')
+      write(u, '(a,i6)') 'threads ', nthr
+      do step = 1, nsteps
+         write(u, '(a,i6,es24.16)') 'step ', step, steptime(step)
+      end do
+      close(u)
+      call mpas_dmpar_finalize(domain % dminfo)
+      stop
+   end if
 
 #ifdef HARNESS_INIT
    if (trim(mode) == 'init') then
@@ -716,14 +617,360 @@ program mpas_ref_harness
 
 contains
 
+   ! One block of the domain (mpas_block_creator.F does this for the real model): its dims,
+   ! parinfo exchange lists, pools and fields.  nblocks > 1: inputs from <indir>/block<ib>/, whose
+   ! block.nml holds the block dims and copy_<loc>_<layer>_<peer>.bin its local-copy lists.
+   subroutine build_block(ib)
+      integer, intent(in) :: ib
+      character(len=16) :: bname
+      type (block_type), pointer :: prevblk
+      if (nblocks > 1) then
+         write(bname, '(a,i0)') '/block', ib
+         indir = trim(rootdir)//trim(bname)
+         open(newunit=u, file=trim(indir)//'/block.nml', status='old')
+         read(u, nml=block)
+         close(u)
+         nC1 = nCells + 1
+         nE1 = nEdges + 1
+         nV1 = nVertices + 1
+      end if
+      cur_nC1 = nC1
+      cur_nE1 = nE1
+      cur_nV1 = nV1
+      prevblk => hblock
+      allocate(hblock)
+      hblock % blockID = ib
+      hblock % localBlockID = ib
+      hblock % domain => domain
+      ! single block on one rank: every exchange list is empty (2 halo layers, no neighbours),
+      ! so mpas_dmpar exchanges (incl. the explicit scale_arr exchange of
+      ! atm_advance_scalars_mono_work, mpas_atm_time_integration.F:4084-4098) are no-ops.
+      allocate(hblock % parinfo)
+      call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % cellsToSend, 2)
+      call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % cellsToRecv, 2)
+      call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % cellsToCopy, 2)
+      call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % edgesToSend, nhalo_ev)
+      call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % edgesToRecv, nhalo_ev)
+      call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % edgesToCopy, nhalo_ev)
+      call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % verticesToSend, nhalo_ev)
+      call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % verticesToRecv, nhalo_ev)
+      call mpas_dmpar_init_multihalo_exchange_list(hblock % parinfo % verticesToCopy, nhalo_ev)
+      if (ib == 0) then
+         domain % blocklist => hblock
+      else
+         prevblk % next => hblock
+         hblock % prev => prevblk
+      end if
+      call mpas_pool_create_pool(hblock % structs)
+      call mpas_pool_create_pool(hblock % dimensions)
+      hblock % configs => configs
+      ! ---- subpools ----
+      call mpas_pool_create_pool(mesh)
+      call mpas_pool_create_pool(state)
+      call mpas_pool_create_pool(diag)
+      call mpas_pool_create_pool(tend)
+      call mpas_pool_create_pool(tend_physics)
+      call mpas_pool_create_pool(diag_physics)
+      call mpas_pool_add_subpool(hblock % structs, 'mesh', mesh)
+      call mpas_pool_add_subpool(hblock % structs, 'state', state)
+      call mpas_pool_add_subpool(hblock % structs, 'diag', diag)
+      call mpas_pool_add_subpool(hblock % structs, 'tend', tend)
+      call mpas_pool_add_subpool(hblock % structs, 'tend_physics', tend_physics)
+      ! empty: only the DO_PHYSICS build looks it up, for driver_microphysics (scheme 'off' -> unused)
+      call mpas_pool_add_subpool(hblock % structs, 'diag_physics', diag_physics)
+   
+      call add_dims(hblock % dimensions)
+      call add_dims(mesh)
+      call add_dims(state)
+      call add_dims(diag)
+      call add_dims(tend)
+      call add_dims(tend_physics)
+      call mpas_pool_add_dimension(state, 'moist_start', 1)
+      call mpas_pool_add_dimension(state, 'moist_end', moist_end)
+      call mpas_pool_add_dimension(state, 'index_qv', 1)
+      call mpas_pool_add_config_real(mesh, 'sphere_radius', sphere_radius)
+      call mpas_pool_add_config_logical(mesh, 'on_a_sphere', .true.)
+      call mpas_pool_add_config_logical(mesh, 'is_periodic', .false.)
+      call mpas_pool_add_config_real(mesh, 'x_period', 0.0_RKIND)
+      call mpas_pool_add_config_real(mesh, 'y_period', 0.0_RKIND)
+   
+      ! ---- thread ranges (replaces mpas_atm_threading.F; static contiguous blocks) ----
+      call thread_ranges(nCells, cts, cte)
+      call thread_ranges(nCells, csts, cste)
+      call thread_ranges(nEdges, ets, ete)
+      call thread_ranges(nEdges, ests, este)
+      call thread_ranges(nVertices, vts, vte)
+      call thread_ranges(nVertices, vsts, vste)
+      call mpas_pool_add_dimension(hblock % dimensions, 'nThreads', nthr)
+      call mpas_pool_add_dimension(hblock % dimensions, 'cellThreadStart', cts)
+      call mpas_pool_add_dimension(hblock % dimensions, 'cellThreadEnd', cte)
+      call mpas_pool_add_dimension(hblock % dimensions, 'cellSolveThreadStart', csts)
+      call mpas_pool_add_dimension(hblock % dimensions, 'cellSolveThreadEnd', cste)
+      call mpas_pool_add_dimension(hblock % dimensions, 'edgeThreadStart', ets)
+      call mpas_pool_add_dimension(hblock % dimensions, 'edgeThreadEnd', ete)
+      call mpas_pool_add_dimension(hblock % dimensions, 'edgeSolveThreadStart', ests)
+      call mpas_pool_add_dimension(hblock % dimensions, 'edgeSolveThreadEnd', este)
+      call mpas_pool_add_dimension(hblock % dimensions, 'vertexThreadStart', vts)
+      call mpas_pool_add_dimension(hblock % dimensions, 'vertexThreadEnd', vte)
+      call mpas_pool_add_dimension(hblock % dimensions, 'vertexSolveThreadStart', vsts)
+      call mpas_pool_add_dimension(hblock % dimensions, 'vertexSolveThreadEnd', vste)
+   
+      ! ---- mesh pool (Registry.xml var_struct "mesh") ----
+      call add_r1(mesh, 'mesh', 'latCell', nC1);  call add_r1(mesh, 'mesh', 'lonCell', nC1)
+      call add_r1(mesh, 'mesh', 'xCell', nC1);    call add_r1(mesh, 'mesh', 'yCell', nC1)
+      call add_r1(mesh, 'mesh', 'zCell', nC1);    call add_r1(mesh, 'mesh', 'areaCell', nC1)
+      call add_r1(mesh, 'mesh', 'invAreaCell', nC1); call add_r1(mesh, 'mesh', 'meshDensity', nC1)
+      call add_r1(mesh, 'mesh', 'meshScalingRegionalCell', nC1); call add_r1(mesh, 'mesh', 'specZoneMaskCell', nC1)
+      call add_r1(mesh, 'mesh', 'latEdge', nE1);  call add_r1(mesh, 'mesh', 'lonEdge', nE1)
+      call add_r1(mesh, 'mesh', 'xEdge', nE1);    call add_r1(mesh, 'mesh', 'yEdge', nE1)
+      call add_r1(mesh, 'mesh', 'zEdge', nE1);    call add_r1(mesh, 'mesh', 'dcEdge', nE1)
+      call add_r1(mesh, 'mesh', 'dvEdge', nE1);   call add_r1(mesh, 'mesh', 'invDcEdge', nE1)
+      call add_r1(mesh, 'mesh', 'invDvEdge', nE1); call add_r1(mesh, 'mesh', 'angleEdge', nE1)
+      call add_r1(mesh, 'mesh', 'fEdge', nE1);    call add_r1(mesh, 'mesh', 'meshScalingDel2', nE1)
+      call add_r1(mesh, 'mesh', 'meshScalingDel4', nE1); call add_r1(mesh, 'mesh', 'meshScalingRegionalEdge', nE1)
+      call add_r1(mesh, 'mesh', 'specZoneMaskEdge', nE1)
+      call add_r1(mesh, 'mesh', 'latVertex', nV1); call add_r1(mesh, 'mesh', 'lonVertex', nV1)
+      call add_r1(mesh, 'mesh', 'xVertex', nV1);  call add_r1(mesh, 'mesh', 'yVertex', nV1)
+      call add_r1(mesh, 'mesh', 'zVertex', nV1);  call add_r1(mesh, 'mesh', 'areaTriangle', nV1)
+      call add_r1(mesh, 'mesh', 'invAreaTriangle', nV1); call add_r1(mesh, 'mesh', 'fVertex', nV1)
+      call add_r1(mesh, 'mesh', 'fzm', K);  call add_r1(mesh, 'mesh', 'fzp', K)
+      call add_r1(mesh, 'mesh', 'rdzw', K); call add_r1(mesh, 'mesh', 'rdzu', K)
+      call add_r1(mesh, 'mesh', 'u_init', K); call add_r1(mesh, 'mesh', 'v_init', K)
+      call add_r1(mesh, 'mesh', 'qv_init', K)
+      call add_r0(mesh, 'mesh', 'cf1'); call add_r0(mesh, 'mesh', 'cf2'); call add_r0(mesh, 'mesh', 'cf3')
+      call add_i1(mesh, 'mesh', 'nEdgesOnCell', nC1); call add_i1(mesh, 'mesh', 'indexToCellID', nC1)
+      call add_i1(mesh, 'mesh', 'bdyMaskCell', nC1);  call add_i1(mesh, 'mesh', 'nearestRelaxationCell', nC1)
+      call add_i1(mesh, 'mesh', 'nEdgesOnEdge', nE1); call add_i1(mesh, 'mesh', 'nAdvCellsForEdge', nE1)
+      call add_i1(mesh, 'mesh', 'bdyMaskEdge', nE1)
+      call add_i2(mesh, 'mesh', 'edgesOnCell', maxEdges_in, nC1)
+      call add_i2(mesh, 'mesh', 'cellsOnCell', maxEdges_in, nC1)
+      call add_i2(mesh, 'mesh', 'verticesOnCell', maxEdges_in, nC1)
+      call add_i2(mesh, 'mesh', 'kiteForCell', maxEdges_in, nC1)
+      call add_i2(mesh, 'mesh', 'cellsOnEdge', 2, nE1)
+      call add_i2(mesh, 'mesh', 'verticesOnEdge', 2, nE1)
+      call add_i2(mesh, 'mesh', 'edgesOnEdge', maxEdges2_in, nE1)
+      call add_i2(mesh, 'mesh', 'advCellsForEdge', 15, nE1)
+      call add_i2(mesh, 'mesh', 'cellsOnVertex', 3, nV1)
+      call add_i2(mesh, 'mesh', 'edgesOnVertex', 3, nV1)
+      call add_r2(mesh, 'mesh', 'edgesOnCell_sign', maxEdges_in, nC1, 1)
+      call add_r2(mesh, 'mesh', 'edgesOnVertex_sign', 3, nV1, 1)
+      call add_r2(mesh, 'mesh', 'kiteAreasOnVertex', 3, nV1, 1)
+      call add_r2(mesh, 'mesh', 'weightsOnEdge', maxEdges2_in, nE1, 1)
+      call add_r2(mesh, 'mesh', 'adv_coefs', 15, nE1, 1)
+      call add_r2(mesh, 'mesh', 'adv_coefs_3rd', 15, nE1, 1)
+      call add_r2(mesh, 'mesh', 'defc_a', maxEdges_in, nC1, 1)
+      call add_r2(mesh, 'mesh', 'defc_b', maxEdges_in, nC1, 1)
+      call add_r2(mesh, 'mesh', 'zgrid', K+1, nC1, 1)
+      call add_r2(mesh, 'mesh', 'zz', K, nC1, 1)
+      call add_r2(mesh, 'mesh', 'zxu', K, nE1, 1)
+      call add_r2(mesh, 'mesh', 'dss', K, nC1, 1)
+      call add_r2(mesh, 'mesh', 't_init', K, nC1, 1)
+      call add_r2(mesh, 'mesh', 'localVerticalUnitVectors', 3, nC1, 1)
+      call add_r2(mesh, 'mesh', 'edgeNormalVectors', 3, nE1, 1)
+      call add_r3(mesh, 'mesh', 'cellTangentPlane', 3, 2, nC1, 1)
+      call add_r3(mesh, 'mesh', 'coeffs_reconstruct', 3, maxEdges_in, nC1, 1)
+      call add_r3(mesh, 'mesh', 'deriv_two', 15, 2, nE1, 1)
+      call add_r3(mesh, 'mesh', 'zb', K+1, 2, nE1, 1)
+      call add_r3(mesh, 'mesh', 'zb3', K+1, 2, nE1, 1)
+      call add_r3(mesh, 'mesh', 'zb_cell', K+1, maxEdges_in, nC1, 1)
+      call add_r3(mesh, 'mesh', 'zb3_cell', K+1, maxEdges_in, nC1, 1)
+      call add_i2(mesh, 'mesh', 'advCells', 21, nC1)   ! core_init_atmosphere Registry (TWENTYONE nCells)
+   
+      write(0, '(a)') 'harness: mesh pool read'
+      ! ---- state pool: 2 time levels (Registry.xml var_struct "state" time_levs="2") ----
+      call add_r2(state, 'state', 'u', K, nE1, 2)
+      call add_r2(state, 'state', 'w', K+1, nC1, 2)
+      call add_r2(state, 'state', 'theta_m', K, nC1, 2)
+      call add_r2(state, 'state', 'rho_zz', K, nC1, 2)
+      call add_r3(state, 'state', 'scalars', ns, K, nC1, 2)
+   
+      ! ---- diag pool ----
+      call add_r2(diag, 'diag', 'theta', K, nC1, 1);        call add_r2(diag, 'diag', 'rho', K, nC1, 1)
+      call add_r2(diag, 'diag', 'rho_base', K, nC1, 1);     call add_r2(diag, 'diag', 'theta_base', K, nC1, 1)
+      call add_r2(diag, 'diag', 'rho_p', K, nC1, 1);        call add_r2(diag, 'diag', 'rho_p_save', K, nC1, 1)
+      call add_r2(diag, 'diag', 'rho_pp', K, nC1, 1);       call add_r2(diag, 'diag', 'rho_zz_old_split', K, nC1, 1)
+      call add_r2(diag, 'diag', 'rtheta_base', K, nC1, 1);  call add_r2(diag, 'diag', 'rtheta_p', K, nC1, 1)
+      call add_r2(diag, 'diag', 'rtheta_p_save', K, nC1, 1); call add_r2(diag, 'diag', 'rtheta_pp', K, nC1, 1)
+      call add_r2(diag, 'diag', 'rtheta_pp_old', K, nC1, 1); call add_r2(diag, 'diag', 'exner', K, nC1, 1)
+      call add_r2(diag, 'diag', 'exner_base', K, nC1, 1);   call add_r2(diag, 'diag', 'pressure_base', K, nC1, 1)
+      call add_r2(diag, 'diag', 'pressure_p', K, nC1, 1);   call add_r2(diag, 'diag', 'h_divergence', K, nC1, 1)
+      call add_r2(diag, 'diag', 'kdiff', K, nC1, 1);        call add_r2(diag, 'diag', 'ke', K, nC1, 1)
+      call add_r2(diag, 'diag', 'divergence', K, nC1, 1);   call add_r2(diag, 'diag', 'pv_cell', K, nC1, 1)
+      call add_r2(diag, 'diag', 'tend_rtheta_adv', K, nC1, 1); call add_r2(diag, 'diag', 'cqw', K, nC1, 1)
+      call add_r2(diag, 'diag', 'cofwr', K, nC1, 1);        call add_r2(diag, 'diag', 'cofwz', K, nC1, 1)
+      call add_r2(diag, 'diag', 'cofwt', K, nC1, 1);        call add_r2(diag, 'diag', 'coftz', K+1, nC1, 1)
+      call add_r2(diag, 'diag', 'a_tri', K, nC1, 1);        call add_r2(diag, 'diag', 'alpha_tri', K, nC1, 1)
+      call add_r2(diag, 'diag', 'gamma_tri', K, nC1, 1);    call add_r1(diag, 'diag', 'cofrz', K)
+      call add_r2(diag, 'diag', 'uReconstructX', K, nC1, 1); call add_r2(diag, 'diag', 'uReconstructY', K, nC1, 1)
+      call add_r2(diag, 'diag', 'uReconstructZ', K, nC1, 1); call add_r2(diag, 'diag', 'uReconstructZonal', K, nC1, 1)
+      call add_r2(diag, 'diag', 'uReconstructMeridional', K, nC1, 1)
+      call add_r2(diag, 'diag', 'rw', K+1, nC1, 1);         call add_r2(diag, 'diag', 'rw_p', K+1, nC1, 1)
+      call add_r2(diag, 'diag', 'rw_save', K+1, nC1, 1);    call add_r2(diag, 'diag', 'wwAvg', K+1, nC1, 1)
+      call add_r2(diag, 'diag', 'wwAvg_split', K+1, nC1, 1)
+      call add_r2(diag, 'diag', 'ru', K, nE1, 1);           call add_r2(diag, 'diag', 'ruAvg', K, nE1, 1)
+      call add_r2(diag, 'diag', 'ruAvg_split', K, nE1, 1);  call add_r2(diag, 'diag', 'ru_p', K, nE1, 1)
+      call add_r2(diag, 'diag', 'ru_save', K, nE1, 1);      call add_r2(diag, 'diag', 'cqu', K, nE1, 1)
+      call add_r2(diag, 'diag', 'rho_edge', K, nE1, 1);     call add_r2(diag, 'diag', 'v', K, nE1, 1)
+      call add_r2(diag, 'diag', 'pv_edge', K, nE1, 1);      call add_r2(diag, 'diag', 'gradPVn', K, nE1, 1)
+      call add_r2(diag, 'diag', 'gradPVt', K, nE1, 1)
+      call add_r2(diag, 'diag', 'vorticity', K, nV1, 1);    call add_r2(diag, 'diag', 'pv_vertex', K, nV1, 1)
+   
+      ! ---- tend / tend_physics pools ----
+      call add_r2(tend, 'tend', 'u', K, nE1, 1);            call add_r2(tend, 'tend', 'u_euler', K, nE1, 1)
+      call add_r2(tend, 'tend', 'w', K+1, nC1, 1);          call add_r2(tend, 'tend', 'w_euler', K+1, nC1, 1)
+      call add_r2(tend, 'tend', 'w_pgf', K+1, nC1, 1);      call add_r2(tend, 'tend', 'w_buoy', K+1, nC1, 1)
+      call add_r2(tend, 'tend', 'theta_m', K, nC1, 1);      call add_r2(tend, 'tend', 'theta_euler', K, nC1, 1)
+      call add_r2(tend, 'tend', 'rho_zz', K, nC1, 1);       call add_r2(tend, 'tend', 'rt_diabatic_tend', K, nC1, 1)
+      call add_r3(tend, 'tend', 'scalars_tend', ns, K, nC1, 1)
+      call add_r2(tend_physics, 'tend_physics', 'rthdynten', K, nC1, 1)
+      call add_r2(tend_physics, 'tend_physics', 'rqvdynten', K, nC1, 1)
+      ! prescribed physics tendencies, handed to the DO_PHYSICS dycore by the physics_get_tend test
+      ! double (shims/mpas_atmphys_todynamics_stub.F90); shapes as allocated in atm_srk3
+      if (file_exists('tend_ru_physics_in')) then
+         call add_r2(tend_physics, 'tend_physics', 'tend_ru_physics_in', K, nE1, 1)
+         call add_r2(tend_physics, 'tend_physics', 'tend_rtheta_physics_in', K, nC1, 1)
+         call add_r2(tend_physics, 'tend_physics', 'tend_rho_physics_in', K, nC1, 1)
+         call add_r3(tend_physics, 'tend_physics', 'scalars_tend_in', ns, K, nC1, 1)
+      end if
+      if (nblocks > 1) call read_copy_lists()
+      registering = .false.
+   end subroutine build_block
+
+   ! the local-copy exchange lists of this block (mpas_dmpar exchList: endPointID = destination
+   ! localBlockID, srcList = owned local indices here, destList = halo local indices there)
+   subroutine read_copy_lists()
+      character(len=8), dimension(3), parameter :: locs = [character(len=8) :: 'cell', 'edge', 'vertex']
+      integer :: il, layer, peer, nb, uu2
+      logical :: ex
+      character(len=320) :: fn
+      type (mpas_multihalo_exchange_list), pointer :: ml
+      type (mpas_exchange_list), pointer :: node, tail
+      do il = 1, 3
+         if (il == 1) ml => hblock % parinfo % cellsToCopy
+         if (il == 2) ml => hblock % parinfo % edgesToCopy
+         if (il == 3) ml => hblock % parinfo % verticesToCopy
+         do layer = 1, size(ml % halos)
+            do peer = 0, nblocks - 1
+               write(fn, '(a,a,i0,a,i0,a)') trim(indir)//'/copy_'//trim(locs(il)), '_', layer, '_', peer, '.bin'
+               inquire(file=trim(fn), exist=ex, size=nb)
+               if (.not. ex) cycle
+               allocate(node)
+               node % endPointID = peer
+               node % nlist = nb / 8
+               allocate(node % srcList(node % nlist), node % destList(node % nlist))
+               nullify(node % next)
+               open(newunit=uu2, file=trim(fn), access='stream', form='unformatted', status='old')
+               read(uu2) node % srcList, node % destList
+               close(uu2)
+               if (.not. associated(ml % halos(layer) % exchList)) then
+                  ml % halos(layer) % exchList => node
+               else
+                  tail => ml % halos(layer) % exchList
+                  do while (associated(tail % next))
+                     tail => tail % next
+                  end do
+                  tail % next => node
+               end if
+            end do
+         end do
+      end do
+   end subroutine read_copy_lists
+
+   ! the block list as mpas_block_creator_finalize_block_phase1 leaves it: every field linked to the
+   ! same field of the neighbouring blocks, and to its block's exchange lists
+   subroutine link_blocks()
+      type (block_type), pointer :: b
+      b => domain % blocklist
+      do while (associated(b))
+         if (associated(b % prev) .and. associated(b % next)) then
+            call mpas_pool_link_pools(b % structs, b % prev % structs, b % next % structs)
+         else if (associated(b % prev)) then
+            call mpas_pool_link_pools(b % structs, b % prev % structs)
+         else if (associated(b % next)) then
+            call mpas_pool_link_pools(b % structs, nextPool=b % next % structs)
+         else
+            call mpas_pool_link_pools(b % structs)
+         end if
+         call mpas_pool_link_parinfo(b, b % structs)
+         b => b % next
+      end do
+   end subroutine link_blocks
+
+   ! atm_mpas_init_block's diagnostics (mpas_atm_core.F:365-421) on one block of a multi-block run
+   subroutine init_block(b)
+      type (block_type), pointer :: b
+      type (mpas_pool_type), pointer :: bm, bs, bd
+      integer, pointer :: nC, nE, nV, bnthr
+      integer, dimension(:), pointer :: a_cts, a_cte, a_csts, a_cste, a_ets, a_ete, a_ests, a_este, &
+                                        a_vts, a_vte, a_vsts, a_vste
+      call mpas_pool_get_subpool(b % structs, 'mesh', bm)
+      call mpas_pool_get_subpool(b % structs, 'state', bs)
+      call mpas_pool_get_subpool(b % structs, 'diag', bd)
+      call mpas_pool_get_dimension(bm, 'nCells', nC)
+      call mpas_pool_get_dimension(bm, 'nEdges', nE)
+      call mpas_pool_get_dimension(bm, 'nVertices', nV)
+      call mpas_pool_get_dimension(b % dimensions, 'nThreads', bnthr)
+      call mpas_pool_get_dimension(b % dimensions, 'cellThreadStart', a_cts)
+      call mpas_pool_get_dimension(b % dimensions, 'cellThreadEnd', a_cte)
+      call mpas_pool_get_dimension(b % dimensions, 'cellSolveThreadStart', a_csts)
+      call mpas_pool_get_dimension(b % dimensions, 'cellSolveThreadEnd', a_cste)
+      call mpas_pool_get_dimension(b % dimensions, 'edgeThreadStart', a_ets)
+      call mpas_pool_get_dimension(b % dimensions, 'edgeThreadEnd', a_ete)
+      call mpas_pool_get_dimension(b % dimensions, 'edgeSolveThreadStart', a_ests)
+      call mpas_pool_get_dimension(b % dimensions, 'edgeSolveThreadEnd', a_este)
+      call mpas_pool_get_dimension(b % dimensions, 'vertexThreadStart', a_vts)
+      call mpas_pool_get_dimension(b % dimensions, 'vertexThreadEnd', a_vte)
+      call mpas_pool_get_dimension(b % dimensions, 'vertexSolveThreadStart', a_vsts)
+      call mpas_pool_get_dimension(b % dimensions, 'vertexSolveThreadEnd', a_vste)
+      allocate(ke_vertex(K, nV + 1))
+      ke_vertex(:, nV + 1) = 0.0_RKIND
+      allocate(ke_edge(K, nE + 1))
+      ke_edge(:, nE + 1) = 0.0_RKIND
+!$OMP PARALLEL DO
+      do t = 1, bnthr
+         call atm_init_coupled_diagnostics(bs, 1, bd, bm, configs, a_cts(t), a_cte(t), a_vts(t), a_vte(t), &
+                                           a_ets(t), a_ete(t), a_csts(t), a_cste(t), a_vsts(t), a_vste(t), &
+                                           a_ests(t), a_este(t))
+         call atm_compute_solve_diagnostics(dt, bs, 1, bd, bm, configs, a_cts(t), a_cte(t), a_vts(t), a_vte(t), &
+                                            a_ets(t), a_ete(t))
+      end do
+!$OMP END PARALLEL DO
+      deallocate(ke_vertex)
+      deallocate(ke_edge)
+      call mpas_rbf_interp_initialize(bm)
+      call mpas_init_reconstruct(bm)
+      call mpas_pool_get_array(bs, 'u', uu, 1)
+      call mpas_pool_get_array(bd, 'uReconstructX', uReconstructX)
+      call mpas_pool_get_array(bd, 'uReconstructY', uReconstructY)
+      call mpas_pool_get_array(bd, 'uReconstructZ', uReconstructZ)
+      call mpas_pool_get_array(bd, 'uReconstructZonal', uReconstructZonal)
+      call mpas_pool_get_array(bd, 'uReconstructMeridional', uReconstructMeridional)
+      call mpas_reconstruct(bm, uu, uReconstructX, uReconstructY, uReconstructZ, uReconstructZonal, &
+                            uReconstructMeridional)
+   end subroutine init_block
+
+   ! every block's pools into <dir>/block<i>
+   subroutine dump_blocks(dir)
+      character(len=*), intent(in) :: dir
+      character(len=16) :: bname
+      type (block_type), pointer :: b
+      b => domain % blocklist
+      do while (associated(b))
+         hblock => b
+         write(bname, '(a,i0)') '/block', b % localBlockID
+         call dump_all(trim(dir)//trim(bname), plist)
+         b => b % next
+      end do
+   end subroutine dump_blocks
+
    subroutine add_dims(p)
       type (mpas_pool_type), pointer :: p
       call mpas_pool_add_dimension(p, 'nCells', nCells)
       call mpas_pool_add_dimension(p, 'nEdges', nEdges)
       call mpas_pool_add_dimension(p, 'nVertices', nVertices)
-      call mpas_pool_add_dimension(p, 'nCellsSolve', nCells)
-      call mpas_pool_add_dimension(p, 'nEdgesSolve', nEdges)
-      call mpas_pool_add_dimension(p, 'nVerticesSolve', nVertices)
+      call mpas_pool_add_dimension(p, 'nCellsSolve', nCellsSolve_in)
+      call mpas_pool_add_dimension(p, 'nEdgesSolve', nEdgesSolve_in)
+      call mpas_pool_add_dimension(p, 'nVerticesSolve', nVerticesSolve_in)
       call mpas_pool_add_dimension(p, 'nVertLevels', K)
       call mpas_pool_add_dimension(p, 'nVertLevelsP1', K+1)
       call mpas_pool_add_dimension(p, 'maxEdges', maxEdges_in)

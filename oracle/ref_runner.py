@@ -72,9 +72,8 @@ def write_physics_inputs(case: dict, d: str, physics: dict):
         img.tofile(os.path.join(d, n + "_in.bin"))
 
 
-def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthreads: int = 0,
-                 moist_end: int = 1, convection_scheme: str = "off", print_minmax: int = 0,
-                 dump_only=()):
+def write_fields(case: dict, d: str):
+    """Every mesh / state / diag array of the case as its Fortran memory image, one .bin per field."""
     F = _fields()
     os.makedirs(d, exist_ok=True)
     names = [n for n in case if n in F.LOCATION or n in F.VERTICAL_1D or n in F.SCALARS_0D]
@@ -85,6 +84,14 @@ def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthr
             np.asarray(case[n], dtype=np.float64).tofile(os.path.join(d, n + ".bin"))
         else:
             to_fortran(case, n).tofile(os.path.join(d, n + ".bin"))
+
+
+def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthreads: int = 0,
+                 moist_end: int = 1, convection_scheme: str = "off", print_minmax: int = 0,
+                 dump_only=(), fields: bool = True, nblocks: int = 1):
+    os.makedirs(d, exist_ok=True)
+    if fields:
+        write_fields(case, d)
     cfg = case["config"]
     ds = list(dump_steps) + [-1] * (16 - len(dump_steps))
 
@@ -123,6 +130,8 @@ def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthr
         nml = nml.replace("&harness\n", f"&harness\n print_minmax={print_minmax},\n")
     if dump_only:
         nml = nml.replace("&harness\n", f"&harness\n dump_only='{','.join(dump_only)}',\n")
+    if nblocks > 1:
+        nml = nml.replace("&harness\n", f"&harness\n nblocks={nblocks},\n")
     nml = nml.replace("e+", "d+").replace("e-", "d-")
     with open(os.path.join(d, "harness.nml"), "w") as f:
         f.write(nml)
@@ -249,6 +258,61 @@ def run_reference_init(case: dict, nthreads: int = 1, timeout: int = 600) -> dic
             a = a.reshape((case[_LOC_N[loc]] + 1,) + inner[::-1])[:-1]
             out[name] = a.astype(np.int64) - 1 if is_int and name != "nAdvCellsForEdge" else a
         return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def write_block_inputs(blocks: list, d: str):
+    """The blocks of one process (mpas_dycore.decomp) for the harness's multi-block mode: per block
+    <d>/block<i>/ with its fields, block.nml (dims, owned counts) and its local-copy exchange lists
+    copy_<loc>_<layer>_<j>.bin (1-based srcList here, then destList in block j, MPAS exchList order)."""
+    local = {b.part: i for i, b in enumerate(blocks)}
+    for i, b in enumerate(blocks):
+        bd = os.path.join(d, f"block{i}")
+        write_fields(b.case, bd)
+        nc, ne, nv = b.solve
+        with open(os.path.join(bd, "block.nml"), "w") as f:
+            f.write(f"&block\n nCells={b.case['nCells']}, nEdges={b.case['nEdges']}, nVertices={b.case['nVertices']},\n"
+                    f" nCellsSolve_in={nc}, nEdgesSolve_in={ne}, nVerticesSolve_in={nv}\n/\n")
+        for loc, layer, peer, idx in b.send:
+            pb = blocks[local[peer]]
+            dst = [x for (l2, y2, q2, x) in pb.recv if l2 == loc and y2 == layer and q2 == b.part]
+            if len(dst) != 1 or len(dst[0]) != len(idx):
+                raise ValueError(f"block {b.part} -> {peer} {loc} layer {layer}: send/recv lists disagree")
+            lists = np.concatenate([np.asarray(idx, np.int32) + 1, np.asarray(dst[0], np.int32) + 1])
+            lists.astype(np.int32).tofile(os.path.join(bd, f"copy_{loc}_{layer}_{local[peer]}.bin"))
+
+
+def run_reference_blocks(case: dict, blocks: list, nsteps: int, dt: float, dump_steps=None, nthreads: int = 0,
+                         moist_end: int = 1, timeout: int = 3000, dump_only=()):
+    """The reference dycore on several blocks in one process (mpas_dmpar local copies between them):
+    returns ({step: [per-block {field: array}]}, [step wall times])."""
+    import shutil
+    if not available():
+        raise RuntimeError(f"{HARNESS} not built (make -C oracle)")
+    dump_steps = [nsteps] if dump_steps is None else dump_steps
+    tmp = tempfile.mkdtemp(prefix="mpasrefb_")
+    try:
+        ind, outd = os.path.join(tmp, "in"), os.path.join(tmp, "out")
+        write_inputs(case, ind, nsteps, dt, dump_steps, nthreads, moist_end, dump_only=dump_only, fields=False,
+                     nblocks=len(blocks))
+        write_block_inputs(blocks, ind)
+        env = dict(os.environ)
+        if nthreads:
+            env["OMP_NUM_THREADS"] = str(nthreads)
+        env.setdefault("OMP_STACKSIZE", "1G")
+        r = subprocess.run([HARNESS, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout,
+                           preexec_fn=_big_stack)
+        if r.returncode != 0:
+            raise RuntimeError(f"multi-block reference failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
+        res = {s: [read_dump(b.case, os.path.join(outd, f"step_{s:04d}", f"block{i}")) for i, b in enumerate(blocks)]
+               for s in dump_steps}
+        times = []
+        with open(os.path.join(outd, "timing.txt")) as f:
+            for line in f:
+                if line.startswith("step"):
+                    times.append(float(line.split()[2]))
+        return res, times
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
