@@ -72,8 +72,8 @@ def varres_case(ncells: int, ratio: float = 20.0, K: int = 56, ns: int = 1, mois
     dt and config_len_disp follow the finest spacing, as MPAS variable-resolution runs do
     (dt ~ 5 s per km of the finest cells, len_disp = finest spacing)."""
     if lloyd_iters is None:
-        lloyd_iters = 40 if ncells <= 200000 else 12
-    key = f"vr_n{ncells}_r{ratio:g}_K{K}_ns{ns}_m{int(moist)}_ll{lloyd_iters}_v4"
+        lloyd_iters = 40 if ncells <= 200000 else 6
+    key = f"vr_n{ncells}_r{ratio:g}_K{K}_ns{ns}_m{int(moist)}_ll{lloyd_iters}_v5"
     path = os.path.join(CACHE, key + ".pkl")
     if cache and os.path.isfile(path):
         with open(path, "rb") as f:  # our own cache file, written below

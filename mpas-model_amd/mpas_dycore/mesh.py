@@ -226,21 +226,51 @@ def _schmidt(p, center_latlon, c):
     return (np.sin(th2) * np.cos(ph))[:, None] * xa + (np.sin(th2) * np.sin(ph))[:, None] * ya + np.cos(th2)[:, None] * zc
 
 
+def _icosahedral_points(n: int) -> np.ndarray:
+    """Generators of an n-times subdivided icosahedron (10 n^2 + 2 points): each face's
+    barycentric grid, projected to the sphere, shared edge / corner points once."""
+    v, f = _icosahedron()
+    i, j = np.meshgrid(np.arange(n + 1), np.arange(n + 1), indexing="ij")
+    keep = (i + j) <= n
+    i, j = i[keep].astype(np.float64), j[keep].astype(np.float64)
+    k = n - i - j
+    pts = np.concatenate([(i[:, None] * v[a] + j[:, None] * v[b] + k[:, None] * v[c]) / n for a, b, c in f])
+    p = _normalize(pts)
+    _, first = np.unique(np.round(p * 1e9).astype(np.int64), axis=0, return_index=True)
+    return p[np.sort(first)]
+
+
 def build_varres_mesh(ncells: int, ratio: float = 20.0, lloyd_iters: int = 10, seed: int = 20250415,
-                      radius: float = SPHERE_RADIUS, sfc: bool = True, **density_kw) -> dict:
+                      radius: float = SPHERE_RADIUS, sfc: bool = True, start: str | None = None,
+                      **density_kw) -> dict:
     """Variable-resolution spherical centroidal Voronoi mesh (BASELINE.json configs[4]:
     x20.835586-like 60-3 km meshes).  A Fibonacci lattice of ``ncells`` generators is
     pulled towards the refinement centre by a Schmidt transform (stretch sqrt(ratio)),
     then relaxed by density-weighted Lloyd iterations on the spherical Delaunay
     triangulation, which is rebuilt every step so the topology (pentagons / hexagons /
-    heptagons in the transition zone) is free to change."""
+    heptagons in the transition zone) is free to change.
+
+    start = "icosahedral" (the default above 200000 cells) begins instead from the n-times
+    subdivided icosahedron with 10 n^2 + 2 ~ ncells points (n = 289: 835212 cells): a few Lloyd
+    iterations from the Fibonacci lattice leave tens of thousands of nearly co-circular quads at
+    that size (Voronoi edges of ~1e-6 of the spacing, which make the dycore blow up within a
+    step), while the stretched icosahedral lattice relaxes to dvEdge / dcEdge >= 0.35 -- at the
+    price of hexagons only (the 5/6/7-gon paths are covered by the smaller Fibonacci meshes)."""
     rho = varres_density(ratio=ratio, **density_kw)
     center = density_kw.get("center_latlon", (30.0, -90.0))
-    p = _schmidt(_fibonacci_sphere(ncells), center, np.sqrt(ratio))
+    if start is None:
+        start = "icosahedral" if ncells > 200000 else "fibonacci"
+    if start == "icosahedral":
+        p0 = _icosahedral_points(max(1, int(round(np.sqrt((ncells - 2) / 10.0)))))
+    else:
+        p0 = _fibonacci_sphere(ncells)
+    p = _schmidt(p0, center, np.sqrt(ratio))
     for it in range(lloyd_iters):
         p = _lloyd_step(p, _delaunay(p), rho)
         if ncells > 200000:  # long builds report progress (a silent GPU-box job looks hung)
             print(f"varres mesh: Lloyd iteration {it + 1}/{lloyd_iters}", file=sys.__stderr__, flush=True)
+    if start == "icosahedral":  # a safety net: the stretched lattice relaxes without such quads
+        p = _untangle_cocircular(p)
     f = _delaunay(p)
     if sfc:
         order = np.argsort(_hilbert3d_keys(p), kind="stable")
@@ -251,6 +281,40 @@ def build_varres_mesh(ncells: int, ratio: float = 20.0, lloyd_iters: int = 10, s
     m = _topology_and_geometry(p, f, radius)
     m["meshDensity"] = rho(p)
     return m
+
+
+def _untangle_cocircular(p, min_ratio=0.05, step=0.15, rounds=10):
+    """Density-weighted Lloyd iterations leave some nearly co-circular generator quads in the
+    refinement's transition zone: their two Delaunay triangles have almost the same circumcentre,
+    so the Voronoi edge between them is ~1e-6 of the cell spacing (a 4-valent vertex in all but
+    name).  Such an edge makes the dycore's 1/dvEdge operators (del4 mixing, vorticity) blow up.
+    Pulling the edge's two generators towards each other by ``step`` of their distance makes that
+    diagonal clearly Delaunay and opens the edge; repeated until every Voronoi edge is at least
+    ``min_ratio`` of its cell-centre distance (MPAS quasi-uniform meshes: ~0.33)."""
+    for _ in range(rounds):
+        f = _delaunay(p)
+        vc = _circumcenters(p, f)
+        pairs = np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]])
+        face = np.concatenate([np.arange(len(f))] * 3)
+        s = np.sort(pairs, axis=1)
+        o = np.lexsort((s[:, 1], s[:, 0]))
+        s, face = s[o], face[o]
+        a, b = s[0::2], s[1::2]
+        fa, fb = face[0::2], face[1::2]
+        dv = np.linalg.norm(vc[fa] - vc[fb], axis=1)
+        dc = np.linalg.norm(p[a[:, 0]] - p[a[:, 1]], axis=1)
+        bad = dv < min_ratio * dc
+        if len(p) > 200000:
+            print(f"varres mesh: {int(bad.sum())} near-degenerate Voronoi edges", file=sys.__stderr__, flush=True)
+        if not np.any(bad):
+            break
+        i, j = a[bad, 0], a[bad, 1]
+        d = p[j] - p[i]
+        q = p.copy()
+        np.add.at(q, i, step * d)
+        np.add.at(q, j, -step * d)
+        p = _normalize(q)
+    return p
 
 
 def _cells_vertices_ccw(p, f, width=None):

@@ -49,8 +49,11 @@ def test_edge_orientation_conventions(mesh):
             assert set(mesh["cellsOnEdge"][e]) == {c, mesh["cellsOnCell"][c, i]}
 
 
-def test_trisk_weights(mesh):
-    """Thuburn et al. (2009): v accuracy for solid-body rotation and energy antisymmetry."""
+def test_trisk_weights(mesh, min_dv_dc=0.0):
+    """Thuburn et al. (2009): v accuracy for solid-body rotation and energy antisymmetry.
+    min_dv_dc: the accuracy bar applies to edges at least that long relative to dcEdge (the
+    variable-resolution mesh opens its near-degenerate edges only to 5 % of dcEdge, where the
+    reconstruction is less accurate; the antisymmetry is exact everywhere)."""
     xc, xe = _xyz(mesh, "Cell"), _xyz(mesh, "Edge")
     c1, c2 = mesh["cellsOnEdge"].T
     n = _normalize(xc[c2] - xc[c1] - np.sum((xc[c2] - xc[c1]) * xe, 1)[:, None] * xe)
@@ -59,7 +62,8 @@ def test_trisk_weights(mesh):
     u, vt = np.sum(U * n, 1), np.sum(U * t, 1)
     eoe, w = mesh["edgesOnEdge"], mesh["weightsOnEdge"]
     v = np.sum(np.where(eoe >= 0, w * u[np.maximum(eoe, 0)], 0.0), 1)
-    assert np.abs(v - vt).max() / np.abs(vt).max() < 0.05
+    ok = mesh["dvEdge"] / mesh["dcEdge"] >= min_dv_dc
+    assert np.abs(v - vt)[ok].max() / np.abs(vt).max() < 0.05
     dc, dv = mesh["dcEdge"], mesh["dvEdge"]
     W = {}
     for e in range(mesh["nEdges"]):
@@ -93,4 +97,16 @@ def test_varres_mesh_conventions(vr_mesh):
     assert abs(m["areaCell"].sum() / (4 * np.pi * R * R) - 1) < 2e-3
     assert m["dcEdge"].max() / m["dcEdge"].min() > 3.0           # really variable resolution
     test_edge_orientation_conventions(m)
+    test_trisk_weights(m)
+
+
+def test_large_varres_start_has_no_degenerate_edges():
+    """The icosahedral start of the large variable-resolution meshes (build_varres_mesh,
+    start="icosahedral"): no nearly co-circular quads, dvEdge / dcEdge well away from 0."""
+    from mpas_dycore.mesh import build_varres_mesh
+    m = build_varres_mesh(10242, ratio=20.0, lloyd_iters=4, start="icosahedral")
+    assert m["nCells"] == 10242
+    r = m["dvEdge"] / m["dcEdge"]
+    assert r.min() > 0.3
+    assert m["dcEdge"].max() / m["dcEdge"].min() > 10.0
     test_trisk_weights(m)
