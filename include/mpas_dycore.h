@@ -91,6 +91,10 @@ void* mpas_dyc_field_device_ptr(mpas_dyc_ctx* ctx, const char* pool, const char*
 /* atm_init_coupled_diagnostics + atm_compute_solve_diagnostics on time level 1
  * (model init, mpas_atm_core.F:387-404). */
 int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt);
+/* The same model init for a restart (config_do_restart, mpas_atm_core.F:387-404): only
+ * atm_compute_solve_diagnostics (with the init exchanges), on a state whose coupled fields
+ * (theta_m, rho_zz, rho_p, rtheta_p, exner, pressure_p, ru, rw, ...) the host has set. */
+int mpas_dyc_solve_diagnostics(mpas_dyc_ctx* ctx, double dt);
 /* atm_timestep -> atm_srk3: advance time level 1 to time level 2 by dt. Asynchronous. */
 int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep);
 /* mpas_pool_shift_time_levels(state): swap time levels 1 and 2 (pointer swap). */

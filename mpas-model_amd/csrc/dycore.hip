@@ -1296,12 +1296,16 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
 }
 
 // model init, mpas_atm_core.F:143-186 (exchanges) and 387-404 (the two routines)
-int init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
+// coupled = false: a restart (config_do_restart without DA cycling, 387-397) skips
+// atm_init_coupled_diagnostics; the coupled state and its perturbations come from the restart file
+int init_diagnostics(mpas_dyc_ctx* ctx, double dt, bool coupled = true) {
   const std::vector<Ptrs> P = block_ptrs(ctx);
   CHK(exchange(ctx, {{"state", "u", 1, ALL_LAYERS}}));           // 145
-  EACH(LAUNCH(k_init_coupled_a, d.nCells, d, p, ctx->index_qv));
-  EACH(LAUNCH(k_init_coupled_b, d.nEdges, d, p));
-  EACH(LAUNCH(k_init_coupled_c, d.nCells, d, p));
+  if (coupled) {
+    EACH(LAUNCH(k_init_coupled_a, d.nCells, d, p, ctx->index_qv));
+    EACH(LAUNCH(k_init_coupled_b, d.nEdges, d, p));
+    EACH(LAUNCH(k_init_coupled_c, d.nCells, d, p));
+  }
   EACH(solve_diagnostics(ctx, d, p, dt, 1, 0));
   EACH(LAUNCH(k_reconstruct, d.nCellsSolve, d, p, p.u1));          // mpas_atm_core.F:411-421
   CHK(exchange(ctx, {{"diag", "pv_edge", 0, ALL_LAYERS}, {"diag", "ru", 0, ALL_LAYERS},  // 180-186
@@ -1937,6 +1941,16 @@ int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
   HIPCHK(hipSetDevice(ctx->device));
   if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
   int r = init_diagnostics(ctx, dt);
+  HIPCHK(hipGetLastError());
+  return r;
+}
+
+int mpas_dyc_solve_diagnostics(mpas_dyc_ctx* ctx, double dt) {
+  if (!ctx) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
+  int r = init_diagnostics(ctx, dt, false);
   HIPCHK(hipGetLastError());
   return r;
 }

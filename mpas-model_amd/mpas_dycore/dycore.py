@@ -173,6 +173,17 @@ class Dycore:
         """Upload an element-major array (0-based indices for index fields)."""
         self.set_raw(pool, name, to_fortran({**self.cases[block], name: arr}, name), time_level, block)
 
+    def get_raw(self, pool: str, name: str, time_level: int = 1, block: int = 0) -> np.ndarray:
+        """Download a field's Fortran memory image (flat, garbage slot included): set_raw's inverse."""
+        nb = self.lib.mpas_dyc_block_field_bytes(self.h, block, pool.encode(), name.encode())
+        if nb <= 0:
+            raise DycoreError(f"unknown field {pool}.{name}")
+        buf = np.empty(nb // 8, dtype=np.float64)
+        self._check(self.lib.mpas_dyc_get_block_field(self.h, block, pool.encode(), name.encode(), time_level,
+                                                      buf.ctypes.data_as(C.c_void_p), buf.nbytes),
+                    f"get {pool}.{name}")
+        return buf
+
     def get(self, pool: str, name: str, time_level: int = 1, block: int = 0) -> np.ndarray:
         """Download a real field as element-major (n, inner) numpy (garbage slot dropped)."""
         nb = self.lib.mpas_dyc_block_field_bytes(self.h, block, pool.encode(), name.encode())
@@ -221,6 +232,11 @@ class Dycore:
     def init_diagnostics(self, dt: float):
         """atm_init_coupled_diagnostics + atm_compute_solve_diagnostics (mpas_atm_core.F:387-404)."""
         self._check(self.lib.mpas_dyc_init_diagnostics(self.h, float(dt)), "init_diagnostics")
+
+    def restart_diagnostics(self, dt: float):
+        """Model init of a restart run (config_do_restart, mpas_atm_core.F:387-404): only
+        atm_compute_solve_diagnostics, on a coupled state the host has set (mpas_dyc_solve_diagnostics)."""
+        self._check(self.lib.mpas_dyc_solve_diagnostics(self.h, float(dt)), "solve_diagnostics")
 
     def atm_timestep(self, dt: float, itimestep: int = 1):
         """atm_timestep -> atm_srk3 (mpas_atm_time_integration.F:87-139); asynchronous."""

@@ -203,6 +203,24 @@ contains
       call register(pname, name, 3, ntl, .false.)
    end subroutine add_r3
 
+   ! a character field of ntl time levels (state xtime, Registry.xml), initialised to `init`
+   subroutine add_c0(pool, pname, name, ntl, init)
+      type (mpas_pool_type), pointer :: pool
+      character(len=*), intent(in) :: pname, name, init
+      integer, intent(in) :: ntl
+      type (field0DChar), dimension(:), pointer :: fa
+      integer :: t
+      allocate(fa(ntl))
+      do t = 1, ntl
+         fa(t) % block => hblock
+         fa(t) % fieldName = name
+         fa(t) % isActive = .false.
+         fa(t) % scalar = init
+      end do
+      call mpas_pool_add_field(pool, name, fa)
+      call register(pname, name, -1, ntl, .false.)
+   end subroutine add_c0
+
    subroutine add_i1(pool, pname, name, d1)
       type (mpas_pool_type), pointer :: pool
       character(len=*), intent(in) :: pname, name
@@ -250,8 +268,21 @@ contains
       type (field3DReal), pointer :: f3
       type (field1DInteger), pointer :: i1
       type (field2DInteger), pointer :: i2
+      type (field0DChar), pointer :: c0
       call execute_command_line('mkdir -p '//trim(dir))
       do i = 1, nf
+         if (frank(i) < 0) then   ! character scalar (state xtime), one text file per time level
+            call mpas_pool_get_subpool(hblock % structs, trim(fpool(i)), p)
+            do t = 1, fntl(i)
+               write(tl, '(a,i1)') '.tl', t
+               call mpas_pool_get_field(p, trim(fname(i)), c0, t)
+               open(newunit=u, file=trim(dir)//'/'//trim(fpool(i))//'.'//trim(fname(i))//trim(tl)//'.txt', &
+                    status='replace')
+               write(u, '(a)') trim(c0 % scalar)
+               close(u)
+            end do
+            cycle
+         end if
          if (fisint(i)) then
             if (.not. dump_ints) cycle
             call mpas_pool_get_subpool(hblock % structs, trim(fpool(i)), p)
@@ -308,6 +339,7 @@ program mpas_ref_harness
    use atm_time_integration
    use mpas_rbf_interpolation
    use mpas_vector_reconstruction
+   use mpas_timekeeping
    use harness_fields
 #ifdef HARNESS_INIT
    use atm_advection, only : atm_initialize_advection_rk, atm_initialize_deformation_weights
@@ -363,9 +395,12 @@ program mpas_ref_harness
    integer, dimension(:), pointer :: cts, cte, csts, cste, ets, ete, ests, este, vts, vte, vsts, vste
    real(kind=RKIND), dimension(:,:), pointer :: uu, uReconstructX, uReconstructY, uReconstructZ, &
                                                 uReconstructZonal, uReconstructMeridional
-   real(kind=RKIND) :: t0, t1
+   real(kind=RKIND) :: t0, t1, tloop
    real(kind=RKIND), allocatable :: steptime(:)
    character(len=16) :: sdir
+   type (MPAS_Time_type) :: nowTime
+   type (MPAS_TimeInterval_type) :: dtInterval
+   character(len=*), parameter :: start_time = '2000-01-01_00:00:00'
 
    call get_command_argument(1, indir)
    call get_command_argument(2, outdir)
@@ -413,6 +448,10 @@ program mpas_ref_harness
    call mpas_log_open()
    call mpas_pool_create_pool(configs)
    domain % configs => configs
+   nullify(domain % clock)
+   ! the time loop passes atm_timestep its nowTime as mpas_atm_core.F does (atm_do_timestep)
+   call mpas_timekeeping_init('gregorian')
+   call mpas_set_time(nowTime, dateTimeString=start_time)
 
    call mpas_atm_set_dims(K, maxEdges_in, maxEdges2_in, ns)
 
@@ -491,9 +530,12 @@ program mpas_ref_harness
       if (any(dump_steps == 0)) call dump_blocks(trim(outdir)//'/step_0000')
       call mpas_pool_get_config(configs, 'config_apply_lbcs', config_apply_lbcs)
       allocate(steptime(max(nsteps,1)))
+      call mpas_set_timeInterval(dtInterval, dt=dt)
+      tloop = omp_get_wtime()
       do step = 1, nsteps
          t0 = omp_get_wtime()
-         call atm_srk3(domain, dt, step)
+         call atm_timestep(domain, dt, nowTime, step)
+         nowTime = nowTime + dtInterval
          t1 = omp_get_wtime()
          steptime(step) = t1 - t0
          write(0, '(a,i6,f10.3)') 'harness: step', step, steptime(step)
@@ -502,15 +544,26 @@ program mpas_ref_harness
          call mpas_pool_shift_time_levels(state)
          if (any(dump_steps == step)) then
             write(sdir, '(a,i4.4)') 'step_', step
+#ifdef MPAS_DYCORE_DROPIN
+            call atm_dycore_to_host(domain)   ! the HBM state into the pools before they are read
+#endif
             call dump_blocks(trim(outdir)//'/'//trim(sdir))
          end if
       end do
+#ifdef MPAS_DYCORE_DROPIN
+      call atm_dycore_wait()   ! the steps run asynchronously: the loop ends when the device is done
+#endif
+      tloop = omp_get_wtime() - tloop
+#ifdef MPAS_DYCORE_DROPIN
+      call atm_dycore_to_host(domain)
+#endif
       call execute_command_line('mkdir -p '//trim(outdir))
       open(newunit=u, file=trim(outdir)//'/timing.txt', status='replace')
       write(u, '(a,i6)') 'threads ', nthr
       do step = 1, nsteps
          write(u, '(a,i6,es24.16)') 'step ', step, steptime(step)
       end do
+      write(u, '(a,es24.16)') 'total ', tloop
       close(u)
       call mpas_dmpar_finalize(domain % dminfo)
       stop
@@ -586,31 +639,43 @@ program mpas_ref_harness
    write(0, '(a)') 'harness: reconstruct done'
    if (any(dump_steps == 0)) call dump_all(trim(outdir)//'/step_0000', plist)
 
-   ! atm_timestep (mpas_atm_time_integration.F:117-118) binds this module pointer before
-   ! calling atm_srk3; the xtime bookkeeping it also does is not needed here.
    call mpas_pool_get_config(configs, 'config_apply_lbcs', config_apply_lbcs)
 
-   ! ---- time loop (mpas_atm_core.F:604-748 -> atm_do_timestep -> atm_srk3) ----
+   ! ---- time loop (mpas_atm_core.F:604-748 -> atm_do_timestep -> atm_timestep -> atm_srk3) ----
    allocate(steptime(max(nsteps,1)))
+   call mpas_set_timeInterval(dtInterval, dt=dt)
+   tloop = omp_get_wtime()
    do step = 1, nsteps
       t0 = omp_get_wtime()
-      call atm_srk3(domain, dt, step)
+      call atm_timestep(domain, dt, nowTime, step)
+      nowTime = nowTime + dtInterval
       t1 = omp_get_wtime()
       steptime(step) = t1 - t0
       write(0, '(a,i6,f10.3)') 'harness: step', step, steptime(step)
       call mpas_pool_shift_time_levels(state)
       if (any(dump_steps == step)) then
          write(sdir, '(a,i4.4)') 'step_', step
+#ifdef MPAS_DYCORE_DROPIN
+         call atm_dycore_to_host(domain)   ! the HBM state into the pools before they are read
+#endif
          call dump_all(trim(outdir)//'/'//trim(sdir), plist)
       end if
    end do
 
+#ifdef MPAS_DYCORE_DROPIN
+   call atm_dycore_wait()   ! the steps run asynchronously: the loop ends when the device is done
+#endif
+   tloop = omp_get_wtime() - tloop
+#ifdef MPAS_DYCORE_DROPIN
+   call atm_dycore_to_host(domain)
+#endif
    call execute_command_line('mkdir -p '//trim(outdir))
    open(newunit=u, file=trim(outdir)//'/timing.txt', status='replace')
    write(u, '(a,i6)') 'threads ', nthr
    do step = 1, nsteps
       write(u, '(a,i6,es24.16)') 'step ', step, steptime(step)
    end do
+   write(u, '(a,es24.16)') 'total ', tloop
    close(u)
 
    call mpas_dmpar_finalize(domain % dminfo)
@@ -783,6 +848,7 @@ contains
       call add_r2(state, 'state', 'theta_m', K, nC1, 2)
       call add_r2(state, 'state', 'rho_zz', K, nC1, 2)
       call add_r3(state, 'state', 'scalars', ns, K, nC1, 2)
+      call add_c0(state, 'state', 'xtime', 2, start_time)
    
       ! ---- diag pool ----
       call add_r2(diag, 'diag', 'theta', K, nC1, 1);        call add_r2(diag, 'diag', 'rho', K, nC1, 1)

@@ -25,6 +25,8 @@ PHYS_HARNESS = os.path.join(HERE, "_ref", "mpas_ref_harness_phys")
 # the same harness driver linked against the Fortran drop-in module + libmpas_dycore.so
 # (make -C oracle dropin): the product behind the reference's own Fortran API, not an oracle
 DROPIN_HARNESS = os.path.join(HERE, "_ref", "mpas_dropin_harness")
+# the drop-in built with -DDO_PHYSICS over the same physics test doubles as PHYS_HARNESS
+DROPIN_PHYS_HARNESS = os.path.join(HERE, "_ref", "mpas_dropin_harness_phys")
 
 _LOC_N = {"cell": "nCells", "edge": "nEdges", "vertex": "nVertices"}
 
@@ -144,7 +146,12 @@ def read_dump(case: dict, stepdir: str) -> dict:
     K, ns = case["nVertLevels"], case["num_scalars"]
     nC, nE, nV = case["nCells"], case["nEdges"], case["nVertices"]
     out = {}
+    text = {}
     for fn in sorted(os.listdir(stepdir)):
+        if fn.endswith(".txt"):  # character fields (state.xtime.tlN)
+            with open(os.path.join(stepdir, fn)) as f:
+                text[fn[:-4]] = f.read().strip()
+            continue
         if not fn.endswith(".bin"):
             continue
         key = fn[:-4]
@@ -163,20 +170,23 @@ def read_dump(case: dict, stepdir: str) -> dict:
                 break
         else:
             shaped[key] = a
+    shaped.update(text)
     return shaped
 
 
 def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads: int = 0,
                   workdir: str | None = None, moist_end: int = 1, timeout: int = 3000, binary: str = HARNESS,
-                  physics: dict | None = None, print_minmax: int = 0, dump_only=()):
-    """Run the reference dycore; returns ({step: {field: array}}, [step wall times]).
+                  physics: dict | None = None, print_minmax: int = 0, dump_only=(), env_extra: dict | None = None,
+                  with_total: bool = False):
+    """Run the reference dycore; returns ({step: {field: array}}, [step wall times]) -- and, with
+    ``with_total``, the wall time of the whole time loop including its final wait for the device.
     ``binary=DROPIN_HARNESS`` runs the same driver on the drop-in module instead.
     ``physics`` (dict of write_physics_inputs' arrays, optional key "convection_scheme") runs the
     DO_PHYSICS build with those tendencies handed over by physics_get_tend every step.
     ``dump_only`` (e.g. ["state.u", "state.w"]) limits the dumps to those fields (full-size runs).
     ``print_minmax`` turns on summarize_timestep's namelist switches (1 global_minmax_vel,
     2 detailed_minmax_vel, 4 global_minmax_sca); the reference's log text is then res["log"]."""
-    if physics is not None:
+    if physics is not None and binary == HARNESS:
         binary = PHYS_HARNESS
     if not available(binary):
         raise RuntimeError(f"{binary} not built (make -C oracle)")
@@ -192,6 +202,7 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     env = dict(os.environ)
     if nthreads:
         env["OMP_NUM_THREADS"] = str(nthreads)
+    env.update(env_extra or {})
     # the reference's automatic arrays (nCells-sized locals in the *_work routines) live on the
     # stack: large meshes need the main thread's stack unlimited and big OpenMP thread stacks
     env.setdefault("OMP_STACKSIZE", "1G")
@@ -206,15 +217,17 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     if print_minmax:
         logs = sorted(fn for fn in os.listdir(tmp) if fn.startswith("log.") and fn.endswith(".out"))
         res["log"] = "".join(open(os.path.join(tmp, fn)).read() for fn in logs)
-    times = []
+    times, total = [], None
     with open(os.path.join(outd, "timing.txt")) as f:
         for line in f:
             if line.startswith("step"):
                 times.append(float(line.split()[2]))
+            elif line.startswith("total"):
+                total = float(line.split()[1])
     if own:
         import shutil
         shutil.rmtree(tmp, ignore_errors=True)
-    return res, times
+    return (res, times, total) if with_total else (res, times)
 
 
 # mode 'init': the reference's mesh-dependent precompute (mpas_atm_advection.F deriv_two / defc_a /
@@ -284,12 +297,14 @@ def write_block_inputs(blocks: list, d: str):
 
 
 def run_reference_blocks(case: dict, blocks: list, nsteps: int, dt: float, dump_steps=None, nthreads: int = 0,
-                         moist_end: int = 1, timeout: int = 3000, dump_only=()):
+                         moist_end: int = 1, timeout: int = 3000, dump_only=(), binary: str = HARNESS,
+                         env_extra: dict | None = None):
     """The reference dycore on several blocks in one process (mpas_dmpar local copies between them):
-    returns ({step: [per-block {field: array}]}, [step wall times])."""
+    returns ({step: [per-block {field: array}]}, [step wall times]).  ``binary=DROPIN_HARNESS``
+    runs the same driver on the drop-in module (its domain context then holds every block)."""
     import shutil
-    if not available():
-        raise RuntimeError(f"{HARNESS} not built (make -C oracle)")
+    if not available(binary):
+        raise RuntimeError(f"{binary} not built (make -C oracle)")
     dump_steps = [nsteps] if dump_steps is None else dump_steps
     tmp = tempfile.mkdtemp(prefix="mpasrefb_")
     try:
@@ -301,7 +316,8 @@ def run_reference_blocks(case: dict, blocks: list, nsteps: int, dt: float, dump_
         if nthreads:
             env["OMP_NUM_THREADS"] = str(nthreads)
         env.setdefault("OMP_STACKSIZE", "1G")
-        r = subprocess.run([HARNESS, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout,
+        env.update(env_extra or {})
+        r = subprocess.run([binary, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout,
                            preexec_fn=_big_stack)
         if r.returncode != 0:
             raise RuntimeError(f"multi-block reference failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")

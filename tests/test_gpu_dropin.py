@@ -13,6 +13,12 @@ The pools it dumps are then checked in three ways:
   * against the reference harness (rel L∞, same tolerances as test_gpu_parity);
   * bit for bit against the Python host driving the same library;
   * for the dump after model init, against the reference's init diagnostics.
+The driver calls atm_timestep with its nowTime, so the xtime stamp (mpas_atm_time_integration.F:
+127-137) is checked too.  The drop-in keeps the state in HBM and the driver calls
+atm_dycore_to_host before each dump; MPAS_DYCORE_SYNC_EVERY_STEP=1 (the per-step copy-back)
+must give the same bits.  Further cases: two blocks in one process (the domain context built from
+domain%blocklist and the parinfo copy lists), and the -DDO_PHYSICS build (physics_get_tend on the
+host, its tendencies into HBM every step) against the reference's DO_PHYSICS build.
 """
 import numpy as np
 import pytest
@@ -30,15 +36,15 @@ INIT = ["state.theta_m.tl1", "state.rho_zz.tl1", "diag.ru", "diag.rw", "diag.pv_
 LOOSE = {"state.w.tl1", "diag.rw"} | set(RECON)   # small components of the zonal JW flow
 
 
-def _runs(case, moist_end=1):
+def _runs(case, moist_end=1, nthreads_dropin=1, env=None):
     from oracle import ref_runner
     if not (ref_runner.available() and ref_runner.available(ref_runner.DROPIN_HARNESS)):
         pytest.skip("oracle/_ref harness binaries not built (make -C oracle all dropin)")
     ref, _ = ref_runner.run_reference(case, nsteps=NSTEPS, dt=DT, dump_steps=[0, NSTEPS], nthreads=4,
                                       moist_end=moist_end)
-    # one thread: the drop-in's first atm_compute_solve_diagnostics call creates the device context
-    got, _ = ref_runner.run_reference(case, nsteps=NSTEPS, dt=DT, dump_steps=[0, NSTEPS], nthreads=1,
-                                      moist_end=moist_end, binary=ref_runner.DROPIN_HARNESS)
+    got, _ = ref_runner.run_reference(case, nsteps=NSTEPS, dt=DT, dump_steps=[0, NSTEPS],
+                                      nthreads=nthreads_dropin, moist_end=moist_end,
+                                      binary=ref_runner.DROPIN_HARNESS, env_extra=env)
     return ref, got
 
 
@@ -58,7 +64,9 @@ def _python_host(case, moist_end=1):
 @pytest.mark.parametrize("moist", [False, True])
 def test_dropin_harness_matches_reference(small_case, moist_case, moist):
     case = moist_case if moist else small_case
-    ref, got = _runs(case)
+    # 3 OpenMP threads: the init calls come per thread, the one whose range starts at cell 1 works
+    ref, got = _runs(case, nthreads_dropin=1 if moist else 3)
+    assert got[NSTEPS]["state.xtime.tl1"] == ref[NSTEPS]["state.xtime.tl1"] == "2000-01-01_02:24:00"
     errs = {}
     for k in INIT:
         errs["init " + k] = rel_linf(got[0][k], ref[0][k])
@@ -71,3 +79,83 @@ def test_dropin_harness_matches_reference(small_case, moist_case, moist):
     for k in PROG + RECON:
         a = got[NSTEPS][k]
         assert np.array_equal(a, py[k].reshape(a.shape)), f"{k}: drop-in differs from the Python host"
+
+
+def test_dropin_sync_every_step_same_bits(small_case):
+    """MPAS_DYCORE_SYNC_EVERY_STEP=1 (copy-back after every step) == on-demand atm_dycore_to_host."""
+    from oracle import ref_runner
+    if not ref_runner.available(ref_runner.DROPIN_HARNESS):
+        pytest.skip("drop-in harness not built")
+    runs = []
+    for env in ({}, {"MPAS_DYCORE_SYNC_EVERY_STEP": "1"}):
+        got, _ = ref_runner.run_reference(small_case, nsteps=NSTEPS, dt=DT, dump_steps=[1, NSTEPS], nthreads=1,
+                                          binary=ref_runner.DROPIN_HARNESS, env_extra=env)
+        runs.append(got)
+    for step in (1, NSTEPS):
+        for k in PROG + RECON + ["diag.pressure_p", "diag.exner", "diag.ru", "diag.pv_edge"]:
+            assert np.array_equal(runs[0][step][k], runs[1][step][k]), f"step {step} {k}"
+
+
+_N = {"cell": "nCells", "edge": "nEdges", "vertex": "nVertices"}
+BLOCK_FIELDS = [("state.u.tl1", "edge"), ("state.theta_m.tl1", "cell"), ("state.rho_zz.tl1", "cell"),
+                ("state.w.tl1", "cell"), ("diag.pv_edge", "edge"), ("diag.ru", "edge"), ("diag.rw", "cell"),
+                ("diag.exner", "cell"), ("diag.uReconstructZonal", "cell")]
+
+
+@pytest.mark.parametrize("nblocks", [2, 3])
+def test_dropin_blocks_bitwise_one_block(nblocks):
+    """The drop-in on several blocks of one process (its domain context from domain%blocklist, the
+    exchange lists from parinfo % xToCopy) equals the one-block drop-in bit for bit on owned
+    elements and halo layer 1, and the reference on the same blocks to the parity tolerances."""
+    from mpas_dycore import decomp
+    from mpas_dycore.cases import jw_case
+    from oracle import ref_runner
+    if not ref_runner.available(ref_runner.DROPIN_HARNESS):
+        pytest.skip("drop-in harness not built")
+    c = jw_case(642, K=26, ns=1, cache=False)
+    blocks = decomp.decompose(c, decomp.partition_sfc(c["nCells"], nblocks))
+    blocks.sort(key=lambda b: (-b.case["nCells"], -b.case["nEdges"]))  # reference: largest block first
+    one, _ = ref_runner.run_reference(c, nsteps=NSTEPS, dt=DT, dump_steps=[0, NSTEPS], nthreads=1,
+                                      binary=ref_runner.DROPIN_HARNESS)
+    multi, _ = ref_runner.run_reference_blocks(c, blocks, nsteps=NSTEPS, dt=DT, dump_steps=[0, NSTEPS], nthreads=2,
+                                               binary=ref_runner.DROPIN_HARNESS)
+    ref, _ = ref_runner.run_reference_blocks(c, blocks, nsteps=NSTEPS, dt=DT, dump_steps=[NSTEPS], nthreads=4)
+    for step in (0, NSTEPS):
+        for key, loc in BLOCK_FIELDS:
+            want_all = one[step][key].reshape((c[_N[loc]], -1))
+            for ib, (m, b) in enumerate(zip(multi[step], blocks)):
+                a = m[key].reshape((b.case[_N[loc]], -1))
+                n1 = b.layer_end[loc][0 if "Reconstruct" in key else 1]
+                got, want = a[:n1], want_all[b.glob[loc][:n1]]
+                assert np.array_equal(got, want), f"step {step} {key} block {b.part}: {rel_linf(got, want):.3e}"
+                if step == NSTEPS:
+                    r = ref[step][ib][key].reshape((b.case[_N[loc]], -1))[:n1]
+                    tol = 1e-11 if key in ("state.w.tl1", "diag.rw", "diag.uReconstructZonal") else 1e-12
+                    assert rel_linf(got, r) <= tol, f"{key} block {b.part} vs reference: {rel_linf(got, r):.3e}"
+        if step == NSTEPS:
+            assert multi[step][0]["state.xtime.tl1"] == one[step]["state.xtime.tl1"]
+
+
+@pytest.mark.parametrize("convection", ["cu_tiedtke", "off"])
+def test_dropin_physics_matches_reference(convection):
+    """The -DDO_PHYSICS drop-in (physics_get_tend on the host each step, tendencies into HBM, state
+    back for the host physics) against the reference's DO_PHYSICS build, both with the prescribed
+    tendencies of the physics_get_tend test double."""
+    from conftest import physics_forcing
+    from mpas_dycore.cases import jw_case
+    from oracle import ref_runner
+    if not (ref_runner.available(ref_runner.PHYS_HARNESS) and ref_runner.available(ref_runner.DROPIN_PHYS_HARNESS)):
+        pytest.skip("physics harness binaries not built (make -C oracle phys dropin)")
+    case = jw_case(642, K=26, ns=3, moist=True, cache=False)
+    dt = float(case["dt"])
+    phys = dict(physics_forcing(case), convection_scheme=convection)
+    n = 6
+    ref, _ = ref_runner.run_reference(case, n, dt, [1, n], nthreads=4, physics=phys)
+    got, _ = ref_runner.run_reference(case, n, dt, [1, n], nthreads=1, physics=phys,
+                                      binary=ref_runner.DROPIN_PHYS_HARNESS)
+    keys = PROG + (["tend_physics.rqvdynten"] if convection != "off" else [])
+    for step in (1, n):
+        for k in keys:
+            err = rel_linf(got[step][k], ref[step][k])
+            assert err <= 1e-10, f"step {step} {k}: rel Linf {err:.3e}"
+    assert got[n]["state.scalars.tl1"].min() >= 0.0
