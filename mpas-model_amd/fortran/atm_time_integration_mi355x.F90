@@ -215,6 +215,7 @@ module atm_time_integration
    type(c_ptr), save, private :: dyc_init = c_null_ptr   ! one block, model init
    logical, save, private :: coupled_init = .false.      ! atm_init_coupled_diagnostics was called
    logical, save, private :: host_stale = .false.        ! the host pools lag the device state
+   logical, save, private :: wait_every_step = .false.   ! MPAS_DYCORE_WAIT_EVERY_STEP=1 (diagnostics)
    integer(c_int32_t), save, private :: summary_flags = 0, physics_flags = 0
    real (kind=RKIND), save, private :: dt_init = 0.0_RKIND
 
@@ -313,6 +314,7 @@ module atm_time_integration
       end if
 #endif
       if (summary_flags /= 0) call summarize_timestep(domain)
+      if (wait_every_step) call check(dyc, mpas_dyc_synchronize(dyc), 'mpas_dyc_synchronize')
    end subroutine atm_srk3
 
    ! Copy the device state into the host pools' time level 1 (the current one once the caller
@@ -532,7 +534,7 @@ module atm_time_integration
          if (lp) summary_flags = ior(summary_flags, SUM_SCA)
       end if
       call check(dyc, mpas_dyc_set_summary(dyc, summary_flags), 'mpas_dyc_set_summary')
-      if (.not. atm_dycore_sync_every_step) call env_sync_switch()
+      call env_sync_switch()
    end subroutine create_domain_context
 
    ! The block's parinfo lists (mpas_multihalo_exchange_list, built by mpas_block_creator):
@@ -851,6 +853,8 @@ module atm_time_integration
       integer :: st
       call get_environment_variable('MPAS_DYCORE_SYNC_EVERY_STEP', v, status=st)
       if (st == 0) atm_dycore_sync_every_step = trim(v) == '1'
+      call get_environment_variable('MPAS_DYCORE_WAIT_EVERY_STEP', v, status=st)
+      if (st == 0) wait_every_step = trim(v) == '1'
    end subroutine env_sync_switch
 
    subroutine block_dims(mesh, state, d)

@@ -119,9 +119,9 @@ def test_configs2_x1_163842_L56_eight_rccl_blocks_bitwise(dry163842, dry163842_g
 
 def test_configs2_dropin_fortran_host_ms_per_dt(dry163842, dry163842_gpu):
     """The Fortran drop-in under the harness driver (mpas_atm_core.F's calls) at configs[2]: same
-    bits as the Python host, and its ms/dt -- the loop's wall time after the first step's set-up,
-    device wait included -- within 10 % of the Python host's on the same case (no per-step
-    copy-back: the state stays in HBM until atm_dycore_to_host)."""
+    bits as the Python host, and its ms/dt -- the wall time of steps 3..10, device wait included --
+    within 10 % of the Python host's on the same case (no per-step copy-back: the state stays in
+    HBM until atm_dycore_to_host)."""
     import time
     from mpas_dycore import Dycore
     from oracle import ref_runner
@@ -135,19 +135,21 @@ def test_configs2_dropin_fortran_host_ms_per_dt(dry163842, dry163842_gpu):
     for _, _, key, _ in PROG:
         a = res[n][key]
         assert np.array_equal(a, dry163842_gpu[key].reshape(a.shape)), f"{key}: drop-in differs from the Python host"
-    ms_dropin = 1e3 * (total - times[0]) / n   # step 1's host call carries the graph capture
+    # steps 3..n: the first launch of each time-level parity's graph loads its kernels
+    ms_dropin = 1e3 * total["after2"] / (n - 2)
     dy = Dycore(c, device=0)
     dy.init_diagnostics(dt)
     dy.use_graph(True)
-    dy.atm_timestep(dt, 1)
-    dy.shift_time_levels()
-    dy.synchronize()
-    t0 = time.perf_counter()
-    for it in range(1, n):
+    for it in range(2):
         dy.atm_timestep(dt, it + 1)
         dy.shift_time_levels()
     dy.synchronize()
-    ms_py = 1e3 * (time.perf_counter() - t0) / (n - 1)
+    t0 = time.perf_counter()
+    for it in range(2, n):
+        dy.atm_timestep(dt, it + 1)
+        dy.shift_time_levels()
+    dy.synchronize()
+    ms_py = 1e3 * (time.perf_counter() - t0) / (n - 2)
     dy.close()
     progress(f"drop-in {ms_dropin:.2f} ms/dt, Python host {ms_py:.2f} ms/dt (host step calls {np.round(times, 4).tolist()})")
     assert ms_dropin <= 1.10 * ms_py, f"drop-in {ms_dropin:.2f} ms/dt vs Python host {ms_py:.2f}"
