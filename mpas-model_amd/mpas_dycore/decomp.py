@@ -23,10 +23,15 @@ would.
 * **Missing neighbours.** Connectivity is remapped to block-local indices, and
   neighbours outside the block become -1, which is the garbage slot n+1 at the
   C ABI (mpas_block_creator.F:1445).
-* **Exchange lists** (mpas_dmpar_get_exch_list). For every (block,
-  location, halo layer), the halo elements are grouped by owning block. The
-  owner sends its owned copies in ascending global index, and the receiver
-  unpacks them in the same order.
+* **Exchange lists** (mpas_dmpar_get_exch_list, mpas_dmpar.F:1483-2038). For
+  every (block, location, halo layer), the halo elements are grouped by owning
+  block, and both sides list them in the same order:
+  * between blocks of different MPI tasks, in ascending global index (the
+    message buffer order of sendList / recvList);
+  * between blocks of one task, in the owner's local order (copyList,
+    :1825-1875).
+  ``tests/test_decomp_pinned.py`` checks local orders, halo layers and both list
+  kinds against the reference's own mpas_block_decomp.F / mpas_block_creator.F.
 * **Partition.** The default partition splits the cells into contiguous ranges
   of the space-filling-curve order of ``mesh.py``. A METIS
   ``graph.info.part.N`` file, as read by mpas_block_decomp.F, is accepted as
@@ -186,28 +191,45 @@ def _local_case(case: dict, glob: dict) -> dict:
     return out
 
 
-def decompose(case: dict, cell_part: np.ndarray, parts=None) -> list[Block]:
+def decompose(case: dict, cell_part: np.ndarray, parts=None, placement: dict | None = None) -> list[Block]:
     """Build the blocks of ``parts`` (default: all) with their send and receive lists.
 
+    ``placement`` maps every block to (rank, local block index), as Dycore.from_blocks takes it;
+    it decides the list order between two blocks (same rank: the owner's local order, else
+    ascending global index, see the module docstring).  Default: one block per rank.
     The element sets of every block are computed (cheap), so a rank can build
     only its own block(s) and still know what each neighbour expects from it."""
     nparts = int(cell_part.max()) + 1
     owners = element_owners(case, cell_part)
     elems = [_block_elements(case, owners, p) for p in range(nparts)]
     want = list(range(nparts)) if parts is None else list(parts)
+    rank_of = {p: (placement[p][0] if placement is not None else p) for p in range(nparts)}
     blocks = [Block(part=p, case=_local_case(case, elems[p][0]), glob=elems[p][0], layer_end=elems[p][1])
               for p in want]
+    g2own_cache = {}
+
+    def g2own(q, loc):   # global index -> owned local index in block q
+        if (q, loc) not in g2own_cache:
+            glob_q, lend_q = elems[q]
+            m = np.full(case[_N[loc]], -1, dtype=np.int64)
+            m[glob_q[loc][:lend_q[loc][0]]] = np.arange(lend_q[loc][0])
+            g2own_cache[(q, loc)] = m
+        return g2own_cache[(q, loc)]
+
+    def message_order(gids, src, dst, loc):   # order of the elements gids sent by block src to dst
+        key = g2own(src, loc)[gids] if rank_of[src] == rank_of[dst] else gids
+        return np.argsort(key, kind="stable")
+
     for b in blocks:
         for loc in LOCS:
-            n_owned = b.layer_end[loc][0]
-            g2own = np.full(case[_N[loc]], -1, dtype=np.int64)
-            g2own[b.glob[loc][:n_owned]] = np.arange(n_owned)
             for layer in range(1, NLAYERS[loc] + 1):
                 # receive: my layer-`layer` halo elements, grouped by owner
                 s, e = b.layer_range(loc, layer)
-                own = owners[loc][b.glob[loc][s:e]]
+                gl = b.glob[loc][s:e]
+                own = owners[loc][gl]
                 for q in np.unique(own):
                     sel = np.flatnonzero(own == q)
+                    sel = sel[message_order(gl[sel], int(q), b.part, loc)]
                     b.recv.append((loc, layer, int(q), (s + sel).astype(np.int32)))
                 # send: every other block's layer-`layer` halo elements that I own
                 for p in range(nparts):
@@ -217,7 +239,8 @@ def decompose(case: dict, cell_part: np.ndarray, parts=None) -> list[Block]:
                     gids = glob_p[loc][lend_p[loc][layer - 1]:lend_p[loc][layer]]
                     gids = gids[owners[loc][gids] == b.part]
                     if gids.size:
-                        b.send.append((loc, layer, p, g2own[gids].astype(np.int32)))
+                        gids = gids[message_order(gids, b.part, p, loc)]
+                        b.send.append((loc, layer, p, g2own(b.part, loc)[gids].astype(np.int32)))
     return blocks
 
 
@@ -254,6 +277,6 @@ def rank_blocks(case: dict, nranks: int, rank: int, blocks_per_rank: int = 1, ce
     if cell_part is None:
         cell_part = partition_sfc(case["nCells"], nparts)
     mine = list(range(rank * blocks_per_rank, (rank + 1) * blocks_per_rank))
-    blocks = decompose(case, cell_part, parts=mine)
     placement = {p: (p // blocks_per_rank, p % blocks_per_rank) for p in range(nparts)}
+    blocks = decompose(case, cell_part, parts=mine, placement=placement)
     return blocks, placement

@@ -361,3 +361,59 @@ def run_reference_kernel(case: dict, restore_dir: str, mode: str, dts: float = 0
         return read_dump(case, os.path.join(outd, "step_0000"))
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+# ---- the reference's domain decomposition (harness/decomp_harness.F90, make -C oracle decomp) ----
+DECOMP_HARNESS = os.path.join(HERE, "_ref", "decomp_harness")
+MPIRUN = "/opt/conda/bin/mpirun"
+
+
+def run_reference_decomp(case: dict, part, nprocs: int = 1, timeout: int = 600) -> dict:
+    """mpas_block_decomp.F + mpas_block_creator.F on the case's mesh and cell partition ``part``
+    (0-based block per cell, written as graph.info.part.N).  With ``nprocs`` > 1 the harness runs
+    under mpirun, one task per block.  Returns {block id: {"<loc>_index": global 0-based ids in
+    local order, "<loc>_solve": end of owned and of each halo layer, "<loc>_<kind>_<layer>": list of
+    (endPointID, srcList, destList) with MPAS's 1-based local indices / buffer positions}}."""
+    import shutil
+    part = np.asarray(part, dtype=np.int64)
+    nblocks = int(part.max()) + 1
+    tmp = tempfile.mkdtemp(prefix="mpasdec_")
+    try:
+        ind, outd = os.path.join(tmp, "in"), os.path.join(tmp, "out")
+        os.makedirs(ind)
+        for name in ("nEdgesOnCell", "cellsOnCell", "edgesOnCell", "verticesOnCell", "cellsOnEdge", "cellsOnVertex"):
+            a = np.asarray(case[name], dtype=np.int64)
+            (a + (0 if name == "nEdgesOnCell" else 1)).astype(np.int32).tofile(os.path.join(ind, f"{name}.bin"))
+        with open(os.path.join(ind, f"graph.info.part.{nblocks}"), "w") as f:
+            f.write("\n".join(str(int(x)) for x in part) + "\n")
+        with open(os.path.join(ind, "decomp.nml"), "w") as f:
+            f.write(f"&decomp\n nCells={case['nCells']}, nEdges={case['nEdges']}, nVertices={case['nVertices']},\n"
+                    f" maxEdges={case['maxEdges']}, nblocks={nblocks}, nHalos=2\n/\n")
+        cmd = [DECOMP_HARNESS, ind, outd]
+        if nprocs > 1:
+            cmd = [MPIRUN, "-np", str(nprocs)] + cmd
+        r = subprocess.run(cmd, cwd=tmp, capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0:
+            raise RuntimeError(f"decomp_harness failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
+        out = {}
+        for bdir in sorted(os.listdir(outd)):
+            b = int(bdir[len("block"):])
+            res = {}
+            for fn in sorted(os.listdir(os.path.join(outd, bdir))):
+                a = np.fromfile(os.path.join(outd, bdir, fn), dtype=np.int32)
+                key = fn[:-4]
+                if key.endswith("_index"):
+                    res[key] = a.astype(np.int64) - 1
+                elif key.endswith("_solve"):
+                    res[key] = a.astype(np.int64)
+                else:
+                    nodes, i = [], 0
+                    while i < a.size:
+                        ep, n = int(a[i]), int(a[i + 1])
+                        nodes.append((ep, a[i + 2:i + 2 + n].astype(np.int64), a[i + 2 + n:i + 2 + 2 * n].astype(np.int64)))
+                        i += 2 + 2 * n
+                    res[key] = nodes
+            out[b] = res
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
