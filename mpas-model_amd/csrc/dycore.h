@@ -99,4 +99,14 @@ struct Ptrs {
 };
 constexpr int CELL_REC = 16, CELL_REC_ME = 7;
 
+// Halo pack fused into a producer (the acoustic cell phase, k_acoustic_cells_r): owned cell c of the
+// block writes its new rtheta_pp (and rho_pp) column also to rt[s] (rho[s]) for s in
+// [start[c], start[c+1]) -- its slots in the RCCL send buffer of the per-sub-step exchange
+// (mpas_atm_time_integration.F:845, 792).  start == nullptr: nothing to pack.
+struct PackMap {
+  const int* start;      // nCellsSolve + 1 offsets
+  double* const* rt;     // send-buffer column of rtheta_pp per slot
+  double* const* rho;    // send-buffer column of rho_pp per slot, or nullptr
+};
+
 }  // namespace mpas

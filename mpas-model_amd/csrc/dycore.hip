@@ -45,6 +45,7 @@ struct XList {
   int loc, layer, dir, peer_rank, peer_block;
   int n = 0;
   int* d_idx = nullptr;  // 0-based local element indices, message order
+  std::vector<int32_t> h_idx;  // the same on the host (fused-pack maps)
 };
 
 // A block: MPAS block_type -- dims, fields and exchange lists of one patch.
@@ -78,6 +79,11 @@ struct XPlan {
   double* recvbuf = nullptr;
   std::vector<XMsg> rsend, rrecv;  // in matching order
   bool warmed = false;              // its RCCL group has run once outside graph capture (warm_rccl)
+  // fused pack (the per-sub-step rtheta_pp [+ rho_pp] exchange with RCCL peers only): the
+  // acoustic cell phase writes the send buffer itself, so exchange() launches no pack kernel
+  bool fused_pack = false;
+  std::vector<PackMap> pack;        // per block
+  std::vector<void*> pack_mem;      // device allocations behind `pack`
 };
 
 // One field of an exchange point: mpas_dmpar_exch_halo_field(field[, haloLayers]).
@@ -109,6 +115,7 @@ struct mpas_dyc_ctx {
   int rank = 0, nranks = 1;
   ncclComm_t comm = nullptr;
   bool rccl_local = false;              // route block-to-block copies of this process through RCCL too
+  bool fused_pack_enabled = true;       // MPAS_DYCORE_FUSED_PACK=0: pack kernel instead (A/B)
   bool planning = false;                // dry run: build exchange plans, launch nothing
   bool planned[2] = {false, false};
   std::map<std::string, XPlan> plans;
@@ -404,6 +411,7 @@ const XList* find_list(const Block& b, int loc, int layer, int dir, int peer_ran
 void free_plan(XPlan& pl) {
   for (void* p : {(void*)pl.d_pre, (void*)pl.d_post, (void*)pl.sendbuf, (void*)pl.recvbuf})
     if (p) (void)hipFree(p);
+  for (void* p : pl.pack_mem) (void)hipFree(p);
   pl = XPlan{};
 }
 
@@ -430,6 +438,8 @@ std::vector<std::pair<int, int>> peers_of(const Block& b, int dir) {
   return peers;
 }
 
+inline bool batched(const Dims& d);
+
 // Message layout: per block, peers in (rank, block) order; per peer, the fields in call
 // order and per field the halo layers in ascending order (both sides agree on it).
 int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
@@ -437,6 +447,13 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   std::vector<XSeg> pre, post;
   std::vector<int64_t> pre_off, post_off;  // buffer offsets, patched once the buffers exist (-1: direct)
   int64_t stotal = 0, rtotal = 0;
+  // the fused pack applies to the per-sub-step exchange (diag rtheta_pp [+ rho_pp], halo layer 1)
+  bool fusable = !fs.empty() && fs.size() <= 2;
+  for (const auto& f : fs)
+    fusable = fusable && std::string(f.pool) == "diag" && f.layers == 0x1u &&
+              (std::string(f.name) == "rtheta_pp" || std::string(f.name) == "rho_pp");
+  struct PackSeg { int block, is_rho; const XList* sx; size_t seg; };
+  std::vector<PackSeg> pack_segs;
   auto field_of = [&](Block& b, const XField& f) -> Field* {
     Field* F = find(b, f.pool, f.name);
     if (!F || F->is_int || F->loc == L_NONE) {
@@ -485,10 +502,12 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
               sg.dst = (double*)PF->buf[slot_of(ctx, *PF, f.tl)] + (size_t)is * nloc(ctx->blk[pr.second], PF->loc) * sub_inner;
               sg.didx = rx->d_idx;
               pre_off.push_back(-1);
+              fusable = false;  // a direct copy would reach the peer's halo before its cell phase reads it
             } else {
               sg.didx = nullptr;
               pre_off.push_back(stotal);
               stotal += (int64_t)sx->n * sub_inner;
+              if (fusable) pack_segs.push_back(PackSeg{bi, std::string(f.name) == "rho_pp" ? 1 : 0, sx, pre.size()});
             }
             pre.push_back(sg);
           }
@@ -556,6 +575,56 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   for (size_t i = 0; i < post.size(); ++i) post[i].src = pl.recvbuf + post_off[i];
   pl.npre = (int)pre.size();
   pl.npost = (int)post.size();
+  if (fusable && !pack_segs.empty()) {
+    for (int bi = 0; bi < nb; ++bi) fusable = fusable && batched(ctx->blk[bi].d);
+  }
+  if (fusable && !pack_segs.empty()) {
+    // per block: CSR over owned cells of (rtheta_pp slot, rho_pp slot) pairs; a cell has one
+    // slot per RCCL peer that needs it (element i of a peer's list in both fields' segments)
+    const bool with_rho = fs.size() == 2;
+    pl.pack.assign(nb, PackMap{});
+    for (int bi = 0; bi < nb; ++bi) {
+      const Dims& d = ctx->blk[bi].d;
+      std::map<std::pair<const XList*, int>, std::pair<double*, double*>> slot;  // (list, i) -> (rt, rho)
+      for (const PackSeg& ps : pack_segs) {
+        if (ps.block != bi) continue;
+        for (int i = 0; i < ps.sx->n; ++i) {
+          double* col = pre[ps.seg].dst + (size_t)i * pre[ps.seg].inner;
+          auto& e = slot[{ps.sx, i}];
+          (ps.is_rho ? e.second : e.first) = col;
+        }
+      }
+      std::vector<std::vector<std::pair<double*, double*>>> per_cell(d.nCellsSolve);
+      for (const auto& kv : slot) per_cell[kv.first.first->h_idx[kv.first.second]].push_back(kv.second);
+      std::vector<int> start(d.nCellsSolve + 1, 0);
+      std::vector<double*> rt, rho;
+      for (int c = 0; c < d.nCellsSolve; ++c) {
+        start[c] = (int)rt.size();
+        for (const auto& e : per_cell[c]) {
+          rt.push_back(e.first);
+          rho.push_back(e.second);
+        }
+      }
+      start[d.nCellsSolve] = (int)rt.size();
+      if (rt.empty()) continue;
+      int* d_start = nullptr;
+      double** d_rt = nullptr;
+      double** d_rho = nullptr;
+      HIPCHK(hipMalloc(&d_start, start.size() * sizeof(int)));
+      HIPCHK(hipMemcpy(d_start, start.data(), start.size() * sizeof(int), hipMemcpyHostToDevice));
+      HIPCHK(hipMalloc(&d_rt, rt.size() * sizeof(double*)));
+      HIPCHK(hipMemcpy(d_rt, rt.data(), rt.size() * sizeof(double*), hipMemcpyHostToDevice));
+      pl.pack_mem.push_back(d_start);
+      pl.pack_mem.push_back(d_rt);
+      if (with_rho) {
+        HIPCHK(hipMalloc(&d_rho, rho.size() * sizeof(double*)));
+        HIPCHK(hipMemcpy(d_rho, rho.data(), rho.size() * sizeof(double*), hipMemcpyHostToDevice));
+        pl.pack_mem.push_back(d_rho);
+      }
+      pl.pack[bi] = PackMap{d_start, d_rt, d_rho};
+    }
+    pl.fused_pack = ctx->fused_pack_enabled;
+  }
   if (pl.npre) {
     HIPCHK(hipMalloc(&pl.d_pre, pre.size() * sizeof(XSeg)));
     HIPCHK(hipMemcpy(pl.d_pre, pre.data(), pre.size() * sizeof(XSeg), hipMemcpyHostToDevice));
@@ -589,7 +658,7 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   }
   if (ctx->planning) return MPAS_DYC_OK;
   XPlan& pl = it->second;
-  if (pl.npre)
+  if (pl.npre && !pl.fused_pack)
     hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_pre + 3) / 4, pl.npre), dim3(256), 0, ctx->stream, pl.d_pre);
   if (!pl.rsend.empty() || !pl.rrecv.empty()) {
     NCCLCHK(ncclGroupStart());
@@ -602,6 +671,14 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   if (pl.npost)
     hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_post + 3) / 4, pl.npost), dim3(256), 0, ctx->stream, pl.d_post);
   return MPAS_DYC_OK;
+}
+
+// The plan of an exchange whose pack the producing kernel does (XPlan::fused_pack), or nullptr
+const XPlan* fused_pack_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
+  if (ctx->planning || !needs_exchange(ctx)) return nullptr;
+  auto it = ctx->plans.find(plan_key(ctx, fs));
+  if (it == ctx->plans.end() || !it->second.fused_pack || it->second.pack.size() != ctx->blk.size()) return nullptr;
+  return &it->second;
 }
 
 // Kernel families: 0 "general" (one column per wave, loads where used -- any mesh), 1 "batched"
@@ -846,18 +923,21 @@ bool fused_recover(const Dims& d) { return batched(d) && (d.maxEdges == 6 || d.m
 // fin = 1: the stage's last sub-step, which also recovers the owned cells (k_acoustic_cells_r<ME,
 // true>) when fused_recover(d); rdt / invNs / rk_step are k_recover_cells1's arguments
 // keep_pp = 0: a fin launch need not store rho_pp / rw_p (see k_acoustic_cells_r)
+// pk: the block's fused-pack map of the exchange that follows (fused_pack_map), or none
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int fin = 0,
-                    double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1) {
+                    double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1, PackMap pk = PackMap{}) {
   if (batched(d) && d.maxEdges == 6) {
     if (fin)
-      LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp);
-    else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1);
+      LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
+             pk);
+    else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, pk);
     return;
   }
   if (batched(d) && d.maxEdges == 7) {
     if (fin)
-      LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp);
-    else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1);
+      LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
+             pk);
+    else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, pk);
     return;
   }
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
@@ -1164,10 +1244,12 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         } else {
           EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2));
         }
-        EACH(acoustic_cells(ctx, d, p, dts, small_step, small_step == nsub, rk_timestep[rk_step - 1],
-                            1 / (double)nsub, rk_step, needs_exchange(ctx) || last_stage));
         std::vector<XField> xf = {{"diag", "rtheta_pp", 0, 0x1u}};  // 845
         if (small_step < nsub) xf.push_back({"diag", "rho_pp", 0, 0x1u});  // 792 of the next sub-step
+        const XPlan* xp = fused_pack_plan(ctx, xf);  // the cell phase packs this exchange's send buffer
+        EACH(acoustic_cells(ctx, d, p, dts, small_step, small_step == nsub, rk_timestep[rk_step - 1],
+                            1 / (double)nsub, rk_step, needs_exchange(ctx) || last_stage,
+                            xp ? xp->pack[ib_] : PackMap{}));
         if (split) {
           CHK(exchange_async(ctx, xf));
         } else {
@@ -1487,6 +1569,7 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   } else {
     g_kernel_tier = 2;
   }
+  if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
   for (auto& b : ctx->blk) {
     build_registry(b);
     for (auto& f : b.fields) {
@@ -1762,6 +1845,7 @@ int mpas_dyc_set_exchange_list(mpas_dyc_ctx* ctx, int32_t block, int32_t locatio
     x->d_idx = nullptr;
   }
   x->n = n;
+  x->h_idx = idx;
   if (n > 0 && !ctx->host_only) {
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipMalloc(&x->d_idx, n * sizeof(int32_t)));

@@ -2386,11 +2386,21 @@ __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p,
 // keep_pp = 0 (FIN only): rho_pp and rw_p are not stored.  After a stage's last sub-step nothing
 // reads them but the 876-887 exchange and the halo-cell recovery; srk3 passes 0 only for a block
 // without exchanges and a stage that is not the dt's last (whose values the pool keeps).
+// the column's new rtheta_pp / rho_pp into its send-buffer slots (PackMap), lane k = level k
+__device__ __forceinline__ void pack_column(const PackMap& pk, int c, int k, bool act, double rt, double rho) {
+  if (!pk.start) return;
+  const int s0 = __builtin_amdgcn_readfirstlane(pk.start[c]), s1 = __builtin_amdgcn_readfirstlane(pk.start[c + 1]);
+  for (int s = s0; s < s1; ++s) {
+    if (act) pk.rt[s][k] = rt;
+    if (act && pk.rho) pk.rho[s][k] = rho;
+  }
+}
+
 template <int ME, bool FIN = false>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs p, double dts, int small_step,
                                                                     double epssm, double rdt = 0.0,
                                                                     double invNs = 0.0, int rk_step = 0,
-                                                                    int keep_pp = 1) {
+                                                                    int keep_pp = 1, PackMap pk = PackMap{}) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
   const int k = lane_id(), K = d.K;
@@ -2488,6 +2498,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       if (!FIN) p.wwAvg[ow] = wwa;
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;  // levels 2..K: recover_cell_fused
     }
+    pack_column(pk, c, k, act, rt_new, rho_new);
     if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rho_new, rt_new, rwp, wwa, rdt, invNs, rk_step);
   } else {
     // specified zone (2710-2719): regional only, masks are 0 for global meshes
@@ -2505,6 +2516,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       if (!FIN) p.wwAvg[ow] = wwa;
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;
     }
+    pack_column(pk, c, k, act, rtpp, rhopp);
     if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rhopp, rtpp, rwp, wwa, rdt, invNs, rk_step);
   }
 }

@@ -112,3 +112,26 @@ def test_rccl_transport_matches_device_copies(small_case):
     b = _blocks(small_case, 2, 2, graph=True, rccl_local=True)
     for name in a:
         assert np.array_equal(a[name], b[name]), name
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_fused_pack_bitwise(small_case, overlap):
+    """The per-sub-step rtheta_pp / rho_pp exchange packed by the acoustic cell phase itself (the
+    PackMap epilogue of k_acoustic_cells_r, no pack kernel) gives the bits of the separate pack
+    kernel (MPAS_DYCORE_FUSED_PACK=0) and of one block; 4 RCCL blocks, graph replay."""
+    import os
+    one = _single(small_case, 3)
+    runs = []
+    for fused in ("1", "0"):
+        old = os.environ.get("MPAS_DYCORE_FUSED_PACK")
+        os.environ["MPAS_DYCORE_FUSED_PACK"] = fused
+        try:
+            runs.append(_blocks(small_case, 4, 3, graph=True, rccl_local=True, overlap=overlap))
+        finally:
+            if old is None:
+                os.environ.pop("MPAS_DYCORE_FUSED_PACK", None)
+            else:
+                os.environ["MPAS_DYCORE_FUSED_PACK"] = old
+    for name in one:
+        assert np.array_equal(runs[0][name], runs[1][name]), f"{name}: fused pack differs from the pack kernel"
+        assert np.array_equal(runs[0][name], one[name]), f"{name}: fused-pack blocks differ from one block"
