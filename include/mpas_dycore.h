@@ -114,6 +114,17 @@ int mpas_dyc_synchronize(mpas_dyc_ctx* ctx);
 #define MPAS_DYC_PHYSICS_TENDENCIES 1
 #define MPAS_DYC_PHYSICS_RQVDYNTEN 2
 int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags);
+/* Regional lateral boundary conditions, config_apply_lbcs (mpas_atm_time_integration.F:683-778,
+ * 934-987, 1109-1180, 1253-1270, 1491-1560, 1672-1790; the routines at 6088-6671).  apply = 1 turns
+ * them on (the pair kernel layout is required).  The host sets, as in the reference's lbc pool
+ * (mpas_atm_boundaries.F): lbc.lbc_u / lbc_ru (K, nEdges+1), lbc.lbc_rho_zz / lbc_rtheta_m
+ * (K, nCells+1) and lbc.lbc_scalars (ns, K, nCells+1), each with time level 1 = the tendency over
+ * the current LBC interval and time level 2 = the interval-end state; the mesh's bdyMaskCell,
+ * bdyMaskEdge, nearestRelaxationCell, meshScalingRegionalCell / Edge; and, before every step,
+ * seconds_to_interval_end = LBC interval end - the step's start time.  A driving value delta
+ * seconds into the step is then state - (seconds_to_interval_end - delta) * tendency, as
+ * mpas_atm_get_bdy_state (:337-409) computes it.  All scalars are driven. */
+int mpas_dyc_set_lbc(mpas_dyc_ctx* ctx, int32_t apply, double seconds_to_interval_end);
 /* atm_compute_output_diagnostics(state, time_level, diag, mesh) (mpas_atm_core.F:753, called
  * before history writes at :544 and :694): diag theta, rho and pressure from theta_m, rho_zz,
  * scalars(index_qv) of the time level, zz, pressure_base and pressure_p.  Asynchronous. */

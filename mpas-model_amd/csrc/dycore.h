@@ -24,6 +24,9 @@ constexpr double RVORD = RV / RGAS;
 constexpr double PRANDTL = 1.0;
 constexpr double P0 = 1.0e5;   // mpas_atm_time_integration.F:2985, 5907
 constexpr double SECONDS_PER_DAY = 86400.0;
+// regional boundary zones (core_atmosphere/dynamics/mpas_atm_boundaries.F:10-12): bdyMask 1..5
+// relaxation, > 5 specified
+constexpr int N_SPEC_ZONE = 2, N_RELAX_ZONE = 5;
 
 struct Dims {
   int nCells, nEdges, nVertices, K, maxEdges, maxEdges2, ns;
@@ -31,6 +34,7 @@ struct Dims {
   int moist_start, moist_end;  // 0-based inclusive range of moist scalars
   int diabatic;                // rt_diabatic_tend holds nonzero data (else it is read as 0)
   int physics;                 // DO_PHYSICS coupling: tend_*_physics and scalars_tend come from the host
+  int lbc;                     // config_apply_lbcs: regional lateral boundary conditions (lbc.hip)
 };
 
 struct Config {
@@ -96,6 +100,15 @@ struct Ptrs {
   // one scalar load.
   const int* cell_rec;
   const double* cell_sdv;
+  // ---- regional LBCs (lbc.hip): zone masks, relaxation scaling, the driving data of the lbc pool
+  // (_t = tendency, lbc_<field> time level 1; _s = interval-end state, time level 2), the seconds
+  // from the step start to the interval end, and the scalar filter's scratch
+  const int *bdyMaskCell, *bdyMaskEdge, *nearestRelaxationCell;
+  const double *meshScalingRegionalCell, *meshScalingRegionalEdge;
+  const double *lbc_u_t, *lbc_u_s, *lbc_ru_t, *lbc_ru_s, *lbc_rho_zz_t, *lbc_rho_zz_s;
+  const double *lbc_rtheta_m_t, *lbc_rtheta_m_s, *lbc_scalars_t, *lbc_scalars_s;
+  const double* lbc_dtr;
+  double* lbc_tmp;
 };
 constexpr int CELL_REC = 16, CELL_REC_ME = 7;
 

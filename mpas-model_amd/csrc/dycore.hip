@@ -19,6 +19,7 @@
 #include "kernels.hip"
 #include "halo.hip"
 #include "summary.hip"
+#include "lbc.hip"
 
 using namespace mpas;
 
@@ -116,6 +117,7 @@ struct mpas_dyc_ctx {
   ncclComm_t comm = nullptr;
   bool rccl_local = false;              // route block-to-block copies of this process through RCCL too
   bool fused_pack_enabled = true;       // MPAS_DYCORE_FUSED_PACK=0: pack kernel instead (A/B)
+  bool lbc = false;                     // config_apply_lbcs (mpas_dyc_set_lbc)
   bool planning = false;                // dry run: build exchange plans, launch nothing
   bool planned[2] = {false, false};
   std::map<std::string, XPlan> plans;
@@ -211,6 +213,12 @@ void build_registry(Block& c) {
                         "meshScalingDel4", "specZoneMaskEdge", "angleEdge", "latEdge", "lonEdge"})
     add(c, "mesh", n, L_EDGE, 1);
   for (const char* n : {"invAreaCell", "specZoneMaskCell", "latCell", "lonCell"}) add(c, "mesh", n, L_CELL, 1);
+  // regional LBCs (lbc.hip): zone masks, nearest relaxation cell, relaxation-zone mesh scaling
+  add(c, "mesh", "bdyMaskCell", L_CELL, 1, 1, true);
+  add(c, "mesh", "bdyMaskEdge", L_EDGE, 1, 1, true);
+  add(c, "mesh", "nearestRelaxationCell", L_CELL, 1, 1, true, T_CELL);
+  add(c, "mesh", "meshScalingRegionalCell", L_CELL, 1);
+  add(c, "mesh", "meshScalingRegionalEdge", L_EDGE, 1);
   add(c, "mesh", "coeffs_reconstruct", L_CELL, 3 * (int64_t)ME);
   for (const char* n : {"invAreaTriangle", "fVertex"}) add(c, "mesh", n, L_VERTEX, 1);
   for (const char* n : {"fzm", "fzp", "rdzw", "rdzu", "u_init", "v_init"}) add(c, "mesh", n, L_NONE, K);
@@ -266,6 +274,14 @@ void build_registry(Block& c) {
   add(c, "tend", "scalars_tend", L_CELL, (int64_t)ns * K);
   c.fields.back().nsub = ns;
   add(c, "tend_physics", "rthdynten", L_CELL, K);
+  // the lbc pool (mpas_atm_boundaries.F): time level 1 = tendency over the LBC interval, 2 = the
+  // interval-end state; "dtr" = seconds from the step start to the interval end
+  for (const char* n : {"lbc_u", "lbc_ru"}) add(c, "lbc", n, L_EDGE, K, 2);
+  for (const char* n : {"lbc_rho_zz", "lbc_rtheta_m"}) add(c, "lbc", n, L_CELL, K, 2);
+  add(c, "lbc", "lbc_scalars", L_CELL, (int64_t)ns * K, 2);
+  c.fields.back().nsub = ns;
+  add(c, "lbc", "dtr", L_NONE, 1);
+  add(c, "scratch", "lbc_tmp", L_CELL, (int64_t)ns * K);
   // module scratch (mpas_atm_time_integration.F:35-71)
   // the physics tendencies of physics_get_tend (module scratch of the reference, 268-279), set by
   // the host when physics coupling is on (mpas_dyc_set_physics)
@@ -298,7 +314,11 @@ Field* find(Block& b, const char* pool, const char* name) {
   return &b.fields[it->second];
 }
 
-int slot_of(const mpas_dyc_ctx* c, const Field& f, int tl) { return (f.ntl == 2) ? ((tl == 2) ? 1 - c->cur : c->cur) : 0; }
+// state fields swap time levels every step; the lbc pool's two levels are fixed (tendency, state)
+int slot_of(const mpas_dyc_ctx* c, const Field& f, int tl) {
+  if (f.ntl == 2 && f.pool == "lbc") return tl == 2 ? 1 : 0;
+  return (f.ntl == 2) ? ((tl == 2) ? 1 - c->cur : c->cur) : 0;
+}
 
 template <class T>
 T* P(mpas_dyc_ctx* c, Block& b, const char* pool, const char* name, int tl = 1) {
@@ -362,6 +382,18 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   p.cell_sdv = P<const double>(c, b, "scratch", "cell_sdv");
   p.zb_p = P<const double>(c, b, "scratch", "zb_p");
   p.zb_m = P<const double>(c, b, "scratch", "zb_m");
+  MI(bdyMaskCell); MI(bdyMaskEdge); MI(nearestRelaxationCell);
+  MR(meshScalingRegionalCell); MR(meshScalingRegionalEdge);
+  p.lbc_u_t = P<const double>(c, b, "lbc", "lbc_u", 1); p.lbc_u_s = P<const double>(c, b, "lbc", "lbc_u", 2);
+  p.lbc_ru_t = P<const double>(c, b, "lbc", "lbc_ru", 1); p.lbc_ru_s = P<const double>(c, b, "lbc", "lbc_ru", 2);
+  p.lbc_rho_zz_t = P<const double>(c, b, "lbc", "lbc_rho_zz", 1);
+  p.lbc_rho_zz_s = P<const double>(c, b, "lbc", "lbc_rho_zz", 2);
+  p.lbc_rtheta_m_t = P<const double>(c, b, "lbc", "lbc_rtheta_m", 1);
+  p.lbc_rtheta_m_s = P<const double>(c, b, "lbc", "lbc_rtheta_m", 2);
+  p.lbc_scalars_t = P<const double>(c, b, "lbc", "lbc_scalars", 1);
+  p.lbc_scalars_s = P<const double>(c, b, "lbc", "lbc_scalars", 2);
+  p.lbc_dtr = P<const double>(c, b, "lbc", "dtr");
+  SC(lbc_tmp);
   // 0-d mesh fields are mirrored on the host
   p.cf1 = b.fields[b.by_name["mesh.cf1"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf1"]].buf[1] : 0.0;
   p.cf2 = b.fields[b.by_name["mesh.cf2"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf2"]].buf[1] : 0.0;
@@ -1138,6 +1170,15 @@ int summary_launch(mpas_dyc_ctx* ctx, int tl) {
   }
 
 // atm_srk3 (mpas_atm_time_integration.F:142-1796)
+// atm_bdy_adjust_scalars (6436-6586) at the end of a transport stage: the scalars' halo first
+// (the filter reads the neighbours), then the relaxation / specified-zone update of owned cells
+int lbc_scalars(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt, double dt_rk) {
+  CHK(exchange(ctx, {{"state", "scalars", 2, ALL_LAYERS}}));
+  EACH(LAUNCH(k_lbc_scalars_tmp, d.nCellsSolve, d, p, dt, dt_rk, dt_rk));
+  EACH(LAUNCH(k_lbc_scalars_copy, d.nCellsSolve, d, p));
+  return MPAS_DYC_OK;
+}
+
 int srk3(mpas_dyc_ctx* ctx, double dt) {
   const Config& cf = ctx->cf;
   const std::vector<Ptrs> P = block_ptrs(ctx);
@@ -1175,6 +1216,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   }
   const bool scalars_in_dynamics = cf.scalar_advection && !cf.split_dynamics_transport;
   const bool split = split_phase(ctx);
+  const bool lbc = ctx->lbc;  // config_apply_lbcs: regional boundary updates at the reference's points
   // 329-338, plus the exner exchange of the first dynamics substep (513): nothing writes exner
   // in between (vert_imp_coefs reads it on owned cells only), so the halo values are the same
   CHK(exchange(ctx, {{"state", "theta_m", 1, ALL_LAYERS}, {"state", "scalars", 1, ALL_LAYERS},
@@ -1205,7 +1247,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         pending = false;
         EACH(dyn_tend(ctx, d, p, rk_step, dt, 2, false, last_stage));
       } else {
-        EACH(dyn_tend(ctx, d, p, rk_step, dt, 0, !split && batched(d), last_stage));  // 561-630
+        EACH(dyn_tend(ctx, d, p, rk_step, dt, 0, !split && batched(d) && !lbc, last_stage));  // 561-630
       }
       const double dts = rk_sub_timestep[rk_step - 1];
       if (split) {  // 642 | 644-678: interior cells overlap the tend_u exchange
@@ -1216,6 +1258,13 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       } else {
         CHK(exchange(ctx, {{"tend", "u", 0, 0x1u}}));             // 642
         EACH(smlstep_pert(ctx, d, p, 0));     // 644-678
+      }
+      if (lbc) {  // 683-778: specified-zone tendencies, then the relaxation zone toward the driving state
+        const double tds = dt_dynamics * (double)(dynamics_substep - 1) + rk_timestep[rk_step - 1];
+        EACH(LAUNCH(k_lbc_spec_tend_cells, d.nCellsSolve, d, p));
+        EACH(LAUNCH(k_lbc_spec_tend_edges, d.nEdgesSolve, d, p));
+        EACH(LAUNCH(k_lbc_relax_cells, d.nCellsSolve, d, p, dt, tds));
+        EACH(LAUNCH(k_lbc_relax_edges, d.nEdges, d, p, dt, tds));
       }
       // Acoustic sub-steps (788-870).
       // * Exchanges.  The reference exchanges rho_pp before every sub-step (792) and rtheta_pp
@@ -1279,9 +1328,15 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2, d.nCellsSolve));
         EACH(if (!fused_recover_edges(d) || ctx->blk[ib_].n_bnd_edges != 0)
                LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
-        CHK(exchange_async(ctx, {{"state", "u", 2, ALL_LAYERS}}));
-        EACH(recover_cells3(ctx, d, p, 0));
-        CHK(exchange_wait(ctx));
+        if (lbc) {  // the w recovery reads ru before the specified-zone overwrite (934-987)
+          EACH(recover_cells3(ctx, d, p, 0));
+          EACH(LAUNCH(k_lbc_u, d.nEdges, d, p, dt_dynamics * (double)(dynamics_substep - 1) + rk_timestep[rk_step - 1]));
+          CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));  // 988
+        } else {
+          CHK(exchange_async(ctx, {{"state", "u", 2, ALL_LAYERS}}));
+          EACH(recover_cells3(ctx, d, p, 0));
+          CHK(exchange_wait(ctx));
+        }
       } else {
         CHK((exchange)(ctx, xrec));
         // 889-930: the owned cells were recovered by the last sub-step if fused_recover
@@ -1292,7 +1347,9 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0);
              else if (ctx->blk[ib_].n_bnd_edges != 0) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
         // stages 1 and 2: also the next stage's h_divergence (dyn_tend then skips k_dyn_cells1)
-        EACH(recover_cells3(ctx, d, p, 0, rk_step < 3));
+        EACH(recover_cells3(ctx, d, p, 0, rk_step < 3 && !lbc));
+        if (lbc)  // 934-987
+          EACH(LAUNCH(k_lbc_u, d.nEdges, d, p, dt_dynamics * (double)(dynamics_substep - 1) + rk_timestep[rk_step - 1]));
         CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));      // 988
       }
       if (scalars_in_dynamics) {                                  // 993-1185
@@ -1301,13 +1358,25 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         } else {
           CHK(advance_scalars_mono(ctx, P, rk_timestep[rk_step - 1], false));
         }
+        if (lbc) CHK(lbc_scalars(ctx, P, dt, rk_timestep[rk_step - 1]));  // 1109-1180
       }
       EACH(solve_diagnostics(ctx, d, p, dt, 2, rk_step,             // 1187-1228
                              dynamics_substep == dynamics_split && rk_step == 3));
       std::vector<XField> xd = {{"state", "w", 2, ALL_LAYERS}, {"diag", "pv_edge", 0, ALL_LAYERS},  // 1234-1249
                                 {"diag", "rho_edge", 0, ALL_LAYERS}};
       if (scalars_in_dynamics) xd.push_back({"state", "scalars", 2, ALL_LAYERS});
-      if (rk_step < 3) {
+      if (lbc) {
+        // regional: 1234-1249, the zero-gradient w of the specified zone and its exchange (1253-1270),
+        // then (end of a dynamics substep) 1282-1297 -- blocking, in the reference's order
+        CHK((exchange)(ctx, xd));
+        EACH(LAUNCH(k_lbc_zero_grad_w, d.nCellsSolve, d, p));
+        CHK((exchange)(ctx, {{"state", "w", 2, ALL_LAYERS}}));
+        if (rk_step == 3 && dynamics_substep < dynamics_split) {
+          CHK((exchange)(ctx, {{"state", "theta_m", 2, ALL_LAYERS}, {"diag", "pressure_p", 0, ALL_LAYERS},
+                               {"diag", "rtheta_p", 0, ALL_LAYERS}, {"diag", "exner", 0, ALL_LAYERS}}));
+          EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));     // 476-510 of the next substep
+        }
+      } else if (rk_step < 3) {
         CHK(xchg(xd));  // waited for inside the next stage's dyn_tend
         pending = true;
       } else if (dynamics_substep < dynamics_split) {
@@ -1348,6 +1417,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       } else {
         CHK(advance_scalars_mono(ctx, P, rk_ts[rk_step - 1], true, true));
       }
+      if (lbc) CHK(lbc_scalars(ctx, P, dt, rk_ts[rk_step - 1]));  // 1491-1560
       if (rk_step == 2 && mono3) {
         // the rk3 limiter's preparation (3737-3777) reads scalars(tl1), scalars_tend, rho_zz(tl1),
         // ruAvg and wwAvg, none of which this exchange touches, and writes none of the scalars(tl2)
@@ -1371,6 +1441,11 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         hipLaunchKernelGGL(k_physics_clip_scalars, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)),
                            dim3(256), 0, ctx->stream, ::P<double>(ctx, b, "state", "scalars", 2), n);
     }
+  }
+  if (lbc) {
+    EACH(LAUNCH(k_lbc_reset_spec, d.nCellsSolve, d, p, dt));       // 1672-1711, at the end of the step
+    CHK(exchange(ctx, {{"state", "scalars", 2, ALL_LAYERS}}));       // 1714-1790
+    EACH(LAUNCH(k_lbc_set_scalars, d.nCellsSolve, d, p, dt));
   }
   // summarize_timestep (1794): the reductions on the device, the log lines on the host
   CHK(summary_launch(ctx, 2));
@@ -2037,6 +2112,30 @@ int mpas_dyc_solve_diagnostics(mpas_dyc_ctx* ctx, double dt) {
   int r = init_diagnostics(ctx, dt, false);
   HIPCHK(hipGetLastError());
   return r;
+}
+
+int mpas_dyc_set_lbc(mpas_dyc_ctx* ctx, int32_t apply, double seconds_to_interval_end) {
+  if (!ctx || (apply != 0 && apply != 1)) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (apply) {
+    for (auto& b : ctx->blk)
+      if (!pair_layout(b.d)) {
+        ctx->err = "regional LBCs need the pair kernel layout (maxEdges <= 7, even nVertLevels <= 64)";
+        return MPAS_DYC_EINVAL;
+      }
+  }
+  if ((apply != 0) != ctx->lbc) {  // other exchange points and kernels: re-plan, re-capture
+    ctx->lbc = apply != 0;
+    for (auto& b : ctx->blk) b.d.lbc = apply;
+    invalidate_plans(ctx);
+  }
+  // the interval-end distance, ordered with the steps on the compute stream (a captured step reads it)
+  for (auto& b : ctx->blk)
+    hipLaunchKernelGGL(k_set_f64, dim3(1), dim3(1), 0, ctx->stream, P<double>(ctx, b, "lbc", "dtr"),
+                       seconds_to_interval_end);
+  HIPCHK(hipGetLastError());
+  return MPAS_DYC_OK;
 }
 
 int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags) {

@@ -1467,6 +1467,7 @@ template <int ME>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert_b(Dims d, Ptrs p, int phase) {
   const int c = wave_elem(0);
   if (c >= d.nCellsSolve) return;
+  if (p.bdyMaskCell[c] > N_RELAX_ZONE) return;  // no conversion in the specified zone (2292; any run)
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
   const int kc = min(k, K - 1), kw = min(k, K);
@@ -2039,7 +2040,23 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
   const d2 uh = ld2(p.ruAvg + o);
   const double sgx = sgn1(uh.x), sgy = sgn1(uh.y);
   const bool hex = na == 10;  // the reference's unrolled hexagon form (3363-3390)
-  const bool st = (h == 0 || hasB) && 2 * l < K;
+  bool st = (h == 0 || hasB) && 2 * l < K;
+  // regional: edges of the two outer relaxation rows take a first-order upwind flux, and
+  // specified-zone edges keep the array's previous values (3359, 3409-3420)
+  const int bm = d.lbc ? sel(h, p.bdyMaskEdge[eA], p.bdyMaskEdge[eB]) : 0;
+  if (bm >= N_RELAX_ZONE - 1) {
+    if (bm > N_RELAX_ZONE) return;
+    const double dv = sel(h, ld_uniform_f64(p.dvEdge + eA), ld_uniform_f64(p.dvEdge + eB));
+    const int c1 = sel(h, p.cellsOnEdge[2 * eA], p.cellsOnEdge[2 * eB]);
+    const int c2 = sel(h, p.cellsOnEdge[2 * eA + 1], p.cellsOnEdge[2 * eB + 1]);
+    const double udx = copysign(0.5, uh.x), udy = copysign(0.5, uh.y);
+    const d2 upos{dv * fabs(udx + 0.5), dv * fabs(udy + 0.5)}, uneg{dv * fabs(udx - 0.5), dv * fabs(udy - 0.5)};
+    for (int is = 0; is < ns; ++is) {
+      const d2 s1 = ld2(p.scalars2 + SIX(c1, 2 * lc, is)), s2 = ld2(p.scalars2 + SIX(c2, 2 * lc, is));
+      if (st) st2(p.horiz_flux_array + HIX(e, 2 * lc, is), d2{upos.x * s1.x + uneg.x * s2.x, upos.y * s1.y + uneg.y * s2.y});
+    }
+    return;
+  }
   for (int is = 0; is < ns; ++is) {
     d2 sv[NA];
 #pragma unroll
@@ -2129,10 +2146,14 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
   d2 fu;
   fu.x = dv * dt * (fmax(0.0, uh.x) * so1.x + fmin(0.0, uh.x) * so2.x);
   fu.y = dv * dt * (fmax(0.0, uh.y) * so1.y + fmin(0.0, uh.y) * so2.y);
+  // 4017-4020 (operator precedence as written: (apply_lbcs .and. mask == 5) .or. mask == 4): the
+  // two outer relaxation rows keep only the upwind flux
+  const int bm = sel(h, p.bdyMaskEdge[eA], p.bdyMaskEdge[eB]);
+  const bool upw = (d.lbc && bm == N_RELAX_ZONE) || bm == N_RELAX_ZONE - 1;
   if ((h == 0 || hasB) && 2 * l < K) {
-    st2(p.flux_arr + o, fa);
+    st2(p.flux_arr + o, upw ? fu : fa);
     st2(p.flux_upwind_tmp + o, fu);
-    st2(p.flux_tmp + o, d2{dt * fa.x - fu.x, dt * fa.y - fu.y});
+    st2(p.flux_tmp + o, upw ? d2{0.0, 0.0} : d2{dt * fa.x - fu.x, dt * fa.y - fu.y});
   }
 }
 
@@ -2883,6 +2904,7 @@ template <int ME>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs p, int phase, int hdiv) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
+  if (p.bdyMaskCell[c] > N_RELAX_ZONE) return;  // no specified-zone update (3069; any run)
   const int k = lane_id(), K = d.K;
   const size_t K1 = K + 1;
   const bool act = k < K;
@@ -3579,6 +3601,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_cells_b(Dims d, Ptrs 
                                                                     double coef_3rd_order) {
   const int c = wave_elem(0);
   if (c >= d.nCellsSolve) return;
+  if (p.bdyMaskCell[c] > N_RELAX_ZONE) return;  // specified zone not updated here (3435; any run)
   const int k = lane_id(), K = d.K, ns = d.ns;
   const bool act = k < K;
   const int kc = min(k, K - 1), kw = min(k, K);
@@ -3752,6 +3775,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2_b(Dims d, Ptrs p,
   const int kc = min(k, K - 1), kw = min(k, K);
   const size_t K1 = K + 1;
   const size_t o = (size_t)c * K + kc, ow = (size_t)c * K1 + kw;
+  // only cells with bdyMaskCell <= nSpecZone get the update copied back (4205; the reference tests
+  // the mask whether or not config_apply_lbcs is set, as at 2292, 3069 and 3435)
+  if (p.bdyMaskCell[c] > N_SPEC_ZONE) return;
   if (c >= d.nCellsSolve) {  // halo cells: scalars_new = max(0, scalar_new) with scalar_new = input copy
     if (act) p.scalars2[SIX(c, k, is)] = fmax(0.0, p.scalars2[SIX(c, k, is)]);
     return;
@@ -3808,6 +3834,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges2_p(Dims d, Ptrs p, 
   };
   const d2 a10 = sc(c1, 0), a11 = sc(c1, 1), a20 = sc(c2, 0), a21 = sc(c2, 1);
   d2 f{dt * fa.x - fu.x, dt * fa.y - fu.y};
+  const int bm = sel(h, p.bdyMaskEdge[eA], p.bdyMaskEdge[eB]);
+  if ((d.lbc && bm == N_RELAX_ZONE) || bm == N_RELAX_ZONE - 1) f = d2{0.0, 0.0};  // 4113-4115
   f.x = fmax(0.0, f.x) * fmin(a11.x, a20.x) + fmin(0.0, f.x) * fmin(a10.x, a21.x);
   f.y = fmax(0.0, f.y) * fmin(a11.y, a20.y) + fmin(0.0, f.y) * fmin(a10.y, a21.y);
   if ((h ? onB : onA) && 2 * l < K) st2(p.flux_arr + o, f);

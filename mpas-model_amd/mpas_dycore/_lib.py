@@ -21,7 +21,7 @@ EXPORTS = (
     "mpas_dyc_set_exchange_list", "mpas_dyc_comm_unique_id_bytes", "mpas_dyc_comm_unique_id", "mpas_dyc_comm_init",
     "mpas_dyc_set_transport", "mpas_dyc_halo_exchange", "mpas_dyc_set_overlap", "mpas_dyc_output_diagnostics",
     "mpas_dyc_set_physics", "mpas_dyc_set_summary", "mpas_dyc_get_summary", "mpas_dyc_plan_exchanges",
-    "mpas_dyc_graph_active", "mpas_dyc_solve_diagnostics",
+    "mpas_dyc_graph_active", "mpas_dyc_solve_diagnostics", "mpas_dyc_set_lbc",
 )
 HOST_ONLY = -2  # MPAS_DYC_HOST_ONLY: planner-only context
 PRINT_GLOBAL_MINMAX_VEL, PRINT_DETAILED_MINMAX_VEL, PRINT_GLOBAL_MINMAX_SCA = 1, 2, 4
@@ -102,6 +102,7 @@ def load() -> C.CDLL:
     lib.mpas_dyc_field_device_ptr.restype = vp
     lib.mpas_dyc_init_diagnostics.argtypes = [vp, dbl]
     lib.mpas_dyc_solve_diagnostics.argtypes = [vp, dbl]
+    lib.mpas_dyc_set_lbc.argtypes = [vp, i32, dbl]
     lib.mpas_dyc_timestep.argtypes = [vp, dbl, i32]
     lib.mpas_dyc_shift_time_levels.argtypes = [vp]
     lib.mpas_dyc_synchronize.argtypes = [vp]

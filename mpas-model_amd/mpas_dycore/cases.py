@@ -93,3 +93,69 @@ def varres_case(ncells: int, ratio: float = 20.0, K: int = 56, ns: int = 1, mois
             pickle.dump(case, f, protocol=pickle.HIGHEST_PROTOCOL)
         os.replace(tmp, path)
     return case
+
+
+def regional_lbc(case: dict, interior_deg: float = 40.0, interval_end: float = 10800.0) -> tuple[dict, dict]:
+    """A limited-area configuration on a global case (config_apply_lbcs): the cells farther than
+    ``interior_deg`` from (0N, 0E) form the boundary zones, ring by ring outward -- bdyMaskCell 1..5
+    relaxation, 6 and 7 (and everything beyond) specified -- as a regional mesh's masks count them
+    (mpas_atm_boundaries.F:10-12).  Edges take the smaller mask of their two cells.  Also sets
+    specZoneMask* and nearestRelaxationCell as mpas_atm_setup_bdy_masks does (:426-495; here every
+    specified cell gets its nearest relaxation cell of mask 5, so no read falls outside the mesh)
+    and meshScalingRegional* as atm_compute_mesh_scaling (mpas_atm_core.F:967-981).  Returns the
+    case with these fields and the driving data of the lbc pool: lbc_<f>_s (interval-end state) and
+    lbc_<f>_t (tendency) for u, ru, rho_zz, rtheta_m and scalars, element-major, plus
+    ``interval_end`` = seconds from the first step's start to the LBC interval end."""
+    import numpy as np
+    from .init_atm import _pow
+    c = dict(case)
+    nC, nE = c["nCells"], c["nEdges"]
+    lat, lon = np.asarray(c["latCell"]), np.asarray(c["lonCell"])
+    ang = np.degrees(np.arccos(np.clip(np.cos(lat) * np.cos(lon), -1.0, 1.0)))
+    mask = np.full(nC, 99, dtype=np.int64)
+    mask[ang < interior_deg] = 0
+    coc, noc = np.asarray(c["cellsOnCell"]), np.asarray(c["nEdgesOnCell"])
+    ring = np.flatnonzero(mask == 0)
+    for r in range(1, 8):
+        nb = coc[ring]
+        nb = nb[np.arange(coc.shape[1])[None, :] < noc[ring][:, None]]
+        nb = np.unique(nb[nb >= 0])
+        ring = nb[mask[nb] == 99]
+        mask[ring] = r
+    mask[mask == 99] = 7
+    coe = np.asarray(c["cellsOnEdge"])
+    emask = np.minimum(mask[coe[:, 0]], mask[coe[:, 1]])
+    c["bdyMaskCell"] = mask.astype(np.int32)
+    c["bdyMaskEdge"] = emask.astype(np.int32)
+    c["specZoneMaskCell"] = (mask > 5).astype(np.float64)
+    c["specZoneMaskEdge"] = (emask > 5).astype(np.float64)
+    xyz = np.stack([np.asarray(c["xCell"]), np.asarray(c["yCell"]), np.asarray(c["zCell"])], 1)
+    relax = np.flatnonzero(mask == 5)
+    near = np.full(nC, -1, dtype=np.int64)
+    for i in np.flatnonzero(mask > 5):
+        d2 = ((xyz[relax] - xyz[i]) ** 2).sum(1)
+        near[i] = relax[np.argmin(d2)]
+    c["nearestRelaxationCell"] = near
+    md = np.asarray(c.get("meshDensity", np.ones(nC)), dtype=np.float64)
+    c["meshScalingRegionalCell"] = 1.0 / _pow(md, 0.25)
+    c["meshScalingRegionalEdge"] = 1.0 / _pow((md[coe[:, 0]] + md[coe[:, 1]]) / 2.0, 0.25)
+    # driving data: the initial state with a smooth perturbation at the interval end, and the
+    # tendency that leads there
+    K, ns = c["nVertLevels"], c["num_scalars"]
+    zz = np.asarray(c["zz"])
+    rho_zz = np.asarray(c["rho"]) / zz
+    sc = np.asarray(c["scalars"]).reshape(nC, K, ns)
+    theta_m = np.asarray(c["theta"]) * (1.0 + 461.6 / 287.0 * sc[:, :, 0])
+    u = np.asarray(c["u"])
+    ru = u * 0.5 * (rho_zz[coe[:, 0]] + rho_zz[coe[:, 1]])
+    lonE, latE = np.asarray(c["lonEdge"]), np.asarray(c["latEdge"])
+    pc, pe = 0.003 * np.cos(lon)[:, None], 0.003 * np.cos(lonE)[:, None]
+    tc, te = 1e-7 * np.sin(lat)[:, None], 1e-7 * np.sin(latE)[:, None]
+    lbc = {"interval_end": float(interval_end)}
+    for name, base, p_, t_ in (("u", u, pe, te), ("ru", ru, pe, te), ("rho_zz", rho_zz, pc, tc),
+                               ("rtheta_m", rho_zz * theta_m, pc, tc)):
+        lbc[f"lbc_{name}_s"] = base * (1.0 + p_)
+        lbc[f"lbc_{name}_t"] = base * t_
+    lbc["lbc_scalars_s"] = sc * (1.0 + 3.0 * pc[:, :, None])
+    lbc["lbc_scalars_t"] = sc * tc[:, :, None]
+    return c, lbc

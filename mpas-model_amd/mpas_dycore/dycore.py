@@ -242,6 +242,13 @@ class Dycore:
         """atm_timestep -> atm_srk3 (mpas_atm_time_integration.F:87-139); asynchronous."""
         self._check(self.lib.mpas_dyc_timestep(self.h, float(dt), int(itimestep)), "atm_timestep")
 
+    def set_lbc(self, apply: bool, seconds_to_interval_end: float = 0.0):
+        """config_apply_lbcs (mpas_dyc_set_lbc): regional boundary conditions on/off, and before every
+        step the seconds from the step's start to the end of the current LBC interval.  The driving
+        data go into pool "lbc" (lbc_u, lbc_ru, lbc_rho_zz, lbc_rtheta_m, lbc_scalars; time level 1 =
+        tendency, 2 = interval-end state) and the masks into the mesh pool."""
+        self._check(self.lib.mpas_dyc_set_lbc(self.h, 1 if apply else 0, float(seconds_to_interval_end)), "set_lbc")
+
     PHYSICS_TENDENCIES, PHYSICS_RQVDYNTEN = 1, 2
 
     def set_physics(self, tendencies: bool = True, rqvdynten: bool = False):

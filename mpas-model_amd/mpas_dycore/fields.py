@@ -12,11 +12,13 @@ from __future__ import annotations
 LOCATION = {}
 for n in ("latCell lonCell xCell yCell zCell areaCell invAreaCell meshDensity nEdgesOnCell indexToCellID "
           "edgesOnCell cellsOnCell verticesOnCell kiteForCell edgesOnCell_sign defc_a defc_b zgrid zz dss "
-          "zb_cell zb3_cell theta rho scalars rho_base theta_base w coeffs_reconstruct t_init").split():
+          "zb_cell zb3_cell theta rho scalars rho_base theta_base w coeffs_reconstruct t_init "
+          "bdyMaskCell nearestRelaxationCell meshScalingRegionalCell specZoneMaskCell").split():
     LOCATION[n] = "cell"
 for n in ("latEdge lonEdge xEdge yEdge zEdge dcEdge dvEdge invDcEdge invDvEdge angleEdge fEdge "
           "meshScalingDel2 meshScalingDel4 nEdgesOnEdge nAdvCellsForEdge cellsOnEdge verticesOnEdge "
-          "edgesOnEdge advCellsForEdge weightsOnEdge adv_coefs adv_coefs_3rd zxu deriv_two zb zb3 u").split():
+          "edgesOnEdge advCellsForEdge weightsOnEdge adv_coefs adv_coefs_3rd zxu deriv_two zb zb3 u "
+          "bdyMaskEdge meshScalingRegionalEdge specZoneMaskEdge").split():
     LOCATION[n] = "edge"
 for n in ("latVertex lonVertex xVertex yVertex zVertex areaTriangle invAreaTriangle fVertex "
           "cellsOnVertex edgesOnVertex edgesOnVertex_sign kiteAreasOnVertex").split():
@@ -27,6 +29,7 @@ INDEX_TARGET = {
     "edgesOnCell": "edge", "cellsOnCell": "cell", "verticesOnCell": "vertex",
     "cellsOnEdge": "cell", "verticesOnEdge": "vertex", "edgesOnEdge": "edge",
     "advCellsForEdge": "cell", "cellsOnVertex": "cell", "edgesOnVertex": "edge",
+    "nearestRelaxationCell": "cell",
 }
 # small-integer arrays stored 0-based in numpy but 1-based in MPAS (not element indices)
 ONE_BASED_SMALL = {"kiteForCell"}

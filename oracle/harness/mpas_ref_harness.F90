@@ -341,6 +341,9 @@ program mpas_ref_harness
    use mpas_vector_reconstruction
    use mpas_timekeeping
    use harness_fields
+#ifndef MPAS_DYCORE_DROPIN
+   use mpas_atm_boundaries, only : harness_seconds_to_interval_end
+#endif
 #ifdef HARNESS_INIT
    use atm_advection, only : atm_initialize_advection_rk, atm_initialize_deformation_weights
    use atm_core_init_ref, only : atm_compute_mesh_scaling, atm_compute_signs, atm_compute_damping_coefs, &
@@ -367,6 +370,8 @@ program mpas_ref_harness
    real(kind=RKIND) :: config_zd, config_xnutr
    logical :: config_h_ScaleWithMesh
    character(len=32) :: mode
+   logical :: config_apply_lbcs_in          ! regional LBCs: lbc pool + masks from the inputs
+   real(kind=RKIND) :: lbc_interval_end     ! seconds from the first step's start to the LBC interval end
    integer :: kernel_small_step, kernel_rk_step
    real(kind=RKIND) :: kernel_dts
    integer :: print_minmax   ! summarize_timestep switches: 1 global_minmax_vel, 2 detailed_minmax_vel, 4 global_minmax_sca
@@ -386,7 +391,7 @@ program mpas_ref_harness
       config_len_disp, config_visc4_2dsmag, config_del4u_div_factor, config_coef_3rd_order, &
       config_smagorinsky_coef, config_epssm, config_smdiv, config_apvm_upwinding, &
       config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days, config_horiz_mixing, config_convection_scheme, &
-      config_zd, config_xnutr, config_h_ScaleWithMesh
+      config_zd, config_xnutr, config_h_ScaleWithMesh, config_apply_lbcs_in, lbc_interval_end
 
    type (domain_type), pointer :: domain
    type (mpas_pool_type), pointer :: configs, dimpool, mesh, state, diag, tend, tend_physics, diag_physics
@@ -416,6 +421,8 @@ program mpas_ref_harness
    kernel_dts = 0.0_RKIND
    print_minmax = 0
    nblocks = 1
+   config_apply_lbcs_in = .false.
+   lbc_interval_end = 0.0_RKIND
    config_zd = 22000.0_RKIND       ! Registry.xml defaults
    config_xnutr = 0.2_RKIND
    config_h_ScaleWithMesh = .true.
@@ -486,7 +493,7 @@ program mpas_ref_harness
    call mpas_pool_add_config_logical(configs, 'config_rayleigh_damp_u', config_rayleigh_damp_u)
    call mpas_pool_add_config_real(configs, 'config_rayleigh_damp_u_timescale_days', config_rayleigh_damp_u_timescale_days)
    call mpas_pool_add_config_int(configs, 'config_number_rayleigh_damp_u_levels', config_number_rayleigh_damp_u_levels)
-   call mpas_pool_add_config_logical(configs, 'config_apply_lbcs', .false.)
+   call mpas_pool_add_config_logical(configs, 'config_apply_lbcs', config_apply_lbcs_in)
    call mpas_pool_add_config_char(configs, 'config_IAU_option', 'off')
    call mpas_pool_add_config_char(configs, 'config_microp_scheme', 'off')
    call mpas_pool_add_config_char(configs, 'config_convection_scheme', trim(config_convection_scheme))
@@ -665,6 +672,9 @@ program mpas_ref_harness
    tloop = omp_get_wtime()
    do step = 1, nsteps
       t0 = omp_get_wtime()
+#ifndef MPAS_DYCORE_DROPIN
+      harness_seconds_to_interval_end = lbc_interval_end - real(step - 1, RKIND) * dt
+#endif
       call atm_timestep(domain, dt, nowTime, step)
       nowTime = nowTime + dtInterval
       t1 = omp_get_wtime()
@@ -881,6 +891,7 @@ contains
       call add_r2(state, 'state', 'rho_zz', K, nC1, 2)
       call add_r3(state, 'state', 'scalars', ns, K, nC1, 2)
       call add_c0(state, 'state', 'xtime', 2, start_time)
+      if (config_apply_lbcs_in) call add_lbc_pool()
    
       ! ---- diag pool ----
       call add_r2(diag, 'diag', 'theta', K, nC1, 1);        call add_r2(diag, 'diag', 'rho', K, nC1, 1)
@@ -1060,6 +1071,26 @@ contains
          b => b % next
       end do
    end subroutine dump_blocks
+
+   ! regional runs: the lbc pool the reference's mpas_atm_boundaries reads (lbc_<field>, time level
+   ! 1 = tendency, 2 = interval-end state; lbc.lbc_<field>.tl<N>.bin inputs) and the moist species
+   ! indices srk3 looks up (state and lbc pools; 0 = absent species)
+   subroutine add_lbc_pool()
+      type (mpas_pool_type), pointer :: lbc
+      character(len=8), dimension(8), parameter :: sp = ['qv', 'qc', 'qr', 'qi', 'qs', 'qg', 'nr', 'ni']
+      integer :: j
+      call mpas_pool_create_pool(lbc)
+      call mpas_pool_add_subpool(hblock % structs, 'lbc', lbc)
+      call add_r2(lbc, 'lbc', 'lbc_u', K, nE1, 2)
+      call add_r2(lbc, 'lbc', 'lbc_ru', K, nE1, 2)
+      call add_r2(lbc, 'lbc', 'lbc_rho_zz', K, nC1, 2)
+      call add_r2(lbc, 'lbc', 'lbc_rtheta_m', K, nC1, 2)
+      call add_r3(lbc, 'lbc', 'lbc_scalars', ns, K, nC1, 2)
+      do j = 1, size(sp)
+         call mpas_pool_add_dimension(lbc, 'index_'//trim(sp(j)), merge(j, 0, j <= moist_end))
+         if (j > 1) call mpas_pool_add_dimension(state, 'index_'//trim(sp(j)), merge(j, 0, j <= moist_end))
+      end do
+   end subroutine add_lbc_pool
 
    subroutine add_dims(p)
       type (mpas_pool_type), pointer :: p

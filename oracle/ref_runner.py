@@ -74,6 +74,30 @@ def write_physics_inputs(case: dict, d: str, physics: dict):
         img.tofile(os.path.join(d, n + "_in.bin"))
 
 
+def lbc_images(case: dict, lbc: dict) -> dict:
+    """cases.regional_lbc's element-major driving data -> {(name, time level): Fortran image}, time
+    level 1 = tendency, 2 = interval-end state (the reference's lbc pool)."""
+    out = {}
+    for name in ("u", "ru", "rho_zz", "rtheta_m", "scalars"):
+        for tl, suf in ((1, "t"), (2, "s")):
+            a = np.asarray(lbc[f"lbc_{name}_{suf}"], dtype=np.float64)
+            img = np.zeros((a.shape[0] + 1,) + a.shape[1:])
+            img[:-1] = a
+            out[(f"lbc_{name}", tl)] = img
+    return out
+
+
+def write_lbc_inputs(case: dict, d: str, lbc: dict):
+    """The lbc pool as the harness reads it (lbc.lbc_<f>.tl<N>.bin) and the regional namelist switches."""
+    for (name, tl), img in lbc_images(case, lbc).items():
+        img.tofile(os.path.join(d, f"lbc.{name}.tl{tl}.bin"))
+    with open(os.path.join(d, "harness.nml")) as f:
+        nml = f.read()
+    iv = repr(float(lbc["interval_end"])).replace("e", "d")
+    with open(os.path.join(d, "harness.nml"), "w") as f:
+        f.write(nml.replace("&harness\n", f"&harness\n config_apply_lbcs_in=.true., lbc_interval_end={iv},\n"))
+
+
 def write_fields(case: dict, d: str):
     """Every mesh / state / diag array of the case as its Fortran memory image, one .bin per field."""
     F = _fields()
@@ -177,8 +201,9 @@ def read_dump(case: dict, stepdir: str) -> dict:
 def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads: int = 0,
                   workdir: str | None = None, moist_end: int = 1, timeout: int = 3000, binary: str = HARNESS,
                   physics: dict | None = None, print_minmax: int = 0, dump_only=(), env_extra: dict | None = None,
-                  with_total: bool = False):
+                  with_total: bool = False, lbc: dict | None = None):
     """Run the reference dycore; returns ({step: {field: array}}, [step wall times]) -- and, with
+    ``lbc`` (cases.regional_lbc's driving data) runs with config_apply_lbcs, the lbc pool and masks.
     ``with_total``, the wall time of the whole time loop including its final wait for the device
     ({"total": s, "after2": s of steps 3.. } when the run has more than 2 steps).
     ``binary=DROPIN_HARNESS`` runs the same driver on the drop-in module instead.
@@ -200,6 +225,8 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
                  (physics or {}).get("convection_scheme", "off"), print_minmax, dump_only)
     if physics is not None:
         write_physics_inputs(case, ind, physics)
+    if lbc is not None:
+        write_lbc_inputs(case, ind, lbc)
     env = dict(os.environ)
     if nthreads:
         env["OMP_NUM_THREADS"] = str(nthreads)
