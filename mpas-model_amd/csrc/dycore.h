@@ -122,4 +122,14 @@ struct PackMap {
   double* const* rho;    // send-buffer column of rho_pp per slot, or nullptr
 };
 
+// Halo unpack fused into the consumer (the next acoustic edge phase, or the stage's last divergence
+// damping, k_acoustic_edges_p / k_divdamp_p): a halo cell h with rt[h - nCellsSolve] >= 0 has its
+// exchanged rtheta_pp column at recv + rt[..] (rho_pp: recv + rho[..]); the consumer reads it there
+// and writes it into the field for the later readers.  recv == nullptr: the fields hold the values.
+struct UnpackMap {
+  const double* recv;
+  const int* rt;
+  const int* rho;  // nullptr: rho_pp not in this exchange
+};
+
 }  // namespace mpas

@@ -84,6 +84,10 @@ struct XPlan {
   // acoustic cell phase writes the send buffer itself, so exchange() launches no pack kernel
   bool fused_pack = false;
   std::vector<PackMap> pack;        // per block
+  // fused unpack: the exchange launches no unpack kernel; its consumer (the next acoustic edge
+  // phase or the stage's last damping) reads the receive buffer through `unpack`
+  bool fused_unpack = false;
+  std::vector<UnpackMap> unpack;    // per block
   std::vector<void*> pack_mem;      // device allocations behind `pack`
 };
 
@@ -471,6 +475,7 @@ std::vector<std::pair<int, int>> peers_of(const Block& b, int dir) {
 }
 
 inline bool batched(const Dims& d);
+inline bool pair_layout(const Dims& d);
 
 // Message layout: per block, peers in (rank, block) order; per peer, the fields in call
 // order and per field the halo layers in ascending order (both sides agree on it).
@@ -485,7 +490,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
     fusable = fusable && std::string(f.pool) == "diag" && f.layers == 0x1u &&
               (std::string(f.name) == "rtheta_pp" || std::string(f.name) == "rho_pp");
   struct PackSeg { int block, is_rho; const XList* sx; size_t seg; };
-  std::vector<PackSeg> pack_segs;
+  std::vector<PackSeg> pack_segs, unpack_segs;
   auto field_of = [&](Block& b, const XField& f) -> Field* {
     Field* F = find(b, f.pool, f.name);
     if (!F || F->is_int || F->loc == L_NONE) {
@@ -577,6 +582,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
             sg.didx = rx->d_idx;
             sg.n = rx->n;
             sg.inner = (int)sub_inner;
+            if (fusable) unpack_segs.push_back(PackSeg{bi, std::string(f.name) == "rho_pp" ? 1 : 0, rx, post.size()});
             post.push_back(sg);
             post_off.push_back(rtotal);
             rtotal += (int64_t)rx->n * sub_inner;
@@ -656,6 +662,38 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
       pl.pack[bi] = PackMap{d_start, d_rt, d_rho};
     }
     pl.fused_pack = ctx->fused_pack_enabled;
+    // unpack maps: halo cell -> its columns in the receive buffer (consumers: pair kernels only)
+    bool pair_all = true;
+    for (int bi = 0; bi < nb; ++bi) pair_all = pair_all && pair_layout(ctx->blk[bi].d);
+    if (pair_all && !unpack_segs.empty() && ctx->fused_pack_enabled) {
+      pl.unpack.assign(nb, UnpackMap{});
+      for (int bi = 0; bi < nb; ++bi) {
+        const Dims& d = ctx->blk[bi].d;
+        const int nh = d.nCells - d.nCellsSolve;
+        std::vector<int> rt(nh, -1), rho(nh, -1);
+        bool any = false;
+        for (const PackSeg& ps : unpack_segs) {
+          if (ps.block != bi) continue;
+          for (int i = 0; i < ps.sx->n; ++i) {
+            const int64_t off = (int64_t)(post[ps.seg].src - pl.recvbuf) + (int64_t)i * post[ps.seg].inner;
+            (ps.is_rho ? rho : rt)[ps.sx->h_idx[i] - d.nCellsSolve] = (int)off;
+            any = true;
+          }
+        }
+        if (!any) continue;
+        int *d_rt = nullptr, *d_rho = nullptr;
+        HIPCHK(hipMalloc(&d_rt, std::max(nh, 1) * sizeof(int)));
+        HIPCHK(hipMemcpy(d_rt, rt.data(), nh * sizeof(int), hipMemcpyHostToDevice));
+        pl.pack_mem.push_back(d_rt);
+        if (with_rho) {
+          HIPCHK(hipMalloc(&d_rho, std::max(nh, 1) * sizeof(int)));
+          HIPCHK(hipMemcpy(d_rho, rho.data(), nh * sizeof(int), hipMemcpyHostToDevice));
+          pl.pack_mem.push_back(d_rho);
+        }
+        pl.unpack[bi] = UnpackMap{pl.recvbuf, d_rt, d_rho};
+      }
+      pl.fused_unpack = true;
+    }
   }
   if (pl.npre) {
     HIPCHK(hipMalloc(&pl.d_pre, pre.size() * sizeof(XSeg)));
@@ -700,7 +738,7 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
       NCCLCHK(ncclRecv(pl.recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
     NCCLCHK(ncclGroupEnd());
   }
-  if (pl.npost)
+  if (pl.npost && !pl.fused_unpack)
     hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_post + 3) / 4, pl.npost), dim3(256), 0, ctx->stream, pl.d_post);
   return MPAS_DYC_OK;
 }
@@ -933,14 +971,20 @@ double coef_divdamp(const mpas_dyc_ctx* ctx, double dts) {  // 2761-2763
 // edge phase of acoustic sub-step `small_step`; damp = 1 also applies the divergence damping of
 // the previous sub-step (k_acoustic_edges<true>); fresh = 1 when that sub-step was sub-step 1,
 // whose edge phase is not launched (its ru_p = ruAvg = dts * tend_u are formed by the readers)
+// um: the block's fused-unpack map of the exchange just completed (pair layout only), or none
 void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int damp,
-                    int phase, int fresh = 0) {
+                    int phase, int fresh = 0, UnpackMap um = UnpackMap{}) {
   if (pair_layout(d)) {
     const int64_t nw = (d.nEdges + 1) / 2;
-    if (damp)
-      LAUNCH_E(k_acoustic_edges_p<true>, nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh);
+    const bool up = um.recv != nullptr;
+    if (damp && up)
+      LAUNCH_E((k_acoustic_edges_p<true, true>), nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh, um);
+    else if (damp)
+      LAUNCH_E((k_acoustic_edges_p<true, false>), nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh, um);
+    else if (up)
+      LAUNCH_E((k_acoustic_edges_p<false, true>), nw, d, p, dts, small_step, 0.0, phase, fresh, um);
     else
-      LAUNCH_E(k_acoustic_edges_p<false>, nw, d, p, dts, small_step, 0.0, phase, fresh);
+      LAUNCH_E((k_acoustic_edges_p<false, false>), nw, d, p, dts, small_step, 0.0, phase, fresh, um);
     return;
   }
   if (damp)
@@ -982,11 +1026,18 @@ bool fused_recover_edges(const Dims& d) { return pair_layout(d) && fused_recover
 // fresh = 1: the stage had a single sub-step (no edge phase launched), see k_divdamp_p;
 // invNs > 0: recover the edges with two owned cells too (fused_recover_edges)
 void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase, int fresh = 0,
-                        double invNs = 0.0) {
+                        double invNs = 0.0, UnpackMap um = UnpackMap{}) {
   // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
-  if (pair_layout(d) && invNs > 0.0 && fused_recover_edges(d))
-    LAUNCH_E(k_divdamp_p<true>, (d.nEdges + 1) / 2, d, p, coef_divdamp(ctx, dts), phase, dts, fresh, invNs);
-  else if (pair_layout(d)) LAUNCH_E(k_divdamp_p<false>, (d.nEdges + 1) / 2, d, p, coef_divdamp(ctx, dts), phase, dts, fresh, 0.0);
+  const bool up = um.recv != nullptr;
+  const int64_t nw = (d.nEdges + 1) / 2;
+  const double cd = coef_divdamp(ctx, dts);
+  if (pair_layout(d) && invNs > 0.0 && fused_recover_edges(d)) {
+    if (up) LAUNCH_E((k_divdamp_p<true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um);
+    else LAUNCH_E((k_divdamp_p<true, false>), nw, d, p, cd, phase, dts, fresh, invNs, um);
+  } else if (pair_layout(d)) {
+    if (up) LAUNCH_E((k_divdamp_p<false, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um);
+    else LAUNCH_E((k_divdamp_p<false, false>), nw, d, p, cd, phase, dts, fresh, 0.0, um);
+  }
   else LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase,
               dts, fresh);
 }
@@ -1283,16 +1334,21 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       //   edge phase of sub-step 2 or, for a one-sub-step stage, the damping, which also stores
       //   ruAvg (on the same edges, so the 876 exchange and the recovery see the same values).
       const int nsub = number_sub_steps[rk_step - 1];
+      // the last Theta''/rho'' exchange whose unpack its consumer does (XPlan::fused_unpack): the
+      // next edge phase, or the stage's last damping
+      const XPlan* unpack_xp = nullptr;
+      auto um_of = [&](size_t ib) { return unpack_xp ? unpack_xp->unpack[ib] : UnpackMap{}; };
       for (int small_step = 1; small_step <= nsub; ++small_step) {
         if (small_step == 1) {
           // 794-837: formed by the readers (above)
         } else if (split) {  // interior edges overlap the exchange issued after the last cell phase
           EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 1, small_step == 2));
           CHK(exchange_wait(ctx));
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 2, small_step == 2));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 2, small_step == 2, um_of(ib_)));
         } else {
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2));
+          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2, um_of(ib_)));
         }
+        unpack_xp = nullptr;
         std::vector<XField> xf = {{"diag", "rtheta_pp", 0, 0x1u}};  // 845
         if (small_step < nsub) xf.push_back({"diag", "rho_pp", 0, 0x1u});  // 792 of the next sub-step
         const XPlan* xp = fused_pack_plan(ctx, xf);  // the cell phase packs this exchange's send buffer
@@ -1304,13 +1360,14 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         } else {
           CHK((exchange)(ctx, xf));  // parenthesised: no ADL lookup of std::exchange
         }
+        if (xp && xp->fused_unpack) unpack_xp = xp;
       }
       if (split) {  // the last sub-step's damping (849-869), interior edges overlapping the exchange
         EACH(divergence_damping(ctx, d, p, dts, 1, nsub == 1, 1 / (double)nsub));
         CHK(exchange_wait(ctx));
-        EACH(divergence_damping(ctx, d, p, dts, 2, nsub == 1));
+        EACH(divergence_damping(ctx, d, p, dts, 2, nsub == 1, 0.0, um_of(ib_)));
       } else {
-        EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1, 1 / (double)nsub));
+        EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1, 1 / (double)nsub, um_of(ib_)));
       }
       const std::vector<XField> xrec = {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},  // 876-887
                                         {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};

@@ -1957,9 +1957,28 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
 // (k_acoustic_cells_r<ME, true>), and nothing between here and k_recover_edges -- the 876-887
 // exchange, k_recover_cells1 on halo cells -- touches ru_save, ruAvg, ru or u there.
 // k_recover_edges then runs on the other edges (phase 2).
-template <bool REC = false>
+// two levels (2*lc, 2*lc+1) of cell c's rtheta_pp (which = 0) or rho_pp (1) column: from the
+// exchange's receive buffer for a halo cell the fused unpack covers -- written back into the field,
+// lanes `st` only, for the later readers -- else from the field
+__device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMap& um, int which, int c, int lc,
+                                    bool st) {
+  double* fld = which ? p.rho_pp : p.rtheta_pp;
+  const size_t o = (size_t)c * d.K + 2 * lc;
+  const int* map = which ? um.rho : um.rt;
+  if (map && c >= d.nCellsSolve && c < d.nCells) {
+    const int off = map[c - d.nCellsSolve];
+    if (off >= 0) {
+      const d2 v = ld2(um.recv + off + 2 * lc);
+      if (st) st2(fld + o, v);
+      return v;
+    }
+  }
+  return ld2(fld + o);
+}
+
+template <bool REC = false, bool UP = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
-                                                            int fresh, double invNs = 0.0) {
+                                                            int fresh, double invNs = 0.0, UnpackMap um = UnpackMap{}) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
@@ -1985,7 +2004,9 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   const bool onA = active(ceA, bA), onB = hasB && active(ceB, bB);
   if (!onA && !onB) return;
   const size_t o1 = (size_t)sel(h, ceA.x, ceB.x) * K + 2 * lc, o2 = (size_t)sel(h, ceA.y, ceB.y) * K + 2 * lc;
-  const d2 r1 = ld2(p.rtheta_pp + o1), r2 = ld2(p.rtheta_pp + o2);
+  const bool lv = 2 * l < K && (h ? onB : onA);
+  const d2 r1 = UP ? ld_pp(d, p, um, 0, sel(h, ceA.x, ceB.x), lc, lv) : ld2(p.rtheta_pp + o1);
+  const d2 r2 = UP ? ld_pp(d, p, um, 0, sel(h, ceA.y, ceB.y), lc, lv) : ld2(p.rtheta_pp + o2);
   const d2 q1 = ld2(p.rtheta_pp_old + o1), q2 = ld2(p.rtheta_pp_old + o2);
   const d2 t1 = ld2(p.theta_m1 + o1), t2 = ld2(p.theta_m1 + o2);
   d2 out;
@@ -2259,9 +2280,11 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs 
 }
 
 // k_acoustic_edges in the pair layout (same expressions, per level)
-template <bool DD>
+// UP: the Theta''/rho'' halo comes from the exchange's receive buffer (fused unpack, UnpackMap)
+template <bool DD, bool UP = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,
-                                                                   double coef_divdamp, int phase, int fresh) {
+                                                                   double coef_divdamp, int phase, int fresh,
+                                                                   UnpackMap um = UnpackMap{}) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const int eB = min(eA + 1, d.nEdges - 1);
@@ -2301,9 +2324,11 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
   const double invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
   const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
   const size_t o1 = (size_t)c1 * K + 2 * lc, o2 = (size_t)c2 * K + 2 * lc;
-  const d2 rt1 = ld2(p.rtheta_pp + o1), rt2 = ld2(p.rtheta_pp + o2);
+  const d2 rt1 = UP ? ld_pp(d, p, um, 0, c1, lc, st) : ld2(p.rtheta_pp + o1);
+  const d2 rt2 = UP ? ld_pp(d, p, um, 0, c2, lc, st) : ld2(p.rtheta_pp + o2);
   const d2 zz1 = ld2(p.zz + o1), zz2 = ld2(p.zz + o2), ex1 = ld2(p.exner + o1), ex2 = ld2(p.exner + o2);
-  const d2 rp1 = ld2(p.rho_pp + o1), rp2 = ld2(p.rho_pp + o2);
+  const d2 rp1 = UP ? ld_pp(d, p, um, 1, c1, lc, st) : ld2(p.rho_pp + o1);
+  const d2 rp2 = UP ? ld_pp(d, p, um, 1, c2, lc, st) : ld2(p.rho_pp + o2);
   d2 ro1{}, ro2{}, th1{}, th2{};
   if (DD) {
     ro1 = ld2(p.rtheta_pp_old + o1);

@@ -88,6 +88,18 @@ def load() -> C.CDLL:
     if not os.path.isfile(LIBPATH):
         raise RuntimeError(f"MI355X dycore library not built: {LIBPATH} (run __graft_entry__.build())")
     lib = C.CDLL(LIBPATH)
+    if os.environ.get("MPAS_DYCORE_LIB"):
+        # an A/B build (tools/ab_*.sh) may predate the newest entry points: bind what it has
+        class _Lenient:
+            def __init__(self, real):
+                object.__setattr__(self, "_real", real)
+
+            def __getattr__(self, name):
+                try:
+                    return getattr(self._real, name)
+                except AttributeError:
+                    return type("Missing", (), {"argtypes": None, "restype": None})()
+        _real, lib = lib, _Lenient(lib)
     vp, i32, i64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_double
     lib.mpas_dyc_create.argtypes = [C.POINTER(Dims), C.POINTER(Config), C.c_int, C.POINTER(vp)]
     lib.mpas_dyc_destroy.argtypes = [vp]
@@ -134,5 +146,7 @@ def load() -> C.CDLL:
     lib.mpas_dyc_plan_exchanges.argtypes = [vp, i32, i32, dbl, C.POINTER(PlanMsg), i64, C.POINTER(i64), C.c_char_p,
                                             i64, C.POINTER(i64)]
     lib.mpas_dyc_graph_active.argtypes = [vp]
+    if os.environ.get("MPAS_DYCORE_LIB"):
+        lib = _real
     _lib = lib
     return lib

@@ -117,8 +117,10 @@ def test_rccl_transport_matches_device_copies(small_case):
 @pytest.mark.parametrize("overlap", [True, False])
 def test_fused_pack_bitwise(small_case, overlap):
     """The per-sub-step rtheta_pp / rho_pp exchange packed by the acoustic cell phase itself (the
-    PackMap epilogue of k_acoustic_cells_r, no pack kernel) gives the bits of the separate pack
-    kernel (MPAS_DYCORE_FUSED_PACK=0) and of one block; 4 RCCL blocks, graph replay."""
+    PackMap epilogue of k_acoustic_cells_r, no pack kernel) and unpacked by its consumer (the next
+    edge phase or the stage's last damping read the receive buffer through an UnpackMap and write
+    the halo columns back, no unpack kernel) gives the bits of the separate pack / unpack kernels
+    (MPAS_DYCORE_FUSED_PACK=0) and of one block; 4 RCCL blocks, graph replay."""
     import os
     one = _single(small_case, 3)
     runs = []
