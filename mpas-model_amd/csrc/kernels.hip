@@ -3213,13 +3213,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_init_coupled_c(Dims d, Ptrs p
 // (K+1, n) array is contiguous over its owned+halo columns, so instead of one column per wave
 // (56 of 64 lanes, 8 B each) every lane moves two doubles.  Same ranges (garbage slot excluded),
 // same expressions.
+// u_1 = u_2 and w_1 = w_2 (6060-6061) are not stored: nothing reads u or w of time level 1
+// before the dt ends -- the substeps read time level 2, and the transport, the exchanges and the
+// summary do not touch u_1 / w_1 -- and after mpas_pool_shift_time_levels that buffer is time
+// level 2, which the next atm_rk_integration_setup overwrites (u_2 = u_1, w_2 = w_1, 1852-1853)
+// before anything reads it.  Time level 1 after the step (the new state) is unchanged.
 __device__ __forceinline__ void fin_edge_pair(const Ptrs& p, int64_t j, int n, int cp, int first, int last, double inv) {
   for (int q = 0; q < n; ++q) {  // n = 2, or 1 for an odd tail
     const int64_t i = j + q;
-    if (cp) {
-      p.ru_save[i] = p.ru[i];
-      p.u1[i] = p.u2[i];
-    }
+    if (cp) p.ru_save[i] = p.ru[i];
     const double ras = first ? p.ruAvg[i] : p.ruAvg[i] + p.ruAvg_split[i];
     p.ruAvg_split[i] = ras;
     if (last) p.ruAvg[i] = ras * inv;
@@ -3233,10 +3235,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_substep_finish_v(Dims d, Ptrs
   const double inv = inv_dynamics_split;
   for (int64_t j = 2 * t0; j < nE; j += 2 * st) {
     if (j + 1 < nE) {
-      if (cp) {
-        st2(p.ru_save + j, ld2(p.ru + j));
-        st2(p.u1 + j, ld2(p.u2 + j));
-      }
+      if (cp) st2(p.ru_save + j, ld2(p.ru + j));
       const d2 a = ld2(p.ruAvg + j);
       d2 ras = a;
       if (!first) {
@@ -3251,10 +3250,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_substep_finish_v(Dims d, Ptrs
   }
   for (int64_t j = 2 * t0; j < nW; j += 2 * st) {
     if (j + 1 < nW) {
-      if (cp) {
-        st2(p.rw_save + j, ld2(p.rw + j));
-        st2(p.w1 + j, ld2(p.w2 + j));
-      }
+      if (cp) st2(p.rw_save + j, ld2(p.rw + j));
       const d2 a = ld2(p.wwAvg + j);
       d2 was = a;
       if (!first) {
@@ -3264,10 +3260,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_substep_finish_v(Dims d, Ptrs
       st2(p.wwAvg_split + j, was);
       if (last) st2(p.wwAvg + j, d2{was.x * inv, was.y * inv});
     } else {
-      if (cp) {
-        p.rw_save[j] = p.rw[j];
-        p.w1[j] = p.w2[j];
-      }
+      if (cp) p.rw_save[j] = p.rw[j];
       const double was = first ? p.wwAvg[j] : p.wwAvg[j] + p.wwAvg_split[j];
       p.wwAvg_split[j] = was;
       if (last) p.wwAvg[j] = was * inv;

@@ -23,7 +23,8 @@ namespace mpas {
 
 constexpr int SUM_REC = 16;         // doubles per field record
 constexpr int SUM_MAX_FIELDS = 40;  // fields per launch
-constexpr int SUM_PARTS = 256;      // workgroups per field in the first pass
+constexpr int SUM_PARTS = 1024;     // workgroups per field in the first pass
+constexpr int SUM_UNROLL = 4;       // columns whose loads a wavefront issues together
 
 // record slots
 enum {
@@ -125,7 +126,9 @@ __device__ SumAcc sum_load(const double* r) {
   return a;
 }
 
-// pass 1: grid (SUM_PARTS, nfields); a wavefront walks whole columns, lane = level
+// pass 1: grid (SUM_PARTS, nfields); a wavefront walks whole columns, lane = level, and issues
+// the loads of SUM_UNROLL columns before reducing them (the reduction is order-free: extrema with
+// index tie-breaks, integer counts)
 __global__ __launch_bounds__(256) void k_summary_partial(SumFields fs, double* __restrict__ part) {
   const SumField& f = fs.f[blockIdx.y];
   SumAcc a;
@@ -133,15 +136,26 @@ __global__ __launch_bounds__(256) void k_summary_partial(SumFields fs, double* _
   const int lane = threadIdx.x & 63;
   const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
-  for (long long c = wave; c < f.ncol; c += nw) {
-    for (int k = lane; k < f.K; k += 64) {
-      const double x = f.a[c * f.stride + k];
-      double s = -1.0e30;  // below the start value: no wind-speed candidate
-      if (f.v) {
-        const double y = f.v[c * f.stride + k];
-        s = sqrt(x * x + y * y);  // spd = sqrt(u*u + v*v) (6893)
+  for (int k0 = 0; k0 < f.K; k0 += 64) {
+    const int k = k0 + lane;
+    const bool lv = k < f.K;
+    for (long long c0 = wave; c0 < f.ncol; c0 += nw * SUM_UNROLL) {
+      double x[SUM_UNROLL], y[SUM_UNROLL];
+#pragma unroll
+      for (int u = 0; u < SUM_UNROLL; ++u) {
+        const long long c = c0 + u * nw;
+        const bool ok = lv && c < f.ncol;
+        x[u] = ok ? f.a[c * f.stride + k] : 0.0;
+        y[u] = (ok && f.v) ? f.v[c * f.stride + k] : 0.0;
       }
-      a.add(x, s, c * f.K + k);
+#pragma unroll
+      for (int u = 0; u < SUM_UNROLL; ++u) {
+        const long long c = c0 + u * nw;
+        if (!lv || c >= f.ncol) continue;
+        double s = -1.0e30;  // below the start value: no wind-speed candidate
+        if (f.v) s = sqrt(x[u] * x[u] + y[u] * y[u]);  // spd = sqrt(u*u + v*v) (6893)
+        a.add(x[u], s, c * f.K + k);
+      }
     }
   }
   sum_block_reduce(a);

@@ -1,0 +1,7 @@
+# Summary-kernel and substep_finish changes: the GPU tests they touch, then a same-box A/B
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out && rm -f gpurun_out/ab.log &&
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_summary.py tests/test_gpu_parity.py tests/test_gpu_decomp.py tests/test_gpu_restart.py tests/test_gpu_configs.py tests/test_gpu_lbc.py > gpurun_out/pytest_copyfix.log 2>&1 &&
+for r in 1 2; do for L in exp/lib_cur.so mpas-model_amd/csrc/libmpas_dycore.so; do
+echo "== $L" >> gpurun_out/ab.log
+MPAS_DYCORE_LIB=$L timeout -k 10 200 python tools/kbench.py --steps 10 >> gpurun_out/ab.log 2>&1 || exit 1; done; done
+echo EXIT $?; tail -3 gpurun_out/pytest_copyfix.log; grep -h "==\|ms_dt" gpurun_out/ab.log | cut -c1-200
