@@ -35,6 +35,8 @@ struct Dims {
   int diabatic;                // rt_diabatic_tend holds nonzero data (else it is read as 0)
   int physics;                 // DO_PHYSICS coupling: tend_*_physics and scalars_tend come from the host
   int lbc;                     // config_apply_lbcs: regional lateral boundary conditions (lbc.hip)
+  // lengths of the compact phase-2 lists of the split-phase kernels (compute_bnd; Ptrs::bnd_*)
+  int n_bnd_edges, n_bnd_pairs, n_bnd_cells;
 };
 
 struct Config {
@@ -93,6 +95,11 @@ struct Ptrs {
   // CELL_HALO_EDGE = an edge of the cell is a halo edge, CELL_BND_EDGE = an edge of the cell has
   // edge_bnd set; halo cells have both bits.
   const int *edge_bnd, *cell_bnd;
+  // phase 2 (halo-boundary elements) of a split kernel walks a compact list instead of testing
+  // the flag on every element: bnd_edges = edges with edge_bnd set (k_recover_edges), bnd_pairs =
+  // those of them with an owned cell (the pair-layout acoustic edge phase and damping),
+  // bnd_cells = owned cells with CELL_HALO_EDGE (k_smlstep_pert_b); ascending element order
+  const int *bnd_edges, *bnd_pairs, *bnd_cells;
   // per-cell stencil records (built on the device from edgesOnCell / cellsOnEdge / dvEdge,
   // k_build_cell_rec): cell_rec = 16 int32 per cell, [0, 7) edgesOnCell, [7, 14) the cell across
   // each of those edges, [14] nEdgesOnCell, unused slots -> garbage element; cell_sdv =

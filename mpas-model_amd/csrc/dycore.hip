@@ -306,6 +306,9 @@ void build_registry(Block& c) {
   add(c, "scratch", "wdtn", L_CELL, K + 1);
   add(c, "scratch", "edge_bnd", L_EDGE, 1, 1, true);
   add(c, "scratch", "cell_bnd", L_CELL, 1, 1, true);
+  add(c, "scratch", "bnd_edges", L_EDGE, 1, 1, true);
+  add(c, "scratch", "bnd_pairs", L_EDGE, 1, 1, true);
+  add(c, "scratch", "bnd_cells", L_CELL, 1, 1, true);
   add(c, "scratch", "cell_rec", L_CELL, CELL_REC, 1, true);
   add(c, "scratch", "cell_sdv", L_CELL, ME);
   add(c, "scratch", "zb_p", L_CELL, (int64_t)ME * (K + 1));
@@ -382,6 +385,9 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   SC(advflux_w); SC(advflux_th);
   p.edge_bnd = P<const int>(c, b, "scratch", "edge_bnd");
   p.cell_bnd = P<const int>(c, b, "scratch", "cell_bnd");
+  p.bnd_edges = P<const int>(c, b, "scratch", "bnd_edges");
+  p.bnd_pairs = P<const int>(c, b, "scratch", "bnd_pairs");
+  p.bnd_cells = P<const int>(c, b, "scratch", "bnd_cells");
   p.cell_rec = P<const int>(c, b, "scratch", "cell_rec");
   p.cell_sdv = P<const double>(c, b, "scratch", "cell_sdv");
   p.zb_p = P<const double>(c, b, "scratch", "zb_p");
@@ -793,6 +799,28 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
     }
     HIPCHK(hipMemcpy(find(b, "scratch", "edge_bnd")->buf[0], eb.data(), eb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(find(b, "scratch", "cell_bnd")->buf[0], cb.data(), cb.size() * 4, hipMemcpyHostToDevice));
+    std::vector<int32_t> le, lp, lc;
+    for (int e = 0; e < d.nEdges; ++e) {
+      if (!eb[e]) continue;
+      le.push_back(e);
+      if (b.h_coe[2 * e] < d.nCellsSolve || b.h_coe[2 * e + 1] < d.nCellsSolve) lp.push_back(e);
+    }
+    for (int c = 0; c < d.nCellsSolve; ++c)
+      if (cb[c] & CELL_HALO_EDGE) lc.push_back(c);
+    if (!le.empty())
+      HIPCHK(hipMemcpy(find(b, "scratch", "bnd_edges")->buf[0], le.data(), le.size() * 4, hipMemcpyHostToDevice));
+    if (!lp.empty())
+      HIPCHK(hipMemcpy(find(b, "scratch", "bnd_pairs")->buf[0], lp.data(), lp.size() * 4, hipMemcpyHostToDevice));
+    if (!lc.empty())
+      HIPCHK(hipMemcpy(find(b, "scratch", "bnd_cells")->buf[0], lc.data(), lc.size() * 4, hipMemcpyHostToDevice));
+    if (b.d.n_bnd_edges != (int)le.size() || b.d.n_bnd_pairs != (int)lp.size() || b.d.n_bnd_cells != (int)lc.size())
+      for (int i = 0; i < 2; ++i) {  // captured steps bake the list lengths into their launches
+        if (ctx->graph_exec[i]) (void)hipGraphExecDestroy(ctx->graph_exec[i]);
+        ctx->graph_exec[i] = nullptr;
+      }
+    b.d.n_bnd_edges = (int)le.size();
+    b.d.n_bnd_pairs = (int)lp.size();
+    b.d.n_bnd_cells = (int)lc.size();
     hipLaunchKernelGGL(k_build_cell_rec, dim3((d.nCells + 1 + 255) / 256), dim3(256), 0, ctx->stream, d,
                        P<const int>(ctx, b, "mesh", "nEdgesOnCell"), P<const int>(ctx, b, "mesh", "edgesOnCell"),
                        P<const int>(ctx, b, "mesh", "cellsOnEdge"), P<const double>(ctx, b, "mesh", "dvEdge"),
@@ -951,9 +979,10 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
 }
 
 void smlstep_pert(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int phase) {
+  const int64_t nb = phase == 2 ? d.n_bnd_cells : d.nCellsSolve;  // phase 2: the bnd_cells list
   if (!batched(d)) LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, phase);
-  else if (d.maxEdges == 6) LAUNCH(k_smlstep_pert_b<6>, d.nCellsSolve, d, p, phase);
-  else LAUNCH(k_smlstep_pert_b<7>, d.nCellsSolve, d, p, phase);
+  else if (d.maxEdges == 6) LAUNCH(k_smlstep_pert_b<6>, nb, d, p, phase);
+  else LAUNCH(k_smlstep_pert_b<7>, nb, d, p, phase);
 }
 
 // hdiv = 1: the batched kernel also computes the next stage's h_divergence (k_recover_cells3_b)
@@ -975,7 +1004,7 @@ double coef_divdamp(const mpas_dyc_ctx* ctx, double dts) {  // 2761-2763
 void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int damp,
                     int phase, int fresh = 0, UnpackMap um = UnpackMap{}) {
   if (pair_layout(d)) {
-    const int64_t nw = (d.nEdges + 1) / 2;
+    const int64_t nw = ((phase == 2 ? d.n_bnd_pairs : d.nEdges) + 1) / 2;  // phase 2: the bnd_pairs list
     const bool up = um.recv != nullptr;
     if (damp && up)
       LAUNCH_E((k_acoustic_edges_p<true, true>), nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh, um);
@@ -1029,7 +1058,7 @@ void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double 
                         double invNs = 0.0, UnpackMap um = UnpackMap{}) {
   // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
   const bool up = um.recv != nullptr;
-  const int64_t nw = (d.nEdges + 1) / 2;
+  const int64_t nw = ((phase == 2 ? d.n_bnd_pairs : d.nEdges) + 1) / 2;  // phase 2: the bnd_pairs list
   const double cd = coef_divdamp(ctx, dts);
   if (pair_layout(d) && invNs > 0.0 && fused_recover_edges(d)) {
     if (up) LAUNCH_E((k_divdamp_p<true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um);
@@ -1383,8 +1412,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1));
         CHK(exchange_wait(ctx));
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2, d.nCellsSolve));
-        EACH(if (!fused_recover_edges(d) || ctx->blk[ib_].n_bnd_edges != 0)
-               LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
+        EACH(LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2));  // phase 2: the bnd_edges list
         if (lbc) {  // the w recovery reads ru before the specified-zone overwrite (934-987)
           EACH(recover_cells3(ctx, d, p, 0));
           EACH(LAUNCH(k_lbc_u, d.nEdges, d, p, dt_dynamics * (double)(dynamics_substep - 1) + rk_timestep[rk_step - 1]));
@@ -1402,7 +1430,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
              else LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0, 0));
         // the edges with two owned cells were recovered by the last damping if fused_recover_edges
         EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0);
-             else if (ctx->blk[ib_].n_bnd_edges != 0) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 2));
+             else LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2));
         // stages 1 and 2: also the next stage's h_divergence (dyn_tend then skips k_dyn_cells1)
         EACH(recover_cells3(ctx, d, p, 0, rk_step < 3 && !lbc));
         if (lbc)  // 934-987

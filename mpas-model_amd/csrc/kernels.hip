@@ -1465,7 +1465,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p, 
 
 template <int ME>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert_b(Dims d, Ptrs p, int phase) {
-  const int c = wave_elem(0);
+  int c = wave_elem(0);
+  if (phase == 2) {  // the compact bnd_cells list (owned cells with CELL_HALO_EDGE)
+    if (c >= d.n_bnd_cells) return;
+    c = __builtin_amdgcn_readfirstlane(p.bnd_cells[c]);
+  }
   if (c >= d.nCellsSolve) return;
   if (p.bdyMaskCell[c] > N_RELAX_ZONE) return;  // no conversion in the specified zone (2292; any run)
   const int k = lane_id(), K = d.K;
@@ -1575,6 +1579,23 @@ __device__ __forceinline__ int pair_wave() {
   return __builtin_amdgcn_readfirstlane(xcd_block() * EDGE_WPB + (threadIdx.x >> 6));
 }
 __device__ __forceinline__ int pair_half() { return (threadIdx.x >> 5) & 1; }
+// the two edges of this wavefront: consecutive edges, or in phase 2 of a split kernel consecutive
+// entries of the compact bnd_pairs list (halo-boundary edges with an owned cell); false: none
+__device__ __forceinline__ bool pair_edges(const Dims& d, const Ptrs& p, int phase, int& eA, int& eB, bool& hasB) {
+  const int i = 2 * pair_wave();
+  if (phase == 2) {
+    if (i >= d.n_bnd_pairs) return false;
+    hasB = i + 1 < d.n_bnd_pairs;
+    eA = __builtin_amdgcn_readfirstlane(p.bnd_pairs[i]);
+    eB = hasB ? __builtin_amdgcn_readfirstlane(p.bnd_pairs[i + 1]) : eA;
+    return true;
+  }
+  if (i >= d.nEdges) return false;
+  hasB = i + 1 < d.nEdges;
+  eA = i;
+  eB = hasB ? i + 1 : i;
+  return true;
+}
 __device__ __forceinline__ int sel(int h, int a, int b) { return h ? b : a; }
 __device__ __forceinline__ double sel(int h, double a, double b) { return h ? b : a; }
 
@@ -1979,10 +2000,9 @@ __device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMa
 template <bool REC = false, bool UP = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
                                                             int fresh, double invNs = 0.0, UnpackMap um = UnpackMap{}) {
-  const int eA = 2 * pair_wave();
-  if (eA >= d.nEdges) return;
-  const bool hasB = eA + 1 < d.nEdges;
-  const int eB = hasB ? eA + 1 : eA;
+  int eA, eB;
+  bool hasB;
+  if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
   const int lc = min(l, K / 2 - 1);
   const int e = sel(h, eA, eB);
@@ -2285,9 +2305,9 @@ template <bool DD, bool UP = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,
                                                                    double coef_divdamp, int phase, int fresh,
                                                                    UnpackMap um = UnpackMap{}) {
-  const int eA = 2 * pair_wave();
-  if (eA >= d.nEdges) return;
-  const int eB = min(eA + 1, d.nEdges - 1);
+  int eA, eB;
+  bool hasB;
+  if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
   const bool lev = 2 * l < K;                     // this lane holds levels 2l, 2l+1
   const int lc = min(l, K / 2 - 1);
@@ -2300,7 +2320,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
   auto active = [&](int2 ce, int bnd) {
     return (ce.x < d.nCellsSolve || ce.y < d.nCellsSolve) && !(phase && ((bnd != 0) != (phase == 2)));
   };
-  const bool onA = active(ceA, bA), onB = eA + 1 < d.nEdges && active(ceB, bB);
+  const bool onA = active(ceA, bA), onB = hasB && active(ceB, bB);
   if (!onA && !onB) return;
   const bool st = lev && (h ? onB : onA);
   if (small_step == 1) {
@@ -2757,8 +2777,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p
 }
 
 // edges (all): 3048-3059
+// phase 2 walks the compact bnd_edges list (the edges with edge_bnd set)
 __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs, int phase) {
-  const int e = wave_elem(0);
+  int e = wave_elem(0);
+  if (phase == 2) {
+    if (e >= d.n_bnd_edges) return;
+    e = __builtin_amdgcn_readfirstlane(p.bnd_edges[e]);
+  }
   if (e >= d.nEdges) return;
   if (phase && ((p.edge_bnd[e] != 0) != (phase == 2))) return;
   const int k = lane_id(), K = d.K;
