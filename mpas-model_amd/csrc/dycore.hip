@@ -1029,23 +1029,34 @@ bool fused_recover(const Dims& d) { return batched(d) && (d.maxEdges == 6 || d.m
 // true>) when fused_recover(d); rdt / invNs / rk_step are k_recover_cells1's arguments
 // keep_pp = 0: a fin launch need not store rho_pp / rw_p (see k_acoustic_cells_r)
 // pk: the block's fused-pack map of the exchange that follows (fused_pack_map), or none
+// dl: store rtheta_pp - rtheta_pp_old for the stage's last damping only (damping_delta)
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int fin = 0,
-                    double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1, PackMap pk = PackMap{}) {
+                    double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1, PackMap pk = PackMap{},
+                    int dl = 0) {
   if (batched(d) && d.maxEdges == 6) {
     if (fin)
       LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
-             pk);
+             pk, dl);
     else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, pk);
     return;
   }
   if (batched(d) && d.maxEdges == 7) {
     if (fin)
       LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
-             pk);
+             pk, dl);
     else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, pk);
     return;
   }
   LAUNCH(k_acoustic_cells, d.nCells, d, p, dts, small_step, ctx->cf.epssm);
+}
+
+// The stage's last cell phase hands its damping rtheta_pp - rtheta_pp_old instead of both
+// fields when nothing else reads them before the next stage: no exchange (the 845 and 876-887
+// exchanges and the halo-cell recovery read rtheta_pp) and not the dt's last stage (whose values
+// the pool keeps); the fused cell recovery takes rtheta_pp from registers.  Pair-layout damping
+// and record cell kernels only.
+inline int damping_delta(const mpas_dyc_ctx* ctx, const Dims& d, bool last_stage) {
+  return (!needs_exchange(ctx) && !last_stage && pair_layout(d) && fused_recover(d)) ? 1 : 0;
 }
 
 // the last damping of a stage also recovers the edges with two owned cells (k_divdamp_p<true>);
@@ -1054,18 +1065,19 @@ bool fused_recover_edges(const Dims& d) { return pair_layout(d) && fused_recover
 
 // fresh = 1: the stage had a single sub-step (no edge phase launched), see k_divdamp_p;
 // invNs > 0: recover the edges with two owned cells too (fused_recover_edges)
+// dl: rtheta_pp_old holds the difference (acoustic_cells with dl); pair layout only
 void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase, int fresh = 0,
-                        double invNs = 0.0, UnpackMap um = UnpackMap{}) {
+                        double invNs = 0.0, UnpackMap um = UnpackMap{}, int dl = 0) {
   // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
   const bool up = um.recv != nullptr;
   const int64_t nw = ((phase == 2 ? d.n_bnd_pairs : d.nEdges) + 1) / 2;  // phase 2: the bnd_pairs list
   const double cd = coef_divdamp(ctx, dts);
   if (pair_layout(d) && invNs > 0.0 && fused_recover_edges(d)) {
-    if (up) LAUNCH_E((k_divdamp_p<true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um);
-    else LAUNCH_E((k_divdamp_p<true, false>), nw, d, p, cd, phase, dts, fresh, invNs, um);
+    if (up) LAUNCH_E((k_divdamp_p<true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl);
+    else LAUNCH_E((k_divdamp_p<true, false>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl);
   } else if (pair_layout(d)) {
-    if (up) LAUNCH_E((k_divdamp_p<false, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um);
-    else LAUNCH_E((k_divdamp_p<false, false>), nw, d, p, cd, phase, dts, fresh, 0.0, um);
+    if (up) LAUNCH_E((k_divdamp_p<false, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl);
+    else LAUNCH_E((k_divdamp_p<false, false>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl);
   }
   else LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase,
               dts, fresh);
@@ -1383,7 +1395,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         const XPlan* xp = fused_pack_plan(ctx, xf);  // the cell phase packs this exchange's send buffer
         EACH(acoustic_cells(ctx, d, p, dts, small_step, small_step == nsub, rk_timestep[rk_step - 1],
                             1 / (double)nsub, rk_step, needs_exchange(ctx) || last_stage,
-                            xp ? xp->pack[ib_] : PackMap{}));
+                            xp ? xp->pack[ib_] : PackMap{}, damping_delta(ctx, d, last_stage)));
         if (split) {
           CHK(exchange_async(ctx, xf));
         } else {
@@ -1396,7 +1408,8 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         CHK(exchange_wait(ctx));
         EACH(divergence_damping(ctx, d, p, dts, 2, nsub == 1, 0.0, um_of(ib_)));
       } else {
-        EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1, 1 / (double)nsub, um_of(ib_)));
+        EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1, 1 / (double)nsub, um_of(ib_),
+                                damping_delta(ctx, d, last_stage)));
       }
       const std::vector<XField> xrec = {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},  // 876-887
                                         {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};

@@ -1997,9 +1997,11 @@ __device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMa
   return ld2(fld + o);
 }
 
+// dl = 1: rtheta_pp_old holds rtheta_pp - rtheta_pp_old (k_acoustic_cells_r<ME, true> with dl)
 template <bool REC = false, bool UP = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
-                                                            int fresh, double invNs = 0.0, UnpackMap um = UnpackMap{}) {
+                                                            int fresh, double invNs = 0.0, UnpackMap um = UnpackMap{},
+                                                            int dl = 0) {
   int eA, eB;
   bool hasB;
   if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
@@ -2025,13 +2027,21 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   if (!onA && !onB) return;
   const size_t o1 = (size_t)sel(h, ceA.x, ceB.x) * K + 2 * lc, o2 = (size_t)sel(h, ceA.y, ceB.y) * K + 2 * lc;
   const bool lv = 2 * l < K && (h ? onB : onA);
-  const d2 r1 = UP ? ld_pp(d, p, um, 0, sel(h, ceA.x, ceB.x), lc, lv) : ld2(p.rtheta_pp + o1);
-  const d2 r2 = UP ? ld_pp(d, p, um, 0, sel(h, ceA.y, ceB.y), lc, lv) : ld2(p.rtheta_pp + o2);
-  const d2 q1 = ld2(p.rtheta_pp_old + o1), q2 = ld2(p.rtheta_pp_old + o2);
+  d2 dd1, dd2;  // rtheta_pp - rtheta_pp_old at the two cells
+  if (dl) {
+    dd1 = ld2(p.rtheta_pp_old + o1);
+    dd2 = ld2(p.rtheta_pp_old + o2);
+  } else {
+    const d2 r1 = UP ? ld_pp(d, p, um, 0, sel(h, ceA.x, ceB.x), lc, lv) : ld2(p.rtheta_pp + o1);
+    const d2 r2 = UP ? ld_pp(d, p, um, 0, sel(h, ceA.y, ceB.y), lc, lv) : ld2(p.rtheta_pp + o2);
+    const d2 q1 = ld2(p.rtheta_pp_old + o1), q2 = ld2(p.rtheta_pp_old + o2);
+    dd1 = d2{r1.x - q1.x, r1.y - q1.y};
+    dd2 = d2{r2.x - q2.x, r2.y - q2.y};
+  }
   const d2 t1 = ld2(p.theta_m1 + o1), t2 = ld2(p.theta_m1 + o2);
   d2 out;
-  out.x = ru.x + coef_divdamp * (-(r2.x - q2.x) - -(r1.x - q1.x)) * (1.0 - mask) / (t1.x + t2.x);
-  out.y = ru.y + coef_divdamp * (-(r2.y - q2.y) - -(r1.y - q1.y)) * (1.0 - mask) / (t1.y + t2.y);
+  out.x = ru.x + coef_divdamp * (-(dd2.x) - -(dd1.x)) * (1.0 - mask) / (t1.x + t2.x);
+  out.y = ru.y + coef_divdamp * (-(dd2.y) - -(dd1.y)) * (1.0 - mask) / (t1.y + t2.y);
   if (!REC) {
     if ((h ? onB : onA) && 2 * l < K) {
       st2(p.ru_p + o, out);
@@ -2452,6 +2462,11 @@ __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p,
 // keep_pp = 0 (FIN only): rho_pp and rw_p are not stored.  After a stage's last sub-step nothing
 // reads them but the 876-887 exchange and the halo-cell recovery; srk3 passes 0 only for a block
 // without exchanges and a stage that is not the dt's last (whose values the pool keeps).
+// dl = 1 (FIN, keep_pp = 0, pair layout): the stage's last damping is the only reader of this
+// sub-step's rtheta_pp and rtheta_pp_old, and it needs only their difference (2771-2772), so the
+// column stores dtheta = rtheta_pp - rtheta_pp_old into rtheta_pp_old (the same subtraction the
+// damping would do) and no rtheta_pp: one stream fewer here and one fewer gather there
+// (k_divdamp_p with dl = 1)
 // the column's new rtheta_pp / rho_pp into its send-buffer slots (PackMap), lane k = level k
 __device__ __forceinline__ void pack_column(const PackMap& pk, int c, int k, bool act, double rt, double rho) {
   if (!pk.start) return;
@@ -2466,7 +2481,7 @@ template <int ME, bool FIN = false>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs p, double dts, int small_step,
                                                                     double epssm, double rdt = 0.0,
                                                                     double invNs = 0.0, int rk_step = 0,
-                                                                    int keep_pp = 1, PackMap pk = PackMap{}) {
+                                                                    int keep_pp = 1, PackMap pk = PackMap{}, int dl = 0) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
   const int k = lane_id(), K = d.K;
@@ -2479,7 +2494,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
   const bool first = small_step == 1;
   double rtpp = first ? 0.0 : p.rtheta_pp[o];
   if (c >= d.nCellsSolve) {
-    if (act) p.rtheta_pp_old[o] = first ? 0.0 : rtpp;
+    if (act) p.rtheta_pp_old[o] = (FIN && dl) ? rtpp - (first ? 0.0 : rtpp) : (first ? 0.0 : rtpp);
     return;
   }
   int re[ME], rc[ME];
@@ -2555,9 +2570,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
     const double rho_new = rs - cofrz * (rwp_p2 - rwp);
     const double rt_new = ts - rdzw * (coftz_p * rwp_p2 - coftz * rwp);
     if (act) {
-      p.rtheta_pp_old[o] = rtpp_old;  // stored last: no store precedes the loads above
+      if (FIN && dl) {
+        p.rtheta_pp_old[o] = rt_new - rtpp_old;
+      } else {
+        p.rtheta_pp_old[o] = rtpp_old;  // stored last: no store precedes the loads above
+        p.rtheta_pp[o] = rt_new;
+      }
       if (!FIN || keep_pp) p.rho_pp[o] = rho_new;
-      p.rtheta_pp[o] = rt_new;
     }
     if (actw) {
       if (!FIN || keep_pp) p.rw_p[ow] = rwp;
@@ -2573,9 +2592,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       rtpp = rtpp + dts * tth;
       rwp = rwp + dts * tw;
       wwa = wwa + 0.5 * (1.0 + epssm) * rwp;
-      p.rtheta_pp_old[o] = rtpp_old;
+      if (FIN && dl) {
+        p.rtheta_pp_old[o] = rtpp - rtpp_old;
+      } else {
+        p.rtheta_pp_old[o] = rtpp_old;
+        p.rtheta_pp[o] = rtpp;
+      }
       p.rho_pp[o] = rhopp;
-      p.rtheta_pp[o] = rtpp;
     }
     if (actw) {
       p.rw_p[ow] = rwp;
