@@ -2397,7 +2397,9 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
 // recover_cells1 (2998-3040) of owned cell c from the final sub-step's new rho_pp / rtheta_pp /
 // rw_p / wwAvg, still in registers (k_acoustic_cells_r<ME, true>): the same expressions as
 // k_recover_cells1, lane for lane (inactive lanes see zz = fzm = fzp = 0 there too).
-// The recovery's own operands (RecIn) are loaded with the sub-step's, before the solve.
+// The recovery's own operands (RecIn) are loaded after the tridiagonal solve: loaded with the
+// sub-step's operands they held 12 more VGPRs across it (134 -> 122 VGPRs, 3 -> 4 waves/SIMD;
+// -0.1 ms per dt same box, profiles/r02_ab_recin_late.log).
 struct RecIn {
   double rps, rb, rtps, rtb, exb, rtd;
 };
@@ -2526,7 +2528,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
   const double rz = p.rho_zz2[o], dss = p.dss[o], rws = p.rw_save[ow], rw = p.rw[ow], w2 = p.w2[ow];
   const double cofrz = p.cofrz[kc], rdzw = p.rdzw[kc], fzm = p.fzm[kc], fzp = p.fzp[kc];
   RecIn ri{};
-  if (FIN) ri = load_rec_in(d, p, o, rk_step);
   const double rtpp_old = (small_step == 1) ? 0.0 : rtpp;
   const double resm = (1.0 - epssm) / (1.0 + epssm);
   if (small_step == 1) { wwa = 0.0; rhopp = 0.0; rtpp = 0.0; rwp = 0.0; }
@@ -2584,6 +2585,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;  // levels 2..K: recover_cell_fused
     }
     pack_column(pk, c, k, act, rt_new, rho_new);
+    if (FIN) ri = load_rec_in(d, p, o, rk_step);
     if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rho_new, rt_new, rwp, wwa, rdt, invNs, rk_step);
   } else {
     // specified zone (2710-2719): regional only, masks are 0 for global meshes
@@ -2606,6 +2608,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;
     }
     pack_column(pk, c, k, act, rtpp, rhopp);
+    if (FIN) ri = load_rec_in(d, p, o, rk_step);
     if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rhopp, rtpp, rwp, wwa, rdt, invNs, rk_step);
   }
 }
