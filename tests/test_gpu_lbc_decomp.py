@@ -66,8 +66,10 @@ def _run(dy, case, lbc, set_lbc_pool):
     dy.synchronize()
 
 
-@pytest.mark.parametrize("moist", [False, True])
-def test_regional_blocks_bitwise_equal_single_block(moist):
+@pytest.mark.parametrize("moist,rccl", [(False, False), (True, False), (True, True)])
+def test_regional_blocks_bitwise_equal_single_block(moist, rccl):
+    """rccl: the blocks exchange through RCCL (send to self) with split-phase exchanges and graph
+    replay, as ranks of a multi-GPU run do."""
     from mpas_dycore import Dycore, decomp
     from oracle import ref_runner
     case, lbc = _case(moist)
@@ -84,7 +86,9 @@ def test_regional_blocks_bitwise_equal_single_block(moist):
     one.close()
 
     blocks = decomp.decompose(case, decomp.partition_sfc(case["nCells"], 8))
-    dy = Dycore.from_blocks(blocks, device=0, moist_end=me)
+    comm_id = Dycore.comm_unique_id() if rccl else None
+    dy = Dycore.from_blocks(blocks, device=0, moist_end=me, comm_id=comm_id, nranks=1, rank=0, rccl_local=rccl)
+    dy.use_graph(rccl)
 
     def pool_blocks(d):
         for i, b in enumerate(blocks):
