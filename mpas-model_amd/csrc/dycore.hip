@@ -2413,23 +2413,23 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
   const Ptrs p = make_ptrs(ctx, b);
   const Dims& d = b.d;
   // the sequence srk3 runs for a `reps`-sub-step acoustic loop: edges, cells, then per further
-  // sub-step the damped edge phase and cells, and the last sub-step's damping on its own
+  // sub-step the damped edge phase and cells, and the last sub-step's damping on its own.  One
+  // event between consecutive launches, read after the loop: the kernels run back to back as in
+  // srk3, and no host launch latency after an idle queue lands inside a kernel's interval.
   double acc[3] = {0, 0, 0};
   float t;
+  std::vector<hipEvent_t> ev(ms_kernels ? 2 * (size_t)reps + 1 : 0);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  auto destroy = [&]() {
+    for (auto& e : ev) (void)hipEventDestroy(e);
+  };
   HIPCHK(hipEventRecord(ctx->ev[0], ctx->stream));
+  if (ms_kernels) HIPCHK(hipEventRecord(ev[0], ctx->stream));
   for (int r = 0; r < reps; ++r) {
-    HIPCHK(hipEventRecord(ctx->ev[1], ctx->stream));
     acoustic_edges(ctx, d, p, dts, small_step, r > 0 ? 1 : 0, 0);
-    HIPCHK(hipEventRecord(ctx->ev[2], ctx->stream));
+    if (ms_kernels) HIPCHK(hipEventRecord(ev[2 * r + 1], ctx->stream));
     acoustic_cells(ctx, d, p, dts, small_step);
-    HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
-    if (ms_kernels) {
-      HIPCHK(hipEventSynchronize(ctx->ev[3]));
-      (void)hipEventElapsedTime(&t, ctx->ev[1], ctx->ev[2]);
-      acc[0] += t;
-      (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]);
-      acc[1] += t;
-    }
+    if (ms_kernels) HIPCHK(hipEventRecord(ev[2 * r + 2], ctx->stream));
   }
   HIPCHK(hipEventRecord(ctx->ev[3], ctx->stream));
   divergence_damping(ctx, d, p, dts, 0);
@@ -2437,6 +2437,13 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
   HIPCHK(hipEventSynchronize(ctx->ev[4]));
   (void)hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]);
   acc[2] += t;
+  for (int r = 0; ms_kernels && r < reps; ++r) {
+    (void)hipEventElapsedTime(&t, ev[2 * r], ev[2 * r + 1]);
+    acc[0] += t;
+    (void)hipEventElapsedTime(&t, ev[2 * r + 1], ev[2 * r + 2]);
+    acc[1] += t;
+  }
+  destroy();
   float tot;
   HIPCHK(hipEventElapsedTime(&tot, ctx->ev[0], ctx->ev[4]));
   if (ms_out) *ms_out = tot / reps;
