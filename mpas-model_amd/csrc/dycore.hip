@@ -56,7 +56,6 @@ struct Block {
   std::map<std::string, int> by_name;  // "pool.name"
   std::vector<XList> xl;
   int64_t nEdges_act = -1;             // edges with an owned cell (from cellsOnEdge), for B_ac
-  int64_t n_bnd_edges = -1;            // edges with a halo (or garbage) cell, from compute_bnd
   std::vector<int32_t> h_coe, h_eoc, h_noc;  // host copies (0-based) for the halo-boundary flags
   // summarize_timestep records (summary.hip): partials and one SUM_REC record per field
   double* sum_part = nullptr;
@@ -783,11 +782,8 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
       return MPAS_DYC_ESTATE;
     }
     std::vector<int32_t> eb(d.nEdges + 1, 1), cb(d.nCells + 1, 1);
-    b.n_bnd_edges = 0;
-    for (int e = 0; e < d.nEdges; ++e) {
+    for (int e = 0; e < d.nEdges; ++e)
       eb[e] = (b.h_coe[2 * e] >= d.nCellsSolve || b.h_coe[2 * e + 1] >= d.nCellsSolve) ? 1 : 0;
-      b.n_bnd_edges += eb[e];
-    }
     for (int c = 0; c < d.nCells; ++c) {
       int bnd = c >= d.nCellsSolve ? CELL_HALO_EDGE | CELL_BND_EDGE : 0;
       for (int i = 0; i < b.h_noc[c]; ++i) {
