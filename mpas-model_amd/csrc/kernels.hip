@@ -2732,14 +2732,18 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_cells_p(Dims d, Ptrs 
     const d2 r = rwp;
     d2 x = r;
     for (int it = 0; it < K / 2; ++it) {
-      const double xm = l == 0 ? 0.0 : lane_shr1(x.y);  // level 2l-1, 0 below the column
+      // the lane shift is taken by every lane before the select: a DPP read from a lane that a
+      // branch has switched off returns the reader's own old value, not the neighbour's
+      const double sh = lane_shr1(x.y);
+      const double xm = l == 0 ? 0.0 : sh;  // level 2l-1, 0 below the column
       x.x = (r.x - afx * xm) * alx;
       x.y = (r.y - afy * x.x) * aly;
     }
     const d2 xf = x;
     const double gbx = ax ? gamma_tri.x : 0.0, gby = ay ? gamma_tri.y : 0.0;
     for (int it = 0; it < K / 2; ++it) {
-      const double xp = 2 * l + 2 <= K ? lane_shl1(x.x) : 0.0;  // level 2l+2; 0 above level K
+      const double sh = lane_shl1(x.x);
+      const double xp = 2 * l + 2 <= K ? sh : 0.0;  // level 2l+2; 0 above level K
       x.y = xf.y - gby * xp;
       x.x = xf.x - gbx * x.y;
     }
