@@ -37,7 +37,6 @@ struct Dims {
   int lbc;                     // config_apply_lbcs: regional lateral boundary conditions (lbc.hip)
   // lengths of the compact phase-2 lists of the split-phase kernels (compute_bnd; Ptrs::bnd_*)
   int n_bnd_edges, n_bnd_pairs, n_bnd_cells;
-  int spec_cells;  // some specZoneMaskCell is nonzero (the acoustic cell phase's specified-zone branch)
 };
 
 struct Config {

@@ -23,9 +23,6 @@
 
 using namespace mpas;
 
-#ifndef ACOUSTIC_CELLS_PAIR
-#define ACOUSTIC_CELLS_PAIR false
-#endif
 namespace {
 
 enum Loc { L_CELL, L_EDGE, L_VERTEX, L_NONE };
@@ -123,7 +120,6 @@ struct mpas_dyc_ctx {
   ncclComm_t comm = nullptr;
   bool rccl_local = false;              // route block-to-block copies of this process through RCCL too
   bool fused_pack_enabled = true;       // MPAS_DYCORE_FUSED_PACK=0: pack kernel instead (A/B)
-  bool cells_pair = ACOUSTIC_CELLS_PAIR;  // MPAS_DYCORE_CELLS_PAIR=0|1: k_acoustic_cells_p or the one-column kernel
   bool lbc = false;                     // config_apply_lbcs (mpas_dyc_set_lbc)
   bool planning = false;                // dry run: build exchange plans, launch nothing
   bool planned[2] = {false, false};
@@ -1029,11 +1025,6 @@ bool fused_recover(const Dims& d) { return batched(d) && (d.maxEdges == 6 || d.m
 // true>) when fused_recover(d); rdt / invNs / rk_step are k_recover_cells1's arguments
 // keep_pp = 0: a fin launch need not store rho_pp / rw_p (see k_acoustic_cells_r)
 // pk: the block's fused-pack map of the exchange that follows (fused_pack_map), or none
-// the pair-layout cell phase (k_acoustic_cells_p) for sub-steps that are not a stage's last: no
-// fused pack, no specified zone; MPAS_DYCORE_CELLS_PAIR=0 keeps the one-column kernel
-inline bool cells_pair(const mpas_dyc_ctx* ctx, const Dims& d, const PackMap& pk) {
-  return ctx->cells_pair && pair_layout(d) && !pk.start && !d.spec_cells && !d.lbc;
-}
 // dl: store rtheta_pp - rtheta_pp_old for the stage's last damping only (damping_delta)
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int fin = 0,
                     double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1, PackMap pk = PackMap{},
@@ -1042,7 +1033,6 @@ void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
     if (fin)
       LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
              pk, dl);
-    else if (cells_pair(ctx, d, pk)) LAUNCH_E(k_acoustic_cells_p<6>, (d.nCells + 1) / 2, d, p, dts, small_step, ctx->cf.epssm);
     else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, pk);
     return;
   }
@@ -1050,7 +1040,6 @@ void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
     if (fin)
       LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
              pk, dl);
-    else if (cells_pair(ctx, d, pk)) LAUNCH_E(k_acoustic_cells_p<7>, (d.nCells + 1) / 2, d, p, dts, small_step, ctx->cf.epssm);
     else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, pk);
     return;
   }
@@ -1750,7 +1739,6 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
     g_kernel_tier = 2;
   }
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
-  if (const char* cp = getenv("MPAS_DYCORE_CELLS_PAIR")) ctx->cells_pair = std::string(cp) != "0";
   for (auto& b : ctx->blk) {
     build_registry(b);
     for (auto& f : b.fields) {
@@ -1912,13 +1900,6 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
       ctx->bnd_ready = false;
     }
     if (f->pool == "mesh" && (f->name == "zb_cell" || f->name == "zb3_cell")) ctx->bnd_ready = false;  // zb_p / zb_m
-    if (f->pool == "mesh" && f->name == "specZoneMaskCell") {
-      const double* h = (const double*)host;
-      int nz = 0;
-      for (int64_t i = 0; i < nb / 8 - 1 && !nz; ++i) nz = h[i] != 0.0;  // the garbage slot aside
-      if (b.d.spec_cells != nz) invalidate_plans(ctx);  // captured steps bake the kernel choice in
-      b.d.spec_cells = nz;
-    }
     if (f->pool == "tend" && f->name == "rt_diabatic_tend") {
       const double* h = (const double*)host;
       int nz = 0;

@@ -2613,182 +2613,6 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
   }
 }
 
-// The cell phase of a sub-step that is not a stage's last (k_acoustic_cells_r<ME, false>) in the
-// pair layout: one wavefront carries two cells (lanes 0-31 and 32-63), each lane the two levels
-// (2l, 2l+1), so every column load is one 16-byte load per lane and the 21 own columns and
-// 2 ME gathers of a cell cost half the load instructions.  The tridiagonal sweeps run as
-// two-level lane-shift sweeps (K/2 iterations each way): every level's final value is evaluated
-// from exactly the operands of the sequential recurrence (2675-2682), as in thomas_column, so the
-// bits are those of k_acoustic_cells_r.  Global meshes (no specified zone) and no fused pack.
-template <int ME>
-__global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_cells_p(Dims d, Ptrs p, double dts, int small_step,
-                                                                   double epssm) {
-  const int cA = 2 * pair_wave();
-  if (cA >= d.nCells) return;
-  const bool hasB = cA + 1 < d.nCells;
-  const int cB = hasB ? cA + 1 : cA;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int c = sel(h, cA, cB);
-  const bool mine = h == 0 || hasB;
-  const int kx = 2 * l, ky = 2 * l + 1;
-  const bool ax = kx < K, ay = ky < K, axw = kx <= K, ayw = ky <= K;
-  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
-  const size_t K1 = K + 1;
-  const size_t o = (size_t)c * K + 2 * lc, ow = (size_t)c * K1 + 2 * lw;
-  const bool first = small_step == 1;
-  auto Z = [](bool a, double v) { return a ? v : 0.0; };
-  d2 rtpp = first ? d2{0.0, 0.0} : ld2(p.rtheta_pp + o);
-  const bool ownA = cA < d.nCellsSolve, ownB = hasB && cB < d.nCellsSolve;
-  const bool own = h ? ownB : ownA;
-  if (!own) {  // halo cell (or no cell): rtheta_pp_old only (2603-2611)
-    if (mine && ax) {
-      const d2 v = first ? d2{0.0, 0.0} : rtpp;
-      if (ay) st2(p.rtheta_pp_old + o, v);
-      else p.rtheta_pp_old[o] = v.x;
-    }
-    if (!ownA && !ownB) return;
-  }
-  // records of both cells (wave-uniform loads), then per half
-  int re[ME], rc[ME];
-  double sdv[ME];
-#pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    re[i] = sel(h, p.cell_rec[(size_t)cA * CELL_REC + i], p.cell_rec[(size_t)cB * CELL_REC + i]);
-    rc[i] = sel(h, p.cell_rec[(size_t)cA * CELL_REC + CELL_REC_ME + i], p.cell_rec[(size_t)cB * CELL_REC + CELL_REC_ME + i]);
-    sdv[i] = sel(h, ld_uniform_f64(p.cell_sdv + (size_t)cA * ME + i), ld_uniform_f64(p.cell_sdv + (size_t)cB * ME + i));
-  }
-  const int ne = sel(h, p.cell_rec[(size_t)cA * CELL_REC + 14], p.cell_rec[(size_t)cB * CELL_REC + 14]);
-  const double invA = sel(h, ld_uniform_f64(p.invAreaCell + cA), ld_uniform_f64(p.invAreaCell + cB));
-  d2 rhopp = first ? d2{0.0, 0.0} : ld2(p.rho_pp + o);
-  d2 rwp = first ? d2{0.0, 0.0} : ld2(p.rw_p + ow);
-  d2 wwa = first ? d2{0.0, 0.0} : ld2(p.wwAvg + ow);
-  const d2 thc = ld2(p.theta_m1 + o), trho = ld2(p.tend_rho + o), tth = ld2(p.tend_theta + o);
-  d2 ru[ME], th[ME];
-  const double* __restrict__ rusrc = first ? p.tend_u : p.ru_p;
-#pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    ru[i] = ld2(rusrc + (size_t)re[i] * K + 2 * lc);
-    th[i] = ld2(p.theta_m1 + (size_t)rc[i] * K + 2 * lc);
-  }
-  if (first) {
-#pragma unroll
-    for (int i = 0; i < ME; ++i) ru[i] = d2{dts * ru[i].x, dts * ru[i].y};
-  }
-  const d2 coftz = ld2(p.coftz + ow);
-  const d2 cofrz = ld2(p.cofrz + 2 * lc), rdzw = ld2(p.rdzw + 2 * lc);
-  const d2 rtpp_old = first ? d2{0.0, 0.0} : rtpp;
-  const double resm = (1.0 - epssm) / (1.0 + epssm);
-  // levels >= K take the values the one-column kernel gives its lanes >= K: zero rho_pp /
-  // rtheta_pp, and level K's rw_p / wwAvg in the slot of level K+1 (which does not exist)
-  if (!ax) { rhopp.x = 0.0; rtpp.x = 0.0; }
-  if (!ay) { rhopp.y = 0.0; rtpp.y = 0.0; }
-  if (!ayw) { rwp.y = rwp.x; wwa.y = wwa.x; }  // a clamped lane loads level K
-  if (!axw) { rwp.x = 0.0; wwa.x = 0.0; rwp.y = 0.0; wwa.y = 0.0; }
-  // horizontal flux divergence (2629-2639)
-  d2 ts{0.0, 0.0}, rs{0.0, 0.0};
-#pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    if (i < ne) {
-      const double fx = dts * sdv[i] * ru[i].x * invA, fy = dts * sdv[i] * ru[i].y * invA;
-      rs.x = rs.x - fx;
-      rs.y = rs.y - fy;
-      ts.x = ts.x - fx * 0.5 * (th[i].x + thc.x);
-      ts.y = ts.y - fy * 0.5 * (th[i].y + thc.y);
-    }
-  }
-  const d2 coftz_p = kp1(coftz), rwp_p = kp1(rwp);
-  if (ax) {
-    rs.x = rhopp.x + dts * trho.x + rs.x - cofrz.x * resm * (rwp_p.x - rwp.x);
-    ts.x = rtpp.x + dts * tth.x + ts.x - resm * rdzw.x * (coftz_p.x * rwp_p.x - coftz.x * rwp.x);
-  }
-  if (ay) {
-    rs.y = rhopp.y + dts * trho.y + rs.y - cofrz.y * resm * (rwp_p.y - rwp.y);
-    ts.y = rtpp.y + dts * tth.y + ts.y - resm * rdzw.y * (coftz_p.y * rwp_p.y - coftz.y * rwp.y);
-  }
-  if (ax && kx >= 1) wwa.x = wwa.x + 0.5 * (1.0 - epssm) * rwp.x;
-  if (ay) wwa.y = wwa.y + 0.5 * (1.0 - epssm) * rwp.y;
-  // rw_p right-hand side (2660-2670); each phase loads its own operands (VGPRs)
-  const d2 tw = ld2(p.tend_w + ow), zz = ld2(p.zz + o), cofwt = ld2(p.cofwt + o), cofwz = ld2(p.cofwz + o), cofwr = ld2(p.cofwr + o);
-  const d2 zzm = km1(zz, l), tsm = km1(ts, l), rsm = km1(rs, l), rtppm = km1(rtpp, l), rhoppm = km1(rhopp, l);
-  const d2 cofwtm = km1(cofwt, l);
-  auto rhs = [&](double rwp_, double tw_, double cofwz_, double zz_, double ts_, double zzm_, double tsm_,
-                 double rtpp_, double rtppm_, double cofwr_, double rs_, double rsm_, double rhopp_, double rhoppm_,
-                 double cofwt_, double cofwtm_) {
-    return rwp_ + dts * tw_ - cofwz_ * ((zz_ * ts_ - zzm_ * tsm_) + resm * (zz_ * rtpp_ - zzm_ * rtppm_)) -
-           cofwr_ * ((rs_ + rsm_) + resm * (rhopp_ + rhoppm_)) + cofwt_ * (ts_ + resm * rtpp_) +
-           cofwtm_ * (tsm_ + resm * rtppm_);
-  };
-  if (ax && kx >= 1)
-    rwp.x = rhs(rwp.x, tw.x, cofwz.x, zz.x, ts.x, zzm.x, tsm.x, rtpp.x, rtppm.x, cofwr.x, rs.x, rsm.x, rhopp.x,
-                rhoppm.x, cofwt.x, cofwtm.x);
-  if (ay)
-    rwp.y = rhs(rwp.y, tw.y, cofwz.y, zz.y, ts.y, zzm.y, tsm.y, rtpp.y, rtppm.y, cofwr.y, rs.y, rsm.y, rhopp.y,
-                rhoppm.y, cofwt.y, cofwtm.y);
-  // tridiagonal solve (2675-2682) as two-level lane-shift sweeps (see thomas_column)
-  {
-    const d2 a_tri = ld2(p.a_tri + o), alpha_tri = ld2(p.alpha_tri + o), gamma_tri = ld2(p.gamma_tri + o);
-    const bool fx = kx >= 1 && ax, fy = ay;
-    const double afx = fx ? a_tri.x : 0.0, alx = fx ? alpha_tri.x : 1.0, afy = fy ? a_tri.y : 0.0, aly = fy ? alpha_tri.y : 1.0;
-    const d2 r = rwp;
-    d2 x = r;
-    for (int it = 0; it < K / 2; ++it) {
-      // the lane shift is taken by every lane before the select: a DPP read from a lane that a
-      // branch has switched off returns the reader's own old value, not the neighbour's
-      const double sh = lane_shr1(x.y);
-      const double xm = l == 0 ? 0.0 : sh;  // level 2l-1, 0 below the column
-      x.x = (r.x - afx * xm) * alx;
-      x.y = (r.y - afy * x.x) * aly;
-    }
-    const d2 xf = x;
-    const double gbx = ax ? gamma_tri.x : 0.0, gby = ay ? gamma_tri.y : 0.0;
-    for (int it = 0; it < K / 2; ++it) {
-      const double sh = lane_shl1(x.x);
-      const double xp = 2 * l + 2 <= K ? sh : 0.0;  // level 2l+2; 0 above level K
-      x.y = xf.y - gby * xp;
-      x.x = xf.x - gbx * x.y;
-    }
-    rwp = x;
-  }
-  // implicit Rayleigh damping of w (2687-2693)
-  const d2 rz = ld2(p.rho_zz2 + o), dss = ld2(p.dss + o), rws = ld2(p.rw_save + ow), rw = ld2(p.rw + ow);
-  const d2 w2 = ld2(p.w2 + ow), fzm = ld2(p.fzm + 2 * lc), fzp = ld2(p.fzp + 2 * lc);
-  const d2 rzm = km1(rz, l);
-  auto ray = [&](double rwp_, double rws_, double rw_, double dss_, double fzm_, double zz_, double fzp_,
-                 double zzm_, double rz_, double rzm_, double w2_) {
-    const double dd = rws_ - rw_;
-    return (rwp_ + dd - dts * dss_ * (fzm_ * zz_ + fzp_ * zzm_) * (fzm_ * rz_ + fzp_ * rzm_) * w2_) / (1.0 + dts * dss_) - dd;
-  };
-  if (ax && kx >= 1) {
-    rwp.x = ray(rwp.x, rws.x, rw.x, dss.x, fzm.x, zz.x, fzp.x, zzm.x, rz.x, rzm.x, w2.x);
-    wwa.x = wwa.x + 0.5 * (1.0 + epssm) * rwp.x;
-  }
-  if (ay) {
-    rwp.y = ray(rwp.y, rws.y, rw.y, dss.y, fzm.y, zz.y, fzp.y, zzm.y, rz.y, rzm.y, w2.y);
-    wwa.y = wwa.y + 0.5 * (1.0 + epssm) * rwp.y;
-  }
-  const d2 rwp_p2 = kp1(rwp);
-  const d2 rho_new{rs.x - cofrz.x * (rwp_p2.x - rwp.x), rs.y - cofrz.y * (rwp_p2.y - rwp.y)};
-  const d2 rt_new{ts.x - rdzw.x * (coftz_p.x * rwp_p2.x - coftz.x * rwp.x),
-                  ts.y - rdzw.y * (coftz_p.y * rwp_p2.y - coftz.y * rwp.y)};
-  if (!own || !mine) return;
-  if (ax && ay) {
-    st2(p.rtheta_pp_old + o, rtpp_old);
-    st2(p.rho_pp + o, rho_new);
-    st2(p.rtheta_pp + o, rt_new);
-  } else if (ax) {
-    p.rtheta_pp_old[o] = rtpp_old.x;
-    p.rho_pp[o] = rho_new.x;
-    p.rtheta_pp[o] = rt_new.x;
-  }
-  if (axw && ayw) {
-    st2(p.rw_p + ow, rwp);
-    st2(p.wwAvg + ow, wwa);
-  } else if (axw) {
-    p.rw_p[ow] = rwp.x;
-    p.wwAvg[ow] = wwa.x;
-  }
-}
-
 // cell phase (2603-2721): rtheta_pp_old for all cells, column solve for owned cells
 __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p, double dts, int small_step, double epssm) {
   const int c = wave_elem(0);
