@@ -1,0 +1,52 @@
+# One runner for every GPU-box job (replaces the one-off tools/gpu_*.sh of rounds 1-2).
+#
+#   gpurun -- 'bash tools/gpu.sh STEP [STEP ...]'
+#
+# Steps run in order and the run stops at the first failure (each GPU step has its own time
+# limit).  Output goes to gpurun_out/<step>.log; a summary line per step goes to stdout.
+#   tests            pytest -m "gpu and not slow"            (TESTS="files or -k expr" to narrow)
+#   tests_full       pytest -m gpu (full-size BASELINE configs included)
+#   bench            bench.py default line (configs[2] mesh, configs[1] line, cpu_baseline)
+#   bench_fast       bench.py without cpu_baseline / configs[1]
+#   moist            bench.py --moist (configs[3])
+#   varres           bench.py --varres 835586 (configs[4])
+#   prof             rocprofv3 --kernel-trace --stats of bench.py (gpurun_out/prof)
+#   pmc              two rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE (gpurun_out/pmc_*)
+#   rank             tools/rank_emulation.py --parts 1 2 4 8
+#   blocks8          bench.py --blocks 8 --rccl-local (the 8-GPU decomposition on one device)
+#   prof8b           rocprofv3 kernel trace of blocks8 (gpurun_out/prof8b)
+#   ab               same-box A/B of AB_LIBS (default exp/lib_base.so vs the in-tree library),
+#                    AB_ROUNDS rounds of tools/kbench.py (AB_ARGS extra arguments)
+#   smoke            __graft_entry__.smoke()
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out || exit 1
+B="--no-cpu-baseline --no-configs1"
+last() { tail -1 "$1" | cut -c1-${2:-400}; }
+step() {
+  case "$1" in
+    tests) timeout -k 10 1000 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m "gpu and not slow" ${TESTS:-tests} > gpurun_out/tests.log 2>&1; r=$?; tail -2 gpurun_out/tests.log; return $r ;;
+    tests_full) timeout -k 10 1100 python -u -m pytest -x -v --timeout 900 --timeout-method thread -m gpu ${TESTS:-tests} > gpurun_out/tests_full.log 2>&1; r=$?; tail -2 gpurun_out/tests_full.log; return $r ;;
+    bench) timeout -k 10 400 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1 && last gpurun_out/bench.log 700 ;;
+    bench_fast) timeout -k 10 300 python bench.py --steps 10 --warmup 2 $B > gpurun_out/bench_fast.log 2>&1 && last gpurun_out/bench_fast.log ;;
+    moist) timeout -k 10 400 python bench.py --steps 10 --warmup 2 --moist $B > gpurun_out/moist.log 2>&1 && last gpurun_out/moist.log 300 ;;
+    varres) timeout -k 10 600 python bench.py --steps 5 --warmup 1 --varres 835586 $B > gpurun_out/varres.log 2>&1 && last gpurun_out/varres.log 300 ;;
+    prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 $B ${PROF_ARGS} > gpurun_out/prof.log 2>&1 && last gpurun_out/prof.log 200 ;;
+    pmc) A="--steps 1 --warmup 1 $B --no-graph --acoustic-reps 5 ${BENCH_ARGS}" &&
+         timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o fetch --output-format csv -- python3 bench.py $A > gpurun_out/pmc_fetch.log 2>&1 &&
+         timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 bench.py $A > gpurun_out/pmc_write.log 2>&1 && echo "pmc done" ;;
+    rank) timeout -k 10 400 python tools/rank_emulation.py --parts 1 2 4 8 > gpurun_out/rank.log 2>&1 && tail -4 gpurun_out/rank.log ;;
+    blocks8) timeout -k 10 400 python bench.py --blocks 8 --rccl-local --steps 5 --warmup 2 $B > gpurun_out/blocks8.log 2>&1 && last gpurun_out/blocks8.log 300 ;;
+    prof8b) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8b -o run --output-format csv -- python3 bench.py --blocks 8 --rccl-local --steps 3 --warmup 1 $B > gpurun_out/prof8b.log 2>&1 && echo "prof8b done" ;;
+    ab) rm -f gpurun_out/ab.log
+        for r in ${AB_ROUNDS:-1 2 3}; do for L in ${AB_LIBS:-exp/lib_base.so mpas-model_amd/csrc/libmpas_dycore.so}; do
+          echo "== $L" >> gpurun_out/ab.log
+          MPAS_DYCORE_LIB=$L timeout -k 10 250 python tools/kbench.py --steps ${AB_STEPS:-10} ${AB_ARGS} >> gpurun_out/ab.log 2>&1 || return 1
+        done; done; grep -h "==\|ms_dt" gpurun_out/ab.log | cut -c1-200 ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && last gpurun_out/smoke.log ;;
+    *) echo "unknown step $1"; return 2 ;;
+  esac
+}
+for s in "$@"; do
+  echo "### $s"
+  step "$s" || { echo "### $s FAILED ($?)"; exit 1; }
+done
+echo "### all steps ok"
