@@ -13,6 +13,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of bench.py (gpurun_out/prof)
 #   pmc              two rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE (gpurun_out/pmc_*)
 #   rank             tools/rank_emulation.py --parts 1 2 4 8
+#   prof8            rocprofv3 kernel trace of one rank's block of an 8-way split (rank emulation)
 #   blocks8          bench.py --blocks 8 --rccl-local (the 8-GPU decomposition on one device)
 #   prof8b           rocprofv3 kernel trace of blocks8 (gpurun_out/prof8b)
 #   ab               same-box A/B of AB_LIBS (default exp/lib_base.so vs the in-tree library),
@@ -34,6 +35,7 @@ step() {
          timeout -s KILL 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o fetch --output-format csv -- python3 bench.py $A > gpurun_out/pmc_fetch.log 2>&1 &&
          timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 bench.py $A > gpurun_out/pmc_write.log 2>&1 && echo "pmc done" ;;
     rank) timeout -k 10 400 python tools/rank_emulation.py --parts 1 2 4 8 > gpurun_out/rank.log 2>&1 && tail -4 gpurun_out/rank.log ;;
+    prof8) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --steps 10 > gpurun_out/prof8.log 2>&1 && echo "prof8 done" ;;
     blocks8) timeout -k 10 400 python bench.py --blocks 8 --rccl-local --steps 5 --warmup 2 $B > gpurun_out/blocks8.log 2>&1 && last gpurun_out/blocks8.log 300 ;;
     prof8b) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8b -o run --output-format csv -- python3 bench.py --blocks 8 --rccl-local --steps 3 --warmup 1 $B > gpurun_out/prof8b.log 2>&1 && echo "prof8b done" ;;
     ab) rm -f gpurun_out/ab.log
