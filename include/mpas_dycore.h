@@ -97,7 +97,11 @@ int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt);
 int mpas_dyc_solve_diagnostics(mpas_dyc_ctx* ctx, double dt);
 /* atm_timestep -> atm_srk3: advance time level 1 to time level 2 by dt. Asynchronous. */
 int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep);
-/* mpas_pool_shift_time_levels(state): swap time levels 1 and 2 (pointer swap). */
+/* mpas_pool_shift_time_levels(state): swap time levels 1 and 2 (pointer swap).  Between steps, only
+ * time level 1 (the state the last step produced) is defined for u and w: the step does not copy
+ * u_2 / w_2 into time level 1 at its substep ends (6060-6061), because nothing reads them before
+ * the next step's atm_rk_integration_setup overwrites that buffer (1852-1853).  Read u and w at
+ * time level 1 after the shift. */
 int mpas_dyc_shift_time_levels(mpas_dyc_ctx* ctx);
 /* Block until all queued device work of the context is complete. */
 int mpas_dyc_synchronize(mpas_dyc_ctx* ctx);
@@ -113,7 +117,17 @@ int mpas_dyc_synchronize(mpas_dyc_ctx* ctx);
  * microphysics driver (1650-1660) stays with the host, after the step. */
 #define MPAS_DYC_PHYSICS_TENDENCIES 1
 #define MPAS_DYC_PHYSICS_RQVDYNTEN 2
+/* MPAS_DYC_PHYSICS_MICROPHYSICS: the host runs driver_microphysics (1650-1660) after each
+ * mpas_dyc_timestep, on time level 2 of the step (uploading what it changes: theta_m and scalars of
+ * time level 2, rtheta_p, exner, pressure_p, rt_diabatic_tend), and then calls mpas_dyc_finish_step,
+ * which runs what follows the microphysics in atm_srk3: the regional reset of the specified zone
+ * (1672-1790, config_apply_lbcs) and summarize_timestep's reductions (1794).  Without this flag
+ * mpas_dyc_timestep runs them itself and mpas_dyc_finish_step does nothing. */
+#define MPAS_DYC_PHYSICS_MICROPHYSICS 4
 int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags);
+/* The end of atm_srk3 after the host's microphysics (see MPAS_DYC_PHYSICS_MICROPHYSICS); call it
+ * before mpas_dyc_shift_time_levels.  Asynchronous. */
+int mpas_dyc_finish_step(mpas_dyc_ctx* ctx, double dt);
 /* Regional lateral boundary conditions, config_apply_lbcs (mpas_atm_time_integration.F:683-778,
  * 934-987, 1109-1180, 1253-1270, 1491-1560, 1672-1790; the routines at 6088-6671).  apply = 1 turns
  * them on (the pair kernel layout is required).  The host sets, as in the reference's lbc pool
@@ -161,6 +175,11 @@ int mpas_dyc_set_summary(mpas_dyc_ctx* ctx, int32_t flags);
  * every rank calls it after the same step).  Waits for the step.  scalar_minmax (may be NULL)
  * receives num_scalars (min, max) pairs of the global_minmax_sca mode; n = its length in doubles. */
 int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scalar_minmax, int32_t n);
+/* The same for one block of this process, reduced over ranks: the reference writes one set of log
+ * lines per block of a task, each reduced over tasks (6945-6983, 6991-7015).  Collective like
+ * mpas_dyc_get_summary: every rank calls it for the same block index after the same step. */
+int mpas_dyc_get_block_summary(mpas_dyc_ctx* ctx, int32_t block, mpas_dyc_summary* out, double* scalar_minmax,
+                               int32_t n);
 
 /* ---- domain decomposition: several blocks per process, halo exchange ----
  *

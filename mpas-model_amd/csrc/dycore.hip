@@ -1267,6 +1267,18 @@ int lbc_scalars(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt, double
   return MPAS_DYC_OK;
 }
 
+// The end of atm_srk3 after the microphysics (1650-1660): the regional reset of the specified
+// zone, "because microphysics has messed with them" (1672-1790), then summarize_timestep (1794) --
+// its reductions on the device, the log lines on the host.
+int step_tail(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt) {
+  if (ctx->lbc) {
+    EACH(LAUNCH(k_lbc_reset_spec, d.nCellsSolve, d, p, dt));       // 1672-1711
+    CHK(exchange(ctx, {{"state", "scalars", 2, ALL_LAYERS}}));       // 1714-1790
+    EACH(LAUNCH(k_lbc_set_scalars, d.nCellsSolve, d, p, dt));
+  }
+  return summary_launch(ctx, 2);
+}
+
 int srk3(mpas_dyc_ctx* ctx, double dt) {
   const Config& cf = ctx->cf;
   const std::vector<Ptrs> P = block_ptrs(ctx);
@@ -1536,13 +1548,9 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
                            dim3(256), 0, ctx->stream, ::P<double>(ctx, b, "state", "scalars", 2), n);
     }
   }
-  if (lbc) {
-    EACH(LAUNCH(k_lbc_reset_spec, d.nCellsSolve, d, p, dt));       // 1672-1711, at the end of the step
-    CHK(exchange(ctx, {{"state", "scalars", 2, ALL_LAYERS}}));       // 1714-1790
-    EACH(LAUNCH(k_lbc_set_scalars, d.nCellsSolve, d, p, dt));
-  }
-  // summarize_timestep (1794): the reductions on the device, the log lines on the host
-  CHK(summary_launch(ctx, 2));
+  // the rest of the step follows the microphysics (1650-1660): when the host runs it, the host
+  // calls mpas_dyc_finish_step after it
+  if (!(ctx->physics & MPAS_DYC_PHYSICS_MICROPHYSICS)) CHK(step_tail(ctx, P, dt));
   return MPAS_DYC_OK;
 }
 
@@ -2085,8 +2093,10 @@ int mpas_dyc_set_summary(mpas_dyc_ctx* ctx, int32_t flags) {
   return MPAS_DYC_OK;
 }
 
-int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scalar_minmax, int32_t n) {
-  if (!ctx || !out) return MPAS_DYC_EINVAL;
+namespace {
+// blocks < 0: every block of the process folded; else that block alone (each reduced over ranks)
+int get_summary(mpas_dyc_ctx* ctx, int32_t blocks, mpas_dyc_summary* out, double* scalar_minmax, int32_t n) {
+  if (!ctx || !out || blocks >= (int32_t)ctx->blk.size()) return MPAS_DYC_EINVAL;
   if (ctx->host_only) return MPAS_DYC_ESTATE;
   const int ns = ctx->blk[0].d.ns;
   if (scalar_minmax && n < 2 * ns) return MPAS_DYC_EINVAL;
@@ -2115,8 +2125,9 @@ int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scala
     acc[16] = std::max(acc[16], x[16]);
     acc[17] += x[17];
   };
-  for (size_t ib = 0; ib < ctx->blk.size(); ++ib) {
+  for (size_t ib = blocks < 0 ? 0 : (size_t)blocks; ib < (blocks < 0 ? ctx->blk.size() : (size_t)blocks + 1); ++ib) {
     Block& b = ctx->blk[ib];
+    const bool first_block = ib == (blocks < 0 ? 0 : (size_t)blocks);
     std::vector<double> rec((size_t)nf * SUM_REC);
     HIPCHK(hipMemcpy(rec.data(), b.sum_out, rec.size() * sizeof(double), hipMemcpyDeviceToHost));
     for (int f = 0; f < nf; ++f) {
@@ -2137,7 +2148,7 @@ int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scala
       x[16] = r[SR_MAX0];
       x[17] = r[SR_NAN];
       double* acc = &pay[(size_t)f * PL];
-      if (ib == 0) std::copy(x, x + PL, acc);
+      if (first_block) std::copy(x, x + PL, acc);
       else fold(acc, x);
     }
   }
@@ -2187,6 +2198,17 @@ int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scala
     }
   return MPAS_DYC_OK;
 }
+}  // namespace
+
+int mpas_dyc_get_summary(mpas_dyc_ctx* ctx, mpas_dyc_summary* out, double* scalar_minmax, int32_t n) {
+  return get_summary(ctx, -1, out, scalar_minmax, n);
+}
+
+int mpas_dyc_get_block_summary(mpas_dyc_ctx* ctx, int32_t block, mpas_dyc_summary* out, double* scalar_minmax,
+                               int32_t n) {
+  if (block < 0) return MPAS_DYC_EINVAL;
+  return get_summary(ctx, block, out, scalar_minmax, n);
+}
 
 int mpas_dyc_init_diagnostics(mpas_dyc_ctx* ctx, double dt) {
   if (!ctx) return MPAS_DYC_EINVAL;
@@ -2233,7 +2255,8 @@ int mpas_dyc_set_lbc(mpas_dyc_ctx* ctx, int32_t apply, double seconds_to_interva
 }
 
 int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags) {
-  if (!ctx || (flags & ~(MPAS_DYC_PHYSICS_TENDENCIES | MPAS_DYC_PHYSICS_RQVDYNTEN))) return MPAS_DYC_EINVAL;
+  if (!ctx || (flags & ~(MPAS_DYC_PHYSICS_TENDENCIES | MPAS_DYC_PHYSICS_RQVDYNTEN | MPAS_DYC_PHYSICS_MICROPHYSICS)))
+    return MPAS_DYC_EINVAL;
   if (ctx->host_only) return MPAS_DYC_ESTATE;
   if ((flags & MPAS_DYC_PHYSICS_RQVDYNTEN) && !(flags & MPAS_DYC_PHYSICS_TENDENCIES)) return MPAS_DYC_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
@@ -2304,6 +2327,17 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
   }
   ctx->graph_ran = false;
   int r = srk3(ctx, dt);
+  HIPCHK(hipGetLastError());
+  return r;
+}
+
+int mpas_dyc_finish_step(mpas_dyc_ctx* ctx, double dt) {
+  if (!ctx || !(dt > 0.0)) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
+  if (!(ctx->physics & MPAS_DYC_PHYSICS_MICROPHYSICS)) return MPAS_DYC_OK;  // the step ran its own tail
+  HIPCHK(hipSetDevice(ctx->device));
+  const std::vector<Ptrs> P = block_ptrs(ctx);
+  int r = step_tail(ctx, P, dt);
   HIPCHK(hipGetLastError());
   return r;
 }

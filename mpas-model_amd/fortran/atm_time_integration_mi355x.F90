@@ -39,6 +39,7 @@ module atm_time_integration
    use mpas_dmpar
    use mpas_log
    use mpas_timekeeping
+   use mpas_atm_boundaries, only : mpas_atm_get_bdy_state
 #ifdef DO_PHYSICS
    use mpas_atmphys_todynamics, only : physics_get_tend
    use mpas_atmphys_driver_microphysics, only : driver_microphysics
@@ -85,7 +86,7 @@ module atm_time_integration
    end type dyc_summary
 
    integer(c_int32_t), parameter, private :: DYC_CELL = 0, DYC_EDGE = 1, DYC_VERTEX = 2, DYC_SEND = 0, DYC_RECV = 1
-   integer(c_int32_t), parameter, private :: PHYS_TENDENCIES = 1, PHYS_RQVDYNTEN = 2
+   integer(c_int32_t), parameter, private :: PHYS_TENDENCIES = 1, PHYS_RQVDYNTEN = 2, PHYS_MICROPHYSICS = 4
    integer(c_int32_t), parameter, private :: SUM_VEL = 1, SUM_DETAILED = 2, SUM_SCA = 4
    integer, parameter, private :: UP = 1, DOWN = 2
 
@@ -205,6 +206,26 @@ module atm_time_integration
          type(c_ptr), value :: scalar_minmax
          integer(c_int32_t), value :: n
       end function
+      integer(c_int) function mpas_dyc_get_block_summary(ctx, block, out, scalar_minmax, n) &
+            bind(C, name='mpas_dyc_get_block_summary')
+         import :: c_int, c_ptr, c_int32_t, dyc_summary
+         type(c_ptr), value :: ctx
+         integer(c_int32_t), value :: block
+         type(dyc_summary), intent(out) :: out
+         type(c_ptr), value :: scalar_minmax
+         integer(c_int32_t), value :: n
+      end function
+      integer(c_int) function mpas_dyc_finish_step(ctx, dt) bind(C, name='mpas_dyc_finish_step')
+         import :: c_int, c_ptr, c_double
+         type(c_ptr), value :: ctx
+         real(c_double), value :: dt
+      end function
+      integer(c_int) function mpas_dyc_set_lbc(ctx, apply, seconds_to_interval_end) bind(C, name='mpas_dyc_set_lbc')
+         import :: c_int, c_ptr, c_int32_t, c_double
+         type(c_ptr), value :: ctx
+         integer(c_int32_t), value :: apply
+         real(c_double), value :: seconds_to_interval_end
+      end function
       type(c_ptr) function mpas_dyc_last_error(ctx) bind(C, name='mpas_dyc_last_error')
          import :: c_ptr
          type(c_ptr), value :: ctx
@@ -218,6 +239,11 @@ module atm_time_integration
    logical, save, private :: wait_every_step = .false.   ! MPAS_DYCORE_WAIT_EVERY_STEP=1 (diagnostics)
    integer(c_int32_t), save, private :: summary_flags = 0, physics_flags = 0
    real (kind=RKIND), save, private :: dt_init = 0.0_RKIND
+   ! regional runs: the host lbc pool's interval-end arrays last uploaded (mpas_atm_update_bdy_tend
+   ! shifts the pool's time levels and reads new ones each time the lbc_in alarm rings), and a
+   ! one-column probe block through which mpas_atm_get_bdy_state reports LBC_intv_end - now
+   type(c_ptr), save, private :: lbc_uploaded = c_null_ptr
+   type (block_type), pointer, save, private :: lbc_probe => null()
 
    ! ---- fields moved between the pools and HBM (Registry.xml var_struct names) ----
    character(len=32), dimension(3), parameter, private :: mesh_i1 = [character(len=32) :: &
@@ -296,19 +322,28 @@ module atm_time_integration
 
       if (.not. c_associated(dyc)) call create_domain_context(domain)
       call mpas_pool_get_config(domain % blocklist % configs, 'config_apply_lbcs', config_apply_lbcs)
-      if (config_apply_lbcs) call fatal(dyc, 'config_apply_lbcs = .true. (regional MPAS) is not supported')
+      if (config_apply_lbcs) call lbc_to_device(domain)
 #ifdef DO_PHYSICS
       call physics_to_device(domain)
 #endif
       call check(dyc, mpas_dyc_timestep(dyc, real(dt, c_double), int(itimestep, c_int32_t)), 'mpas_dyc_timestep')
+#ifdef DO_PHYSICS
+      if (iand(physics_flags, PHYS_MICROPHYSICS) /= 0) then
+         ! the microphysics on time level 2 of the step (1650-1660), then the rest of atm_srk3: the
+         ! specified-zone reset (1672-1790) and summarize_timestep's reductions (1794)
+         call pools_to_host(domain, 2, 2)
+         call physics_after_step(domain, dt, itimestep)
+         call check(dyc, mpas_dyc_finish_step(dyc, real(dt, c_double)), 'mpas_dyc_finish_step')
+      end if
+#endif
       ! the device swaps now; the caller swaps the host pools right after (mpas_atm_core.F:671)
       call check(dyc, mpas_dyc_shift_time_levels(dyc), 'mpas_dyc_shift_time_levels')
 #ifdef DO_PHYSICS
-      call pools_to_host(domain, 2)
-      call physics_after_step(domain, dt, itimestep)
+      ! the host physics reads the new state every step
+      if (iand(physics_flags, PHYS_MICROPHYSICS) == 0 .or. config_apply_lbcs) call pools_to_host(domain, 2, 1)
 #else
       if (atm_dycore_sync_every_step) then
-         call pools_to_host(domain, 2)
+         call pools_to_host(domain, 2, 1)
       else
          host_stale = .true.
       end if
@@ -324,7 +359,7 @@ module atm_time_integration
    subroutine atm_dycore_to_host(domain)
       type (domain_type), intent(inout) :: domain
       if (.not. c_associated(dyc) .or. .not. host_stale) return
-      call pools_to_host(domain, 1)
+      call pools_to_host(domain, 1, 1)
       host_stale = .false.
    end subroutine atm_dycore_to_host
 
@@ -452,6 +487,7 @@ module atm_time_integration
       integer(c_int64_t) :: idbytes
       integer, allocatable, target :: idwords(:)
       logical, pointer :: lp
+      character (len=StrKIND), pointer :: microp
 
       nb = count_blocks(domain)
       nprocs = domain % dminfo % nprocs
@@ -513,10 +549,31 @@ module atm_time_integration
          block => block % next
       end do
       call check(dyc, mpas_dyc_use_graph(dyc, 1_c_int32_t), 'mpas_dyc_use_graph')
+      ! regional runs (config_apply_lbcs): the boundary-zone masks and relaxation scaling of the mesh
+      ! pool (mpas_atm_setup_bdy_masks, atm_compute_mesh_scaling); the lbc pool follows every step
+      call mpas_pool_get_config(domain % blocklist % configs, 'config_apply_lbcs', lp)
+      if (associated(lp)) then
+         if (lp) then
+            block => domain % blocklist
+            ib = 0
+            do while (associated(block))
+               call mpas_pool_get_subpool(block % structs, 'mesh', mesh)
+               call xfer(dyc, ib, mesh, 'mesh', 'bdyMaskCell', 1, 1, UP, .true.)
+               call xfer(dyc, ib, mesh, 'mesh', 'bdyMaskEdge', 1, 1, UP, .true.)
+               call xfer(dyc, ib, mesh, 'mesh', 'nearestRelaxationCell', 1, 1, UP, .true.)
+               call xfer(dyc, ib, mesh, 'mesh', 'meshScalingRegionalCell', 1, 1, UP, .true.)
+               call xfer(dyc, ib, mesh, 'mesh', 'meshScalingRegionalEdge', 1, 1, UP, .true.)
+               ib = ib + 1
+               block => block % next
+            end do
+         end if
+      end if
 #ifdef DO_PHYSICS
       physics_flags = PHYS_TENDENCIES
       block => domain % blocklist
       if (rqvdynten_wanted(block % configs)) physics_flags = ior(physics_flags, PHYS_RQVDYNTEN)
+      call mpas_pool_get_config(block % configs, 'config_microp_scheme', microp)
+      if (trim(microp) /= 'off') physics_flags = ior(physics_flags, PHYS_MICROPHYSICS)
       call check(dyc, mpas_dyc_set_physics(dyc, physics_flags), 'mpas_dyc_set_physics')
 #endif
       ! summarize_timestep's namelist switches (Registry.xml defaults when a core lacks them)
@@ -652,10 +709,10 @@ module atm_time_integration
       end if
    end subroutine upload_block
 
-   ! the device state (current time level) into host time level host_tl of every block
-   subroutine pools_to_host(domain, host_tl)
+   ! the device state of time level dev_tl into host time level host_tl of every block
+   subroutine pools_to_host(domain, host_tl, dev_tl)
       type (domain_type), intent(inout) :: domain
-      integer, intent(in) :: host_tl
+      integer, intent(in) :: host_tl, dev_tl
       type (block_type), pointer :: block
       type (mpas_pool_type), pointer :: state, diag, tend_physics
       integer :: ib, i
@@ -665,7 +722,7 @@ module atm_time_integration
          call mpas_pool_get_subpool(block % structs, 'state', state)
          call mpas_pool_get_subpool(block % structs, 'diag', diag)
          do i = 1, size(state_names)
-            call xfer(dyc, ib, state, 'state', trim(state_names(i)), host_tl, 1, DOWN, .true.)
+            call xfer(dyc, ib, state, 'state', trim(state_names(i)), host_tl, dev_tl, DOWN, .true.)
          end do
          do i = N_DIAG_IN + 1, size(diag_names)
             call xfer(dyc, ib, diag, 'diag', trim(diag_names(i)), 1, 1, DOWN, .false.)
@@ -722,8 +779,9 @@ module atm_time_integration
       end do
    end subroutine physics_to_device
 
-   ! the microphysics call of 1650-1660 on the host (rqvdynten and the clip ran on the device);
-   ! what it changes -- theta_m, scalars, rtheta_p, exner, pressure_p, rt_diabatic_tend -- goes back
+   ! the microphysics call of 1650-1660 on the host, on time level 2 of the step before the shift
+   ! (rqvdynten and the clip ran on the device); what it changes -- theta_m, scalars, rtheta_p,
+   ! exner, pressure_p, rt_diabatic_tend -- goes back to the device before mpas_dyc_finish_step
    subroutine physics_after_step(domain, dt, itimestep)
       type (domain_type), intent(inout) :: domain
       real (kind=RKIND), intent(in) :: dt
@@ -753,8 +811,8 @@ module atm_time_integration
                                      cellSolveThreadStart(thread), cellSolveThreadEnd(thread))
          end do
 !$OMP END PARALLEL DO
-         call xfer(dyc, ib, state, 'state', 'theta_m', 2, 1, UP, .true.)
-         call xfer(dyc, ib, state, 'state', 'scalars', 2, 1, UP, .true.)
+         call xfer(dyc, ib, state, 'state', 'theta_m', 2, 2, UP, .true.)
+         call xfer(dyc, ib, state, 'state', 'scalars', 2, 2, UP, .true.)
          call xfer(dyc, ib, diag, 'diag', 'rtheta_p', 1, 1, UP, .true.)
          call xfer(dyc, ib, diag, 'diag', 'exner', 1, 1, UP, .true.)
          call xfer(dyc, ib, diag, 'diag', 'pressure_p', 1, 1, UP, .true.)
@@ -775,37 +833,48 @@ module atm_time_integration
 #endif
 
    ! summarize_timestep (:6675-7018): the device reduced the extrema over the owned elements of
-   ! every block and task (mpas_dyc_get_summary); the host writes the reference's log lines
+   ! each block, each over all tasks (mpas_dyc_get_block_summary); the host writes the reference's
+   ! log lines, one set per block as the reference's block loops do
    subroutine summarize_timestep(domain)
       type (domain_type), intent(inout) :: domain
-      type(dyc_summary) :: s
+      type(dyc_summary), allocatable :: s(:)
       integer, pointer :: num_scalars
       type (mpas_pool_type), pointer :: state
-      real(c_double), allocatable, target :: sca(:)
-      integer :: i
+      real(c_double), allocatable, target :: sca(:,:)
+      integer :: i, ib, nb
       call mpas_pool_get_subpool(domain % blocklist % structs, 'state', state)
       call mpas_pool_get_dimension(state, 'num_scalars', num_scalars)
-      allocate(sca(2 * num_scalars))
-      call check(dyc, mpas_dyc_get_summary(dyc, s, c_loc(sca), int(size(sca), c_int32_t)), 'mpas_dyc_get_summary')
+      nb = count_blocks(domain)
+      allocate(s(nb), sca(2 * num_scalars, nb))
+      do ib = 1, nb
+         call check(dyc, mpas_dyc_get_block_summary(dyc, int(ib - 1, c_int32_t), s(ib), c_loc(sca(1, ib)), &
+                    int(2 * num_scalars, c_int32_t)), 'mpas_dyc_get_block_summary')
+      end do
       if (iand(summary_flags, SUM_DETAILED) /= 0) then
          call mpas_log_write('')
-         call located(' global min w: ', s % w_min_at)
-         call located(' global max w: ', s % w_max_at)
-         call located(' global min u: ', s % u_min_at)
-         call located(' global max u: ', s % u_max_at)
-         call located(' global max wsp: ', s % wsp_max_at)
-         if (s % nan_w > 0) call mpas_log_write('NaN detected in ''w'' field.', messageType=MPAS_LOG_CRIT)
-         if (s % nan_u > 0) call mpas_log_write('NaN detected in ''u'' field.', messageType=MPAS_LOG_CRIT)
+         do ib = 1, nb
+            call located(' global min w: ', s(ib) % w_min_at)
+            call located(' global max w: ', s(ib) % w_max_at)
+            call located(' global min u: ', s(ib) % u_min_at)
+            call located(' global max u: ', s(ib) % u_max_at)
+            call located(' global max wsp: ', s(ib) % wsp_max_at)
+            if (s(ib) % nan_w > 0) call mpas_log_write('NaN detected in ''w'' field.', messageType=MPAS_LOG_CRIT)
+            if (s(ib) % nan_u > 0) call mpas_log_write('NaN detected in ''u'' field.', messageType=MPAS_LOG_CRIT)
+         end do
       else if (iand(summary_flags, SUM_VEL) /= 0) then
          call mpas_log_write('')
-         call mpas_log_write('global min, max w $r $r', realArgs=(/s % w_min, s % w_max/))
-         call mpas_log_write('global min, max u $r $r', realArgs=(/s % u_min, s % u_max/))
+         do ib = 1, nb
+            call mpas_log_write('global min, max w $r $r', realArgs=(/s(ib) % w_min, s(ib) % w_max/))
+            call mpas_log_write('global min, max u $r $r', realArgs=(/s(ib) % u_min, s(ib) % u_max/))
+         end do
       end if
       if (iand(summary_flags, SUM_SCA) /= 0) then
          if (iand(summary_flags, SUM_VEL + SUM_DETAILED) == 0) call mpas_log_write('')
-         do i = 1, num_scalars
-            call mpas_log_write(' global min, max scalar $i $r $r', intArgs=(/i/), &
-                                realArgs=(/sca(2 * i - 1), sca(2 * i)/))
+         do ib = 1, nb
+            do i = 1, num_scalars
+               call mpas_log_write(' global min, max scalar $i $r $r', intArgs=(/i/), &
+                                   realArgs=(/sca(2 * i - 1, ib), sca(2 * i, ib)/))
+            end do
          end do
       end if
    contains
@@ -816,6 +885,71 @@ module atm_time_integration
                              realArgs=(/real(e % value, RKIND), real(e % lat, RKIND), real(e % lon, RKIND)/))
       end subroutine located
    end subroutine summarize_timestep
+
+   ! Regional runs (config_apply_lbcs), before every step: the lbc pool into HBM whenever the host
+   ! read new boundary data (mpas_atm_update_bdy_tend, called by atm_core_run on the lbc_in alarm,
+   ! mpas_atm_core.F:584-627, shifts the pool's time levels and reads the interval-end state into
+   ! time level 2, so its array moves), and the seconds from the step's start to the LBC interval
+   ! end.  The module keeps that interval end private (LBC_intv_end); its public getter reports it:
+   ! mpas_atm_get_bdy_state(clock, block, ..., delta_t = 0) returns state - (LBC_intv_end - now) *
+   ! tendency (mpas_atm_boundaries.F:337-409), and a probe block whose lbc pool holds state 0 and
+   ! tendency -1 gets back exactly LBC_intv_end - now.
+   subroutine lbc_to_device(domain)
+      type (domain_type), intent(inout) :: domain
+      type (block_type), pointer :: block
+      type (mpas_pool_type), pointer :: lbc
+      real (kind=RKIND), dimension(:,:), pointer :: u2
+      real (kind=RKIND), dimension(1, 2) :: probe
+      character(len=32), dimension(4), parameter :: lbc2 = [character(len=32) :: &
+         'lbc_u', 'lbc_ru', 'lbc_rho_zz', 'lbc_rtheta_m']
+      integer :: ib, i, tl
+      block => domain % blocklist
+      call mpas_pool_get_subpool(block % structs, 'lbc', lbc)
+      if (.not. associated(lbc)) call fatal(dyc, 'config_apply_lbcs: the block has no lbc pool')
+      call mpas_pool_get_array(lbc, 'lbc_u', u2, 2)
+      if (.not. c_associated(lbc_uploaded, c_loc(u2(1,1)))) then
+         ib = 0
+         do while (associated(block))
+            call mpas_pool_get_subpool(block % structs, 'lbc', lbc)
+            do tl = 1, 2
+               do i = 1, size(lbc2)
+                  call xfer(dyc, ib, lbc, 'lbc', trim(lbc2(i)), tl, tl, UP, .true.)
+               end do
+               call xfer(dyc, ib, lbc, 'lbc', 'lbc_scalars', tl, tl, UP, .true.)
+            end do
+            ib = ib + 1
+            block => block % next
+         end do
+         lbc_uploaded = c_loc(u2(1,1))
+      end if
+      if (.not. associated(lbc_probe)) call make_lbc_probe()
+      probe = mpas_atm_get_bdy_state(domain % clock, lbc_probe, 1, 1, 'dyc_probe', 0.0_RKIND)
+      call check(dyc, mpas_dyc_set_lbc(dyc, 1_c_int32_t, real(probe(1, 1), c_double)), 'mpas_dyc_set_lbc')
+   end subroutine lbc_to_device
+
+   ! the probe block of lbc_to_device: an lbc pool with one field lbc_dyc_probe(1, 1+1) of two time
+   ! levels, tendency (time level 1) -1, state (time level 2) 0
+   subroutine make_lbc_probe()
+      type (mpas_pool_type), pointer :: lbc
+      type (field2DReal), dimension(:), pointer :: fa
+      integer :: t
+      allocate(lbc_probe)
+      call mpas_pool_create_pool(lbc_probe % structs)
+      call mpas_pool_create_pool(lbc)
+      call mpas_pool_add_subpool(lbc_probe % structs, 'lbc', lbc)
+      allocate(fa(2))
+      do t = 1, 2
+         fa(t) % block => lbc_probe
+         fa(t) % fieldName = 'lbc_dyc_probe'
+         fa(t) % isActive = .true.
+         fa(t) % dimSizes(1) = 1
+         fa(t) % dimSizes(2) = 2
+         allocate(fa(t) % array(1, 2))
+      end do
+      fa(1) % array = -1.0_RKIND
+      fa(2) % array = 0.0_RKIND
+      call mpas_pool_add_field(lbc, 'lbc_dyc_probe', fa)
+   end subroutine make_lbc_probe
 
    ! ------------------------------------------------------------------ helpers
    integer function count_blocks(domain)

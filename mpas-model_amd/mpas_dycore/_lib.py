@@ -21,7 +21,8 @@ EXPORTS = (
     "mpas_dyc_set_exchange_list", "mpas_dyc_comm_unique_id_bytes", "mpas_dyc_comm_unique_id", "mpas_dyc_comm_init",
     "mpas_dyc_set_transport", "mpas_dyc_halo_exchange", "mpas_dyc_set_overlap", "mpas_dyc_output_diagnostics",
     "mpas_dyc_set_physics", "mpas_dyc_set_summary", "mpas_dyc_get_summary", "mpas_dyc_plan_exchanges",
-    "mpas_dyc_graph_active", "mpas_dyc_solve_diagnostics", "mpas_dyc_set_lbc",
+    "mpas_dyc_graph_active", "mpas_dyc_solve_diagnostics", "mpas_dyc_set_lbc", "mpas_dyc_finish_step",
+    "mpas_dyc_get_block_summary",
 )
 HOST_ONLY = -2  # MPAS_DYC_HOST_ONLY: planner-only context
 PRINT_GLOBAL_MINMAX_VEL, PRINT_DETAILED_MINMAX_VEL, PRINT_GLOBAL_MINMAX_SCA = 1, 2, 4
@@ -143,6 +144,8 @@ def load() -> C.CDLL:
     lib.mpas_dyc_set_overlap.argtypes = [vp, i32]
     lib.mpas_dyc_set_summary.argtypes = [vp, i32]
     lib.mpas_dyc_get_summary.argtypes = [vp, C.POINTER(Summary), C.POINTER(dbl), i32]
+    lib.mpas_dyc_get_block_summary.argtypes = [vp, i32, C.POINTER(Summary), C.POINTER(dbl), i32]
+    lib.mpas_dyc_finish_step.argtypes = [vp, dbl]
     lib.mpas_dyc_plan_exchanges.argtypes = [vp, i32, i32, dbl, C.POINTER(PlanMsg), i64, C.POINTER(i64), C.c_char_p,
                                             i64, C.POINTER(i64)]
     lib.mpas_dyc_graph_active.argtypes = [vp]

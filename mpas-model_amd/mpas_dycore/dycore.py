@@ -249,14 +249,22 @@ class Dycore:
         tendency, 2 = interval-end state) and the masks into the mesh pool."""
         self._check(self.lib.mpas_dyc_set_lbc(self.h, 1 if apply else 0, float(seconds_to_interval_end)), "set_lbc")
 
-    PHYSICS_TENDENCIES, PHYSICS_RQVDYNTEN = 1, 2
+    PHYSICS_TENDENCIES, PHYSICS_RQVDYNTEN, PHYSICS_MICROPHYSICS = 1, 2, 4
 
-    def set_physics(self, tendencies: bool = True, rqvdynten: bool = False):
+    def set_physics(self, tendencies: bool = True, rqvdynten: bool = False, microphysics: bool = False):
         """Physics coupling (the reference's DO_PHYSICS build): the host sets tend_physics.
         tend_ru_physics / tend_rtheta_physics / tend_rho_physics and tend.scalars_tend before each
-        step (as physics_get_tend does, mpas_atm_time_integration.F:424-449)."""
-        flags = (self.PHYSICS_TENDENCIES if tendencies else 0) | (self.PHYSICS_RQVDYNTEN if rqvdynten else 0)
+        step (as physics_get_tend does, mpas_atm_time_integration.F:424-449).  ``microphysics``: the
+        host runs the microphysics on time level 2 after each step and then calls finish_step(),
+        which runs the rest of atm_srk3 (the regional specified-zone reset, summarize_timestep)."""
+        flags = ((self.PHYSICS_TENDENCIES if tendencies else 0) | (self.PHYSICS_RQVDYNTEN if rqvdynten else 0)
+                 | (self.PHYSICS_MICROPHYSICS if microphysics else 0))
         self._check(self.lib.mpas_dyc_set_physics(self.h, flags), "set_physics")
+
+    def finish_step(self, dt: float):
+        """The end of atm_srk3 after the host's microphysics (1672-1794); a no-op unless
+        set_physics(microphysics=True).  Call before shift_time_levels."""
+        self._check(self.lib.mpas_dyc_finish_step(self.h, float(dt)), "finish_step")
 
     def output_diagnostics(self, time_level: int = 1):
         """atm_compute_output_diagnostics (mpas_atm_core.F:753-800): diag theta, rho, pressure."""
@@ -271,13 +279,19 @@ class Dycore:
                  | (_lib.PRINT_GLOBAL_MINMAX_SCA if global_minmax_sca else 0))
         self._check(self.lib.mpas_dyc_set_summary(self.h, flags), "set_summary")
 
-    def summarize_timestep(self, log=None) -> dict:
+    def summarize_timestep(self, log=None, block: int | None = None) -> dict:
         """summarize_timestep (mpas_atm_time_integration.F:6675-7018) of the last step: the global
         extrema over all blocks and ranks, and the reference's log lines (passed to ``log`` if given).
+        ``block``: that block of this process only, reduced over ranks -- the reference writes one
+        set of lines per block (6945-6983).
         In detailed mode a NaN in w or u raises DycoreError, as the reference aborts (6926-6940)."""
         s = _lib.Summary()
         mm = (C.c_double * (2 * self.ns))()
-        self._check(self.lib.mpas_dyc_get_summary(self.h, C.byref(s), mm, 2 * self.ns), "summarize_timestep")
+        if block is None:
+            rc = self.lib.mpas_dyc_get_summary(self.h, C.byref(s), mm, 2 * self.ns)
+        else:
+            rc = self.lib.mpas_dyc_get_block_summary(self.h, int(block), C.byref(s), mm, 2 * self.ns)
+        self._check(rc, "summarize_timestep")
         out = {"flags": s.flags, "w_min": s.w_min, "w_max": s.w_max, "u_min": s.u_min, "u_max": s.u_max,
                "nan_w": s.nan_w, "nan_u": s.nan_u, "scalars": [(mm[2 * i], mm[2 * i + 1]) for i in range(self.ns)]}
         for n in ("w_min_at", "w_max_at", "u_min_at", "u_max_at", "wsp_max_at"):

@@ -341,9 +341,7 @@ program mpas_ref_harness
    use mpas_vector_reconstruction
    use mpas_timekeeping
    use harness_fields
-#ifndef MPAS_DYCORE_DROPIN
    use mpas_atm_boundaries, only : harness_seconds_to_interval_end
-#endif
 #ifdef HARNESS_INIT
    use atm_advection, only : atm_initialize_advection_rk, atm_initialize_deformation_weights
    use atm_core_init_ref, only : atm_compute_mesh_scaling, atm_compute_signs, atm_compute_damping_coefs, &
@@ -366,7 +364,7 @@ program mpas_ref_harness
    real(kind=RKIND) :: config_len_disp, config_visc4_2dsmag, config_del4u_div_factor, config_coef_3rd_order
    real(kind=RKIND) :: config_smagorinsky_coef, config_epssm, config_smdiv, config_apvm_upwinding
    real(kind=RKIND) :: config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days
-   character(len=64) :: config_horiz_mixing, config_convection_scheme
+   character(len=64) :: config_horiz_mixing, config_convection_scheme, config_microp_scheme
    real(kind=RKIND) :: config_zd, config_xnutr
    logical :: config_h_ScaleWithMesh
    character(len=32) :: mode
@@ -391,7 +389,7 @@ program mpas_ref_harness
       config_len_disp, config_visc4_2dsmag, config_del4u_div_factor, config_coef_3rd_order, &
       config_smagorinsky_coef, config_epssm, config_smdiv, config_apvm_upwinding, &
       config_mpas_cam_coef, config_rayleigh_damp_u_timescale_days, config_horiz_mixing, config_convection_scheme, &
-      config_zd, config_xnutr, config_h_ScaleWithMesh, config_apply_lbcs_in, lbc_interval_end
+      config_microp_scheme, config_zd, config_xnutr, config_h_ScaleWithMesh, config_apply_lbcs_in, lbc_interval_end
 
    type (domain_type), pointer :: domain
    type (mpas_pool_type), pointer :: configs, dimpool, mesh, state, diag, tend, tend_physics, diag_physics
@@ -415,6 +413,7 @@ program mpas_ref_harness
    moist_end = 1
    config_horiz_mixing = '2d_smagorinsky'
    config_convection_scheme = 'off'
+   config_microp_scheme = 'off'
    mode = 'run'
    kernel_small_step = 2
    kernel_rk_step = 1
@@ -495,7 +494,7 @@ program mpas_ref_harness
    call mpas_pool_add_config_int(configs, 'config_number_rayleigh_damp_u_levels', config_number_rayleigh_damp_u_levels)
    call mpas_pool_add_config_logical(configs, 'config_apply_lbcs', config_apply_lbcs_in)
    call mpas_pool_add_config_char(configs, 'config_IAU_option', 'off')
-   call mpas_pool_add_config_char(configs, 'config_microp_scheme', 'off')
+   call mpas_pool_add_config_char(configs, 'config_microp_scheme', trim(config_microp_scheme))
    call mpas_pool_add_config_char(configs, 'config_convection_scheme', trim(config_convection_scheme))
    call mpas_pool_add_config_logical(configs, 'config_print_global_minmax_vel', iand(print_minmax, 1) /= 0)
    call mpas_pool_add_config_logical(configs, 'config_print_detailed_minmax_vel', iand(print_minmax, 2) /= 0)
@@ -672,9 +671,8 @@ program mpas_ref_harness
    tloop = omp_get_wtime()
    do step = 1, nsteps
       t0 = omp_get_wtime()
-#ifndef MPAS_DYCORE_DROPIN
+      ! LBC_intv_end - the clock time at the step's start, as mpas_atm_get_bdy_state computes it
       harness_seconds_to_interval_end = lbc_interval_end - real(step - 1, RKIND) * dt
-#endif
       call atm_timestep(domain, dt, nowTime, step)
       nowTime = nowTime + dtInterval
       t1 = omp_get_wtime()

@@ -114,7 +114,7 @@ def write_fields(case: dict, d: str):
 
 def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthreads: int = 0,
                  moist_end: int = 1, convection_scheme: str = "off", print_minmax: int = 0,
-                 dump_only=(), fields: bool = True, nblocks: int = 1):
+                 dump_only=(), fields: bool = True, nblocks: int = 1, microp_scheme: str = "off"):
     os.makedirs(d, exist_ok=True)
     if fields:
         write_fields(case, d)
@@ -149,7 +149,8 @@ def write_inputs(case: dict, d: str, nsteps: int, dt: float, dump_steps=(), nthr
  config_smdiv={cfg['config_smdiv']!r}, config_apvm_upwinding={cfg['config_apvm_upwinding']!r},
  config_mpas_cam_coef={cfg['config_mpas_cam_coef']!r},
  config_rayleigh_damp_u_timescale_days={cfg['config_rayleigh_damp_u_timescale_days']!r},
- config_horiz_mixing='{cfg['config_horiz_mixing']}', config_convection_scheme='{convection_scheme}'
+ config_horiz_mixing='{cfg['config_horiz_mixing']}', config_convection_scheme='{convection_scheme}',
+ config_microp_scheme='{microp_scheme}'
 /
 """
     if print_minmax:
@@ -207,8 +208,10 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     ``with_total``, the wall time of the whole time loop including its final wait for the device
     ({"total": s, "after2": s of steps 3.. } when the run has more than 2 steps).
     ``binary=DROPIN_HARNESS`` runs the same driver on the drop-in module instead.
-    ``physics`` (dict of write_physics_inputs' arrays, optional key "convection_scheme") runs the
-    DO_PHYSICS build with those tendencies handed over by physics_get_tend every step.
+    ``physics`` (dict of write_physics_inputs' arrays, optional keys "convection_scheme" and
+    "microp_scheme" -- "mp_test_double" selects the microphysics test double of
+    shims/mpas_atmphys_driver_microphysics_stub.F90) runs the DO_PHYSICS build with those tendencies
+    handed over by physics_get_tend every step.
     ``dump_only`` (e.g. ["state.u", "state.w"]) limits the dumps to those fields (full-size runs).
     ``print_minmax`` turns on summarize_timestep's namelist switches (1 global_minmax_vel,
     2 detailed_minmax_vel, 4 global_minmax_sca); the reference's log text is then res["log"]."""
@@ -222,7 +225,8 @@ def run_reference(case: dict, nsteps: int, dt: float, dump_steps=None, nthreads:
     tmp = tempfile.mkdtemp(prefix="mpasref_") if own else workdir
     ind, outd = os.path.join(tmp, "in"), os.path.join(tmp, "out")
     write_inputs(case, ind, nsteps, dt, dump_steps, nthreads, moist_end,
-                 (physics or {}).get("convection_scheme", "off"), print_minmax, dump_only)
+                 (physics or {}).get("convection_scheme", "off"), print_minmax, dump_only,
+                 microp_scheme=(physics or {}).get("microp_scheme", "off"))
     if physics is not None:
         write_physics_inputs(case, ind, physics)
     if lbc is not None:

@@ -159,3 +159,72 @@ def test_dropin_physics_matches_reference(convection):
             err = rel_linf(got[step][k], ref[step][k])
             assert err <= 1e-10, f"step {step} {k}: rel Linf {err:.3e}"
     assert got[n]["state.scalars.tl1"].min() >= 0.0
+
+
+@pytest.mark.parametrize("moist", [False, True])
+def test_dropin_regional_matches_reference(moist):
+    """A regional run (config_apply_lbcs) through the drop-in: the boundary-zone masks go up with the
+    mesh, the lbc pool whenever the host has read new boundary data, and before every step the
+    seconds to the LBC interval end, read through mpas_atm_get_bdy_state (the reference's own
+    getter; here the test double of oracle/shims, which the harness drives as the clock would).
+    Against the reference run regionally by the same harness, 6 steps, at test_gpu_lbc's bars."""
+    from mpas_dycore.cases import jw_case, regional_lbc
+    from oracle import ref_runner
+    if not (ref_runner.available() and ref_runner.available(ref_runner.DROPIN_HARNESS)):
+        pytest.skip("oracle/_ref harness binaries not built (make -C oracle all dropin)")
+    case = jw_case(2562, K=26, ns=6 if moist else 1, moist=moist, cache=False)
+    case, lbc = regional_lbc(case)
+    dt, n, me = float(case["dt"]), 6, 6 if moist else 1
+    ref, _ = ref_runner.run_reference(case, n, dt, [1, n], nthreads=4, lbc=lbc, moist_end=me)
+    got, _ = ref_runner.run_reference(case, n, dt, [1, n], nthreads=1, lbc=lbc, moist_end=me,
+                                      binary=ref_runner.DROPIN_HARNESS)
+    for step in (1, n):
+        for k in PROG:
+            tol = 1e-9 if k in ("state.w.tl1", "state.scalars.tl1") else 1e-10
+            err = rel_linf(got[step][k], ref[step][k])
+            assert err <= tol, f"regional step {step} {k}: rel Linf {err:.3e}"
+    # the boundary conditions act: the same drop-in run without them differs
+    glob, _ = ref_runner.run_reference(case, n, dt, [n], nthreads=1, moist_end=me, binary=ref_runner.DROPIN_HARNESS,
+                                       dump_only=["state.theta_m"])
+    assert rel_linf(glob[n]["state.theta_m.tl1"], got[n]["state.theta_m.tl1"]) > 1e-6
+
+
+@pytest.mark.parametrize("regional", [False, True])
+def test_dropin_microphysics_then_step_tail_matches_reference(regional):
+    """-DDO_PHYSICS with a microphysics step (the test double of oracle/shims selected by
+    config_microp_scheme = 'mp_test_double'): the reference runs it inside atm_srk3 (1650-1660) and
+    only then resets the specified zone (1672-1790) and writes summarize_timestep's lines (1794).  The
+    drop-in runs it on the host between mpas_dyc_timestep and mpas_dyc_finish_step, so the reset and
+    the logged scalar extrema see the microphysics' theta_m / qv.  Prognostics at 1e-10 (w and the
+    mixing ratios 1e-9) after 4 steps, and the logged global min/max lines equal to 1e-10."""
+    import re
+    from conftest import physics_forcing
+    from mpas_dycore.cases import jw_case, regional_lbc
+    from oracle import ref_runner
+    if not (ref_runner.available(ref_runner.PHYS_HARNESS) and ref_runner.available(ref_runner.DROPIN_PHYS_HARNESS)):
+        pytest.skip("physics harness binaries not built (make -C oracle phys dropin)")
+    case = jw_case(2562, K=26, ns=3, moist=True, cache=False)
+    lbc = None
+    if regional:
+        case, lbc = regional_lbc(case)
+    dt, n = float(case["dt"]), 4
+    phys = dict(physics_forcing(case, scale=0.2), microp_scheme="mp_test_double")
+    kw = dict(nsteps=n, dt=dt, dump_steps=[n], physics=phys, lbc=lbc, moist_end=3, print_minmax=1 | 4)
+    ref, _ = ref_runner.run_reference(case, nthreads=4, **kw)
+    got, _ = ref_runner.run_reference(case, nthreads=1, binary=ref_runner.DROPIN_PHYS_HARNESS, **kw)
+    for k in PROG:
+        tol = 1e-9 if k in ("state.w.tl1", "state.scalars.tl1") else 1e-10
+        err = rel_linf(got[n][k], ref[n][k])
+        assert err <= tol, f"step {n} {k}: rel Linf {err:.3e}"
+    # the microphysics test double really runs: without it the reference trajectory differs
+    off, _ = ref_runner.run_reference(case, nthreads=4, **dict(kw, physics=dict(phys, microp_scheme="off")))
+    assert rel_linf(off[n]["state.theta_m.tl1"], ref[n]["state.theta_m.tl1"]) > 1e-8
+    num = r"(-?[0-9.]+(?:E[-+][0-9]+)?)"
+    pat = re.compile(rf"global min, max (w|u|scalar\s+\d+) {num} {num}")
+    lines_ref, lines_got = pat.findall(ref["log"]), pat.findall(got["log"])
+    assert len(lines_ref) == n * (2 + 3) and len(lines_got) == len(lines_ref)
+    for a, b in zip(lines_ref, lines_got):
+        assert a[0] == b[0]
+        for x, y in ((a[1], b[1]), (a[2], b[2])):
+            x, y = float(x), float(y)
+            assert abs(x - y) <= 1e-10 * abs(x) + 1e-300, f"{a[0]}: {x} vs {y}"
