@@ -78,6 +78,9 @@ struct Ptrs {
   double *exner, *exner_base, *pressure_base, *pressure_p, *pressure, *h_divergence, *kdiff, *ke, *divergence;
   double *pv_cell, *tend_rtheta_adv, *cqw, *cofwr, *cofwz, *cofwt, *coftz, *a_tri, *alpha_tri, *gamma_tri, *cofrz;
   double *rw, *rw_p, *rw_save, *wwAvg, *wwAvg_split;
+  // what the acoustic cell phase reads for rw, w (tl2) and rho_zz (tl2): the fields themselves,
+  // except in a dynamics substep's first stage (srk3 stage_fin), whose recovery writes the fields
+  const double *rw_rd, *w2_rd, *rho_zz2_rd;
   double *ru, *ruAvg, *ruAvg_split, *ru_p, *ru_save, *cqu, *rho_edge, *v, *pv_edge, *gradPVn, *gradPVt;
   double *vorticity, *pv_vertex;
   double *uReconstructX, *uReconstructY, *uReconstructZ, *uReconstructZonal, *uReconstructMeridional;

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -37,6 +38,10 @@ struct Field {
   int ntl;
   int nsub = 1;       // > 1: scalar-major [nsub][n+1][inner/nsub] in HBM, Fortran image (nsub, inner/nsub, n+1)
   void* buf[2] = {nullptr, nullptr};
+  // buffer rotation of the step (srk3 rotate_saves / swap_theta): rot >= 0 names the partner field
+  // (X <-> X_save) whose buffer this field trades at every rotation, rot_pos counts the trades mod 2
+  // (which of the two buffers it holds); flip = the time levels of a state field are swapped
+  int rot = -1, rot_pos = 0, flip = 0;
 };
 
 // One entry of a block's multihalo exchange list (mpas_multihalo_exchange_list:
@@ -113,8 +118,10 @@ struct mpas_dyc_ctx {
   hipEvent_t ev[8] = {};
   bool use_graph = false;
   bool graph_ran = false;               // the last step replayed a captured graph
-  hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
-  double graph_dt[2] = {0, 0};
+  // captured steps, by buffer layout (layout_sig: the time level and the buffers the step's
+  // rotations move, srk3 rotate_saves / swap_theta), and the dt each was captured for
+  std::map<std::string, hipGraphExec_t> graphs;
+  std::map<std::string, double> graph_dt;
   // halo exchange
   int rank = 0, nranks = 1;
   ncclComm_t comm = nullptr;
@@ -122,7 +129,7 @@ struct mpas_dyc_ctx {
   bool fused_pack_enabled = true;       // MPAS_DYCORE_FUSED_PACK=0: pack kernel instead (A/B)
   bool lbc = false;                     // config_apply_lbcs (mpas_dyc_set_lbc)
   bool planning = false;                // dry run: build exchange plans, launch nothing
-  bool planned[2] = {false, false};
+  std::set<std::string> planned;        // layouts whose exchange plans exist (plan_all)
   std::map<std::string, XPlan> plans;
   std::vector<std::string>* record = nullptr;  // mpas_dyc_plan_exchanges: keys of the calls, in order
   // split-phase exchanges: packs, RCCL and unpacks run on the exchange stream while the
@@ -312,6 +319,12 @@ void build_registry(Block& c) {
   add(c, "scratch", "cell_sdv", L_CELL, ME);
   add(c, "scratch", "zb_p", L_CELL, (int64_t)ME * (K + 1));
   add(c, "scratch", "zb_m", L_CELL, (int64_t)ME * (K + 1));
+  // the saves srk3 rotates instead of copying (rotate_saves)
+  for (const char* n : {"ru", "rw", "rtheta_p", "rho_p"}) {
+    const int a = c.by_name[std::string("diag.") + n], b = c.by_name[std::string("diag.") + n + "_save"];
+    c.fields[a].rot = b;
+    c.fields[b].rot = a;
+  }
 }
 
 Field* find(Block& b, const char* pool, const char* name) {
@@ -403,6 +416,9 @@ Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
   p.lbc_scalars_s = P<const double>(c, b, "lbc", "lbc_scalars", 2);
   p.lbc_dtr = P<const double>(c, b, "lbc", "dtr");
   SC(lbc_tmp);
+  p.rw_rd = p.rw;
+  p.w2_rd = p.w2;
+  p.rho_zz2_rd = p.rho_zz2;
   // 0-d mesh fields are mirrored on the host
   p.cf1 = b.fields[b.by_name["mesh.cf1"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf1"]].buf[1] : 0.0;
   p.cf2 = b.fields[b.by_name["mesh.cf2"]].buf[1] ? *(double*)b.fields[b.by_name["mesh.cf2"]].buf[1] : 0.0;
@@ -436,9 +452,16 @@ inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + WAVES_PER_BLOCK - 
 // ---------------------------------------------------------------------------
 bool needs_exchange(const mpas_dyc_ctx* ctx) { return ctx->blk.size() > 1 || ctx->nranks > 1; }
 
-std::string plan_key(const mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
+// An exchange plan holds the fields' buffers, so its key names them: the time level and, per field,
+// which of the buffers that the step's rotations move it is (buffer index of block 0)
+std::string plan_key(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   std::string k = std::to_string(ctx->cur);
-  for (const auto& f : fs) k += "|" + std::string(f.pool) + "." + f.name + "." + std::to_string(f.tl) + "." + std::to_string(f.layers);
+  for (const auto& f : fs) {
+    k += "|" + std::string(f.pool) + "." + f.name + "." + std::to_string(f.tl) + "." + std::to_string(f.layers);
+    Field* F = ctx->blk.empty() ? nullptr : find(ctx->blk[0], f.pool, f.name);
+    if (F && F->rot >= 0) k += "@" + std::to_string(F->rot_pos);
+    else if (F && F->ntl == 2 && F->pool == "state") k += "@" + std::to_string(slot_of(ctx, *F, f.tl) ^ F->flip);
+  }
   return k;
 }
 
@@ -456,16 +479,20 @@ void free_plan(XPlan& pl) {
   pl = XPlan{};
 }
 
+// captured steps bake pointers, list lengths and flags in: drop them when any of those changes
+void drop_graphs(mpas_dyc_ctx* ctx) {
+  for (auto& kv : ctx->graphs)
+    if (kv.second) (void)hipGraphExecDestroy(kv.second);
+  ctx->graphs.clear();
+  ctx->graph_dt.clear();
+}
+
 void invalidate_plans(mpas_dyc_ctx* ctx) {
   if (!ctx->host_only) (void)hipStreamSynchronize(ctx->stream);
   for (auto& kv : ctx->plans) free_plan(kv.second);
   ctx->plans.clear();
-  ctx->planned[0] = ctx->planned[1] = false;
-  for (auto& g : ctx->graph_exec)
-    if (g) {
-      (void)hipGraphExecDestroy(g);
-      g = nullptr;
-    }
+  ctx->planned.clear();
+  drop_graphs(ctx);
 }
 
 bool is_local(const mpas_dyc_ctx* ctx, int peer_rank) { return peer_rank == ctx->rank && !ctx->rccl_local; }
@@ -810,10 +837,7 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
     if (!lc.empty())
       HIPCHK(hipMemcpy(find(b, "scratch", "bnd_cells")->buf[0], lc.data(), lc.size() * 4, hipMemcpyHostToDevice));
     if (b.d.n_bnd_edges != (int)le.size() || b.d.n_bnd_pairs != (int)lp.size() || b.d.n_bnd_cells != (int)lc.size())
-      for (int i = 0; i < 2; ++i) {  // captured steps bake the list lengths into their launches
-        if (ctx->graph_exec[i]) (void)hipGraphExecDestroy(ctx->graph_exec[i]);
-        ctx->graph_exec[i] = nullptr;
-      }
+      drop_graphs(ctx);  // captured steps bake the list lengths into their launches
     b.d.n_bnd_edges = (int)le.size();
     b.d.n_bnd_pairs = (int)lp.size();
     b.d.n_bnd_cells = (int)lc.size();
@@ -869,24 +893,117 @@ int exchange_wait(mpas_dyc_ctx* ctx) {
 // ---------------------------------------------------------------------------
 // reference routines, one host function each (per block)
 // ---------------------------------------------------------------------------
-// atm_rk_integration_setup (1847-1857): copies over owned+halo elements (not the garbage slot)
-void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
-  const int64_t K = d.K, K1 = d.K + 1;
-  CopyList c{};
-  const double* src[10] = {p.ru, p.rw, p.rtheta_p, p.rho_p, p.u1, p.w1, p.theta_m1, p.rho_zz1, p.rho_zz1, p.scalars1};
-  double* dst[10] = {p.ru_save, p.rw_save, p.rtheta_p_save, p.rho_p_save, p.u2,
-                     p.w2, p.theta_m2, p.rho_zz2, p.rho_zz_old_split, p.scalars2};
-  const int64_t n[10] = {d.nEdges * K, d.nCells * K1, d.nCells * K, d.nCells * K, d.nEdges * K,
-                         d.nCells * K1, d.nCells * K, d.nCells * K, d.nCells * K, (d.nCells + 1) * K * d.ns};
-  int64_t nmax = 0;
-  for (int i = 0; i < 10; ++i) {
-    c.src[i] = src[i];
-    c.dst[i] = dst[i];
-    c.n[i] = n[i];
-    nmax = std::max(nmax, n[i]);
+// The saves of atm_rk_integration_setup (1847-1850) and of atm_rk_dynamics_substep_finish
+// (6051-6054) -- ru_save = ru, rw_save = rw, rtheta_p_save = rtheta_p, rho_p_save = rho_p -- are
+// buffer rotations: X_save takes X's buffer, which holds exactly those values, and X takes the
+// other one.  The first stage's recovery (2998-3059) overwrites X on every element before any
+// kernel reads X again; until then the readers of X read X_save (stage_pre), which holds the same
+// values bit for bit.
+void rotate_saves(mpas_dyc_ctx* ctx) {
+  for (auto& b : ctx->blk)
+    for (const char* n : {"ru", "rw", "rtheta_p", "rho_p"}) {
+      Field* x = find(b, "diag", n);
+      Field* xs = &b.fields[x->rot];
+      std::swap(x->buf[0], xs->buf[0]);
+      x->rot_pos ^= 1;
+      xs->rot_pos ^= 1;
+    }
+}
+
+// theta_m_1 = theta_m_2 at the end of a dynamics substep (6058): the two time levels trade buffers;
+// time level 2 then holds stale values until the next first-stage recovery, and its readers before
+// that read time level 1 (stage_pre)
+void swap_theta(mpas_dyc_ctx* ctx) {
+  for (auto& b : ctx->blk) {
+    Field* f = find(b, "state", "theta_m");
+    std::swap(f->buf[0], f->buf[1]);
+    f->flip ^= 1;
   }
-  const unsigned gx = (unsigned)std::min<int64_t>((nmax + 255) / 256, 2048);
-  if (!ctx->planning) hipLaunchKernelGGL(k_copy_many, dim3(gx, 10), dim3(256), 0, ctx->stream, c);
+}
+
+// The pointers the kernels of a dynamics substep's first stage see until its recovery: X -> X_save
+// for the rotated saves, time level 2 -> time level 1 of theta_m (swapped buffers) and, in the
+// first dynamics substep, of u, w and rho_zz, whose copies of atm_rk_integration_setup (1852-1855)
+// are not made either: the first stage's recovery writes time level 2 of all of them on every
+// element (u: 3048-3059, w: 3013 and 3063-3097, rho_zz: 2998-3001 with the garbage slot, 2989-2991).
+Ptrs stage_pre(const Ptrs& p0, bool first_substep) {
+  Ptrs p = p0;
+  p.ru = p.ru_save;
+  p.rw = p.rw_save;
+  p.rw_rd = p.rw_save;
+  p.rtheta_p = p.rtheta_p_save;
+  p.theta_m2 = p.theta_m1;
+  if (first_substep) {
+    p.u2 = p.u1;
+    p.w2 = p.w1;
+    p.w2_rd = p.w1;
+    p.rho_zz2 = p.rho_zz1;
+    p.rho_zz2_rd = p.rho_zz1;
+  }
+  return p;
+}
+
+// The first stage's last cell phase reads as stage_pre (rw_rd, w2_rd, rho_zz2_rd) but its fused
+// recovery (k_acoustic_cells_r<ME, true>) writes the fields themselves
+Ptrs stage_fin(const Ptrs& p0, bool first_substep) {
+  Ptrs p = p0;
+  p.rw_rd = p.rw_save;
+  if (first_substep) {
+    p.w2_rd = p.w1;
+    p.rho_zz2_rd = p.rho_zz1;
+  }
+  return p;
+}
+
+// the rotations one atm_srk3 makes (rk_integration_setup + each substep_finish that is not the last)
+int step_rotations(const Config& cf) { return cf.split_dynamics_transport ? cf.dynamics_split_steps : 1; }
+
+// replay of a captured step: its rotations happened on the host at capture time; repeat them
+void apply_step_rotations(mpas_dyc_ctx* ctx) {
+  const int n = step_rotations(ctx->cf);
+  if (n & 1) rotate_saves(ctx);
+  if ((n - 1) & 1) swap_theta(ctx);
+}
+
+// the buffer layout a step starts from: time level parity and the rotations' positions
+std::string layout_sig(mpas_dyc_ctx* ctx) {
+  Block& b = ctx->blk[0];
+  return std::to_string(ctx->cur) + "." + std::to_string(find(b, "diag", "ru")->rot_pos) + "." +
+         std::to_string(find(b, "state", "theta_m")->flip);
+}
+
+// the rotated fields' buffers and positions, to undo the rotations of a dry run (plan_all)
+struct Layout {
+  std::vector<std::tuple<Field*, void*, void*, int, int>> f;
+};
+Layout save_layout(mpas_dyc_ctx* ctx) {
+  Layout l;
+  for (auto& b : ctx->blk)
+    for (auto& f : b.fields)
+      if (f.rot >= 0 || (f.pool == "state" && f.name == "theta_m")) l.f.emplace_back(&f, f.buf[0], f.buf[1], f.rot_pos, f.flip);
+  return l;
+}
+void restore_layout(const Layout& l) {
+  for (const auto& t : l.f) {
+    Field* f = std::get<0>(t);
+    f->buf[0] = std::get<1>(t);
+    f->buf[1] = std::get<2>(t);
+    f->rot_pos = std::get<3>(t);
+    f->flip = std::get<4>(t);
+  }
+}
+
+// atm_rk_integration_setup (1847-1857): the saves and the time level 2 copies are rotate_saves /
+// stage_pre; scalars_2 = scalars_1 (1856) is copied over owned+halo elements (the scalar
+// transport writes owned columns of time level 2 and exchanges the rest, and with scalar advection
+// off time level 2 must hold the old values)
+void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
+  CopyList c{};
+  c.src[0] = p.scalars1;
+  c.dst[0] = p.scalars2;
+  c.n[0] = (int64_t)(d.nCells + 1) * d.K * d.ns;
+  const unsigned gx = (unsigned)std::min<int64_t>((c.n[0] + 255) / 256, 2048);
+  if (!ctx->planning) hipLaunchKernelGGL(k_copy_many, dim3(gx, 1), dim3(256), 0, ctx->stream, c);
 }
 
 
@@ -1247,15 +1364,17 @@ int summary_launch(mpas_dyc_ctx* ctx, int tl) {
   return MPAS_DYC_OK;
 }
 
-// run `body(d, p)` for every block (the reference's `block => domain % blocklist` loops)
-#define EACH(...)                                       \
+// run `body(d, p)` for every block (the reference's `block => domain % blocklist` loops), with the
+// blocks' pointers from the vector V (EACH: P)
+#define EACHV(V, ...)                                   \
   for (size_t ib_ = 0; ib_ < ctx->blk.size(); ++ib_) {  \
     const Dims& d = ctx->blk[ib_].d;                    \
-    const Ptrs& p = P[ib_];                             \
+    const Ptrs& p = (V)[ib_];                           \
     (void)d;                                            \
     (void)p;                                            \
     __VA_ARGS__;                                        \
   }
+#define EACH(...) EACHV(P, __VA_ARGS__)
 
 // atm_srk3 (mpas_atm_time_integration.F:142-1796)
 // atm_bdy_adjust_scalars (6436-6586) at the end of a transport stage: the scalars' halo first
@@ -1281,7 +1400,18 @@ int step_tail(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt) {
 
 int srk3(mpas_dyc_ctx* ctx, double dt) {
   const Config& cf = ctx->cf;
-  const std::vector<Ptrs> P = block_ptrs(ctx);
+  // P: the fields; Ppre / Pfin: what a dynamics substep's first stage reads before its recovery
+  // (stage_pre, stage_fin), rebuilt after every rotation of the buffers
+  std::vector<Ptrs> P = block_ptrs(ctx), Ppre, Pfin;
+  auto relayout = [&](bool first_substep) {
+    P = block_ptrs(ctx);
+    Ppre.clear();
+    Pfin.clear();
+    for (const Ptrs& q : P) {
+      Ppre.push_back(stage_pre(q, first_substep));
+      Pfin.push_back(stage_fin(q, first_substep));
+    }
+  };
   int dynamics_split = cf.dynamics_split_steps;
   double dt_dynamics;
   if (cf.split_dynamics_transport) {
@@ -1322,7 +1452,9 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   CHK(exchange(ctx, {{"state", "theta_m", 1, ALL_LAYERS}, {"state", "scalars", 1, ALL_LAYERS},
                      {"diag", "pressure_p", 0, ALL_LAYERS}, {"diag", "rtheta_p", 0, ALL_LAYERS},
                      {"diag", "exner", 0, ALL_LAYERS}}));
-  EACH(rk_integration_setup(ctx, d, p));                          // 341-381
+  rotate_saves(ctx);                                              // 341-381: the saves,
+  relayout(true);                                                 // time level 2 via stage_pre
+  EACH(rk_integration_setup(ctx, d, p));
   EACH(LAUNCH(k_moist_cells, d.nCells, d, p));                    // 383-422
   EACH(LAUNCH(k_moist_edges, d.nEdges, d, p));
   // physics tendencies are zero without DO_PHYSICS (450-457): scratch arrays stay zero.
@@ -1335,36 +1467,39 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   auto xwait = [&]() { return split ? exchange_wait(ctx) : MPAS_DYC_OK; };
   bool pending = false;  // an xchg whose xwait is still due
   bool final_pending = false;  // the last substep's 1234-1249 exchange, waited for after substep_finish
-  EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));           // 476-510 of dynamics substep 1
+  EACHV(Ppre, vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));    // 476-510 of dynamics substep 1
   for (int dynamics_substep = 1; dynamics_substep <= dynamics_split; ++dynamics_substep) {
     // 513 (exner): carried by the step-start exchange and by the 1282-1297 exchange below
     for (int rk_step = 1; rk_step <= 3; ++rk_step) {
       if (cf.time_integration_order == 3 && rk_step == 2) EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[1]));
       const bool last_stage = dynamics_substep == dynamics_split && rk_step == 3;
+      // the first stage reads time level 2 and the saved fields through stage_pre until its recovery
+      const std::vector<Ptrs>& PS = rk_step == 1 ? Ppre : P;
+      const std::vector<Ptrs>& PF = rk_step == 1 ? Pfin : P;  // the stage's last cell phase
       if (pending) {  // 561-630, k_dyn_cells1 overlapping the exchange
-        EACH(dyn_tend(ctx, d, p, rk_step, dt, 1, !split && batched(d)));
+        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 1, !split && batched(d)));
         CHK(xwait());
         pending = false;
-        EACH(dyn_tend(ctx, d, p, rk_step, dt, 2, false, last_stage));
+        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 2, false, last_stage));
       } else {
-        EACH(dyn_tend(ctx, d, p, rk_step, dt, 0, !split && batched(d) && !lbc, last_stage));  // 561-630
+        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 0, !split && batched(d) && !lbc, last_stage));  // 561-630
       }
       const double dts = rk_sub_timestep[rk_step - 1];
       if (split) {  // 642 | 644-678: interior cells overlap the tend_u exchange
         CHK(exchange_async(ctx, {{"tend", "u", 0, 0x1u}}));
-        EACH(smlstep_pert(ctx, d, p, 1));
+        EACHV(PS, smlstep_pert(ctx, d, p, 1));
         CHK(exchange_wait(ctx));
-        EACH(smlstep_pert(ctx, d, p, 2));
+        EACHV(PS, smlstep_pert(ctx, d, p, 2));
       } else {
         CHK(exchange(ctx, {{"tend", "u", 0, 0x1u}}));             // 642
-        EACH(smlstep_pert(ctx, d, p, 0));     // 644-678
+        EACHV(PS, smlstep_pert(ctx, d, p, 0));     // 644-678
       }
       if (lbc) {  // 683-778: specified-zone tendencies, then the relaxation zone toward the driving state
         const double tds = dt_dynamics * (double)(dynamics_substep - 1) + rk_timestep[rk_step - 1];
-        EACH(LAUNCH(k_lbc_spec_tend_cells, d.nCellsSolve, d, p));
-        EACH(LAUNCH(k_lbc_spec_tend_edges, d.nEdgesSolve, d, p));
-        EACH(LAUNCH(k_lbc_relax_cells, d.nCellsSolve, d, p, dt, tds));
-        EACH(LAUNCH(k_lbc_relax_edges, d.nEdges, d, p, dt, tds));
+        EACHV(PS, LAUNCH(k_lbc_spec_tend_cells, d.nCellsSolve, d, p));
+        EACHV(PS, LAUNCH(k_lbc_spec_tend_edges, d.nEdgesSolve, d, p));
+        EACHV(PS, LAUNCH(k_lbc_relax_cells, d.nCellsSolve, d, p, dt, tds));
+        EACHV(PS, LAUNCH(k_lbc_relax_edges, d.nEdges, d, p, dt, tds));
       }
       // Acoustic sub-steps (788-870).
       // * Exchanges.  The reference exchanges rho_pp before every sub-step (792) and rtheta_pp
@@ -1391,17 +1526,18 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         if (small_step == 1) {
           // 794-837: formed by the readers (above)
         } else if (split) {  // interior edges overlap the exchange issued after the last cell phase
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 1, small_step == 2));
+          EACHV(PS, acoustic_edges(ctx, d, p, dts, small_step, 1, 1, small_step == 2));
           CHK(exchange_wait(ctx));
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 2, small_step == 2, um_of(ib_)));
+          EACHV(PS, acoustic_edges(ctx, d, p, dts, small_step, 1, 2, small_step == 2, um_of(ib_)));
         } else {
-          EACH(acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2, um_of(ib_)));
+          EACHV(PS, acoustic_edges(ctx, d, p, dts, small_step, 1, 0, small_step == 2, um_of(ib_)));
         }
         unpack_xp = nullptr;
         std::vector<XField> xf = {{"diag", "rtheta_pp", 0, 0x1u}};  // 845
         if (small_step < nsub) xf.push_back({"diag", "rho_pp", 0, 0x1u});  // 792 of the next sub-step
         const XPlan* xp = fused_pack_plan(ctx, xf);  // the cell phase packs this exchange's send buffer
-        EACH(acoustic_cells(ctx, d, p, dts, small_step, small_step == nsub, rk_timestep[rk_step - 1],
+        EACHV(small_step == nsub ? PF : PS,
+              acoustic_cells(ctx, d, p, dts, small_step, small_step == nsub, rk_timestep[rk_step - 1],
                             1 / (double)nsub, rk_step, needs_exchange(ctx) || last_stage,
                             xp ? xp->pack[ib_] : PackMap{}, damping_delta(ctx, d, last_stage)));
         if (split) {
@@ -1507,6 +1643,11 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
     if (!ctx->planning)                                           // 1304-1341
       EACH(hipLaunchKernelGGL(k_substep_finish_v, dim3(2048), dim3(BLOCK_THREADS), 0, ctx->stream, d, p,
                               dynamics_substep, dynamics_split, 1.0 / (double)dynamics_split));
+    if (dynamics_substep < dynamics_split) {  // the saves and theta_m_1 = theta_m_2 of 6051-6058
+      rotate_saves(ctx);
+      swap_theta(ctx);
+      relayout(false);
+    }
     if (final_pending) {
       CHK(exchange_wait(ctx));
       final_pending = false;
@@ -1684,12 +1825,15 @@ int warm_rccl(mpas_dyc_ctx* ctx) {
 
 int plan_all(mpas_dyc_ctx* ctx, double dt) {
   if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
-  if (!needs_exchange(ctx) || ctx->planned[ctx->cur]) return MPAS_DYC_OK;
+  const std::string sig = layout_sig(ctx);
+  if (!needs_exchange(ctx) || ctx->planned.count(sig)) return MPAS_DYC_OK;
+  const Layout l = save_layout(ctx);  // the dry run rotates buffers as the step does
   ctx->planning = true;
   int r = srk3(ctx, dt);
   ctx->planning = false;
+  restore_layout(l);
   if (r == MPAS_DYC_OK) {
-    ctx->planned[ctx->cur] = true;
+    ctx->planned.insert(sig);
     r = warm_rccl(ctx);
   }
   return r;
@@ -2086,10 +2230,7 @@ int mpas_dyc_set_summary(mpas_dyc_ctx* ctx, int32_t flags) {
   HIPCHK(hipStreamSynchronize(ctx->stream));
   ctx->summary_flags = flags;
   ctx->summary_tl = 0;
-  for (int i = 0; i < 2; ++i) {  // captured steps bake the modes in
-    if (ctx->graph_exec[i]) (void)hipGraphExecDestroy(ctx->graph_exec[i]);
-    ctx->graph_exec[i] = nullptr;
-  }
+  drop_graphs(ctx);  // captured steps bake the modes in
   return MPAS_DYC_OK;
 }
 
@@ -2263,10 +2404,7 @@ int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags) {
   HIPCHK(hipStreamSynchronize(ctx->stream));
   ctx->physics = flags;
   for (auto& b : ctx->blk) b.d.physics = (flags & MPAS_DYC_PHYSICS_TENDENCIES) ? 1 : 0;
-  for (int i = 0; i < 2; ++i) {  // captured steps bake the flags in
-    if (ctx->graph_exec[i]) (void)hipGraphExecDestroy(ctx->graph_exec[i]);
-    ctx->graph_exec[i] = nullptr;
-  }
+  drop_graphs(ctx);  // captured steps bake the flags in
   return MPAS_DYC_OK;
 }
 
@@ -2290,21 +2428,26 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
   HIPCHK(hipSetDevice(ctx->device));
   CHK(plan_all(ctx, dt));
   if (ctx->use_graph) {
-    const int parity = ctx->cur;
-    if (!ctx->graph_exec[parity] || ctx->graph_dt[parity] != dt) {
-      if (ctx->graph_exec[parity]) (void)hipGraphExecDestroy(ctx->graph_exec[parity]);
-      ctx->graph_exec[parity] = nullptr;
+    // one captured graph per buffer layout the step starts from; capturing runs srk3, whose
+    // rotations move the host's view of the buffers, and a replay repeats them
+    const std::string sig = layout_sig(ctx);
+    auto git = ctx->graphs.find(sig);
+    if (git == ctx->graphs.end() || ctx->graph_dt[sig] != dt) {
+      if (git != ctx->graphs.end() && git->second) (void)hipGraphExecDestroy(git->second);
+      ctx->graphs.erase(sig);
       hipGraph_t g = nullptr;
+      hipGraphExec_t ge = nullptr;
+      const Layout l0 = save_layout(ctx);
       HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
       int r = srk3(ctx, dt);
       hipError_t e = hipStreamEndCapture(ctx->stream, &g);
       if (r && r != MPAS_DYC_ECOMM) return r;
       if (r == MPAS_DYC_ECOMM && e == hipSuccess) e = hipErrorUnknown;  // RCCL refused to be captured
-      if (e == hipSuccess) e = hipGraphInstantiate(&ctx->graph_exec[parity], g, nullptr, nullptr, 0);
+      if (e == hipSuccess) e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
       if (g) (void)hipGraphDestroy(g);
       if (e != hipSuccess) {
         (void)hipGetLastError();
-        ctx->graph_exec[parity] = nullptr;
+        restore_layout(l0);  // nothing ran: the eager step below rotates from the start
         if (ctx->nranks > 1) {  // every rank captures or the job fails: no rank goes eager alone
           ctx->err = std::string("hipGraph capture of the step failed on rank ") + std::to_string(ctx->rank) + ": " +
                      hipGetErrorString(e);
@@ -2319,9 +2462,14 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
         HIPCHK(hipGetLastError());
         return r;
       }
-      ctx->graph_dt[parity] = dt;
+      ctx->graphs[sig] = ge;
+      ctx->graph_dt[sig] = dt;
+      HIPCHK(hipGraphLaunch(ge, ctx->stream));  // the capture made the step's rotations already
+      ctx->graph_ran = true;
+      return MPAS_DYC_OK;
     }
-    HIPCHK(hipGraphLaunch(ctx->graph_exec[parity], ctx->stream));
+    HIPCHK(hipGraphLaunch(git->second, ctx->stream));
+    apply_step_rotations(ctx);
     ctx->graph_ran = true;
     return MPAS_DYC_OK;
   }
@@ -2360,12 +2508,14 @@ int mpas_dyc_plan_exchanges(mpas_dyc_ctx* ctx, int32_t nranks, int32_t rank, dou
   ctx->record = &seq;
   ctx->planning = true;
   const int cur0 = ctx->cur;
+  const Layout l0 = save_layout(ctx);
   int r = init_diagnostics(ctx, dt);
   for (int step = 0; step < 2 && r == MPAS_DYC_OK; ++step) {
     r = srk3(ctx, dt);
     ctx->cur ^= 1;  // mpas_dyc_shift_time_levels
   }
   ctx->cur = cur0;
+  restore_layout(l0);
   ctx->planning = false;
   ctx->record = nullptr;
   if (r) return r;

@@ -2525,7 +2525,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
   }
   const double coftz = p.coftz[ow], zz = p.zz[o], cofwt = p.cofwt[o], cofwz = p.cofwz[o], cofwr = p.cofwr[o];
   const double a_tri = p.a_tri[o], alpha_tri = p.alpha_tri[o], gamma_tri = p.gamma_tri[o];
-  const double rz = p.rho_zz2[o], dss = p.dss[o], rws = p.rw_save[ow], rw = p.rw[ow], w2 = p.w2[ow];
+  // rho_zz (tl2), rw and w (tl2) through the *_rd pointers: in a dynamics substep's first stage
+  // they name the buffers that hold these values until the recovery (srk3, stage_fin)
+  const double rz = p.rho_zz2_rd[o], dss = p.dss[o], rws = p.rw_save[ow], rw = p.rw_rd[ow], w2 = p.w2_rd[ow];
   const double cofrz = p.cofrz[kc], rdzw = p.rdzw[kc], fzm = p.fzm[kc], fzp = p.fzp[kc];
   RecIn ri{};
   const double rtpp_old = (small_step == 1) ? 0.0 : rtpp;
@@ -2678,10 +2680,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p
     // implicit Rayleigh damping of w (2687-2693)
     if (act && k >= 1) {
       const double fzm = p.fzm[k], fzp = p.fzp[k];
-      const double rz = p.rho_zz2[o], rzm = p.rho_zz2[o - 1];
+      const double rz = p.rho_zz2_rd[o], rzm = p.rho_zz2_rd[o - 1];
       const double dss = p.dss[o];
-      const double dd = p.rw_save[ow] - p.rw[ow];
-      rwp = (rwp + dd - dts * dss * (fzm * zz + fzp * zzm) * (fzm * rz + fzp * rzm) * p.w2[ow]) / (1.0 + dts * dss) - dd;
+      const double dd = p.rw_save[ow] - p.rw_rd[ow];
+      rwp = (rwp + dd - dts * dss * (fzm * zz + fzp * zzm) * (fzm * rz + fzp * rzm) * p.w2_rd[ow]) / (1.0 + dts * dss) - dd;
       wwa = wwa + 0.5 * (1.0 + epssm) * rwp;
     }
     const double rwp_p2 = dn1(rwp);
@@ -3260,80 +3262,50 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_init_coupled_c(Dims d, Ptrs p
 // ============================================================================
 // atm_rk_dynamics_substep_finish  (mpas_atm_time_integration.F:6051-6079)
 // ============================================================================
-// Called at 1304-1341; flat 16-byte streams: each (K, n) /
-// (K+1, n) array is contiguous over its owned+halo columns, so instead of one column per wave
-// (56 of 64 lanes, 8 B each) every lane moves two doubles.  Same ranges (garbage slot excluded),
-// same expressions.
-// u_1 = u_2 and w_1 = w_2 (6060-6061) are not stored: nothing reads u or w of time level 1
-// before the dt ends -- the substeps read time level 2, and the transport, the exchanges and the
-// summary do not touch u_1 / w_1 -- and after mpas_pool_shift_time_levels that buffer is time
-// level 2, which the next atm_rk_integration_setup overwrites (u_2 = u_1, w_2 = w_1, 1852-1853)
-// before anything reads it.  Time level 1 after the step (the new state) is unchanged.
-__device__ __forceinline__ void fin_edge_pair(const Ptrs& p, int64_t j, int n, int cp, int first, int last, double inv) {
+// Called at 1304-1341; flat 16-byte streams: each (K, n) / (K+1, n) array is contiguous over its
+// owned+halo columns, so every lane moves two doubles.  Same ranges (garbage slot excluded), same
+// expressions.  Only the averaging of ruAvg / wwAvg over the dynamics substeps (6064-6078) is
+// stored here.  The copies of 6051-6061 are not:
+//  * ru_save = ru, rw_save = rw, rtheta_p_save = rtheta_p, rho_p_save = rho_p: srk3 rotates each
+//    pair's buffers instead (rotate_saves), see stage_pre;
+//  * theta_m_1 = theta_m_2: srk3 swaps the two time-level buffers (swap_theta);
+//  * u_1 = u_2, w_1 = w_2, rho_zz_1 = rho_zz_2 and, at the last substep, rho_zz_1 =
+//    rho_zz_old_split: nothing in the dynamics reads time level 1 of u, w or rho_zz (the substeps
+//    read time level 2, the acoustic step and dyn_tend theta_m of time level 1), so rho_zz_1 keeps
+//    the step's starting value, which is what the last substep restores (1824, 6079) and the
+//    split transport reads; u_1 / w_1 are overwritten by the next atm_rk_integration_setup after
+//    mpas_pool_shift_time_levels before anything reads them.
+__device__ __forceinline__ void fin_avg(double* avg, double* split, int64_t j, int n, int first, int last, double inv) {
   for (int q = 0; q < n; ++q) {  // n = 2, or 1 for an odd tail
     const int64_t i = j + q;
-    if (cp) p.ru_save[i] = p.ru[i];
-    const double ras = first ? p.ruAvg[i] : p.ruAvg[i] + p.ruAvg_split[i];
-    p.ruAvg_split[i] = ras;
-    if (last) p.ruAvg[i] = ras * inv;
+    const double a = first ? avg[i] : avg[i] + split[i];
+    split[i] = a;
+    if (last) avg[i] = a * inv;
   }
 }
 __global__ __launch_bounds__(BLOCK_THREADS) void k_substep_finish_v(Dims d, Ptrs p, int dynamics_substep,
                                                                      int dynamics_split, double inv_dynamics_split) {
-  const int64_t nE = (int64_t)d.nEdges * d.K, nW = (int64_t)d.nCells * (d.K + 1), nC = (int64_t)d.nCells * d.K;
+  const int64_t nE = (int64_t)d.nEdges * d.K, nW = (int64_t)d.nCells * (d.K + 1);
   const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
-  const int cp = dynamics_substep < dynamics_split, first = dynamics_substep == 1, last = dynamics_substep == dynamics_split;
+  const int first = dynamics_substep == 1, last = dynamics_substep == dynamics_split;
   const double inv = inv_dynamics_split;
-  for (int64_t j = 2 * t0; j < nE; j += 2 * st) {
-    if (j + 1 < nE) {
-      if (cp) st2(p.ru_save + j, ld2(p.ru + j));
-      const d2 a = ld2(p.ruAvg + j);
-      d2 ras = a;
-      if (!first) {
-        const d2 b = ld2(p.ruAvg_split + j);
-        ras = d2{a.x + b.x, a.y + b.y};
+  for (int w = 0; w < 2; ++w) {
+    double* avg = w ? p.wwAvg : p.ruAvg;
+    double* split = w ? p.wwAvg_split : p.ruAvg_split;
+    const int64_t n = w ? nW : nE;
+    for (int64_t j = 2 * t0; j < n; j += 2 * st) {
+      if (j + 1 < n) {
+        const d2 a = ld2(avg + j);
+        d2 s2 = a;
+        if (!first) {
+          const d2 b = ld2(split + j);
+          s2 = d2{a.x + b.x, a.y + b.y};
+        }
+        st2(split + j, s2);
+        if (last) st2(avg + j, d2{s2.x * inv, s2.y * inv});
+      } else {
+        fin_avg(avg, split, j, 1, first, last, inv);
       }
-      st2(p.ruAvg_split + j, ras);
-      if (last) st2(p.ruAvg + j, d2{ras.x * inv, ras.y * inv});
-    } else {
-      fin_edge_pair(p, j, 1, cp, first, last, inv);
-    }
-  }
-  for (int64_t j = 2 * t0; j < nW; j += 2 * st) {
-    if (j + 1 < nW) {
-      if (cp) st2(p.rw_save + j, ld2(p.rw + j));
-      const d2 a = ld2(p.wwAvg + j);
-      d2 was = a;
-      if (!first) {
-        const d2 b = ld2(p.wwAvg_split + j);
-        was = d2{a.x + b.x, a.y + b.y};
-      }
-      st2(p.wwAvg_split + j, was);
-      if (last) st2(p.wwAvg + j, d2{was.x * inv, was.y * inv});
-    } else {
-      if (cp) p.rw_save[j] = p.rw[j];
-      const double was = first ? p.wwAvg[j] : p.wwAvg[j] + p.wwAvg_split[j];
-      p.wwAvg_split[j] = was;
-      if (last) p.wwAvg[j] = was * inv;
-    }
-  }
-  for (int64_t j = 2 * t0; j < nC; j += 2 * st) {
-    if (j + 1 < nC) {
-      if (cp) {
-        st2(p.rtheta_p_save + j, ld2(p.rtheta_p + j));
-        st2(p.rho_p_save + j, ld2(p.rho_p + j));
-        st2(p.theta_m1 + j, ld2(p.theta_m2 + j));
-        st2(p.rho_zz1 + j, ld2(p.rho_zz2 + j));
-      }
-      if (last) st2(p.rho_zz1 + j, ld2(p.rho_zz_old_split + j));
-    } else {
-      if (cp) {
-        p.rtheta_p_save[j] = p.rtheta_p[j];
-        p.rho_p_save[j] = p.rho_p[j];
-        p.theta_m1[j] = p.theta_m2[j];
-        p.rho_zz1[j] = p.rho_zz2[j];
-      }
-      if (last) p.rho_zz1[j] = p.rho_zz_old_split[j];
     }
   }
 }

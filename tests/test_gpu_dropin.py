@@ -172,8 +172,8 @@ def test_dropin_regional_matches_reference(moist):
     from oracle import ref_runner
     if not (ref_runner.available() and ref_runner.available(ref_runner.DROPIN_HARNESS)):
         pytest.skip("oracle/_ref harness binaries not built (make -C oracle all dropin)")
-    case = jw_case(2562, K=26, ns=6 if moist else 1, moist=moist, cache=False)
-    case, lbc = regional_lbc(case)
+    case0 = jw_case(2562, K=26, ns=6 if moist else 1, moist=moist, cache=False)
+    case, lbc = regional_lbc(case0)
     dt, n, me = float(case["dt"]), 6, 6 if moist else 1
     ref, _ = ref_runner.run_reference(case, n, dt, [1, n], nthreads=4, lbc=lbc, moist_end=me)
     got, _ = ref_runner.run_reference(case, n, dt, [1, n], nthreads=1, lbc=lbc, moist_end=me,
@@ -183,9 +183,10 @@ def test_dropin_regional_matches_reference(moist):
             tol = 1e-9 if k in ("state.w.tl1", "state.scalars.tl1") else 1e-10
             err = rel_linf(got[step][k], ref[step][k])
             assert err <= tol, f"regional step {step} {k}: rel Linf {err:.3e}"
-    # the boundary conditions act: the same drop-in run without them differs
-    glob, _ = ref_runner.run_reference(case, n, dt, [n], nthreads=1, moist_end=me, binary=ref_runner.DROPIN_HARNESS,
+    # the boundary conditions act: the global drop-in run of the same state differs
+    glob, _ = ref_runner.run_reference(case0, n, dt, [n], nthreads=1, moist_end=me, binary=ref_runner.DROPIN_HARNESS,
                                        dump_only=["state.theta_m"])
+    assert np.isfinite(glob[n]["state.theta_m.tl1"]).all()
     assert rel_linf(glob[n]["state.theta_m.tl1"], got[n]["state.theta_m.tl1"]) > 1e-6
 
 

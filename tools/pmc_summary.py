@@ -30,9 +30,9 @@ def main():
     nC, K, ns = (int(x) for x in sys.argv[2:5]) if len(sys.argv) > 4 else (163842, 56, 1)
     fetch = load(os.path.join(d, "pmc_fetch", "fetch_counter_collection.csv"))
     write = load(os.path.join(d, "pmc_write", "write_counter_collection.csv"))
-    # calibration: k_copy_many moves (nE*K + 2 nC*(K+1) + 6 nC*K + nC*K*ns) doubles each way
-    nE = 3 * nC - 6 if nC > 12 else 0
-    known = 8.0 * (2 * nE * K + 2 * nC * (K + 1) + 5 * nC * K + nC * K * ns)
+    # calibration: k_copy_many (atm_rk_integration_setup's scalars_2 = scalars_1, the one copy the
+    # step still makes) moves (nC + 1) * K * ns doubles each way
+    known = 8.0 * (nC + 1) * K * ns
     cf = known / (sum(x[0] for x in fetch["k_copy_many"]) / len(fetch["k_copy_many"]))
     cw = known / (sum(x[0] for x in write["k_copy_many"]) / len(write["k_copy_many"]))
     rows = []
