@@ -18,6 +18,7 @@
 #   prof8b           rocprofv3 kernel trace of blocks8 (gpurun_out/prof8b)
 #   ab               same-box A/B of AB_LIBS (default exp/lib_base.so vs the in-tree library),
 #                    AB_ROUNDS rounds of tools/kbench.py (AB_ARGS extra arguments)
+#   kprof            rocprofv3 kernel stats of tools/kbench.py for each of AB_LIBS (gpurun_out/kprof_<i>)
 #   smoke            __graft_entry__.smoke()
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out || exit 1
 B="--no-cpu-baseline --no-configs1"
@@ -43,6 +44,9 @@ step() {
           echo "== $L" >> gpurun_out/ab.log
           MPAS_DYCORE_LIB=$L timeout -k 10 250 python tools/kbench.py --steps ${AB_STEPS:-10} ${AB_ARGS} >> gpurun_out/ab.log 2>&1 || return 1
         done; done; grep -h "==\|ms_dt" gpurun_out/ab.log | cut -c1-200 ;;
+    kprof) i=0; for L in ${AB_LIBS:-exp/lib_base.so mpas-model_amd/csrc/libmpas_dycore.so}; do
+          MPAS_DYCORE_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof_$i -o run --output-format csv -- python3 tools/kbench.py --steps ${AB_STEPS:-10} ${AB_ARGS} > gpurun_out/kprof_$i.log 2>&1 || return 1
+          echo "kprof_$i = $L"; i=$((i+1)); done ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && last gpurun_out/smoke.log ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
