@@ -47,7 +47,7 @@ def jw_len_disp(level: int) -> float:
 def jw_case(ncells: int, K: int = 56, ns: int = 1, moist: bool = False, order: int = 2,
             lloyd_iters: int = 20, cache: bool = True) -> dict:
     level = level_for(ncells)
-    key = f"jw_l{level}_K{K}_ns{ns}_m{int(moist)}_o{order}_ll{lloyd_iters}_v4"
+    key = f"jw_l{level}_K{K}_ns{ns}_m{int(moist)}_o{order}_ll{lloyd_iters}_v6"
     path = os.path.join(CACHE, key + ".pkl")
     if cache and os.path.isfile(path):
         with open(path, "rb") as f:  # our own cache file, written below
@@ -73,7 +73,7 @@ def varres_case(ncells: int, ratio: float = 20.0, K: int = 56, ns: int = 1, mois
     (dt ~ 5 s per km of the finest cells, len_disp = finest spacing)."""
     if lloyd_iters is None:
         lloyd_iters = 40 if ncells <= 200000 else 6
-    key = f"vr_n{ncells}_r{ratio:g}_K{K}_ns{ns}_m{int(moist)}_ll{lloyd_iters}_v5"
+    key = f"vr_n{ncells}_r{ratio:g}_K{K}_ns{ns}_m{int(moist)}_ll{lloyd_iters}_v6"
     path = os.path.join(CACHE, key + ".pkl")
     if cache and os.path.isfile(path):
         with open(path, "rb") as f:  # our own cache file, written below

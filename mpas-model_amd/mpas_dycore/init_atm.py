@@ -5,9 +5,11 @@ restated in numpy so the GPU box (which never sees /root/reference) can build
 the synthetic inputs of BASELINE.json's configs on its own:
 
 * vertical grid and metrics       -- core_init_atmosphere/mpas_init_atm_cases.F:615-706
-* Jablonowski-Williamson state    -- mpas_init_atm_cases.F:367-1160 (``rebalance``
-                                     replaced by the analytic JW wind, the path the
-                                     reference takes with rebalance=.false., 1005-1011)
+* Jablonowski-Williamson state    -- mpas_init_atm_cases.F:367-1160, with the
+                                     reference's rebalance = .true. (the zonal wind
+                                     geostrophically rebalanced on a 721-latitude
+                                     grid, 720-838 and 1215-1312) or, with
+                                     rebalance=False, the analytic JW wind (1005-1011)
 * zb / zb3 terrain flux metrics   -- mpas_init_atm_cases.F:1045-1093
 * deriv_two (quadratic LSQ fit)   -- core_init_atmosphere/mpas_atm_advection.F:21-394
 * defc_a / defc_b                 -- core_init_atmosphere/mpas_atm_advection.F:744-946
@@ -65,9 +67,9 @@ def vertical_grid(K: int, zt: float = 45000.0):
     nz1, nz = K, K + 1
     dz = zt / float(nz1)
     k = np.arange(nz)
-    sh = (k * dz / zt) ** 1.5
+    sh = _pow(k * dz / zt, 1.5)
     zw = k * dz
-    ah = 1.0 - np.cos(0.5 * PII * k * dz / zt) ** 6
+    ah = 1.0 - _ipow(np.cos(0.5 * PII * k * dz / zt), 6)
     dzw = zw[1:] - zw[:-1]
     rdzw = 1.0 / dzw
     dzu = np.zeros(nz1)
@@ -90,10 +92,11 @@ def vertical_grid(K: int, zt: float = 45000.0):
 def _jw_hx(phi, r_earth):
     u0 = 35.0
     etavs = (1.0 - 0.252) * PII / 2.0
-    return (u0 / GRAVITY * np.cos(etavs) ** 1.5
-            * ((-2.0 * np.sin(phi) ** 6 * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0)
-               * u0 * np.cos(etavs) ** 1.5
-               + (1.6 * np.cos(phi) ** 3 * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * r_earth * OMEGA))
+    ce15 = _pow(np.cos(etavs), 1.5)
+    return (u0 / GRAVITY * ce15
+            * ((-2.0 * _ipow(np.sin(phi), 6) * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0)
+               * u0 * ce15
+               + (1.6 * _ipow(np.cos(phi), 3) * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * r_earth * OMEGA))
 
 
 # ---- the reference's spherical geometry (core_init_atmosphere/mpas_atm_advection.F:397-537),
@@ -106,6 +109,27 @@ _LIBM_ACOS = np.frompyfunc(math.acos, 1, 1)
 
 
 _LIBM_POW = np.frompyfunc(math.pow, 2, 1)
+_LIBM_EXP = np.frompyfunc(math.exp, 1, 1)
+_LIBM_TAN = np.frompyfunc(math.tan, 1, 1)
+
+
+# The JW initial state follows the compiled reference's arithmetic (checked against amdflang's
+# lowering): x**n with an integer n is the product x*x*...*x from the left, x**r with a real r and
+# exp / tan / asin are the C library's; numpy's own exp, tan and pow differ from it in the last
+# bit for about 5 % of arguments (sin, cos, sqrt agree).
+def _ipow(x, n):
+    r = x
+    for _ in range(n - 1):
+        r = r * x
+    return r
+
+
+def _exp(x):
+    return np.asarray(_LIBM_EXP(np.asarray(x, dtype=np.float64)), dtype=np.float64)
+
+
+def _tan(x):
+    return np.asarray(_LIBM_TAN(np.asarray(x, dtype=np.float64)), dtype=np.float64)
 
 
 def _pow(x, y):
@@ -383,9 +407,13 @@ def adv_coef_compression(m, d2):
 
 
 def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: dict | None = None,
-               init_case: int = 2) -> dict:
+               init_case: int = 2, rebalance: bool = True) -> dict:
     """Build every mesh/state/diag input array of the dycore for the JW case.
 
+    ``rebalance`` (default): the zonal wind as the reference computes it (its parameter rebalance =
+    .true., mpas_init_atm_cases.F:440): the JW wind on a 721-point latitude grid, rebalanced
+    geostrophically (init_atm_recompute_geostrophic_wind) and integrated over each edge's
+    latitude span (init_atm_calc_flux_zonal).  False: the analytic JW wind (1005-1011).
     Returns a flat dict keyed by MPAS field name (0-based index arrays, element-major
     (n, K) float arrays, i.e. the transpose of the Fortran (K, n) layout)."""
     cfg = dict(DEFAULT_CONFIG)
@@ -440,20 +468,25 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
     if init_case == 2:
         lat_pert, lon_pert = 40.0 * PII / 180.0, 20.0 * PII / 180.0
         le, lo = m["latEdge"], m["lonEdge"]
-        arg = np.sin(le) * np.sin(lat_pert) + np.cos(le) * np.cos(lat_pert) * np.cos(lo - lon_pert)
-        r_pert = np.arccos(np.clip(arg, -1.0, 1.0)) / 0.1
-        u_pert = 1.0 * np.exp(-r_pert ** 2) * (lat2 - lat1) * R / m["dvEdge"]
+        # sphere_distance(latEdge, lonEdge, lat_pert, lon_pert, 1) (mpas_init_atm_static.F:1314-1328)
+        arg1 = np.sqrt(np.sin(0.5 * (lat_pert - le)) ** 2 + np.cos(le) * np.cos(lat_pert) * np.sin(0.5 * (lon_pert - lo)) ** 2)
+        r_pert = 2.0 * 1.0 * _asin(arg1) / 0.1
+        u_pert = 1.0 * _exp(-r_pert ** 2) * (lat2 - lat1) * R / m["dvEdge"]
     else:
         u_pert = np.zeros(nE)
-    etavs = (0.5 * (ppb[c1] + ppb[c2] + pp[c1] + pp[c2]) / P0 - 0.252) * PII / 2.0
-    u = u0 * flux[:, None] * np.cos(etavs) ** 1.5 + u_pert[:, None]
+    if rebalance:
+        u = u0 * _jw_flux_zonal(lat1, lat2, m["dvEdge"], R, vg, moist) / (0.5 * (rb[c1] + rb[c2] + rr[c1] + rr[c2])) \
+            + u_pert[:, None]
+    else:
+        etavs = (0.5 * (ppb[c1] + ppb[c2] + pp[c1] + pp[c2]) / P0 - 0.252) * PII / 2.0
+        u = u0 * flux[:, None] * _pow(np.cos(etavs), 1.5) + u_pert[:, None]
     ru = 0.5 * (rho_zz[c1] + rho_zz[c2]) * u
 
     fEdge = 2.0 * OMEGA * np.sin(m["latEdge"])
     fVertex = 2.0 * OMEGA * np.sin(m["latVertex"])
 
     # ---- deriv_two, zb/zb3 (mpas_init_atm_cases.F:1045-1093, theta_adv_order = 3)
-    d2 = compute_deriv_two(m)
+    d2 = m["deriv_two"] if "deriv_two" in m else compute_deriv_two(m)  # an init file may carry it
     nEoC, coc, eoc = m["nEdgesOnCell"], m["cellsOnCell"], m["edgesOnCell"]
     d2c1 = d2[:, 0, 0][:, None] * zgrid[c1]
     d2c2 = d2[:, 1, 0][:, None] * zgrid[c2]
@@ -465,25 +498,36 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
     dcE = m["dcEdge"][:, None]
     z_edge = 0.5 * (zgrid[c1] + zgrid[c2]) - dcE ** 2 * (d2c1 + d2c2) / 12.0
     z_edge3 = -dcE ** 2 * (d2c1 - d2c2) / 12.0
-    dvA1 = (m["dvEdge"] / m["areaCell"][c1])[:, None]
-    dvA2 = (m["dvEdge"] / m["areaCell"][c2])[:, None]
+    dv = m["dvEdge"][:, None]
+    a1, a2 = m["areaCell"][c1][:, None], m["areaCell"][c2][:, None]
     zb = np.zeros((nE, 2, nz))
     zb3 = np.zeros((nE, 2, nz))
-    zb[:, 0, :nz1] = ((z_edge - zgrid[c1]) * dvA1)[:, :nz1]
-    zb[:, 1, :nz1] = ((z_edge - zgrid[c2]) * dvA2)[:, :nz1]
-    zb3[:, 0, :nz1] = (z_edge3 * dvA1)[:, :nz1]
-    zb3[:, 1, :nz1] = (z_edge3 * dvA2)[:, :nz1]
+    zb[:, 0, :nz1] = ((z_edge - zgrid[c1]) * dv / a1)[:, :nz1]
+    zb[:, 1, :nz1] = ((z_edge - zgrid[c2]) * dv / a2)[:, :nz1]
+    zb3[:, 0, :nz1] = (z_edge3 * dv / a1)[:, :nz1]
+    zb3[:, 1, :nz1] = (z_edge3 * dv / a2)[:, :nz1]
 
     # ---- rw / w from terrain (mpas_init_atm_cases.F:1096-1126)
     coef3 = cfg["config_coef_3rd_order"]
     rw = np.zeros((nC, nz))
+    # the reference adds the edges' contributions in edge order (1103-1118): per cell, its edges in
+    # ascending order, as cellsOnEdge(2) +A -B or as cellsOnEdge(1) -C +D
+    eoc_sorted = np.sort(np.where(np.arange(m["maxEdges"])[None, :] < nEoC[:, None], eoc, nE), axis=1)
     for k in range(1, nz1):
         fl = fzm[k] * ru[:, k] + fzp[k] * ru[:, k - 1]
         z2 = fzm[k] * zz[c2, k] + fzp[k] * zz[c2, k - 1]
         z1 = fzm[k] * zz[c1, k] + fzp[k] * zz[c1, k - 1]
         sg = np.copysign(1.0, ru[:, k])
-        rw[:, k] += np.bincount(c2, weights=z2 * zb[:, 1, k] * fl - sg * coef3 * z2 * zb3[:, 1, k] * fl, minlength=nC)
-        rw[:, k] += np.bincount(c1, weights=-z1 * zb[:, 0, k] * fl + sg * coef3 * z1 * zb3[:, 0, k] * fl, minlength=nC)
+        a2, b2 = z2 * zb[:, 1, k] * fl, sg * coef3 * z2 * zb3[:, 1, k] * fl
+        a1, b1 = z1 * zb[:, 0, k] * fl, sg * coef3 * z1 * zb3[:, 0, k] * fl
+        x = np.zeros(nC)
+        for j in range(m["maxEdges"]):
+            e = eoc_sorted[:, j]
+            ok = e < nE
+            ee = np.where(ok, e, 0)
+            second = c2[ee] == np.arange(nC)
+            x = np.where(ok & second, (x + a2[ee]) - b2[ee], np.where(ok, (x - a1[ee]) + b1[ee], x))
+        rw[:, k] = x
     w = np.zeros((nC, nz))
     w[:, 1:nz1] = rw[:, 1:nz1] / (fzp[1:] * rho_zz[:, :-1] + fzm[1:] * rho_zz[:, 1:])
 
@@ -599,8 +643,8 @@ def _jw_columns(lat, zgrid, zz, vg, R, moist):
     znut = eta_t
     zzT = np.ascontiguousarray(zz.T)
     ztemp = np.ascontiguousarray(0.5 * (zgrid[:, 1:] + zgrid[:, :-1]).T)
-    ppb = P0 * np.exp(-GRAVITY * ztemp / (RGAS * t0b))
-    pb = (ppb / P0) ** (RGAS / CP)
+    ppb = P0 * _exp(-GRAVITY * ztemp / (RGAS * t0b))
+    pb = _pow(ppb / P0, RGAS / CP)
     rb = ppb / (RGAS * t0b * zzT)
     tb = t0b / pb
     pp = np.zeros_like(ppb)
@@ -608,16 +652,16 @@ def _jw_columns(lat, zgrid, zz, vg, R, moist):
     qv = np.zeros_like(ppb)
     phi = lat[None, :]
     dzw, dzu, fzp, fzm = vg["dzw"], vg["dzu"], vg["fzp"], vg["fzm"]
-    geo = ((-2.0 * np.sin(phi) ** 6 * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0), 
-           (1.6 * np.cos(phi) ** 3 * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * R * OMEGA)
+    geo = ((-2.0 * _ipow(np.sin(phi), 6) * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0),
+           (1.6 * _ipow(np.cos(phi), 3) * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * R * OMEGA)
     for _ in range(10):
         eta = (ppb + pp) / P0
         etav = (eta - 0.252) * PII / 2.0
         dlt = znut - eta
-        teta = t0 * eta ** (RGAS * dtdz / GRAVITY) + np.where(eta >= znut, 0.0, delta_t * (dlt * dlt * dlt * dlt * dlt))
+        teta = t0 * _pow(eta, RGAS * dtdz / GRAVITY) + np.where(eta >= znut, 0.0, delta_t * (dlt * dlt * dlt * dlt * dlt))
         ce = np.cos(etav)
         temperature = teta + 0.75 * eta * PII * u0 / RGAS * np.sin(etav) * np.sqrt(ce) * (
-            geo[0] * 2.0 * u0 * ce ** 1.5 + geo[1]) / (1.0 + 0.61 * qv)
+            geo[0] * 2.0 * u0 * _pow(ce, 1.5) + geo[1]) / (1.0 + 0.61 * qv)
         if moist:
             ptemp = ppb + pp
             relhum = np.where(ptemp < 50000.0, 0.0, np.where(ptemp > P0, 1.0, 1.0 - (np.maximum(P0 - ptemp, 0.0) / 50000.0) ** 1.25))
@@ -641,6 +685,76 @@ def _jw_columns(lat, zgrid, zz, vg, R, moist):
             for k in range(nz1 - 1):
                 ppi[k + 1] = ppi[k] - dzu[k + 1] * GRAVITY * (term[k] * fzp[k + 1] + term[k + 1] * fzm[k + 1])
             pp = 0.2 * ppi + 0.8 * pp
-    p = ((ppb + pp) / P0) ** (RGAS / CP)
+    p = _pow((ppb + pp) / P0, RGAS / CP)
     t = tt / p
     return ppb, pp, rb, rr, tb, t, qv
+
+
+NLAT = 721  # mpas_init_atm_cases.F:441
+
+
+def _jw_flux_zonal(lat1_in, lat2_in, dvEdge, R, vg, moist):
+    """The rebalanced JW zonal flux of every edge, (nE, K): the JW state on the 721-point
+    latitude grid (720-838), init_atm_recompute_geostrophic_wind (1215-1312), then
+    init_atm_calc_flux_zonal per edge (1162-1213): the integral of u_2d over the edge's latitude
+    span, linear interpolation in each latitude interval, summed in latitude order."""
+    u0 = 35.0
+    nz1 = vg["rdzw"].shape[0]
+    dlat = 0.5 * PII / float(NLAT - 1)
+    lat_2d = np.arange(NLAT, dtype=np.float64) * dlat
+    hx = _jw_hx(lat_2d, R)
+    zgrid = (1.0 - vg["ah"])[None, :] * (vg["sh"][None, :] * (vg["zt"] - hx[:, None]) + hx[:, None]) \
+        + vg["ah"][None, :] * vg["sh"][None, :] * vg["zt"]                              # (nlat, K+1)
+    zz = (vg["zw"][1:] - vg["zw"][:-1])[None, :] / (zgrid[:, 1:] - zgrid[:, :-1])
+    # the 2-D columns never carry moisture (qv_2d stays 0 with the reference's moisture = .false.)
+    ppb, pp, rb, rr, tb, t, qv = _jw_columns(lat_2d, zgrid, zz, vg, R, False)            # (K, nlat)
+    rho_2d = rr + rb
+    etavs_2d = ((ppb + pp) / P0 - 0.252) * PII / 2.0
+    u_2d = u0 * (np.sin(2.0 * lat_2d) ** 2)[None, :] * _pow(np.cos(etavs_2d), 1.5)
+    # init_atm_recompute_geostrophic_wind (1215-1312)
+    zx = ((zgrid[1:, :] - zgrid[:-1, :]) / (dlat * R)).T                               # (K+1, nlat-1)
+    rdx = 1.0 / (dlat * R)
+    zzT = zz.T
+    pgrad = rdx * (pp[:, 1:] / zzT[:, 1:] - pp[:, :-1] / zzT[:, :-1])
+    fzm, fzp, rdzw = vg["fzm"], vg["fzp"], vg["rdzw"]
+    dpzx = np.zeros((nz1 + 1, NLAT - 1))
+    dpzx[0] = .5 * zx[0] * (vg["cf1"] * (pp[0, 1:] + pp[0, :-1]) + vg["cf2"] * (pp[1, 1:] + pp[1, :-1])
+                            + vg["cf3"] * (pp[2, 1:] + pp[2, :-1]))
+    for k in range(1, nz1):
+        dpzx[k] = .5 * zx[k] * (fzm[k] * (pp[k, 1:] + pp[k, :-1]) + fzp[k] * (pp[k - 1, 1:] + pp[k - 1, :-1]))
+    pgrad = pgrad - rdzw[:, None] * (dpzx[1:] - dpzx[:-1])
+    u = .5 * (u_2d[:, :-1] + u_2d[:, 1:])
+    ru = u * (rho_2d[:, :-1] + rho_2d[:, 1:]) * .5
+    phi = (lat_2d[:-1] + lat_2d[1:]) / 2.0
+    f = 2.0 * OMEGA * np.sin(phi)
+    qtot = .5 * (qv[:, :-1] + qv[:, 1:])
+    for _ in range(50):
+        ru = np.where(f == 0.0, 0.0,
+                      -(1.0 / (1.0 + qtot) * pgrad + (_tan(phi) / R)[None, :] * u * ru) / np.where(f == 0.0, 1.0, f))
+        u = ru * 2.0 / (rho_2d[:, :-1] + rho_2d[:, 1:])
+    u_2d = u_2d.copy()
+    u_2d[:, 1:-1] = (ru[:, :-1] + ru[:, 1:]) * .5
+    u_2d[:, 0] = (3.0 * u_2d[:, 1] - u_2d[:, 2]) * .5
+    u_2d[:, -1] = (3.0 * u_2d[:, -2] - u_2d[:, -3]) * .5
+    # init_atm_calc_flux_zonal (1162-1213), all edges at once: the latitude intervals i each edge
+    # overlaps, in ascending order
+    a1, a2 = np.abs(lat1_in), np.abs(lat2_in)
+    lo = np.where(a2 <= a1, a2, a1)
+    hi = np.where(a2 <= a1, a1, a2)
+    i0 = np.maximum(np.floor(lo / dlat).astype(np.int64) - 1, 0)
+    i1 = np.minimum(np.ceil(hi / dlat).astype(np.int64) + 1, NLAT - 2)
+    acc = np.zeros((lo.shape[0], nz1))
+    dl_last = np.zeros(lo.shape[0])
+    for j in range(int((i1 - i0).max()) + 1):
+        i = np.minimum(i0 + j, NLAT - 2)
+        ok = (i0 + j <= i1) & (lo <= lat_2d[i + 1]) & (hi >= lat_2d[i])
+        dl = lat_2d[i + 1] - lat_2d[i]
+        da = (np.maximum(lo, lat_2d[i]) - lat_2d[i]) / dl
+        db = (np.minimum(hi, lat_2d[i + 1]) - lat_2d[i]) / dl
+        w1 = (db - da) - 0.5 * (db - da) ** 2
+        w2 = 0.5 * (db - da) ** 2
+        acc = np.where(ok[:, None], acc + w1[:, None] * u_2d[:, i].T + w2[:, None] * u_2d[:, i + 1].T, acc)
+        dl_last = np.where(ok, dl, dl_last)
+    sgn = np.copysign(1.0, lat2_in - lat1_in)
+    # the reference scales by its loop variable dlat: the width of the last interval it summed
+    return sgn[:, None] * acc * dl_last[:, None] * R / dvEdge[:, None] / u0

@@ -344,6 +344,7 @@ program mpas_ref_harness
    use mpas_atm_boundaries, only : harness_seconds_to_interval_end
 #ifdef HARNESS_INIT
    use atm_advection, only : atm_initialize_advection_rk, atm_initialize_deformation_weights
+   use atm_jw_ref, only : init_atm_case_jw
    use atm_core_init_ref, only : atm_compute_mesh_scaling, atm_compute_signs, atm_compute_damping_coefs, &
                                  atm_adv_coef_compression, atm_couple_coef_3rd_order
 #endif
@@ -483,6 +484,9 @@ program mpas_ref_harness
    call mpas_pool_add_config_logical(configs, 'config_positive_definite', config_positive_definite)
    call mpas_pool_add_config_logical(configs, 'config_monotonic', config_monotonic)
    call mpas_pool_add_config_real(configs, 'config_coef_3rd_order', config_coef_3rd_order)
+   ! init_atmosphere namelist keys the JW case reads (mode 'jw'): Registry defaults of core_init_atmosphere
+   call mpas_pool_add_config_int(configs, 'config_init_case', 2)
+   call mpas_pool_add_config_int(configs, 'config_theta_adv_order', 3)
    call mpas_pool_add_config_real(configs, 'config_smagorinsky_coef', config_smagorinsky_coef)
    call mpas_pool_add_config_logical(configs, 'config_mix_full', config_mix_full)
    call mpas_pool_add_config_real(configs, 'config_epssm', config_epssm)
@@ -606,6 +610,15 @@ program mpas_ref_harness
       call atm_couple_coef_3rd_order(mesh, configs)
       call atm_compute_mesh_scaling(mesh, configs)
       call atm_compute_damping_coefs(mesh, configs)
+      call dump_all(trim(outdir)//'/step_0000', plist)
+      call mpas_dmpar_finalize(domain % dminfo)
+      stop
+   end if
+   if (trim(mode) == 'jw') then
+      ! the reference's Jablonowski-Williamson initial state (init_atmosphere, config_init_case = 2,
+      ! mpas_init_atm_cases.F:367-1160) on the case's mesh given on the unit sphere: it scales the
+      ! mesh, computes deriv_two / defc, the vertical grid and metrics, the state, zb / zb3, rw / w
+      call init_atm_case_jw(mesh, nCells, K, state, diag, configs, 2)
       call dump_all(trim(outdir)//'/step_0000', plist)
       call mpas_dmpar_finalize(domain % dminfo)
       stop
@@ -866,6 +879,8 @@ contains
       call add_r2(mesh, 'mesh', 'defc_a', maxEdges_in, nC1, 1)
       call add_r2(mesh, 'mesh', 'defc_b', maxEdges_in, nC1, 1)
       call add_r2(mesh, 'mesh', 'zgrid', K+1, nC1, 1)
+      call add_r2(mesh, 'mesh', 'hx', K+1, nC1, 1)       ! terrain height (the JW init's own use)
+      call add_r1(mesh, 'mesh', 'dzu', K)
       call add_r2(mesh, 'mesh', 'zz', K, nC1, 1)
       call add_r2(mesh, 'mesh', 'zxu', K, nE1, 1)
       call add_r2(mesh, 'mesh', 'dss', K, nC1, 1)
@@ -921,6 +936,7 @@ contains
       call add_r2(diag, 'diag', 'pv_edge', K, nE1, 1);      call add_r2(diag, 'diag', 'gradPVn', K, nE1, 1)
       call add_r2(diag, 'diag', 'gradPVt', K, nE1, 1)
       call add_r2(diag, 'diag', 'vorticity', K, nV1, 1);    call add_r2(diag, 'diag', 'pv_vertex', K, nV1, 1)
+      call add_r1(diag, 'diag', 'surface_pressure', nC1)
    
       ! ---- tend / tend_physics pools ----
       call add_r2(tend, 'tend', 'u', K, nE1, 1);            call add_r2(tend, 'tend', 'u_euler', K, nE1, 1)

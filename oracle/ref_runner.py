@@ -309,6 +309,66 @@ def run_reference_init(case: dict, nthreads: int = 1, timeout: int = 600) -> dic
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+# mode 'jw': the reference's JW initial state (core_init_atmosphere init_atm_case_jw, :367-1312) on
+# the case's mesh.  The reference scales a unit-sphere grid (:474-489), so lengths go in divided by
+# the sphere radius and areas by its square.  Outputs: everything the routine computes.
+JW_OUTPUTS = ("u", "w", "theta", "rho", "rho_base", "theta_base", "scalars", "zgrid", "zz", "zxu", "rdzw", "rdzu",
+              "fzm", "fzp", "cf1", "cf2", "cf3", "zb", "zb3", "deriv_two", "defc_a", "defc_b", "fEdge", "fVertex",
+              "dss")
+_UNIT_LENGTH = ("xCell", "yCell", "zCell", "xEdge", "yEdge", "zEdge", "xVertex", "yVertex", "zVertex", "dvEdge",
+                "dcEdge")
+_UNIT_AREA = ("areaCell", "areaTriangle", "kiteAreasOnVertex")
+
+
+def unit_sphere(mesh: dict) -> tuple[dict, dict]:
+    """(unit-sphere grid, the same grid scaled as init_atm_case_jw scales it, :474-489): lengths
+    divided by the sphere radius and multiplied back, areas by its square (R**2 is exact for an
+    integral radius).  Our restatement run on the scaled fields and the reference run on the unit
+    ones then see the same geometry bit for bit."""
+    R = float(mesh["sphere_radius"])
+    unit = {k: np.asarray(mesh[k], dtype=np.float64) / R for k in _UNIT_LENGTH}
+    unit.update({k: np.asarray(mesh[k], dtype=np.float64) / (R * R) for k in _UNIT_AREA})
+    scaled = {k: unit[k] * R for k in _UNIT_LENGTH}
+    scaled.update({k: unit[k] * (R * R) for k in _UNIT_AREA})
+    return unit, scaled
+
+
+def run_reference_jw(case: dict, unit: dict | None = None, nthreads: int = 1, timeout: int = 600) -> dict:
+    """Run init_atm_case_jw (harness mode 'jw') on the case's mesh, given on the unit sphere
+    (``unit``, from unit_sphere(); default: the case's lengths / R and areas / R**2); returns its
+    dumps keyed 'pool.name' (state fields as 'state.<name>.tlN'), element-major where the shape is
+    known, else the flat Fortran image."""
+    import shutil
+    R = float(case["sphere_radius"])
+    inp = {k: v for k, v in case.items() if k not in JW_OUTPUTS}
+    if unit is None:
+        unit = unit_sphere(case)[0]
+    inp.update(unit)
+    for k in ("u", "w", "theta", "rho", "rho_base", "theta_base", "scalars"):  # zero inputs of the shapes
+        inp[k] = np.zeros_like(np.asarray(case[k], dtype=np.float64))
+    tmp = tempfile.mkdtemp(prefix="mpasjw_")
+    try:
+        ind, outd = os.path.join(tmp, "in"), os.path.join(tmp, "out")
+        write_inputs(inp, ind, 0, 1.0, [], nthreads)
+        with open(os.path.join(ind, "harness.nml")) as f:
+            nml = f.read()
+        with open(os.path.join(ind, "harness.nml"), "w") as f:
+            f.write(nml.replace("&harness\n", "&harness\n mode='jw',\n"))
+        env = dict(os.environ, OMP_NUM_THREADS=str(nthreads))
+        r = subprocess.run([HARNESS, ind, outd], cwd=tmp, env=env, capture_output=True, text=True, timeout=timeout,
+                           preexec_fn=_big_stack)
+        if r.returncode != 0:
+            raise RuntimeError(f"reference JW init failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
+        out = read_dump(case, os.path.join(outd, "step_0000"))
+        K, nE = case["nVertLevels"], case["nEdges"]
+        for name, shape in (("mesh.zb", (nE + 1, 2, K + 1)), ("mesh.zb3", (nE + 1, 2, K + 1)),
+                            ("mesh.deriv_two", (nE + 1, 2, 15))):
+            out[name] = np.asarray(out[name]).reshape(shape)[:-1]
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def write_block_inputs(blocks: list, d: str):
     """The blocks of one process (mpas_dycore.decomp) for the harness's multi-block mode: per block
     <d>/block<i>/ with its fields, block.nml (dims, owned counts) and its local-copy exchange lists

@@ -21,8 +21,12 @@ inputs/outputs as compressed npz (data only -- no reference source).
       core_init_atmosphere/mpas_atm_advection.F; signs, kiteForCell, adv_coefs compression,
       3rd-order coupling, mesh scaling, dss from mpas_atm_core.F:927-1288) on the quasi-uniform
       and the variable-resolution test meshes, with a checksum of the mesh it ran on.
+  tests/golden/jw_x1.642_K26.npz
+      the reference's init_atm_case_jw (core_init_atmosphere/mpas_init_atm_cases.F:367-1312, harness
+      mode 'jw') on x1.642 given on the unit sphere: vertical grid, metrics, the dry JW state with
+      the rebalanced wind, zb / zb3, deriv_two; with a checksum of the grid it ran on.
 
-Usage: python tools/make_golden.py [acoustic|srk3|reconstruct|init ...]   (needs oracle/_ref built)
+Usage: python tools/make_golden.py [acoustic|srk3|reconstruct|init|jw ...]   (needs oracle/_ref built)
 """
 from __future__ import annotations
 
@@ -96,6 +100,33 @@ def srk3_fixture():
     np.savez_compressed(os.path.join(GOLD, "srk3_x1.642_K26_ns3.npz"), **out)
 
 
+JW_EXACT = ("mesh.zgrid", "mesh.zz", "mesh.zxu", "mesh.rdzw", "mesh.rdzu", "mesh.fzm", "mesh.fzp", "mesh.cf1",
+            "mesh.cf2", "mesh.cf3", "diag.theta", "diag.rho", "diag.rho_base", "diag.theta_base")
+JW_CLOSE = ("state.u.tl1", "state.w.tl1", "mesh.zb", "mesh.zb3", "mesh.deriv_two")
+
+
+def jw_inputs(level: int = 3, K: int = 26):
+    """The JW pin's mesh: the x1.N grid on the unit sphere (what the reference reads) and scaled as
+    init_atm_case_jw scales it (what init_atm reads)."""
+    from mpas_dycore.cases import _mesh
+    m = _mesh(level, 20)
+    unit, scaled = ref_runner.unit_sphere(m)
+    return m, unit, scaled
+
+
+def jw_fixture():
+    """init_atm_case_jw of the reference (harness mode 'jw') on x1.642, K = 26: the vertical grid and
+    metrics, the dry JW state with the rebalanced wind, zb / zb3 and deriv_two."""
+    from mpas_dycore.init_atm import build_case
+    m, unit, scaled = jw_inputs()
+    case = build_case({**m, **scaled}, K=26, ns=1)
+    ref = ref_runner.run_reference_jw(case, unit)
+    out = {"checksum": case_checksum({**{k: v for k, v in m.items() if isinstance(v, np.ndarray)}, **unit})}
+    for k in JW_EXACT + JW_CLOSE:
+        out[k] = np.asarray(ref[k])
+    np.savez_compressed(os.path.join(GOLD, "jw_x1.642_K26.npz"), **out)
+
+
 def reconstruct_fixture():
     """mpas_rbf_interp_initialize + mpas_init_reconstruct outputs of the reference on x1.642."""
     case = jw_case(642, K=8, ns=1, cache=False)
@@ -147,5 +178,7 @@ if __name__ == "__main__":
         reconstruct_fixture()
     if not only or "init" in only:
         init_fixture()
+    if not only or "jw" in only:
+        jw_fixture()
     for f in sorted(os.listdir(GOLD)):
         print(f, os.path.getsize(os.path.join(GOLD, f)))
