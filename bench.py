@@ -49,8 +49,15 @@ def cpu_baseline(case, dt, nthreads, steps, moist_end=1):
                                         moist_end=moist_end)
     use = times[1:] if len(times) > 1 else times  # first step pays allocation / first-touch
     t = sum(use) / len(use)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return dict(value=case["nCells"] * case["nVertLevels"] / t, unit="cell-updates/s", cores=nthreads,
-                kind="reference", cpu_model=_cpu_model(),
+                kind="reference", cpu_model=_cpu_model(), host_nproc=os.cpu_count(), affinity=affinity,
+                omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
+                cores_note="threads = the host-CPU share the GPU pool gives one GPU (OMP_NUM_THREADS on the box); "
+                           "host_nproc counts the whole machine, shared by its 8 GPUs",
                 sample=f"unmodified reference atm_srk3 (amdflang -O2, OpenMP {nthreads} threads) on the same "
                        f"{case['nCells']}-cell x {case['nVertLevels']} JW case: {steps} dt steps, mean of the "
                        f"{len(use)} timed steps 2..{steps} ({t:.2f} s/step)")
@@ -126,7 +133,7 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=4, help="reference steps; the first is untimed")
     ap.add_argument("--order", type=int, default=3, choices=(2, 3),
                     help="config_time_integration_order of the synthetic cases (SURVEY.md §8d: 3)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: OMP_NUM_THREADS (the box's share), else 16")
     ap.add_argument("--acoustic-reps", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=1, help="blocks per GPU (MPAS blocks with halos)")
     ap.add_argument("--rccl-local", action="store_true", help="route in-process block exchanges through RCCL")
@@ -295,7 +302,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            nthreads = min(args.cpu_threads, os.cpu_count() or 1)
+            # the box's CPU share for one GPU (OMP_NUM_THREADS there), not the machine's nproc
+            nthreads = min(args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(case, dt, nthreads, args.cpu_steps, moist_end)
         except Exception as e:  # the measured GPU number stands on its own
             out["cpu_baseline"] = {"error": str(e)[:200]}

@@ -7,7 +7,8 @@
 #   tests            pytest -m "gpu and not slow"            (TESTS="files or -k expr" to narrow)
 #   tests_full       pytest -m gpu (full-size BASELINE configs included)
 #   bench            bench.py default line (configs[2] mesh, configs[1] line, cpu_baseline)
-#   bench_fast       bench.py without cpu_baseline / configs[1]
+#   bench_fast       bench.py without cpu_baseline / configs[1] (BENCH_ARGS extra arguments)
+#   bench55          bench_fast at 55 levels (the reference's default nVertLevels)
 #   moist            bench.py --moist (configs[3])
 #   varres           bench.py --varres 835586 (configs[4])
 #   prof             rocprofv3 --kernel-trace --stats of bench.py (gpurun_out/prof)
@@ -19,6 +20,8 @@
 #   ab               same-box A/B of AB_LIBS (default exp/lib_base.so vs the in-tree library),
 #                    AB_ROUNDS rounds of tools/kbench.py (AB_ARGS extra arguments)
 #   kprof            rocprofv3 kernel stats of tools/kbench.py for each of AB_LIBS (gpurun_out/kprof_<i>)
+#   kpmc             two rocprofv3 --pmc passes (SQ wait/active cycles; TA/TCP/TCC traffic) of one
+#                    eager tools/kbench.py dt for each of AB_LIBS (gpurun_out/kpmc_<lib>_<set>)
 #   smoke            __graft_entry__.smoke()
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out || exit 1
 B="--no-cpu-baseline --no-configs1"
@@ -28,7 +31,8 @@ step() {
     tests) timeout -k 10 1000 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m "gpu and not slow" ${TESTS:-tests} > gpurun_out/tests.log 2>&1; r=$?; tail -2 gpurun_out/tests.log; return $r ;;
     tests_full) timeout -k 10 1100 python -u -m pytest -x -v --timeout 900 --timeout-method thread -m gpu ${TESTS:-tests} > gpurun_out/tests_full.log 2>&1; r=$?; tail -2 gpurun_out/tests_full.log; return $r ;;
     bench) timeout -k 10 400 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1 && last gpurun_out/bench.log 700 ;;
-    bench_fast) timeout -k 10 300 python bench.py --steps 10 --warmup 2 $B > gpurun_out/bench_fast.log 2>&1 && last gpurun_out/bench_fast.log ;;
+    bench_fast) timeout -k 10 300 python bench.py --steps 10 --warmup 2 $B ${BENCH_ARGS} > gpurun_out/bench_fast.log 2>&1 && last gpurun_out/bench_fast.log ;;
+    bench55) timeout -k 10 300 python bench.py --steps 10 --warmup 2 $B --levels 55 > gpurun_out/bench55.log 2>&1 && last gpurun_out/bench55.log ;;
     moist) timeout -k 10 400 python bench.py --steps 10 --warmup 2 --moist $B > gpurun_out/moist.log 2>&1 && last gpurun_out/moist.log 300 ;;
     varres) timeout -k 10 600 python bench.py --steps 5 --warmup 1 --varres 835586 $B > gpurun_out/varres.log 2>&1 && last gpurun_out/varres.log 300 ;;
     prof) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 $B ${PROF_ARGS} > gpurun_out/prof.log 2>&1 && last gpurun_out/prof.log 200 ;;
@@ -47,6 +51,10 @@ step() {
     kprof) i=0; for L in ${AB_LIBS:-exp/lib_base.so mpas-model_amd/csrc/libmpas_dycore.so}; do
           MPAS_DYCORE_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof_$i -o run --output-format csv -- python3 tools/kbench.py --steps ${AB_STEPS:-10} ${AB_ARGS} > gpurun_out/kprof_$i.log 2>&1 || return 1
           echo "kprof_$i = $L"; i=$((i+1)); done ;;
+    kpmc) i=0; for L in ${AB_LIBS:-mpas-model_amd/csrc/libmpas_dycore.so}; do j=0
+          for C in "${KPMC_SET1:-SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES}" "${KPMC_SET2:-TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum}"; do
+            MPAS_DYCORE_LIB=$L timeout -s KILL 240 rocprofv3 --pmc $C -d gpurun_out/kpmc_${i}_$j -o pmc --output-format csv -- python3 tools/kbench.py --steps 1 --reps 1 --no-graph > gpurun_out/kpmc_${i}_$j.log 2>&1 || return 1
+            j=$((j+1)); done; echo "kpmc_$i = $L"; i=$((i+1)); done ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && last gpurun_out/smoke.log ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
