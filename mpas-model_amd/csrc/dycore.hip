@@ -639,7 +639,9 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   });
   if (ctx->host_only) return MPAS_DYC_OK;  // the dry run keeps the message lists only
   if (stotal) HIPCHK(hipMalloc(&pl.sendbuf, stotal * sizeof(double)));
-  if (rtotal) HIPCHK(hipMalloc(&pl.recvbuf, rtotal * sizeof(double)));
+  // 256 B of slack: a fused unpack (ld_pp) reads the two levels of its lane's pair, one past the
+  // last column at an odd K
+  if (rtotal) HIPCHK(hipMalloc(&pl.recvbuf, rtotal * sizeof(double) + 256));
   for (size_t i = 0; i < pre.size(); ++i)
     if (pre_off[i] >= 0) pre[i].dst = pl.sendbuf + pre_off[i];
   for (size_t i = 0; i < post.size(); ++i) post[i].src = pl.recvbuf + post_off[i];
@@ -794,8 +796,11 @@ inline bool batched(const Dims& d) {
 }
 
 
-// pair-layout edge kernels (k_*_p: two edges per wave, two levels per lane) need an even K
-inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K % 2 == 0 && d.K <= 64; }
+// pair-layout edge kernels (k_*_p: two edges per wave, two levels per lane); at an odd K the last
+// pair's second level is past the column: loaded (the 256 B of slack behind every field covers the
+// last column), never stored, and every level-dependent expression masks it as it masks the
+// levels above K at an even K
+inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K <= 64; }
 
 // Halo-boundary flags of the split-phase exchanges: an edge is "boundary" when one of its
 // cells is a halo cell (it reads exchanged cell data); an owned cell is "boundary" when
@@ -2378,7 +2383,7 @@ int mpas_dyc_set_lbc(mpas_dyc_ctx* ctx, int32_t apply, double seconds_to_interva
   if (apply) {
     for (auto& b : ctx->blk)
       if (!pair_layout(b.d)) {
-        ctx->err = "regional LBCs need the pair kernel layout (maxEdges <= 7, even nVertLevels <= 64)";
+        ctx->err = "regional LBCs need the pair kernel layout (maxEdges <= 7)";
         return MPAS_DYC_EINVAL;
       }
   }

@@ -1575,6 +1575,12 @@ __device__ __forceinline__ d2 ld2(const double* __restrict__ a) {
   return r;
 }
 __device__ __forceinline__ void st2(double* a, d2 v) { __builtin_memcpy(a, &v, 16); }
+// store of a lane's two levels; two = false (odd K, last pair): its second level is level K, past
+// the column, so only the first is stored
+__device__ __forceinline__ void pst(double* a, d2 v, bool two) {
+  if (two) st2(a, v);
+  else a[0] = v.x;
+}
 __device__ __forceinline__ int pair_wave() {
   return __builtin_amdgcn_readfirstlane(xcd_block() * EDGE_WPB + (threadIdx.x >> 6));
 }
@@ -1635,7 +1641,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  const int lc = min(l, (K + 1) / 2 - 1), lw = min(l, K / 2);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t K1 = K + 1;
   const size_t o = (size_t)e * K + 2 * lc;
@@ -1651,7 +1658,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   const int kx = 2 * l, ky = 2 * l + 1;  // true levels of the two components
   const bool stx = mine && kx < K, sty = mine && ky < K;
   auto store = [&](double* a, d2 v) {
-    if (stx && sty) st2(a + o, v);
+    if (stx) pst(a + o, v, sty);
   };
   // rk1 del^2 of u (4856-4883), all edges
   auto del2 = [&](d2 tue, d2 dv1, d2 dv2, d2 vo1, d2 vo2, d2 kd1, d2 kd2, double invDv, double msd2) {
@@ -1781,7 +1788,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_pgf_p(Dims d, Ptrs p
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, K / 2 - 1);
+  const int lc = min(l, (K + 1) / 2 - 1);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const bool solve = h ? (hasB && eB < d.nEdgesSolve) : (eA < d.nEdgesSolve);
@@ -1814,8 +1822,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_pgf_p(Dims d, Ptrs p
   out.x = tue.x + re.x * (0.5 * (kd1.x + kd2.x)) * ud.x * msd2;
   out.y = tue.y + re.y * (0.5 * (kd1.y + kd2.y)) * ud.y * msd2;
   if ((h == 0 || hasB) && 2 * l < K) {
-    st2(p.delsq_u + o, d2{0.0 + ud.x, 0.0 + ud.y});
-    st2(p.tend_u_euler + o, out);
+    pst(p.delsq_u + o, d2{0.0 + ud.x, 0.0 + ud.y}, two);
+    pst(p.tend_u_euler + o, out, two);
   }
 }
 
@@ -1827,7 +1835,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  const int lc = min(l, (K + 1) / 2 - 1), lw = min(l, K / 2);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const size_t K1 = K + 1;
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
@@ -1885,8 +1894,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
     }
   }
   if ((h ? onB : onA) && 2 * l < K) {
-    st2(p.advflux_w + o, fw);
-    st2(p.advflux_th + o, ft);
+    pst(p.advflux_w + o, fw, two);
+    pst(p.advflux_th + o, ft, two);
   }
 }
 
@@ -1900,7 +1909,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, K / 2 - 1);
+  const int lc = min(l, (K + 1) / 2 - 1);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
@@ -1948,11 +1958,11 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
         vv.y = vv.y + wgt[j] * uu[j].y;
       }
     }
-    if (st) st2(p.v + o, vv);
+    if (st) pst(p.v + o, vv, two);
   } else {
     vv = ld2(p.v + o);
   }
-  if (st) st2(p.rho_edge + o, d2{0.5 * (h1.x + h2.x), 0.5 * (h1.y + h2.y)});
+  if (st) pst(p.rho_edge + o, d2{0.5 * (h1.x + h2.x), 0.5 * (h1.y + h2.y)}, two);
   d2 pve{0.5 * (pv1.x + pv2.x), 0.5 * (pv1.y + pv2.y)};
   if (apvm > 0.0) {
     const double r = apvm * dt;
@@ -1961,13 +1971,13 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
     const d2 gt{(pv2.x - pv1.x) * r1, (pv2.y - pv1.y) * r1};
     const d2 gn{(pc2.x - pc1.x) * r2, (pc2.y - pc1.y) * r2};
     if (st && store_grad) {
-      st2(p.gradPVt + o, gt);
-      st2(p.gradPVn + o, gn);
+      pst(p.gradPVt + o, gt, two);
+      pst(p.gradPVn + o, gn, two);
     }
     pve.x = pve.x - r * (vv.x * gt.x + ue.x * gn.x);
     pve.y = pve.y - r * (vv.y * gt.y + ue.y * gn.y);
   }
-  if (st) st2(p.pv_edge + o, pve);
+  if (st) pst(p.pv_edge + o, pve, two);
 }
 
 // k_divdamp in the pair layout
@@ -1990,7 +2000,7 @@ __device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMa
     const int off = map[c - d.nCellsSolve];
     if (off >= 0) {
       const d2 v = ld2(um.recv + off + 2 * lc);
-      if (st) st2(fld + o, v);
+      if (st) pst(fld + o, v, 2 * lc + 1 < d.K);
       return v;
     }
   }
@@ -2006,7 +2016,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   bool hasB;
   if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, K / 2 - 1);
+  const int lc = min(l, (K + 1) / 2 - 1);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
@@ -2044,8 +2055,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   out.y = ru.y + coef_divdamp * (-(dd2.y) - -(dd1.y)) * (1.0 - mask) / (t1.y + t2.y);
   if (!REC) {
     if ((h ? onB : onA) && 2 * l < K) {
-      st2(p.ru_p + o, out);
-      if (fresh) st2(p.ruAvg + o, ru);
+      pst(p.ru_p + o, out, two);
+      if (fresh) pst(p.ruAvg + o, ru, two);
     }
     return;
   }
@@ -2055,14 +2066,14 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   const d2 ra = fresh ? ru : ld2(p.ruAvg + o);  // fresh: sub-step 1 left ruAvg = dts * tend_u
   const d2 z1 = ld2(p.rho_zz2 + o1), z2 = ld2(p.rho_zz2 + o2);
   if ((h ? onB : onA) && 2 * l < K) {
-    st2(p.ru_p + o, out);
+    pst(p.ru_p + o, out, two);
     if (h ? rB : rA) {  // recover_edges (3048-3059), same expressions
-      st2(p.ruAvg + o, d2{rs.x + (ra.x * invNs), rs.y + (ra.y * invNs)});
+      pst(p.ruAvg + o, d2{rs.x + (ra.x * invNs), rs.y + (ra.y * invNs)}, two);
       const d2 rr{rs.x + out.x, rs.y + out.y};
-      st2(p.ru + o, rr);
-      st2(p.u2 + o, d2{2. * rr.x / (z1.x + z2.x), 2. * rr.y / (z1.y + z2.y)});
+      pst(p.ru + o, rr, two);
+      pst(p.u2 + o, d2{2. * rr.x / (z1.x + z2.x), 2. * rr.y / (z1.y + z2.y)}, two);
     } else if (fresh) {
-      st2(p.ruAvg + o, ru);
+      pst(p.ruAvg + o, ru, two);
     }
   }
 }
@@ -2075,7 +2086,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31, ns = d.ns;
-  const int lc = min(l, K / 2 - 1);
+  const int lc = min(l, (K + 1) / 2 - 1);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int na = sel(h, p.nAdvCellsForEdge[eA], p.nAdvCellsForEdge[eB]);
@@ -2104,7 +2116,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
     const d2 upos{dv * fabs(udx + 0.5), dv * fabs(udy + 0.5)}, uneg{dv * fabs(udx - 0.5), dv * fabs(udy - 0.5)};
     for (int is = 0; is < ns; ++is) {
       const d2 s1 = ld2(p.scalars2 + SIX(c1, 2 * lc, is)), s2 = ld2(p.scalars2 + SIX(c2, 2 * lc, is));
-      if (st) st2(p.horiz_flux_array + HIX(e, 2 * lc, is), d2{upos.x * s1.x + uneg.x * s2.x, upos.y * s1.y + uneg.y * s2.y});
+      if (st) pst(p.horiz_flux_array + HIX(e, 2 * lc, is), d2{upos.x * s1.x + uneg.x * s2.x, upos.y * s1.y + uneg.y * s2.y}, two);
     }
     return;
   }
@@ -2130,7 +2142,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
         }
       }
     }
-    if (st) st2(p.horiz_flux_array + HIX(e, 2 * lc, is), acc);
+    if (st) pst(p.horiz_flux_array + HIX(e, 2 * lc, is), acc, two);
   }
 }
 
@@ -2142,7 +2154,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31, ns = d.ns;
-  const int lc = min(l, K / 2 - 1);
+  const int lc = min(l, (K + 1) / 2 - 1);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
@@ -2202,9 +2215,9 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
   const int bm = sel(h, p.bdyMaskEdge[eA], p.bdyMaskEdge[eB]);
   const bool upw = (d.lbc && bm == N_RELAX_ZONE) || bm == N_RELAX_ZONE - 1;
   if ((h == 0 || hasB) && 2 * l < K) {
-    st2(p.flux_arr + o, upw ? fu : fa);
-    st2(p.flux_upwind_tmp + o, fu);
-    st2(p.flux_tmp + o, upw ? d2{0.0, 0.0} : d2{dt * fa.x - fu.x, dt * fa.y - fu.y});
+    pst(p.flux_arr + o, upw ? fu : fa, two);
+    pst(p.flux_upwind_tmp + o, fu, two);
+    pst(p.flux_tmp + o, upw ? d2{0.0, 0.0} : d2{dt * fa.x - fu.x, dt * fa.y - fu.y}, two);
   }
 }
 
@@ -2224,7 +2237,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs 
   const bool hasB = cA + 1 < d.nCellsSolve;
   const int c = sel(h, cA, hasB ? cA + 1 : cA);
   const bool mine = h == 0 || hasB;
-  const int lc = min(l, K / 2 - 1);
+  const int lc = min(l, (K + 1) / 2 - 1);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int kx = 2 * l, ky = 2 * l + 1;
   const bool ax = kx < K, ay = ky < K;  // "act" of the two levels
   const size_t o = (size_t)c * K + 2 * lc;
@@ -2273,7 +2287,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs 
   // sequential LU recurrence (2124-2127) as a lane-shift sweep
   const bool fx = kx >= 1 && ax, fy = ay;
   d2 alpha{0.0, 0.0}, gamma{0.0, 0.0};
-  for (int it = 0; it < K / 2; ++it) {
+  for (int it = 0; it < (K + 1) / 2; ++it) {
     const double gpx = lane_shr1(gamma.y);
     if (fx) {
       alpha.x = 1. / (b.x - a.x * (l == 0 ? 0.0 : gpx));
@@ -2289,13 +2303,13 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs 
       p.cofwr[o + 1] = cofwr.y;
       p.cofwz[o + 1] = cofwz.y;
     } else {
-      st2(p.cofwr + o, cofwr);
-      st2(p.cofwz + o, cofwz);
+      pst(p.cofwr + o, cofwr, two);
+      pst(p.cofwz + o, cofwz, two);
     }
-    st2(p.cofwt + o, cofwt);
-    st2(p.a_tri + o, a);
-    st2(p.alpha_tri + o, alpha);
-    st2(p.gamma_tri + o, gamma);
+    pst(p.cofwt + o, cofwt, two);
+    pst(p.a_tri + o, a, two);
+    pst(p.alpha_tri + o, alpha, two);
+    pst(p.gamma_tri + o, gamma, two);
   }
   // coftz(1) = coftz(K+1) = 0: levels 0..K, the lane holding level K stores that one level
   if (mine && kx <= K) {
@@ -2320,7 +2334,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
   if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
   const bool lev = 2 * l < K;                     // this lane holds levels 2l, 2l+1
-  const int lc = min(l, K / 2 - 1);
+  const int lc = min(l, (K + 1) / 2 - 1);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
@@ -2336,8 +2351,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
   if (small_step == 1) {
     const d2 rup = {dts * tu.x, dts * tu.y};
     if (st) {
-      st2(p.ru_p + o, rup);
-      st2(p.ruAvg + o, rup);
+      pst(p.ru_p + o, rup, two);
+      pst(p.ruAvg + o, rup, two);
     }
     return;
   }
@@ -2385,8 +2400,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
   rup.y = level(rup.y, tu.y, cqu.y, zxu.y, rt1.y, rt2.y, zz1.y, zz2.y, ex1.y, ex2.y, rp1.y, rp2.y, ro1.y, ro2.y,
                 th1.y, th2.y);
   if (st) {
-    st2(p.ru_p + o, rup);
-    st2(p.ruAvg + o, d2{rua.x + rup.x, rua.y + rup.y});
+    pst(p.ru_p + o, rup, two);
+    pst(p.ruAvg + o, d2{rua.x + rup.x, rua.y + rup.y}, two);
   }
 }
 
@@ -3859,7 +3874,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges2_p(Dims d, Ptrs p, 
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, K / 2 - 1);
+  const int lc = min(l, (K + 1) / 2 - 1);
+  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
@@ -3879,7 +3895,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges2_p(Dims d, Ptrs p, 
   if ((d.lbc && bm == N_RELAX_ZONE) || bm == N_RELAX_ZONE - 1) f = d2{0.0, 0.0};  // 4113-4115
   f.x = fmax(0.0, f.x) * fmin(a11.x, a20.x) + fmin(0.0, f.x) * fmin(a10.x, a21.x);
   f.y = fmax(0.0, f.y) * fmin(a11.y, a20.y) + fmin(0.0, f.y) * fmin(a10.y, a21.y);
-  if ((h ? onB : onA) && 2 * l < K) st2(p.flux_arr + o, f);
+  if ((h ? onB : onA) && 2 * l < K) pst(p.flux_arr + o, f, two);
 }
 
 // ============================================================================

@@ -125,8 +125,9 @@ def test_kernel_families_give_identical_bits(which, request):
             assert np.array_equal(got[n], ref[n]), f"{fam}: {n}"
 
 
-def test_odd_level_count_runs_the_single_column_kernels():
-    """K = 25 (odd): the pair layout does not apply, the batched kernels run; they match the general ones."""
+def test_odd_level_count_pair_layout_matches_general():
+    """K = 25 (odd): the pair layout's last pair holds level K-1 and a level past the column that is
+    loaded and never stored; the pair family matches the general one (one column per wave)."""
     from mpas_dycore.cases import jw_case
     case = jw_case(642, K=25, ns=2, moist=True, cache=False)
     ref = _steps_with_kernels(case, "general", nsteps=2)
