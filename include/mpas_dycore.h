@@ -44,6 +44,12 @@ extern "C" {
 #define MPAS_DYC_ESTATE -3    /* call out of sequence */
 #define MPAS_DYC_ECOMM -4     /* halo exchange failure */
 
+/* nVertLevels: 4..MPAS_DYC_MAX_LEVELS.  Up to MPAS_DYC_MAX_LEVELS_WAVE a column is one 64-lane
+ * wavefront (lane = level, every kernel family); above, one 128-lane workgroup whose cross-level
+ * moves go through LDS (the one-column-per-element kernels, no regional LBCs). */
+#define MPAS_DYC_MAX_LEVELS_WAVE 63
+#define MPAS_DYC_MAX_LEVELS 127
+
 typedef struct mpas_dyc_ctx mpas_dyc_ctx;
 
 /* Registry.xml dims (8-46) for one block; *Solve = owned counts (mpas_block_creator.F). */

@@ -16,6 +16,12 @@
 #include <tuple>
 #include <vector>
 
+// The library links two builds of this file (gen_api.py): MPAS_API_TAG=n, one wavefront per
+// column (nVertLevels 4..63), and MPAS_API_TAG=w with MPAS_WIDE, one workgroup per column
+// (64..127); each build's entry points are renamed, and api_dispatch.cpp routes the public ones.
+#ifdef MPAS_API_TAG
+#include "api_rename.h"
+#endif
 #include "../../include/mpas_dycore.h"
 #include "kernels.hip"
 #include "halo.hip"
@@ -440,6 +446,12 @@ inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + WAVES_PER_BLOCK - 
     if ((n) > 0 && !ctx->planning)                                                                         \
       hipLaunchKernelGGL(kern, dim3((unsigned)(((n) + EDGE_WPB - 1) / EDGE_WPB)), dim3(EDGE_THREADS), 0,    \
                          ctx->stream, __VA_ARGS__);                                                        \
+  } while (0)
+// a pair-layout kernel in its even-K or odd-K instance (its last template parameter, ODD)
+#define LAUNCH_PE(kern_even, kern_odd, n, ...)        \
+  do {                                               \
+    if (d.K & 1) LAUNCH_E(kern_odd, n, __VA_ARGS__);   \
+    else LAUNCH_E(kern_even, n, __VA_ARGS__);          \
   } while (0)
 #define LAUNCH(kern, n, ...)                                                                               \
   do {                                                                                                     \
@@ -1014,7 +1026,7 @@ void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
 
 void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
   if (pair_layout(d))
-    LAUNCH_E(k_vert_imp_coefs_p, std::max((d.nCellsSolve + 1) / 2, 1), d, p, dts, ctx->cf.epssm);
+    LAUNCH_PE((k_vert_imp_coefs_p<false>), (k_vert_imp_coefs_p<true>), std::max((d.nCellsSolve + 1) / 2, 1), d, p, dts, ctx->cf.epssm);
   else
     LAUNCH(k_vert_imp_coefs, std::max(d.nCellsSolve, 1), d, p, dts, ctx->cf.epssm);
 }
@@ -1052,11 +1064,11 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   if (part == 1) return;
   if (pair_layout(d)) {
     const int64_t nw = (d.nEdges + 1) / 2;
-    if (rk_step == 1) LAUNCH_E(k_dyn_edges_pgf_p, nw, d, p);
-    if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 10, true>), nw, d, p, cf, s, 0);
-    if (d.maxEdges == 6 && rk_step != 1) LAUNCH_E((k_dyn_edges_p<false, 10>), nw, d, p, cf, s, 1);
-    if (d.maxEdges == 7 && rk_step == 1) LAUNCH_E((k_dyn_edges_p<true, 12, true>), nw, d, p, cf, s, 0);
-    if (d.maxEdges == 7 && rk_step != 1) LAUNCH_E((k_dyn_edges_p<false, 12>), nw, d, p, cf, s, 1);
+    if (rk_step == 1) LAUNCH_PE((k_dyn_edges_pgf_p<false>), (k_dyn_edges_pgf_p<true>), nw, d, p);
+    if (d.maxEdges == 6 && rk_step == 1) LAUNCH_PE((k_dyn_edges_p<true, 10, true, false>), (k_dyn_edges_p<true, 10, true, true>), nw, d, p, cf, s, 0);
+    if (d.maxEdges == 6 && rk_step != 1) LAUNCH_PE((k_dyn_edges_p<false, 10, false, false>), (k_dyn_edges_p<false, 10, false, true>), nw, d, p, cf, s, 1);
+    if (d.maxEdges == 7 && rk_step == 1) LAUNCH_PE((k_dyn_edges_p<true, 12, true, false>), (k_dyn_edges_p<true, 12, true, true>), nw, d, p, cf, s, 0);
+    if (d.maxEdges == 7 && rk_step != 1) LAUNCH_PE((k_dyn_edges_p<false, 12, false, false>), (k_dyn_edges_p<false, 12, false, true>), nw, d, p, cf, s, 1);
   } else if (batched(d)) {
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_b<true, 10>), d.nEdges, d, p, cf, s, 0);
     if (d.maxEdges == 6 && rk_step != 1) LAUNCH_E((k_dyn_edges_b<false, 10>), d.nEdges, d, p, cf, s, 1);
@@ -1082,8 +1094,8 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     }
   }
   if (!batched(d)) LAUNCH(k_dyn_advflux, d.nEdges, d, p);
-  else if (pair_layout(d) && d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_p<10>, (d.nEdges + 1) / 2, d, p);
-  else if (pair_layout(d)) LAUNCH_E(k_dyn_advflux_p<12>, (d.nEdges + 1) / 2, d, p);
+  else if (pair_layout(d) && d.maxEdges == 6) LAUNCH_PE((k_dyn_advflux_p<10, false>), (k_dyn_advflux_p<10, true>), (d.nEdges + 1) / 2, d, p);
+  else if (pair_layout(d)) LAUNCH_PE((k_dyn_advflux_p<12, false>), (k_dyn_advflux_p<12, true>), (d.nEdges + 1) / 2, d, p);
   else if (d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_b<10>, d.nEdges, d, p);
   else LAUNCH_E(k_dyn_advflux_b<12>, d.nEdges, d, p);
   if (batched(d)) {
@@ -1125,13 +1137,13 @@ void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts,
     const int64_t nw = ((phase == 2 ? d.n_bnd_pairs : d.nEdges) + 1) / 2;  // phase 2: the bnd_pairs list
     const bool up = um.recv != nullptr;
     if (damp && up)
-      LAUNCH_E((k_acoustic_edges_p<true, true>), nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh, um);
+      LAUNCH_PE((k_acoustic_edges_p<true, true, false>), (k_acoustic_edges_p<true, true, true>), nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh, um);
     else if (damp)
-      LAUNCH_E((k_acoustic_edges_p<true, false>), nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh, um);
+      LAUNCH_PE((k_acoustic_edges_p<true, false, false>), (k_acoustic_edges_p<true, false, true>), nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh, um);
     else if (up)
-      LAUNCH_E((k_acoustic_edges_p<false, true>), nw, d, p, dts, small_step, 0.0, phase, fresh, um);
+      LAUNCH_PE((k_acoustic_edges_p<false, true, false>), (k_acoustic_edges_p<false, true, true>), nw, d, p, dts, small_step, 0.0, phase, fresh, um);
     else
-      LAUNCH_E((k_acoustic_edges_p<false, false>), nw, d, p, dts, small_step, 0.0, phase, fresh, um);
+      LAUNCH_PE((k_acoustic_edges_p<false, false, false>), (k_acoustic_edges_p<false, false, true>), nw, d, p, dts, small_step, 0.0, phase, fresh, um);
     return;
   }
   if (damp)
@@ -1191,11 +1203,11 @@ void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double 
   const int64_t nw = ((phase == 2 ? d.n_bnd_pairs : d.nEdges) + 1) / 2;  // phase 2: the bnd_pairs list
   const double cd = coef_divdamp(ctx, dts);
   if (pair_layout(d) && invNs > 0.0 && fused_recover_edges(d)) {
-    if (up) LAUNCH_E((k_divdamp_p<true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl);
-    else LAUNCH_E((k_divdamp_p<true, false>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl);
+    if (up) LAUNCH_PE((k_divdamp_p<true, true, false>), (k_divdamp_p<true, true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl);
+    else LAUNCH_PE((k_divdamp_p<true, false, false>), (k_divdamp_p<true, false, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl);
   } else if (pair_layout(d)) {
-    if (up) LAUNCH_E((k_divdamp_p<false, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl);
-    else LAUNCH_E((k_divdamp_p<false, false>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl);
+    if (up) LAUNCH_PE((k_divdamp_p<false, true, false>), (k_divdamp_p<false, true, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl);
+    else LAUNCH_PE((k_divdamp_p<false, false, false>), (k_divdamp_p<false, false, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl);
   }
   else LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase,
               dts, fresh);
@@ -1221,8 +1233,8 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double d
     if (d.maxEdges == 6) LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
     else LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
     const int64_t nw = (d.nEdges + 1) / 2;
-    if (d.maxEdges == 6) LAUNCH_E(k_diag_edges_p<10>, nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
-    else LAUNCH_E(k_diag_edges_p<12>, nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
+    if (d.maxEdges == 6) LAUNCH_PE((k_diag_edges_p<10, false>), (k_diag_edges_p<10, true>), nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
+    else LAUNCH_PE((k_diag_edges_p<12, false>), (k_diag_edges_p<12, true>), nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
   } else if (d.maxEdges == 6) {
     LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
     LAUNCH_E(k_diag_edges_b<10>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
@@ -1241,8 +1253,8 @@ void advance_scalars(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt,
     if (rk_step == 3) wt_new = 1.;
   }
   if (batched(d) && pair_layout(d)) {
-    if (d.maxEdges == 6) LAUNCH_E(k_scalars_edges_p<10>, (d.nEdges + 1) / 2, d, p);
-    else LAUNCH_E(k_scalars_edges_p<12>, (d.nEdges + 1) / 2, d, p);
+    if (d.maxEdges == 6) LAUNCH_PE((k_scalars_edges_p<10, false>), (k_scalars_edges_p<10, true>), (d.nEdges + 1) / 2, d, p);
+    else LAUNCH_PE((k_scalars_edges_p<12, false>), (k_scalars_edges_p<12, true>), (d.nEdges + 1) / 2, d, p);
   } else {
     LAUNCH(k_scalars_edges, d.nEdges, d, p);
   }
@@ -1280,8 +1292,8 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
       else if (m6) LAUNCH(k_mono_bounds_b<6>, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
       else LAUNCH(k_mono_bounds_b<7>, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
       if (batched(d) && pair_layout(d)) {
-        if (d.maxEdges == 6) LAUNCH_E(k_mono_edges1_p<10>, (d.nEdges + 1) / 2, d, P[b], is, dt);
-        else LAUNCH_E(k_mono_edges1_p<12>, (d.nEdges + 1) / 2, d, P[b], is, dt);
+        if (d.maxEdges == 6) LAUNCH_PE((k_mono_edges1_p<10, false>), (k_mono_edges1_p<10, true>), (d.nEdges + 1) / 2, d, P[b], is, dt);
+        else LAUNCH_PE((k_mono_edges1_p<12, false>), (k_mono_edges1_p<12, true>), (d.nEdges + 1) / 2, d, P[b], is, dt);
       } else {
         LAUNCH(k_mono_edges1, d.nEdges, d, P[b], is, dt);
       }
@@ -1297,7 +1309,7 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
         LAUNCH(k_mono_cells2, d.nCells, d, P[b], is, ad);
         continue;
       }
-      if (pair_layout(d)) LAUNCH_E(k_mono_edges2_p, (d.nEdges + 1) / 2, d, P[b], dt);
+      if (pair_layout(d)) LAUNCH_PE((k_mono_edges2_p<false>), (k_mono_edges2_p<true>), (d.nEdges + 1) / 2, d, P[b], dt);
       else LAUNCH(k_mono_edges2, d.nEdges, d, P[b], dt);
       if (d.maxEdges == 6) LAUNCH(k_mono_cells2_b<6>, d.nCells, d, P[b], is, ad);
       else LAUNCH(k_mono_cells2_b<7>, d.nCells, d, P[b], is, ad);
@@ -1726,7 +1738,15 @@ int init_diagnostics(mpas_dyc_ctx* ctx, double dt, bool coupled = true) {
 namespace {
 
 int fill_dims(Dims& d, const mpas_dyc_dims* dims) {
-  if (dims->nVertLevels < 4 || dims->nVertLevels > 63) return MPAS_DYC_EINVAL;  // column = one wavefront
+#ifdef MPAS_WIDE
+  // column = one workgroup of WIDE_THREADS lanes (levels 0..K of w)
+  if (dims->nVertLevels <= MPAS_DYC_MAX_LEVELS_WAVE || dims->nVertLevels > MPAS_DYC_MAX_LEVELS)
+    return MPAS_DYC_EINVAL;
+  static_assert(MPAS_DYC_MAX_LEVELS < WIDE_THREADS, "a wide column holds K + 1 levels");
+#else
+  // column = one wavefront (levels 0..K of w)
+  if (dims->nVertLevels < 4 || dims->nVertLevels > MPAS_DYC_MAX_LEVELS_WAVE) return MPAS_DYC_EINVAL;
+#endif
   if (dims->maxEdges < 3 || dims->maxEdges2 < dims->maxEdges || dims->num_scalars < 1) return MPAS_DYC_EINVAL;
   if (dims->nCells < 1 || dims->nEdges < 1 || dims->nVertices < 1) return MPAS_DYC_EINVAL;
   if (dims->nCellsSolve < 1 || dims->nCellsSolve > dims->nCells || dims->nEdgesSolve > dims->nEdges ||
@@ -1895,6 +1915,9 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   } else {
     g_kernel_tier = 2;
   }
+#ifdef MPAS_WIDE
+  g_kernel_tier = 0;  // the wide build runs the one-column-per-element kernels only
+#endif
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
   for (auto& b : ctx->blk) {
     build_registry(b);
@@ -2241,7 +2264,7 @@ int mpas_dyc_set_summary(mpas_dyc_ctx* ctx, int32_t flags) {
 
 namespace {
 // blocks < 0: every block of the process folded; else that block alone (each reduced over ranks)
-int get_summary(mpas_dyc_ctx* ctx, int32_t blocks, mpas_dyc_summary* out, double* scalar_minmax, int32_t n) {
+static int get_summary(mpas_dyc_ctx* ctx, int32_t blocks, mpas_dyc_summary* out, double* scalar_minmax, int32_t n) {
   if (!ctx || !out || blocks >= (int32_t)ctx->blk.size()) return MPAS_DYC_EINVAL;
   if (ctx->host_only) return MPAS_DYC_ESTATE;
   const int ns = ctx->blk[0].d.ns;

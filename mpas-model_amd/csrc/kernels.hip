@@ -17,8 +17,17 @@
 
 namespace mpas {
 
+#ifdef MPAS_WIDE
+// Wide columns (the library's second build, nVertLevels 64..WIDE_THREADS-1; dycore.hip picks the
+// build per context): one column per workgroup of WIDE_THREADS lanes, lane = level, and the
+// cross-lane moves below go through LDS.  The kernel bodies are the same source.
+#define WIDE_THREADS 128
+#define WAVES_PER_BLOCK 1
+#define BLOCK_THREADS WIDE_THREADS
+#else
 #define WAVES_PER_BLOCK 4
 #define BLOCK_THREADS (64 * WAVES_PER_BLOCK)
+#endif
 
 // XCD-aware block order.  Workgroups are dealt round-robin to the 8 XCDs, each with
 // its own 4 MiB L2; remapping blockIdx so that XCD x runs one contiguous 1/8 of the
@@ -35,14 +44,24 @@ __device__ __forceinline__ int xcd_block() {
 }
 
 // element of this wavefront, wave-uniform (scalar register)
+#ifdef MPAS_WIDE
+__device__ __forceinline__ int wave_elem(int start) { return __builtin_amdgcn_readfirstlane(start + xcd_block()); }
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+#else
 __device__ __forceinline__ int wave_elem(int start) {
   int e = start + xcd_block() * WAVES_PER_BLOCK + (threadIdx.x >> 6);
   return __builtin_amdgcn_readfirstlane(e);
 }
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+#endif
 
 // edge-stencil kernels (TRiSK / advection / acoustic edge phases) run EDGE_WPB waves per
 // workgroup: consecutive (SFC-ordered) edges of one workgroup share neighbour columns in the CU's L1
+#ifdef MPAS_WIDE
+#define EDGE_WPB 1
+#define EDGE_THREADS WIDE_THREADS
+__device__ __forceinline__ int wave_elem_e() { return __builtin_amdgcn_readfirstlane(xcd_block()); }
+#else
 #ifndef EDGE_WPB
 #define EDGE_WPB 4
 #endif
@@ -51,6 +70,7 @@ __device__ __forceinline__ int wave_elem_e() {
   int e = xcd_block() * EDGE_WPB + (threadIdx.x >> 6);
   return __builtin_amdgcn_readfirstlane(e);
 }
+#endif
 
 // Scalar arrays are scalar-major in HBM: scalars / scalars_tend as [ns][nCells+1][K],
 // horiz_flux_array as [ns][nEdges+1][K], so every per-scalar access is a contiguous
@@ -67,7 +87,26 @@ __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlan
 // __shfl_down do).  DPP wavefront shifts (wave_shr:1 / wave_shl:1, GFX9 DPP controls 0x138 /
 // 0x130) move the two halves of a double through the VALU, without the LDS round trip of
 // ds_bpermute.
-#ifndef MPAS_SHFL_BPERMUTE
+#ifdef MPAS_WIDE
+// the column spans several wavefronts: every move is a store to LDS, a barrier and a load.  Every
+// call site is reached by all lanes of the workgroup (the kernels keep these moves out of
+// lane-dependent branches, which the wavefront DPP forms need as well); the first barrier keeps a
+// move from overwriting the previous one's values before every lane has read them.
+__device__ __forceinline__ double col_move(double x, int delta, bool zero_end) {
+  __shared__ double col_buf[WIDE_THREADS];
+  __syncthreads();
+  col_buf[threadIdx.x] = x;
+  __syncthreads();
+  const int s = (int)threadIdx.x + delta;
+  if (s < 0 || s >= WIDE_THREADS) return zero_end ? 0.0 : x;
+  return col_buf[s];
+}
+__device__ __forceinline__ double up1(double x) { return col_move(x, -1, false); }
+__device__ __forceinline__ double dn1(double x) { return col_move(x, 1, false); }
+__device__ __forceinline__ double up2(double x) { return col_move(x, -2, false); }
+__device__ __forceinline__ double up1z(double x) { return col_move(x, -1, true); }
+__device__ __forceinline__ double dn1z(double x) { return col_move(x, 1, true); }
+#elif !defined(MPAS_SHFL_BPERMUTE)
 __device__ __forceinline__ double up1(double x) {
   const int lo = __double2loint(x), hi = __double2hiint(x);
   return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x138, 0xf, 0xf, false),
@@ -82,6 +121,7 @@ __device__ __forceinline__ double dn1(double x) {
 __device__ __forceinline__ double up1(double x) { return __shfl_up(x, 1, 64); }
 __device__ __forceinline__ double dn1(double x) { return __shfl_down(x, 1, 64); }
 #endif
+#ifndef MPAS_WIDE
 __device__ __forceinline__ double up2(double x) { return __shfl_up(x, 2, 64); }
 // lane-1 / lane+1 value with 0.0 shifted in at the end lane
 // (bound_ctrl: the out-of-range lane reads 0)
@@ -95,6 +135,7 @@ __device__ __forceinline__ double dn1z(double x) {
   return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, 0x130, 0xf, 0xf, true),
                           __builtin_amdgcn_mov_dpp(lo, 0x130, 0xf, 0xf, true));
 }
+#endif
 
 // The column's tridiagonal sweeps (mpas_atm_time_integration.F:2675-2682) with lane = level.
 // Forward x(k) = (x(k) - a(k) x(k-1)) alpha(k), k = 2..K (lanes 1..K-1), then backward
@@ -121,11 +162,21 @@ __device__ __forceinline__ double ld_uniform_f64(const double* a) {
   return __hiloint2double(q[1], q[0]);
 }
 
+#ifdef MPAS_WIDE
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  __shared__ double rl_buf[WIDE_THREADS];
+  __syncthreads();
+  rl_buf[threadIdx.x] = v;
+  __syncthreads();
+  return rl_buf[l];
+}
+#else
 __device__ __forceinline__ double readlane_d(double v, int l) {
   int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
   return __hiloint2double(hi, lo);
 }
+#endif
 
 // Fortran sign(1.0_RKIND, x): IEEE copysign semantics
 __device__ __forceinline__ double sgn1(double x) { return copysign(1.0, x); }
@@ -1632,7 +1683,7 @@ __device__ __forceinline__ d2 kp1(d2 v) {  // levels (k+1)
 // k_dyn_edges_b in the pair layout (NE2 = 2*maxEdges-2 TRiSK neighbours).  SPLIT (rk1 only): this
 // launch computes tend_u alone and k_dyn_edges_pgf_p the PGF part of tend_u_euler and del2 --
 // at rk1 the two are independent (no finalize), and together they need 244 VGPRs (2 waves/SIMD).
-template <bool RK1, int NE2, bool SPLIT = false>
+template <bool RK1, int NE2, bool SPLIT = false, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Config cf, DynTendScal s,
                                                               int finalize) {
   constexpr bool PGF = RK1 && !SPLIT;
@@ -1641,8 +1692,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, (K + 1) / 2 - 1), lw = min(l, K / 2);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1), lw = min(l, K / 2);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t K1 = K + 1;
   const size_t o = (size_t)e * K + 2 * lc;
@@ -1658,7 +1709,11 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   const int kx = 2 * l, ky = 2 * l + 1;  // true levels of the two components
   const bool stx = mine && kx < K, sty = mine && ky < K;
   auto store = [&](double* a, d2 v) {
-    if (stx) pst(a + o, v, sty);
+    if (ODD) {
+      if (stx) pst(a + o, v, sty);
+    } else if (stx && sty) {
+      st2(a + o, v);
+    }
   };
   // rk1 del^2 of u (4856-4883), all edges
   auto del2 = [&](d2 tue, d2 dv1, d2 dv2, d2 vo1, d2 vo2, d2 kd1, d2 kd2, double invDv, double msd2) {
@@ -1782,14 +1837,15 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
 
 // rk1, all edges: the PGF part of tend_u_euler (4781-4788, edges 1..nEdgesSolve) and the del2 of u
 // (4856-4883) -- the half of k_dyn_edges_p<true> that SPLIT leaves out
+template <bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_pgf_p(Dims d, Ptrs p) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, (K + 1) / 2 - 1);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const bool solve = h ? (hasB && eB < d.nEdgesSolve) : (eA < d.nEdgesSolve);
@@ -1828,15 +1884,15 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_pgf_p(Dims d, Ptrs p
 }
 
 // k_dyn_advflux_b in the pair layout
-template <int NA>
+template <int NA, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, (K + 1) / 2 - 1), lw = min(l, K / 2);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1), lw = min(l, K / 2);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const size_t K1 = K + 1;
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
@@ -1900,7 +1956,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
 }
 
 // k_diag_edges_b in the pair layout
-template <int NE2>
+template <int NE2, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, const double* __restrict__ u,
                                                                const double* __restrict__ hh, int reconstruct_v,
                                                                double apvm, double dt, int store_grad) {
@@ -1909,8 +1965,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, (K + 1) / 2 - 1);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
@@ -1991,6 +2047,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
 // two levels (2*lc, 2*lc+1) of cell c's rtheta_pp (which = 0) or rho_pp (1) column: from the
 // exchange's receive buffer for a halo cell the fused unpack covers -- written back into the field,
 // lanes `st` only, for the later readers -- else from the field
+template <bool ODD>
 __device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMap& um, int which, int c, int lc,
                                     bool st) {
   double* fld = which ? p.rho_pp : p.rtheta_pp;
@@ -2000,7 +2057,7 @@ __device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMa
     const int off = map[c - d.nCellsSolve];
     if (off >= 0) {
       const d2 v = ld2(um.recv + off + 2 * lc);
-      if (st) pst(fld + o, v, 2 * lc + 1 < d.K);
+      if (st) pst(fld + o, v, !ODD || 2 * lc + 1 < d.K);
       return v;
     }
   }
@@ -2008,7 +2065,7 @@ __device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMa
 }
 
 // dl = 1: rtheta_pp_old holds rtheta_pp - rtheta_pp_old (k_acoustic_cells_r<ME, true> with dl)
-template <bool REC = false, bool UP = false>
+template <bool REC = false, bool UP = false, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
                                                             int fresh, double invNs = 0.0, UnpackMap um = UnpackMap{},
                                                             int dl = 0) {
@@ -2016,8 +2073,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   bool hasB;
   if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, (K + 1) / 2 - 1);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
@@ -2043,8 +2100,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
     dd1 = ld2(p.rtheta_pp_old + o1);
     dd2 = ld2(p.rtheta_pp_old + o2);
   } else {
-    const d2 r1 = UP ? ld_pp(d, p, um, 0, sel(h, ceA.x, ceB.x), lc, lv) : ld2(p.rtheta_pp + o1);
-    const d2 r2 = UP ? ld_pp(d, p, um, 0, sel(h, ceA.y, ceB.y), lc, lv) : ld2(p.rtheta_pp + o2);
+    const d2 r1 = UP ? ld_pp<ODD>(d, p, um, 0, sel(h, ceA.x, ceB.x), lc, lv) : ld2(p.rtheta_pp + o1);
+    const d2 r2 = UP ? ld_pp<ODD>(d, p, um, 0, sel(h, ceA.y, ceB.y), lc, lv) : ld2(p.rtheta_pp + o2);
     const d2 q1 = ld2(p.rtheta_pp_old + o1), q2 = ld2(p.rtheta_pp_old + o2);
     dd1 = d2{r1.x - q1.x, r1.y - q1.y};
     dd2 = d2{r2.x - q2.x, r2.y - q2.y};
@@ -2079,15 +2136,15 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
 }
 
 // k_scalars_edges in the pair layout (atm_advance_scalars_work, 3357-3426)
-template <int NA>
+template <int NA, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31, ns = d.ns;
-  const int lc = min(l, (K + 1) / 2 - 1);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int na = sel(h, p.nAdvCellsForEdge[eA], p.nAdvCellsForEdge[eB]);
@@ -2147,15 +2204,15 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
 }
 
 // k_mono_edges1 in the pair layout (atm_advance_scalars_mono_work, 3916-3961, 4007-4022)
-template <int NA>
+template <int NA, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, int is, double dt) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31, ns = d.ns;
-  const int lc = min(l, (K + 1) / 2 - 1);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
@@ -2226,6 +2283,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
 // runs as a lane-shift sweep: each iteration finalizes one more lane (two levels, the second from
 // the first in registers), K/2 iterations instead of K-1, each from exactly the operands of the
 // sequential recurrence -- and a wave now carries two columns, halving the DP work per column.
+template <bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs p, double dts, double epssm) {
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
   const double dtseps = .5 * dts * (1. + epssm);
@@ -2237,8 +2295,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs 
   const bool hasB = cA + 1 < d.nCellsSolve;
   const int c = sel(h, cA, hasB ? cA + 1 : cA);
   const bool mine = h == 0 || hasB;
-  const int lc = min(l, (K + 1) / 2 - 1);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int kx = 2 * l, ky = 2 * l + 1;
   const bool ax = kx < K, ay = ky < K;  // "act" of the two levels
   const size_t o = (size_t)c * K + 2 * lc;
@@ -2287,7 +2345,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs 
   // sequential LU recurrence (2124-2127) as a lane-shift sweep
   const bool fx = kx >= 1 && ax, fy = ay;
   d2 alpha{0.0, 0.0}, gamma{0.0, 0.0};
-  for (int it = 0; it < (K + 1) / 2; ++it) {
+  for (int it = 0; it < (ODD ? K + 1 : K) / 2; ++it) {
     const double gpx = lane_shr1(gamma.y);
     if (fx) {
       alpha.x = 1. / (b.x - a.x * (l == 0 ? 0.0 : gpx));
@@ -2325,7 +2383,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs 
 
 // k_acoustic_edges in the pair layout (same expressions, per level)
 // UP: the Theta''/rho'' halo comes from the exchange's receive buffer (fused unpack, UnpackMap)
-template <bool DD, bool UP = false>
+template <bool DD, bool UP = false, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,
                                                                    double coef_divdamp, int phase, int fresh,
                                                                    UnpackMap um = UnpackMap{}) {
@@ -2334,8 +2392,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
   if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
   const bool lev = 2 * l < K;                     // this lane holds levels 2l, 2l+1
-  const int lc = min(l, (K + 1) / 2 - 1);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
@@ -2369,11 +2427,11 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs 
   const double invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
   const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
   const size_t o1 = (size_t)c1 * K + 2 * lc, o2 = (size_t)c2 * K + 2 * lc;
-  const d2 rt1 = UP ? ld_pp(d, p, um, 0, c1, lc, st) : ld2(p.rtheta_pp + o1);
-  const d2 rt2 = UP ? ld_pp(d, p, um, 0, c2, lc, st) : ld2(p.rtheta_pp + o2);
+  const d2 rt1 = UP ? ld_pp<ODD>(d, p, um, 0, c1, lc, st) : ld2(p.rtheta_pp + o1);
+  const d2 rt2 = UP ? ld_pp<ODD>(d, p, um, 0, c2, lc, st) : ld2(p.rtheta_pp + o2);
   const d2 zz1 = ld2(p.zz + o1), zz2 = ld2(p.zz + o2), ex1 = ld2(p.exner + o1), ex2 = ld2(p.exner + o2);
-  const d2 rp1 = UP ? ld_pp(d, p, um, 1, c1, lc, st) : ld2(p.rho_pp + o1);
-  const d2 rp2 = UP ? ld_pp(d, p, um, 1, c2, lc, st) : ld2(p.rho_pp + o2);
+  const d2 rp1 = UP ? ld_pp<ODD>(d, p, um, 1, c1, lc, st) : ld2(p.rho_pp + o1);
+  const d2 rp2 = UP ? ld_pp<ODD>(d, p, um, 1, c2, lc, st) : ld2(p.rho_pp + o2);
   d2 ro1{}, ro2{}, th1{}, th2{};
   if (DD) {
     ro1 = ld2(p.rtheta_pp_old + o1);
@@ -3868,14 +3926,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2_b(Dims d, Ptrs p,
   p.scalars2[SIX(c, k, is)] = fmax(0.0, snew);
 }
 
+template <bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges2_p(Dims d, Ptrs p, double dt) {
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
-  const int lc = min(l, (K + 1) / 2 - 1);
-  const bool two = 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);

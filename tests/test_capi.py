@@ -38,3 +38,28 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(RuntimeError):
         _lib.load()
+
+
+def test_two_builds_are_dispatched_by_level_count():
+    """The library links two builds of dycore.hip (one wavefront per column up to
+    MPAS_DYC_MAX_LEVELS_WAVE levels, one workgroup per column above): the public entry points
+    (api_dispatch.cpp) and the builds' renames (api_rename.h) are generated from the header and
+    up to date, every public function forwards to both builds, and both builds are in the library."""
+    import subprocess
+    import sys
+    gen = os.path.join(ROOT, "mpas-model_amd", "csrc", "gen_api.py")
+    r = subprocess.run([sys.executable, gen, "--check"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    src = open(HEADER).read()
+    assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS_WAVE (\d+)", src).group(1)) == 63
+    assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS (\d+)", src).group(1)) == 127
+    disp = open(os.path.join(ROOT, "mpas-model_amd", "csrc", "api_dispatch.cpp")).read()
+    for f in declared_functions():
+        assert re.search(rf"\b{f}\(", disp), f
+    from mpas_dycore import _lib
+    if not os.path.isfile(_lib.LIBPATH):
+        pytest.skip("libmpas_dycore.so not built (__graft_entry__.build())")
+    lib = ctypes.CDLL(_lib.LIBPATH)
+    for tag in ("n", "w"):
+        missing = [f for f in declared_functions() if not hasattr(lib, f.replace("mpas_dyc_", f"mpas_dyc{tag}_"))]
+        assert not missing, (tag, missing)
