@@ -808,6 +808,11 @@ inline bool batched(const Dims& d) {
 }
 
 
+// atm_set_smlstep_pert_variables fused into the batched k_dyn_cells3_r for the cells without a halo
+// edge (MPAS_DYCORE_FUSE_SMLSTEP=0, read when a context is created: the separate kernel for all)
+int g_fuse_smlstep = 1;
+inline bool fuse_smlstep(const Dims& d) { return g_fuse_smlstep && batched(d); }
+
 // pair-layout edge kernels (k_*_p: two edges per wave, two levels per lane); at an odd K the last
 // pair's second level is past the column: loaded (the 256 B of slack behind every field covers the
 // last column), never stored, and every level-dependent expression masks it as it masks the
@@ -1099,16 +1104,25 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   else if (d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_b<10>, d.nEdges, d, p);
   else LAUNCH_E(k_dyn_advflux_b<12>, d.nEdges, d, p);
   if (batched(d)) {
-    if (d.maxEdges == 6 && rk_step == 1) LAUNCH((k_dyn_cells3_r<6, true>), d.nCellsSolve, d, p, cf, s);
-    if (d.maxEdges == 6 && rk_step != 1) LAUNCH((k_dyn_cells3_r<6, false>), d.nCellsSolve, d, p, cf, s);
-    if (d.maxEdges == 7 && rk_step == 1) LAUNCH((k_dyn_cells3_r<7, true>), d.nCellsSolve, d, p, cf, s);
-    if (d.maxEdges == 7 && rk_step != 1) LAUNCH((k_dyn_cells3_r<7, false>), d.nCellsSolve, d, p, cf, s);
+    const bool sml = fuse_smlstep(d);
+    if (d.maxEdges == 6 && rk_step == 1 && sml) LAUNCH((k_dyn_cells3_r<6, true, true>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 6 && rk_step != 1 && sml) LAUNCH((k_dyn_cells3_r<6, false, true>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 7 && rk_step == 1 && sml) LAUNCH((k_dyn_cells3_r<7, true, true>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 7 && rk_step != 1 && sml) LAUNCH((k_dyn_cells3_r<7, false, true>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 6 && rk_step == 1 && !sml) LAUNCH((k_dyn_cells3_r<6, true>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 6 && rk_step != 1 && !sml) LAUNCH((k_dyn_cells3_r<6, false>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 7 && rk_step == 1 && !sml) LAUNCH((k_dyn_cells3_r<7, true>), d.nCellsSolve, d, p, cf, s);
+    if (d.maxEdges == 7 && rk_step != 1 && !sml) LAUNCH((k_dyn_cells3_r<7, false>), d.nCellsSolve, d, p, cf, s);
     return;
   }
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
 }
 
 void smlstep_pert(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int phase) {
+  if (fuse_smlstep(d)) {  // k_dyn_cells3_r did the cells without a halo edge
+    if (phase == 1) return;
+    phase = 2;
+  }
   const int64_t nb = phase == 2 ? d.n_bnd_cells : d.nCellsSolve;  // phase 2: the bnd_cells list
   if (!batched(d)) LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, phase);
   else if (d.maxEdges == 6) LAUNCH(k_smlstep_pert_b<6>, nb, d, p, phase);
@@ -1918,6 +1932,8 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
 #ifdef MPAS_WIDE
   g_kernel_tier = 0;  // the wide build runs the one-column-per-element kernels only
 #endif
+  g_fuse_smlstep = 1;
+  if (const char* fs = getenv("MPAS_DYCORE_FUSE_SMLSTEP")) g_fuse_smlstep = std::string(fs) != "0";
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
   for (auto& b : ctx->blk) {
     build_registry(b);

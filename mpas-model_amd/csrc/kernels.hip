@@ -1127,7 +1127,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_advflux(Dims d, Ptrs p) {
 // k_dyn_cells3 on the per-cell stencil record (ME = maxEdges <= 7, RK1 = rk_step == 1): the
 // edge columns of every edge of the cell (and the cells across them) are loaded in one batch
 // after a single scalar round trip; the sums keep the reference order edge by edge.
-template <int ME, bool RK1>
+template <int ME, bool RK1, bool SML = false>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3_r(Dims d, Ptrs p, Config cf, DynTendScal s) {
   const int c = wave_elem(0);
   if (c >= d.nCellsSolve) return;
@@ -1266,8 +1266,31 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3_r(Dims d, Ptrs p, 
       }
     }
   }
+  double twf = (act && k >= 1) ? tw : 0.0;
+  // SML: atm_set_smlstep_pert_variables (2290-2307) of this cell, fused: the cell's edges are all
+  // owned (no halo edge), so their tend_u is final here and needs no exchange (the cells with a
+  // halo edge run k_smlstep_pert_b after the 642 exchange); same expressions as k_smlstep_pert_b
+  if (SML && !(p.cell_bnd[c] & CELL_HALO_EDGE) && p.bdyMaskCell[c] <= N_RELAX_ZONE) {
+    double ut[ME], zs[ME];
+#pragma unroll
+    for (int i = 0; i < ME; ++i) ut[i] = p.tend_u[(size_t)uni(st.e[i]) * K + kc];
+#pragma unroll
+    for (int i = 0; i < ME; ++i) zs[i] = (sgn1(ut[i]) > 0.0 ? p.zb_p : p.zb_m)[((size_t)c * ME + i) * K1 + kw];
+    const double zz = p.zz[o];
+    double wt = twf;
+#pragma unroll
+    for (int i = 0; i < ME; ++i) {
+      const double utm = up1(ut[i]);
+      if (i < st.ne && act && k >= 1) {
+        const double flux = st.sg(i) * (fzm * ut[i] + fzp * utm);
+        wt = wt - zs[i] * flux;
+      }
+    }
+    const double zzm = up1(zz);
+    if (act && k >= 1) twf = (fzm * zz + fzp * zzm) * wt;
+  }
   if (actw) {
-    p.tend_w[ow] = (act && k >= 1) ? tw : 0.0;
+    p.tend_w[ow] = twf;
     if (RK1) p.tend_w_euler[ow] = twe;
   }
   if (act) {
