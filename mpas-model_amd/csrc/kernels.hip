@@ -2146,7 +2146,10 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   const d2 ra = fresh ? ru : ld2(p.ruAvg + o);  // fresh: sub-step 1 left ruAvg = dts * tend_u
   const d2 z1 = ld2(p.rho_zz2 + o1), z2 = ld2(p.rho_zz2 + o2);
   if ((h ? onB : onA) && 2 * l < K) {
-    pst(p.ru_p + o, out, two);
+    // dl (one block, not the dt's last stage, see damping_delta): nothing reads ru_p of a
+    // recovered edge before the next stage's sub-step 1 forms it again from tend_u, so only the
+    // edges k_recover_edges still recovers from it get it stored
+    if (!(dl && (h ? rB : rA))) pst(p.ru_p + o, out, two);
     if (h ? rB : rA) {  // recover_edges (3048-3059), same expressions
       pst(p.ruAvg + o, d2{rs.x + (ra.x * invNs), rs.y + (ra.y * invNs)}, two);
       const d2 rr{rs.x + out.x, rs.y + out.y};
