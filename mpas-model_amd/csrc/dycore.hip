@@ -1236,24 +1236,27 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double d
   const double* u = (tl == 1) ? p.u1 : p.u2;
   const double* h = (tl == 1) ? p.rho_zz1 : p.rho_zz2;
   const int reconstruct_v = (rk_step == 0 || rk_step == 3) ? 1 : 0;
+  // divergence and vorticity are read only by the rk1 dyn_tend (the del2 of u, 4856-4883): the
+  // calls that precede an rk 2 / 3 stage need not store them (the pool keeps the dt's last values)
+  const int store_dv = (rk_step == 0 || rk_step == 3) ? 1 : 0;
   if (!batched(d)) {
-    LAUNCH(k_diag_vertices, d.nVertices, d, p, u);
-    LAUNCH(k_diag_cells, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
+    LAUNCH(k_diag_vertices, d.nVertices, d, p, u, store_dv);
+    LAUNCH(k_diag_cells, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     LAUNCH(k_diag_edges, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
     return;
   }
-  LAUNCH(k_diag_vertices, d.nVertices, d, p, u);  // the batched variant measured slower
+  LAUNCH(k_diag_vertices, d.nVertices, d, p, u, store_dv);  // the batched variant measured slower
   if (pair_layout(d)) {
-    if (d.maxEdges == 6) LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
-    else LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
+    if (d.maxEdges == 6) LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
+    else LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     const int64_t nw = (d.nEdges + 1) / 2;
     if (d.maxEdges == 6) LAUNCH_PE((k_diag_edges_p<10, false>), (k_diag_edges_p<10, true>), nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
     else LAUNCH_PE((k_diag_edges_p<12, false>), (k_diag_edges_p<12, true>), nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
   } else if (d.maxEdges == 6) {
-    LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
+    LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     LAUNCH_E(k_diag_edges_b<10>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
   } else {
-    LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding);
+    LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     LAUNCH_E(k_diag_edges_b<12>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
   }
 }

@@ -2969,7 +2969,8 @@ __device__ __forceinline__ double ke_edge_of(const Ptrs& p, const double* u, int
   return efac * (uu * uu);
 }
 
-__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_vertices(Dims d, Ptrs p, const double* __restrict__ u) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_vertices(Dims d, Ptrs p, const double* __restrict__ u,
+                                                                 int store_dv = 1) {
   const int v = wave_elem(0);
   if (v >= d.nVertices) return;
   const int k = lane_id(), K = d.K;
@@ -2985,12 +2986,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_vertices(Dims d, Ptrs p,
   const double r = 0.25 * p.invAreaTriangle[v];
   kev = (ke_edge_of(p, u, e1, K, k) + ke_edge_of(p, u, e2, K, k) + ke_edge_of(p, u, e3, K, k)) * r;
   const size_t o = (size_t)v * K + k;
-  p.vorticity[o] = vort;
+  if (store_dv) p.vorticity[o] = vort;
   p.ke_vertex[o] = kev;
   p.pv_vertex[o] = (p.fVertex[v] + vort);
 }
 
-__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells(Dims d, Ptrs p, const double* __restrict__ u, double apvm) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells(Dims d, Ptrs p, const double* __restrict__ u, double apvm,
+                                                              int store_dv = 1) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
   const int k = lane_id(), K = d.K;
@@ -3019,7 +3021,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells(Dims d, Ptrs p, co
     pvc = pvc + kite * p.pv_vertex[(size_t)iv * K + k] * r;
   }
   const size_t o = (size_t)c * K + k;
-  p.divergence[o] = div;
+  if (store_dv) p.divergence[o] = div;
   p.ke[o] = ke;
   if (apvm > 0.0) p.pv_cell[o] = pvc;
 }
@@ -3137,7 +3139,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs
 
 template <int ME>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells_b(Dims d, Ptrs p, const double* __restrict__ u,
-                                                                double apvm) {
+                                                                double apvm, int store_dv = 1) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
   const int k = lane_id(), K = d.K;
@@ -3186,7 +3188,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_diag_cells_b(Dims d, Ptrs p, 
     }
   }
   const size_t o = (size_t)c * K + k;
-  p.divergence[o] = div;
+  if (store_dv) p.divergence[o] = div;
   p.ke[o] = ke;
   if (apvm > 0.0) p.pv_cell[o] = pvc;
 }

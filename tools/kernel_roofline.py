@@ -52,8 +52,8 @@ VARIANT = {
     "k_dyn_cells3_r<6, false": {"drop": {"delsq_theta", "delsq_w", "dpdz", "pressure_p", "t_init", "zgrid",
                                          "cqw", "meshScalingDel4", "rdzu", "tend_rtheta_physics"},
                                 "drop_w": {"tend_theta_euler", "tend_w_euler", "rthdynten", "tend_rtheta_adv"}},
-    "k_dyn_cells3_r<6, true": {"drop": {"tend_theta_euler", "tend_w_euler", "ru_save", "rw_save",
-                                        "tend_rtheta_physics"},
+    # rk1 reads tend_w_euler / tend_theta_euler (k_dyn_cells2's del2 terms) and rw_save; not ru_save
+    "k_dyn_cells3_r<6, true": {"drop": {"ru_save", "tend_rtheta_physics"},
                                "drop_w": {"rthdynten", "tend_rtheta_adv"}},
     "k_acoustic_cells_r<6, false": {"drop": {"rho_base", "rho_p_save", "rtheta_base", "rtheta_p_save", "exner_base"},
                                     "drop_w": {"exner", "pressure_p", "rho_p", "rho_zz2", "rtheta_p", "rw", "theta_m2",
