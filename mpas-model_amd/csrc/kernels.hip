@@ -2528,7 +2528,9 @@ __device__ __forceinline__ void recover_cell_fused(const Dims& d, const Ptrs& p,
   double rz = 0.0;
   if (act) {
     const double rho_p = rps + rhopp;
-    p.rho_p[o] = rho_p;
+    // rho_p is read only as rho_p_save, after the rotation at the next substep start, and by
+    // the pool after the dt: the stage-3 value; stages 1-2 do not store it
+    if (rk_step == 3) p.rho_p[o] = rho_p;
     rz = rho_p + rb;
     p.rho_zz2[o] = rz;
   }
@@ -2873,7 +2875,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p
   double rz = 0.0;
   if (act) {
     const double rho_p = p.rho_p_save[o] + p.rho_pp[o];
-    p.rho_p[o] = rho_p;
+    if (rk_step == 3) p.rho_p[o] = rho_p;  // stored at stage 3 only (recover_cell_fused)
     rz = rho_p + p.rho_base[o];
     p.rho_zz2[o] = rz;
   }
