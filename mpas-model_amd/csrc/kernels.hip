@@ -1174,6 +1174,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3_r(Dims d, Ptrs p, 
   const double tte0 = p.tend_theta_euler[o];
   const double th = p.theta_m2[o], rws = p.rw_save[ow];
   const double rtd = d.diabatic ? p.rt_diabatic_tend[o] : 0.0;
+  // SML: the fused smlstep's tend_u of the cell's edges, issued with the rest (the zb column its
+  // sign selects is loaded at the end: early, it would cost a wave per SIMD)
+  const bool sml = SML && !(p.cell_bnd[c] & CELL_HALO_EDGE) && p.bdyMaskCell[c] <= N_RELAX_ZONE;
+  double ut[ME], zz = 0.0;
+  if (sml) {
+#pragma unroll
+    for (int i = 0; i < ME; ++i) ut[i] = p.tend_u[(size_t)uni(st.e[i]) * K + kc];
+    zz = p.zz[o];
+  }
   // ---- horizontal advection of w (5046-5074) and theta (5231-5252)
   double tw = 0.0, tt = 0.0;
 #pragma unroll
@@ -1270,13 +1279,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells3_r(Dims d, Ptrs p, 
   // SML: atm_set_smlstep_pert_variables (2290-2307) of this cell, fused: the cell's edges are all
   // owned (no halo edge), so their tend_u is final here and needs no exchange (the cells with a
   // halo edge run k_smlstep_pert_b after the 642 exchange); same expressions as k_smlstep_pert_b
-  if (SML && !(p.cell_bnd[c] & CELL_HALO_EDGE) && p.bdyMaskCell[c] <= N_RELAX_ZONE) {
-    double ut[ME], zs[ME];
-#pragma unroll
-    for (int i = 0; i < ME; ++i) ut[i] = p.tend_u[(size_t)uni(st.e[i]) * K + kc];
+  if (sml) {
+    double zs[ME];
 #pragma unroll
     for (int i = 0; i < ME; ++i) zs[i] = (sgn1(ut[i]) > 0.0 ? p.zb_p : p.zb_m)[((size_t)c * ME + i) * K1 + kw];
-    const double zz = p.zz[o];
     double wt = twf;
 #pragma unroll
     for (int i = 0; i < ME; ++i) {
