@@ -649,6 +649,37 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   std::sort(pl.rrecv.begin(), pl.rrecv.end(), [](const XMsg& a, const XMsg& b) {
     return std::make_tuple(a.peer_rank, a.peer_block, a.block) < std::make_tuple(b.peer_rank, b.peer_block, b.block);
   });
+  // One RCCL message per peer rank, as mpas_dmpar packs one buffer per processor for all its
+  // blocks (mpas_dmpar.F:5386-5552): the block-pair messages to one rank are laid out back to back
+  // in the order both sides sort them above, and go as one send / one receive.  (With one block
+  // per rank nothing changes; with several, e.g. bench.py --blocks B or --rccl-local, the group
+  // holds one message per peer rank instead of one per block pair.)
+  auto merge_by_rank = [](std::vector<XMsg>& msgs, std::vector<int64_t>& offs) {
+    std::map<int64_t, int64_t> base;  // message start, old layout -> new layout
+    int64_t cur = 0;
+    for (const XMsg& m : msgs) {
+      base[m.off] = cur;
+      cur += m.count;
+    }
+    for (int64_t& o : offs) {
+      if (o < 0) continue;  // a direct in-process copy
+      auto it = std::prev(base.upper_bound(o));
+      o = it->second + (o - it->first);
+    }
+    std::vector<XMsg> merged;
+    for (XMsg m : msgs) {
+      m.off = base[m.off];
+      if (!merged.empty() && merged.back().peer_rank == m.peer_rank) {
+        merged.back().count += m.count;
+        merged.back().block = merged.back().peer_block = -1;  // several block pairs
+      } else {
+        merged.push_back(m);
+      }
+    }
+    msgs.swap(merged);
+  };
+  merge_by_rank(pl.rsend, pre_off);
+  merge_by_rank(pl.rrecv, post_off);
   if (ctx->host_only) return MPAS_DYC_OK;  // the dry run keeps the message lists only
   if (stotal) HIPCHK(hipMalloc(&pl.sendbuf, stotal * sizeof(double)));
   // 256 B of slack: a fused unpack (ld_pp) reads the two levels of its lane's pair, one past the
