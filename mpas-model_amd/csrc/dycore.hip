@@ -1441,6 +1441,13 @@ int summary_launch(mpas_dyc_ctx* ctx, int tl) {
   }
 #define EACH(...) EACHV(P, __VA_ARGS__)
 
+// mpas_reconstruct (operators/mpas_vector_reconstruction.F:195-294): the cell-centre velocity
+void reconstruct(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, const double* u) {
+  if (batched(d) && d.maxEdges == 6) LAUNCH(k_reconstruct_b<6>, d.nCellsSolve, d, p, u);
+  else if (batched(d)) LAUNCH(k_reconstruct_b<7>, d.nCellsSolve, d, p, u);
+  else LAUNCH(k_reconstruct, d.nCellsSolve, d, p, u);
+}
+
 // atm_srk3 (mpas_atm_time_integration.F:142-1796)
 // atm_bdy_adjust_scalars (6436-6586) at the end of a transport stage: the scalars' halo first
 // (the filter reads the neighbours), then the relaxation / specified-zone update of owned cells
@@ -1532,22 +1539,30 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   auto xwait = [&]() { return split ? exchange_wait(ctx) : MPAS_DYC_OK; };
   bool pending = false;  // an xchg whose xwait is still due
   bool final_pending = false;  // the last substep's 1234-1249 exchange, waited for after substep_finish
+  // The w recovery of a stage computes the next stage's h_divergence (k_recover_cells3_b with hdiv),
+  // so that stage's k_dyn_cells1 (which computes nothing else at rk 2 / 3) is not launched.  Without
+  // split-phase exchanges: after stages 1 and 2.  With them, k_dyn_cells1 is the work that overlaps
+  // the 1234-1249 exchange; at rk 2 of order 3 vert_imp_coefs overlaps it as well, so the fusion is
+  // kept after stage 1 only.  Not with LBCs (the reference recomputes h_divergence from the
+  // overwritten ru).
+  bool hdiv_prev = false;  // the previous stage's w recovery computed this stage's h_divergence
   EACHV(Ppre, vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));    // 476-510 of dynamics substep 1
   for (int dynamics_substep = 1; dynamics_substep <= dynamics_split; ++dynamics_substep) {
     // 513 (exner): carried by the step-start exchange and by the 1282-1297 exchange below
     for (int rk_step = 1; rk_step <= 3; ++rk_step) {
       if (cf.time_integration_order == 3 && rk_step == 2) EACH(vert_imp_coefs(ctx, d, p, rk_sub_timestep[1]));
       const bool last_stage = dynamics_substep == dynamics_split && rk_step == 3;
+      const bool hdiv_next = !lbc && rk_step < 3 && (!split || (rk_step == 1 && cf.time_integration_order == 3));
       // the first stage reads time level 2 and the saved fields through stage_pre until its recovery
       const std::vector<Ptrs>& PS = rk_step == 1 ? Ppre : P;
       const std::vector<Ptrs>& PF = rk_step == 1 ? Pfin : P;  // the stage's last cell phase
       if (pending) {  // 561-630, k_dyn_cells1 overlapping the exchange
-        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 1, !split && batched(d)));
+        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 1, hdiv_prev && batched(d)));
         CHK(xwait());
         pending = false;
         EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 2, false, last_stage));
       } else {
-        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 0, !split && batched(d) && !lbc, last_stage));  // 561-630
+        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 0, hdiv_prev && batched(d), last_stage));  // 561-630
       }
       const double dts = rk_sub_timestep[rk_step - 1];
       if (split) {  // 642 | 644-678: interior cells overlap the tend_u exchange
@@ -1641,7 +1656,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
           CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));  // 988
         } else {
           CHK(exchange_async(ctx, {{"state", "u", 2, ALL_LAYERS}}));
-          EACH(recover_cells3(ctx, d, p, 0));
+          EACH(recover_cells3(ctx, d, p, 0, hdiv_next));
           CHK(exchange_wait(ctx));
         }
       } else {
@@ -1654,7 +1669,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0);
              else LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2));
         // stages 1 and 2: also the next stage's h_divergence (dyn_tend then skips k_dyn_cells1)
-        EACH(recover_cells3(ctx, d, p, 0, rk_step < 3 && !lbc));
+        EACH(recover_cells3(ctx, d, p, 0, hdiv_next));
         if (lbc)  // 934-987
           EACH(LAUNCH(k_lbc_u, d.nEdges, d, p, dt_dynamics * (double)(dynamics_substep - 1) + rk_timestep[rk_step - 1]));
         CHK(exchange(ctx, {{"state", "u", 2, ALL_LAYERS}}));      // 988
@@ -1704,6 +1719,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       } else {
         CHK((exchange)(ctx, xd));
       }
+      hdiv_prev = hdiv_next;
     }
     if (!ctx->planning)                                           // 1304-1341
       EACH(hipLaunchKernelGGL(k_substep_finish_v, dim3(2048), dim3(BLOCK_THREADS), 0, ctx->stream, d, p,
@@ -1741,7 +1757,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       }
     }
   }
-  EACH(LAUNCH(k_reconstruct, d.nCellsSolve, d, p, p.u2));          // mpas_reconstruct (1581-1603)
+  EACH(reconstruct(ctx, d, p, p.u2));                              // mpas_reconstruct (1581-1603)
   if (ctx->physics & MPAS_DYC_PHYSICS_TENDENCIES) {                // DO_PHYSICS block, 1610-1648
     // rqvdynten (1629-1643) for cu_grell_freitas / cu_tiedtke / cu_ntiedtke, from the scalars before
     // the clip; the microphysics call itself (1650-1660) belongs to the host, after this step
@@ -1772,7 +1788,7 @@ int init_diagnostics(mpas_dyc_ctx* ctx, double dt, bool coupled = true) {
     EACH(LAUNCH(k_init_coupled_c, d.nCells, d, p));
   }
   EACH(solve_diagnostics(ctx, d, p, dt, 1, 0));
-  EACH(LAUNCH(k_reconstruct, d.nCellsSolve, d, p, p.u1));          // mpas_atm_core.F:411-421
+  EACH(reconstruct(ctx, d, p, p.u1));                              // mpas_atm_core.F:411-421
   CHK(exchange(ctx, {{"diag", "pv_edge", 0, ALL_LAYERS}, {"diag", "ru", 0, ALL_LAYERS},  // 180-186
                      {"diag", "rw", 0, ALL_LAYERS}}));
   return MPAS_DYC_OK;
