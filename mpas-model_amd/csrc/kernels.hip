@@ -4023,4 +4023,47 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_reconstruct(Dims d, Ptrs p, c
   p.uReconstructMeridional[o] = -(x * clon + y * slon) * slat + z * clat;
 }
 
+
+// k_reconstruct on the per-cell stencil record (ME = maxEdges, 6 or 7): the edge indices come from
+// the record in one scalar round trip, the ME columns of u and the coefficient rows are issued
+// together (slots beyond nEdgesOnCell name the garbage edge and are not summed), then the sums in
+// the reference order (mpas_vector_reconstruction.F:245-294)
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_reconstruct_b(Dims d, Ptrs p, const double* __restrict__ u) {
+  const int c = wave_elem(0);
+  if (c >= d.nCellsSolve) return;
+  const int k = lane_id(), K = d.K;
+  const int kc = min(k, K - 1);
+  const CellSten<ME> st = load_sten<ME>(p, c);
+  double ue[ME], cx[ME], cy[ME], cz[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) ue[i] = u[(size_t)st.e[i] * K + kc];
+  const double* cf = p.coeffs_reconstruct + (size_t)c * ME * 3;
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    cx[i] = ld_uniform_f64(cf + 3 * i);
+    cy[i] = ld_uniform_f64(cf + 3 * i + 1);
+    cz[i] = ld_uniform_f64(cf + 3 * i + 2);
+  }
+  const double lat = ld_uniform_f64(p.latCell + c), lon = ld_uniform_f64(p.lonCell + c);
+  double x = 0.0, y = 0.0, z = 0.0;
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    if (i < st.ne) {
+      x = x + cx[i] * ue[i];
+      y = y + cy[i] * ue[i];
+      z = z + cz[i] * ue[i];
+    }
+  }
+  if (k >= K) return;
+  const size_t o = (size_t)c * K + k;
+  p.uReconstructX[o] = x;
+  p.uReconstructY[o] = y;
+  p.uReconstructZ[o] = z;
+  const double clat = cos(lat), slat = sin(lat);
+  const double clon = cos(lon), slon = sin(lon);
+  p.uReconstructZonal[o] = -x * slon + y * clon;
+  p.uReconstructMeridional[o] = -(x * clon + y * slon) * slat + z * clat;
+}
+
 }  // namespace mpas

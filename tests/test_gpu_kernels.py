@@ -105,7 +105,9 @@ def _steps_with_kernels(case, family, nsteps=3, dt=None):
         dy.shift_time_levels()
     dy.synchronize()
     out = {n: dy.get("state", n, 1) for n in ("u", "w", "theta_m", "rho_zz", "scalars")}
-    out.update({n: dy.get("diag", n) for n in ("pv_edge", "rho_edge", "exner", "ru", "rw")})
+    out.update({n: dy.get("diag", n) for n in ("pv_edge", "rho_edge", "exner", "ru", "rw", "uReconstructX",
+                                                "uReconstructY", "uReconstructZ", "uReconstructZonal",
+                                                "uReconstructMeridional")})
     dy.close()
     return out
 
