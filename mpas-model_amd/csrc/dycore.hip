@@ -1276,18 +1276,20 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double d
     LAUNCH(k_diag_edges, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
     return;
   }
-  LAUNCH(k_diag_vertices, d.nVertices, d, p, u, store_dv);  // the batched variant measured slower
   if (pair_layout(d)) {
-    const int64_t nc = (d.nCells + 1) / 2;
-    if (d.maxEdges == 6) LAUNCH_PE((k_diag_cells_p<6, false>), (k_diag_cells_p<6, true>), nc, d, p, u, ctx->cf.apvm_upwinding, store_dv);
-    else LAUNCH_PE((k_diag_cells_p<7, false>), (k_diag_cells_p<7, true>), nc, d, p, u, ctx->cf.apvm_upwinding, store_dv);
+    LAUNCH_PE((k_diag_vertices_p<false>), (k_diag_vertices_p<true>), (d.nVertices + 1) / 2, d, p, u, store_dv);
+    // (a pair-layout k_diag_cells, two cells per wave, measured 18 % slower than the batched one)
+    if (d.maxEdges == 6) LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
+    else LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     const int64_t nw = (d.nEdges + 1) / 2;
     if (d.maxEdges == 6) LAUNCH_PE((k_diag_edges_p<10, false>), (k_diag_edges_p<10, true>), nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
     else LAUNCH_PE((k_diag_edges_p<12, false>), (k_diag_edges_p<12, true>), nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
   } else if (d.maxEdges == 6) {
+    LAUNCH(k_diag_vertices, d.nVertices, d, p, u, store_dv);  // (a batched one-column variant measured slower)
     LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     LAUNCH_E(k_diag_edges_b<10>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
   } else {
+    LAUNCH(k_diag_vertices, d.nVertices, d, p, u, store_dv);
     LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     LAUNCH_E(k_diag_edges_b<12>, d.nEdges, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
   }

@@ -1984,76 +1984,52 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
   }
 }
 
-// k_diag_cells_b in the pair layout: two cells per wavefront (lanes 0-31 cell 2w, 32-63 cell 2w+1),
-// two levels per lane, so the 3 * maxEdges column gathers (u at the edges, ke_vertex and pv_vertex
-// at the vertices) are 16-byte loads, half the load instructions.  Same expressions, same order.
-template <int ME, bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_diag_cells_p(Dims d, Ptrs p, const double* __restrict__ u,
-                                                               double apvm, int store_dv) {
-  const int cA = 2 * pair_wave();
-  if (cA >= d.nCells) return;
-  const bool hasB = cA + 1 < d.nCells;
-  const int cB = hasB ? cA + 1 : cA;
+// k_diag_vertices in the pair layout: two vertices per wavefront, two levels per lane (16-byte
+// gathers of u at the three edges); same expressions in the same order
+template <bool ODD = false>
+__global__ __launch_bounds__(EDGE_THREADS) void k_diag_vertices_p(Dims d, Ptrs p, const double* __restrict__ u,
+                                                                  int store_dv) {
+  const int vA = 2 * pair_wave();
+  if (vA >= d.nVertices) return;
+  const bool hasB = vA + 1 < d.nVertices;
+  const int vB = hasB ? vA + 1 : vA;
   const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
-  const int c = sel(h, cA, cB);
-  const int ne = sel(h, p.nEdgesOnCell[cA], p.nEdgesOnCell[cB]);
-  int ei[ME], vi[ME];
-  double sdv[ME], dcdv[ME], kite[ME];
+  const int v = sel(h, vA, vB);
+  int ei[3];
+  double sd[3], ef[3];
 #pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    const int eA = p.edgesOnCell[(size_t)cA * ME + i], eB = p.edgesOnCell[(size_t)cB * ME + i];
-    const int vA = p.verticesOnCell[(size_t)cA * ME + i], vB = p.verticesOnCell[(size_t)cB * ME + i];
-    const int kA = p.kiteForCell[(size_t)cA * ME + i], kB = p.kiteForCell[(size_t)cB * ME + i];
-    const double dvA = ld_uniform_f64(p.dvEdge + eA), dvB = ld_uniform_f64(p.dvEdge + eB);
-    const double sgA = ld_uniform_f64(p.edgesOnCell_sign + (size_t)cA * ME + i);
-    const double sgB = ld_uniform_f64(p.edgesOnCell_sign + (size_t)cB * ME + i);
-    sdv[i] = sel(h, sgA * dvA, sgB * dvB);
-    dcdv[i] = sel(h, ld_uniform_f64(p.dcEdge + eA) * dvA, ld_uniform_f64(p.dcEdge + eB) * dvB);
-    kite[i] = sel(h, ld_uniform_f64(p.kiteAreasOnVertex + 3 * vA + kA), ld_uniform_f64(p.kiteAreasOnVertex + 3 * vB + kB));
+  for (int i = 0; i < 3; ++i) {
+    const int eA = p.edgesOnVertex[3 * vA + i], eB = p.edgesOnVertex[3 * vB + i];
+    const double dcA = ld_uniform_f64(p.dcEdge + eA), dcB = ld_uniform_f64(p.dcEdge + eB);
+    sd[i] = sel(h, ld_uniform_f64(p.edgesOnVertex_sign + 3 * vA + i) * dcA,
+                ld_uniform_f64(p.edgesOnVertex_sign + 3 * vB + i) * dcB);
+    ef[i] = sel(h, dcA * ld_uniform_f64(p.dvEdge + eA), dcB * ld_uniform_f64(p.dvEdge + eB));  // ke_edge_of
     ei[i] = sel(h, eA, eB);
-    vi[i] = sel(h, vA, vB);
   }
-  const double r = sel(h, ld_uniform_f64(p.invAreaCell + cA), ld_uniform_f64(p.invAreaCell + cB));
-  d2 ue[ME], kv[ME], pvv[ME];
+  d2 uu[3];
 #pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    ue[i] = ld2(u + (size_t)ei[i] * K + 2 * lc);
-    kv[i] = ld2(p.ke_vertex + (size_t)vi[i] * K + 2 * lc);
-    pvv[i] = apvm > 0.0 ? ld2(p.pv_vertex + (size_t)vi[i] * K + 2 * lc) : d2{0.0, 0.0};
-  }
-  d2 div{0.0, 0.0}, ke{0.0, 0.0};
-  // divergence (5626-5640) and the edge part of ke (5650-5660)
+  for (int i = 0; i < 3; ++i) uu[i] = ld2(u + (size_t)ei[i] * K + 2 * lc);
+  const double iat = sel(h, ld_uniform_f64(p.invAreaTriangle + vA), ld_uniform_f64(p.invAreaTriangle + vB));
+  const double fv = sel(h, ld_uniform_f64(p.fVertex + vA), ld_uniform_f64(p.fVertex + vB));
+  d2 vort{0.0, 0.0};
 #pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    if (i < ne) {
-      div.x = div.x + sdv[i] * ue[i].x;
-      div.y = div.y + sdv[i] * ue[i].y;
-      ke.x = ke.x + 0.25 * (dcdv[i] * (ue[i].x * ue[i].x));  // ke_edge (5600)
-      ke.y = ke.y + 0.25 * (dcdv[i] * (ue[i].y * ue[i].y));
-    }
+  for (int i = 0; i < 3; ++i) {
+    vort.x = vort.x + sd[i] * uu[i].x;
+    vort.y = vort.y + sd[i] * uu[i].y;
   }
-  div.x = div.x * r;
-  div.y = div.y * r;
-  const double ke_fact = 1.0 - .375;
-  ke.x = ke_fact * (ke.x * r);
-  ke.y = ke_fact * (ke.y * r);
-  d2 pvc{0.0, 0.0};
-#pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    if (i < ne) {
-      ke.x = ke.x + (1. - ke_fact) * kite[i] * kv[i].x * r;
-      ke.y = ke.y + (1. - ke_fact) * kite[i] * kv[i].y * r;
-      pvc.x = pvc.x + kite[i] * pvv[i].x * r;
-      pvc.y = pvc.y + kite[i] * pvv[i].y * r;
-    }
-  }
+  vort.x = vort.x * iat;
+  vort.y = vort.y * iat;
+  const double r = 0.25 * iat;
+  d2 kev;
+  kev.x = (ef[0] * (uu[0].x * uu[0].x) + ef[1] * (uu[1].x * uu[1].x) + ef[2] * (uu[2].x * uu[2].x)) * r;
+  kev.y = (ef[0] * (uu[0].y * uu[0].y) + ef[1] * (uu[1].y * uu[1].y) + ef[2] * (uu[2].y * uu[2].y)) * r;
   if ((h == 0 || hasB) && 2 * l < K) {
-    const size_t o = (size_t)c * K + 2 * lc;
-    if (store_dv) pst(p.divergence + o, div, two);
-    pst(p.ke + o, ke, two);
-    if (apvm > 0.0) pst(p.pv_cell + o, pvc, two);
+    const size_t o = (size_t)v * K + 2 * lc;
+    if (store_dv) pst(p.vorticity + o, vort, two);
+    pst(p.ke_vertex + o, kev, two);
+    pst(p.pv_vertex + o, d2{fv + vort.x, fv + vort.y}, two);
   }
 }
 

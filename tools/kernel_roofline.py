@@ -64,7 +64,7 @@ VARIANT = {
     "k_diag_edges_p": {"drop_w": {"gradPVn", "gradPVt"}},
 }
 EXTRA_READS = {  # pointer arguments, not Ptrs members
-    "k_diag_vertices": {"state.u"}, "k_diag_cells_b": {"state.u"}, "k_diag_cells_p": {"state.u"},
+    "k_diag_vertices": {"state.u"}, "k_diag_cells_b": {"state.u"}, "k_diag_vertices_p": {"state.u"},
     "k_diag_edges_p": {"state.u", "state.rho_zz"}, "k_reconstruct": {"state.u"}, "k_reconstruct_b": {"state.u"},
 }
 
