@@ -142,4 +142,26 @@ struct UnpackMap {
   const int* rho;  // nullptr: rho_pp not in this exchange
 };
 
+// The same for the exchange before the large-step recovery (mpas_atm_time_integration.F:876-887:
+// rw_p, ru_p, rho_pp all halo layers, rtheta_pp layer 2), whose producers are the stage's last
+// acoustic cell phase (cells) and last damping (edges) and whose consumers are the recovery of the
+// halo cells and halo edges (k_recover_cells1 / k_recover_edges), so the exchange launches no
+// k_halo_copy.  Fields by index: cells 0 = rw_p (K+1 levels), 1 = rho_pp, 2 = rtheta_pp; edges
+// 0 = ru_p.
+// XPack: owned element i writes field fid[s] of its new column also to dst[s], s in
+// [start[i], start[i+1]).  start == nullptr: nothing to pack.
+struct XPack {
+  const int* start;
+  const int* fid;
+  double* const* dst;
+};
+// XUnpack: halo element i (i >= nSolve) has field f's received column at recv + off[f * nh + i -
+// nSolve] (-1: not in this exchange); the consumer reads it there and writes it into the field.
+// recv == nullptr: the fields hold the values.
+struct XUnpack {
+  const double* recv;
+  const int* off;
+  int nh;
+};
+
 }  // namespace mpas

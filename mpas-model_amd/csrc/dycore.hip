@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <set>
 #include <string>
@@ -99,6 +100,12 @@ struct XPlan {
   bool fused_unpack = false;
   std::vector<UnpackMap> unpack;    // per block
   std::vector<void*> pack_mem;      // device allocations behind `pack`
+  // the 876-887 and 642 exchanges fused into their producers and consumers (XPack / XUnpack,
+  // dycore.h): then
+  // fused_pack and fused_unpack are set too and these hold the per-block maps
+  int fused_rec = 0;  // 1: the 876-887 exchange, 2: the tend_u exchange (642)
+  std::vector<XPack> rpk_cell, rpk_edge;
+  std::vector<XUnpack> rup_cell, rup_edge;
 };
 
 // One field of an exchange point: mpas_dmpar_exch_halo_field(field[, haloLayers]).
@@ -133,6 +140,7 @@ struct mpas_dyc_ctx {
   ncclComm_t comm = nullptr;
   bool rccl_local = false;              // route block-to-block copies of this process through RCCL too
   bool fused_pack_enabled = true;       // MPAS_DYCORE_FUSED_PACK=0: pack kernel instead (A/B)
+  bool plain_exchange = false;          // mpas_dyc_halo_exchange: no fused pack / unpack
   bool lbc = false;                     // config_apply_lbcs (mpas_dyc_set_lbc)
   bool planning = false;                // dry run: build exchange plans, launch nothing
   std::set<std::string> planned;        // layouts whose exchange plans exist (plan_all)
@@ -467,7 +475,7 @@ bool needs_exchange(const mpas_dyc_ctx* ctx) { return ctx->blk.size() > 1 || ctx
 // An exchange plan holds the fields' buffers, so its key names them: the time level and, per field,
 // which of the buffers that the step's rotations move it is (buffer index of block 0)
 std::string plan_key(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
-  std::string k = std::to_string(ctx->cur);
+  std::string k = std::to_string(ctx->cur) + (ctx->plain_exchange ? "plain" : "");
   for (const auto& f : fs) {
     k += "|" + std::string(f.pool) + "." + f.name + "." + std::to_string(f.tl) + "." + std::to_string(f.layers);
     Field* F = ctx->blk.empty() ? nullptr : find(ctx->blk[0], f.pool, f.name);
@@ -529,12 +537,37 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   std::vector<int64_t> pre_off, post_off;  // buffer offsets, patched once the buffers exist (-1: direct)
   int64_t stotal = 0, rtotal = 0;
   // the fused pack applies to the per-sub-step exchange (diag rtheta_pp [+ rho_pp], halo layer 1)
-  bool fusable = !fs.empty() && fs.size() <= 2;
+  bool fusable = !fs.empty() && fs.size() <= 2 && !ctx->plain_exchange;
   for (const auto& f : fs)
     fusable = fusable && std::string(f.pool) == "diag" && f.layers == 0x1u &&
               (std::string(f.name) == "rtheta_pp" || std::string(f.name) == "rho_pp");
   struct PackSeg { int block, is_rho; const XList* sx; size_t seg; };
   std::vector<PackSeg> pack_segs, unpack_segs;
+  // the 876-887 exchange (rw_p, ru_p, rho_pp all layers, rtheta_pp layer 2) is fused into the stage's
+  // last cell phase and damping (pack) and the halo recovery (unpack): XPack / XUnpack, dycore.h
+  std::function<int(const XField&)> rec_fid = [](const XField& f) -> int {
+    const std::string n(f.name);
+    if (std::string(f.pool) != "diag") return -1;
+    if (n == "rw_p" && f.layers == ALL_LAYERS) return 0;
+    if (n == "rho_pp" && f.layers == ALL_LAYERS) return 1;
+    if (n == "rtheta_pp" && f.layers == 0x2u) return 2;
+    if (n == "ru_p" && f.layers == ALL_LAYERS) return 0;  // the edge field
+    return -1;
+  };
+  // 1: the 876-887 exchange; 2: the tend_u exchange (642), packed by the stage's final tend_u kernel
+  // (k_dyn_edges_p with finalize, k_dyn_edges_rk1b_b) and unpacked by k_smlstep_pert_b
+  int fkind = 0;
+  if (!ctx->plain_exchange && fs.size() == 4) {
+    fkind = 1;
+    for (const auto& f : fs) fkind = rec_fid(f) >= 0 ? fkind : 0;
+  } else if (!ctx->plain_exchange && fs.size() == 1 && std::string(fs[0].pool) == "tend" &&
+             std::string(fs[0].name) == "u" && fs[0].layers == 0x1u) {
+    fkind = 2;
+  }
+  if (fkind == 2) rec_fid = [](const XField&) -> int { return 0; };
+  bool recfuse = fkind != 0;
+  struct RecSeg { int block, fid; Loc loc; const XList* x; size_t seg; };
+  std::vector<RecSeg> rec_pack, rec_unpack;
   auto field_of = [&](Block& b, const XField& f) -> Field* {
     Field* F = find(b, f.pool, f.name);
     if (!F || F->is_int || F->loc == L_NONE) {
@@ -584,11 +617,13 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
               sg.didx = rx->d_idx;
               pre_off.push_back(-1);
               fusable = false;  // a direct copy would reach the peer's halo before its cell phase reads it
+              recfuse = false;
             } else {
               sg.didx = nullptr;
               pre_off.push_back(stotal);
               stotal += (int64_t)sx->n * sub_inner;
               if (fusable) pack_segs.push_back(PackSeg{bi, std::string(f.name) == "rho_pp" ? 1 : 0, sx, pre.size()});
+              if (recfuse) rec_pack.push_back(RecSeg{bi, rec_fid(f), F->loc, sx, pre.size()});
             }
             pre.push_back(sg);
           }
@@ -627,6 +662,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
             sg.n = rx->n;
             sg.inner = (int)sub_inner;
             if (fusable) unpack_segs.push_back(PackSeg{bi, std::string(f.name) == "rho_pp" ? 1 : 0, rx, post.size()});
+            if (recfuse) rec_unpack.push_back(RecSeg{bi, rec_fid(f), F->loc, rx, post.size()});
             post.push_back(sg);
             post_off.push_back(rtotal);
             rtotal += (int64_t)rx->n * sub_inner;
@@ -772,6 +808,72 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
       pl.fused_unpack = true;
     }
   }
+  if (recfuse && (!rec_pack.empty() || !rec_unpack.empty()) && ctx->fused_pack_enabled) {
+    bool pair_all = true;
+    for (int bi = 0; bi < nb; ++bi) pair_all = pair_all && pair_layout(ctx->blk[bi].d);
+    if (pair_all) {
+      auto upload = [&](const void* h, size_t bytes, void** dptr) -> int {
+        HIPCHK(hipMalloc(dptr, std::max<size_t>(bytes, 4)));
+        if (bytes) HIPCHK(hipMemcpy(*dptr, h, bytes, hipMemcpyHostToDevice));
+        pl.pack_mem.push_back(*dptr);
+        return MPAS_DYC_OK;
+      };
+      pl.rpk_cell.assign(nb, XPack{});
+      pl.rpk_edge.assign(nb, XPack{});
+      pl.rup_cell.assign(nb, XUnpack{});
+      pl.rup_edge.assign(nb, XUnpack{});
+      for (int bi = 0; bi < nb; ++bi) {
+        const Dims& d = ctx->blk[bi].d;
+        for (const Loc loc : {L_CELL, L_EDGE}) {
+          const int nsolve = loc == L_CELL ? d.nCellsSolve : d.nEdgesSolve;
+          const int nh = (loc == L_CELL ? d.nCells : d.nEdges) - nsolve;
+          const int nf = loc == L_CELL ? 3 : 1;
+          // pack: per owned element, (field, send-buffer column) slots in element order
+          std::vector<std::vector<std::pair<int, double*>>> per(nsolve);
+          for (const RecSeg& rs : rec_pack) {
+            if (rs.block != bi || rs.loc != loc) continue;
+            for (int i = 0; i < rs.x->n; ++i)
+              per[rs.x->h_idx[i]].emplace_back(rs.fid, pre[rs.seg].dst + (size_t)i * pre[rs.seg].inner);
+          }
+          std::vector<int> start(nsolve + 1, 0), fid;
+          std::vector<double*> dst;
+          for (int i = 0; i < nsolve; ++i) {
+            start[i] = (int)fid.size();
+            for (const auto& sl : per[i]) {
+              fid.push_back(sl.first);
+              dst.push_back(sl.second);
+            }
+          }
+          start[nsolve] = (int)fid.size();
+          if (!fid.empty()) {
+            void *ds = nullptr, *df = nullptr, *dd = nullptr;
+            CHK(upload(start.data(), start.size() * sizeof(int), &ds));
+            CHK(upload(fid.data(), fid.size() * sizeof(int), &df));
+            CHK(upload(dst.data(), dst.size() * sizeof(double*), &dd));
+            (loc == L_CELL ? pl.rpk_cell : pl.rpk_edge)[bi] = XPack{(const int*)ds, (const int*)df, (double* const*)dd};
+          }
+          // unpack: per field and halo element, its column in the receive buffer
+          std::vector<int> off((size_t)nf * std::max(nh, 0), -1);
+          bool any = false;
+          for (const RecSeg& rs : rec_unpack) {
+            if (rs.block != bi || rs.loc != loc) continue;
+            for (int i = 0; i < rs.x->n; ++i) {
+              off[(size_t)rs.fid * nh + (rs.x->h_idx[i] - nsolve)] =
+                  (int)((post[rs.seg].src - pl.recvbuf) + (int64_t)i * post[rs.seg].inner);
+              any = true;
+            }
+          }
+          if (any) {
+            void* doff = nullptr;
+            CHK(upload(off.data(), off.size() * sizeof(int), &doff));
+            (loc == L_CELL ? pl.rup_cell : pl.rup_edge)[bi] = XUnpack{pl.recvbuf, (const int*)doff, nh};
+          }
+        }
+      }
+      pl.fused_rec = fkind;
+      pl.fused_pack = pl.fused_unpack = true;
+    }
+  }
   if (pl.npre) {
     HIPCHK(hipMalloc(&pl.d_pre, pre.size() * sizeof(XSeg)));
     HIPCHK(hipMemcpy(pl.d_pre, pre.data(), pre.size() * sizeof(XSeg), hipMemcpyHostToDevice));
@@ -825,6 +927,15 @@ const XPlan* fused_pack_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   if (ctx->planning || !needs_exchange(ctx)) return nullptr;
   auto it = ctx->plans.find(plan_key(ctx, fs));
   if (it == ctx->plans.end() || !it->second.fused_pack || it->second.pack.size() != ctx->blk.size()) return nullptr;
+  return &it->second;
+}
+
+// The plan of the 876-887 or 642 exchange when its pack and unpack are fused (XPlan::fused_rec), or
+// nullptr
+const XPlan* fused_rec_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
+  if (ctx->planning || !needs_exchange(ctx)) return nullptr;
+  auto it = ctx->plans.find(plan_key(ctx, fs));
+  if (it == ctx->plans.end() || !it->second.fused_rec || it->second.rpk_cell.size() != ctx->blk.size()) return nullptr;
   return &it->second;
 }
 
@@ -1071,8 +1182,9 @@ void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts)
 // diagnostics (1234-1249) or at the substep boundary (1282-1297) delivers; 2 = the rest
 // hdiv_done: the previous stage's w recovery computed h_divergence (recover_cells3 with hdiv), so
 // at rk_step 2 / 3, where k_dyn_cells1 computes nothing else, it is not launched
+// tp: the block's pack map of the tend_u exchange that follows (642, XPlan::fused_rec), or none
 void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, double dt, int part = 0,
-              bool hdiv_done = false, bool last = true) {
+              bool hdiv_done = false, bool last = true, XPack tp = XPack{}) {
   const Config& cf = ctx->cf;
   DynTendScal s{};
   s.rk_step = rk_step;
@@ -1102,9 +1214,9 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     const int64_t nw = (d.nEdges + 1) / 2;
     if (rk_step == 1) LAUNCH_PE((k_dyn_edges_pgf_p<false>), (k_dyn_edges_pgf_p<true>), nw, d, p);
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH_PE((k_dyn_edges_p<true, 10, true, false>), (k_dyn_edges_p<true, 10, true, true>), nw, d, p, cf, s, 0);
-    if (d.maxEdges == 6 && rk_step != 1) LAUNCH_PE((k_dyn_edges_p<false, 10, false, false>), (k_dyn_edges_p<false, 10, false, true>), nw, d, p, cf, s, 1);
+    if (d.maxEdges == 6 && rk_step != 1) LAUNCH_PE((k_dyn_edges_p<false, 10, false, false>), (k_dyn_edges_p<false, 10, false, true>), nw, d, p, cf, s, 1, tp);
     if (d.maxEdges == 7 && rk_step == 1) LAUNCH_PE((k_dyn_edges_p<true, 12, true, false>), (k_dyn_edges_p<true, 12, true, true>), nw, d, p, cf, s, 0);
-    if (d.maxEdges == 7 && rk_step != 1) LAUNCH_PE((k_dyn_edges_p<false, 12, false, false>), (k_dyn_edges_p<false, 12, false, true>), nw, d, p, cf, s, 1);
+    if (d.maxEdges == 7 && rk_step != 1) LAUNCH_PE((k_dyn_edges_p<false, 12, false, false>), (k_dyn_edges_p<false, 12, false, true>), nw, d, p, cf, s, 1, tp);
   } else if (batched(d)) {
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH_E((k_dyn_edges_b<true, 10>), d.nEdges, d, p, cf, s, 0);
     if (d.maxEdges == 6 && rk_step != 1) LAUNCH_E((k_dyn_edges_b<false, 10>), d.nEdges, d, p, cf, s, 1);
@@ -1124,7 +1236,7 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
         if (m6) LAUNCH(k_dyn_delsq_vc_b<6>, d.nVertices + d.nCells, d, p);
         else LAUNCH(k_dyn_delsq_vc_b<7>, d.nVertices + d.nCells, d, p);
       }
-      LAUNCH(k_dyn_edges_rk1b_b, d.nEdgesSolve, d, p, cf, s);
+      LAUNCH(k_dyn_edges_rk1b_b, d.nEdgesSolve, d, p, cf, s, tp);
       if (m6) LAUNCH(k_dyn_cells2_b<6>, d.nCells, d, p);
       else LAUNCH(k_dyn_cells2_b<7>, d.nCells, d, p);
     }
@@ -1149,15 +1261,16 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   LAUNCH(k_dyn_cells3, d.nCellsSolve, d, p, cf, s);
 }
 
-void smlstep_pert(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int phase) {
+// tu_up: the block's fused-unpack map of the tend_u exchange (642), used by phase 2, or none
+void smlstep_pert(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int phase, XUnpack tu_up = XUnpack{}) {
   if (fuse_smlstep(d)) {  // k_dyn_cells3_r did the cells without a halo edge
     if (phase == 1) return;
     phase = 2;
   }
   const int64_t nb = phase == 2 ? d.n_bnd_cells : d.nCellsSolve;  // phase 2: the bnd_cells list
   if (!batched(d)) LAUNCH(k_smlstep_pert, d.nCellsSolve, d, p, phase);
-  else if (d.maxEdges == 6) LAUNCH(k_smlstep_pert_b<6>, nb, d, p, phase);
-  else LAUNCH(k_smlstep_pert_b<7>, nb, d, p, phase);
+  else if (d.maxEdges == 6) LAUNCH(k_smlstep_pert_b<6>, nb, d, p, phase, tu_up);
+  else LAUNCH(k_smlstep_pert_b<7>, nb, d, p, phase, tu_up);
 }
 
 // hdiv = 1: the batched kernel also computes the next stage's h_divergence (k_recover_cells3_b)
@@ -1205,20 +1318,21 @@ bool fused_recover(const Dims& d) { return batched(d) && (d.maxEdges == 6 || d.m
 // keep_pp = 0: a fin launch need not store rho_pp / rw_p (see k_acoustic_cells_r)
 // pk: the block's fused-pack map of the exchange that follows (fused_pack_map), or none
 // dl: store rtheta_pp - rtheta_pp_old for the stage's last damping only (damping_delta)
+// rp (fin only): the block's pack map of the 876-887 exchange that follows the stage (XPlan::fused_rec)
 void acoustic_cells(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int fin = 0,
                     double rdt = 0.0, double invNs = 0.0, int rk_step = 0, int keep_pp = 1, PackMap pk = PackMap{},
-                    int dl = 0) {
+                    int dl = 0, XPack rp = XPack{}) {
   if (batched(d) && d.maxEdges == 6) {
     if (fin)
       LAUNCH((k_acoustic_cells_r<6, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
-             pk, dl);
+             pk, dl, rp);
     else LAUNCH((k_acoustic_cells_r<6, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, pk);
     return;
   }
   if (batched(d) && d.maxEdges == 7) {
     if (fin)
       LAUNCH((k_acoustic_cells_r<7, true>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, rdt, invNs, rk_step, keep_pp,
-             pk, dl);
+             pk, dl, rp);
     else LAUNCH((k_acoustic_cells_r<7, false>), d.nCells, d, p, dts, small_step, ctx->cf.epssm, 0.0, 0.0, 0, 1, pk);
     return;
   }
@@ -1241,18 +1355,19 @@ bool fused_recover_edges(const Dims& d) { return pair_layout(d) && fused_recover
 // fresh = 1: the stage had a single sub-step (no edge phase launched), see k_divdamp_p;
 // invNs > 0: recover the edges with two owned cells too (fused_recover_edges)
 // dl: rtheta_pp_old holds the difference (acoustic_cells with dl); pair layout only
+// rp: the block's pack map of the 876-887 exchange (XPlan::fused_rec), or none
 void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase, int fresh = 0,
-                        double invNs = 0.0, UnpackMap um = UnpackMap{}, int dl = 0) {
+                        double invNs = 0.0, UnpackMap um = UnpackMap{}, int dl = 0, XPack rp = XPack{}) {
   // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
   const bool up = um.recv != nullptr;
   const int64_t nw = ((phase == 2 ? d.n_bnd_pairs : d.nEdges) + 1) / 2;  // phase 2: the bnd_pairs list
   const double cd = coef_divdamp(ctx, dts);
   if (pair_layout(d) && invNs > 0.0 && fused_recover_edges(d)) {
-    if (up) LAUNCH_PE((k_divdamp_p<true, true, false>), (k_divdamp_p<true, true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl);
-    else LAUNCH_PE((k_divdamp_p<true, false, false>), (k_divdamp_p<true, false, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl);
+    if (up) LAUNCH_PE((k_divdamp_p<true, true, false>), (k_divdamp_p<true, true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl, rp);
+    else LAUNCH_PE((k_divdamp_p<true, false, false>), (k_divdamp_p<true, false, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl, rp);
   } else if (pair_layout(d)) {
-    if (up) LAUNCH_PE((k_divdamp_p<false, true, false>), (k_divdamp_p<false, true, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl);
-    else LAUNCH_PE((k_divdamp_p<false, false, false>), (k_divdamp_p<false, false, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl);
+    if (up) LAUNCH_PE((k_divdamp_p<false, true, false>), (k_divdamp_p<false, true, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl, rp);
+    else LAUNCH_PE((k_divdamp_p<false, false, false>), (k_divdamp_p<false, false, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl, rp);
   }
   else LAUNCH(k_divdamp<DIVDAMP_EPW>, (d.nEdges + DIVDAMP_EPW - 1) / DIVDAMP_EPW, d, p, coef_divdamp(ctx, dts), phase,
               dts, fresh);
@@ -1559,23 +1674,29 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       // the first stage reads time level 2 and the saved fields through stage_pre until its recovery
       const std::vector<Ptrs>& PS = rk_step == 1 ? Ppre : P;
       const std::vector<Ptrs>& PF = rk_step == 1 ? Pfin : P;  // the stage's last cell phase
+      // the tend_u exchange (642) packed by the final tend_u kernel and unpacked by smlstep_pert
+      // (XPlan::fused_rec), or nullptr
+      const std::vector<XField> xtu = {{"tend", "u", 0, 0x1u}};
+      const XPlan* xt = fused_rec_plan(ctx, xtu);
+      auto tpk = [&](size_t ib) { return xt ? xt->rpk_edge[ib] : XPack{}; };
+      auto tup = [&](size_t ib) { return xt ? xt->rup_edge[ib] : XUnpack{}; };
       if (pending) {  // 561-630, k_dyn_cells1 overlapping the exchange
         EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 1, hdiv_prev && batched(d)));
         CHK(xwait());
         pending = false;
-        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 2, false, last_stage));
+        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 2, false, last_stage, tpk(ib_)));
       } else {
-        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 0, hdiv_prev && batched(d), last_stage));  // 561-630
+        EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 0, hdiv_prev && batched(d), last_stage, tpk(ib_)));  // 561-630
       }
       const double dts = rk_sub_timestep[rk_step - 1];
       if (split) {  // 642 | 644-678: interior cells overlap the tend_u exchange
-        CHK(exchange_async(ctx, {{"tend", "u", 0, 0x1u}}));
+        CHK(exchange_async(ctx, xtu));
         EACHV(PS, smlstep_pert(ctx, d, p, 1));
         CHK(exchange_wait(ctx));
-        EACHV(PS, smlstep_pert(ctx, d, p, 2));
+        EACHV(PS, smlstep_pert(ctx, d, p, 2, tup(ib_)));
       } else {
-        CHK(exchange(ctx, {{"tend", "u", 0, 0x1u}}));             // 642
-        EACHV(PS, smlstep_pert(ctx, d, p, 0));     // 644-678
+        CHK(exchange(ctx, xtu));                                  // 642
+        EACHV(PS, smlstep_pert(ctx, d, p, 0, tup(ib_)));          // 644-678
       }
       if (lbc) {  // 683-778: specified-zone tendencies, then the relaxation zone toward the driving state
         const double tds = dt_dynamics * (double)(dynamics_substep - 1) + rk_timestep[rk_step - 1];
@@ -1601,6 +1722,15 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       //   edge phase of sub-step 2 or, for a one-sub-step stage, the damping, which also stores
       //   ruAvg (on the same edges, so the 876 exchange and the recovery see the same values).
       const int nsub = number_sub_steps[rk_step - 1];
+      const std::vector<XField> xrec = {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},  // 876-887
+                                        {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};
+      // the 876-887 exchange packed by the stage's last cell phase and damping and unpacked by the
+      // halo recovery (XPlan::fused_rec), or nullptr
+      const XPlan* xr = fused_rec_plan(ctx, xrec);
+      auto rpc = [&](size_t ib) { return xr ? xr->rpk_cell[ib] : XPack{}; };
+      auto rpe = [&](size_t ib) { return xr ? xr->rpk_edge[ib] : XPack{}; };
+      auto ruc = [&](size_t ib) { return xr ? xr->rup_cell[ib] : XUnpack{}; };
+      auto rue = [&](size_t ib) { return xr ? xr->rup_edge[ib] : XUnpack{}; };
       // the last Theta''/rho'' exchange whose unpack its consumer does (XPlan::fused_unpack): the
       // next edge phase, or the stage's last damping
       const XPlan* unpack_xp = nullptr;
@@ -1622,7 +1752,8 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         EACHV(small_step == nsub ? PF : PS,
               acoustic_cells(ctx, d, p, dts, small_step, small_step == nsub, rk_timestep[rk_step - 1],
                             1 / (double)nsub, rk_step, needs_exchange(ctx) || last_stage,
-                            xp ? xp->pack[ib_] : PackMap{}, damping_delta(ctx, d, last_stage)));
+                            xp ? xp->pack[ib_] : PackMap{}, damping_delta(ctx, d, last_stage),
+                            small_step == nsub ? rpc(ib_) : XPack{}));
         if (split) {
           CHK(exchange_async(ctx, xf));
         } else {
@@ -1631,15 +1762,13 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         if (xp && xp->fused_unpack) unpack_xp = xp;
       }
       if (split) {  // the last sub-step's damping (849-869), interior edges overlapping the exchange
-        EACH(divergence_damping(ctx, d, p, dts, 1, nsub == 1, 1 / (double)nsub));
+        EACH(divergence_damping(ctx, d, p, dts, 1, nsub == 1, 1 / (double)nsub, UnpackMap{}, 0, rpe(ib_)));
         CHK(exchange_wait(ctx));
-        EACH(divergence_damping(ctx, d, p, dts, 2, nsub == 1, 0.0, um_of(ib_)));
+        EACH(divergence_damping(ctx, d, p, dts, 2, nsub == 1, 0.0, um_of(ib_), 0, rpe(ib_)));
       } else {
         EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1, 1 / (double)nsub, um_of(ib_),
-                                damping_delta(ctx, d, last_stage)));
+                                damping_delta(ctx, d, last_stage), rpe(ib_)));
       }
-      const std::vector<XField> xrec = {{"diag", "rw_p", 0, ALL_LAYERS}, {"diag", "ru_p", 0, ALL_LAYERS},  // 876-887
-                                        {"diag", "rho_pp", 0, ALL_LAYERS}, {"diag", "rtheta_pp", 0, 0x2u}};
       const double invNs = 1 / (double)number_sub_steps[rk_step - 1];
       const double rdt = rk_timestep[rk_step - 1];
       if (split) {
@@ -1651,8 +1780,9 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         // edges with two owned cells: recovered by the last damping (fused_recover_edges) or here
         EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1));
         CHK(exchange_wait(ctx));
-        EACH(LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2, d.nCellsSolve));
-        EACH(LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2));  // phase 2: the bnd_edges list
+        EACH(LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2, d.nCellsSolve,
+                    ruc(ib_)));
+        EACH(LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2, rue(ib_)));  // phase 2: the bnd_edges list
         if (lbc) {  // the w recovery reads ru before the specified-zone overwrite (934-987)
           EACH(recover_cells3(ctx, d, p, 0));
           EACH(LAUNCH(k_lbc_u, d.nEdges, d, p, dt_dynamics * (double)(dynamics_substep - 1) + rk_timestep[rk_step - 1]));
@@ -1666,11 +1796,11 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         CHK((exchange)(ctx, xrec));
         // 889-930: the owned cells were recovered by the last sub-step if fused_recover
         EACH(if (fused_recover(d)) LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2,
-                                          d.nCellsSolve);
-             else LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0, 0));
+                                          d.nCellsSolve, ruc(ib_));
+             else LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0, 0, ruc(ib_)));
         // the edges with two owned cells were recovered by the last damping if fused_recover_edges
-        EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0);
-             else LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2));
+        EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0, rue(ib_));
+             else LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2, rue(ib_)));
         // stages 1 and 2: also the next stage's h_divergence (dyn_tend then skips k_dyn_cells1)
         EACH(recover_cells3(ctx, d, p, 0, hdiv_next));
         if (lbc)  // 934-987
@@ -2313,7 +2443,10 @@ int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name
   if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   std::string sp(pool), sn(name);
+  // a plain exchange: its own plan (key suffix), never one whose pack / unpack a kernel of the step does
+  ctx->plain_exchange = true;
   int r = exchange(ctx, {{sp.c_str(), sn.c_str(), time_level, (unsigned)layer_mask}});
+  ctx->plain_exchange = false;
   if (r) return r;
   HIPCHK(hipGetLastError());
   return MPAS_DYC_OK;

@@ -280,6 +280,11 @@ __device__ __forceinline__ CellSten<ME> load_sten(const Ptrs& p, int c) {
   return s;
 }
 
+// receive-buffer offset of field f of element i in a fused unpack (XUnpack), -1: not received
+__device__ __forceinline__ int rec_off(const XUnpack& u, int f, int i, int nsolve) {
+  return (u.recv && i >= nsolve && i - nsolve < u.nh) ? u.off[(size_t)f * u.nh + (i - nsolve)] : -1;
+}
+
 // ============================================================================
 // atm_compute_moist_coefficients  (mpas_atm_time_integration.F:1899-1931)
 // ============================================================================
@@ -917,7 +922,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_delsq_vc_b(Dims d, Ptrs p
   }
 }
 
-__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_rk1b_b(Dims d, Ptrs p, Config cf, DynTendScal s) {
+// tp: the final tend_u also goes to the 642 exchange's send buffer (XPack), or nothing
+__global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_rk1b_b(Dims d, Ptrs p, Config cf, DynTendScal s,
+                                                                    XPack tp = XPack{}) {
   const int e = wave_elem(0);
   if (e >= d.nEdgesSolve) return;
   const int k = lane_id(), K = d.K;
@@ -986,7 +993,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_edges_rk1b_b(Dims d, Ptrs
     const double coef = (double)(k + 1 - (K - cf.number_rayleigh_damp_u_levels)) * s.rayleigh_coef_inverse;
     tu = tu - re * uk * coef;
   }
-  p.tend_u[o] = tu + tue + PHYS(p.tend_ru_physics, o);
+  const double tuf = tu + tue + PHYS(p.tend_ru_physics, o);
+  p.tend_u[o] = tuf;
+  if (tp.start) {
+    const int s0 = __builtin_amdgcn_readfirstlane(tp.start[e]), s1 = __builtin_amdgcn_readfirstlane(tp.start[e + 1]);
+    for (int sl = s0; sl < s1; ++sl) tp.dst[sl][k] = tuf;
+  }
 }
 
 template <int ME>
@@ -1544,27 +1556,38 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert(Dims d, Ptrs p, 
 }
 
 template <int ME>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert_b(Dims d, Ptrs p, int phase) {
+// tu_up: the 642 exchange's fused unpack (XUnpack, edge field tend_u): the cell's halo edges read
+// their received tend_u from the receive buffer and write it into tend_u for the later readers (every
+// reader of a halo edge's tend_u reads an edge of an owned cell, and such an edge has exactly one)
+__global__ __launch_bounds__(BLOCK_THREADS) void k_smlstep_pert_b(Dims d, Ptrs p, int phase,
+                                                                  XUnpack tu_up = XUnpack{}) {
   int c = wave_elem(0);
   if (phase == 2) {  // the compact bnd_cells list (owned cells with CELL_HALO_EDGE)
     if (c >= d.n_bnd_cells) return;
     c = __builtin_amdgcn_readfirstlane(p.bnd_cells[c]);
   }
   if (c >= d.nCellsSolve) return;
-  if (p.bdyMaskCell[c] > N_RELAX_ZONE) return;  // no conversion in the specified zone (2292; any run)
   const int k = lane_id(), K = d.K;
   const bool act = k < K;
   const int kc = min(k, K - 1), kw = min(k, K);
   const size_t K1 = K + 1;
-  const int bnd = phase ? p.cell_bnd[c] : 0;
   const CellSten<ME> st = load_sten<ME>(p, c);
+  int uoff[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    uoff[i] = rec_off(tu_up, 0, uni(st.e[i]), d.nEdgesSolve);
+    if (uoff[i] >= 0 && act) p.tend_u[(size_t)uni(st.e[i]) * K + k] = tu_up.recv[uoff[i] + k];
+  }
+  if (p.bdyMaskCell[c] > N_RELAX_ZONE) return;  // no conversion in the specified zone (2292; any run)
+  const int bnd = phase ? p.cell_bnd[c] : 0;
   double wt = p.tend_w[(size_t)c * K1 + kw];
   const double zz = p.zz[(size_t)c * K + kc];
   const double fzm = p.fzm[kc], fzp = p.fzp[kc];
   if (phase && (((bnd & CELL_HALO_EDGE) != 0) != (phase == 2))) return;
   double ut[ME];
 #pragma unroll
-  for (int i = 0; i < ME; ++i) ut[i] = p.tend_u[(size_t)uni(st.e[i]) * K + kc];
+  for (int i = 0; i < ME; ++i)
+    ut[i] = uoff[i] >= 0 ? tu_up.recv[uoff[i] + kc] : p.tend_u[(size_t)uni(st.e[i]) * K + kc];
   // zb_cell + sign(1,ut) * zb3_cell, loaded as the one of zb_p / zb_m the sign selects (k_build_zb)
   double zs[ME];
 #pragma unroll
@@ -1709,12 +1732,30 @@ __device__ __forceinline__ d2 kp1(d2 v) {  // levels (k+1)
   return d2{v.y, lane_shl1(v.x)};
 }
 
+// an edge field of the wavefront's two edges (pair layout) into their slots of a fused exchange's
+// send buffer (XPack over owned edges: the damped ru_p of 876-887, the final tend_u of 642); st: this
+// lane stores its edge's levels
+__device__ __forceinline__ void pack_rec_edge(const XPack& pk, const Dims& d, int eA, int eB, bool hasB, int h,
+                                              int lc, bool st, bool two, d2 v) {
+  if (!pk.start) return;
+  for (int half = 0; half < (hasB ? 2 : 1); ++half) {
+    const int e = half ? eB : eA;
+    if (e >= d.nEdgesSolve) continue;
+    const int s0 = __builtin_amdgcn_readfirstlane(pk.start[e]), s1 = __builtin_amdgcn_readfirstlane(pk.start[e + 1]);
+    for (int s = s0; s < s1; ++s) {
+      double* dst = pk.dst[s];
+      if (h == half && st) pst(dst + 2 * lc, v, two);
+    }
+  }
+}
+
 // k_dyn_edges_b in the pair layout (NE2 = 2*maxEdges-2 TRiSK neighbours).  SPLIT (rk1 only): this
 // launch computes tend_u alone and k_dyn_edges_pgf_p the PGF part of tend_u_euler and del2 --
 // at rk1 the two are independent (no finalize), and together they need 244 VGPRs (2 waves/SIMD).
+// tp: with finalize, the final tend_u also goes to the 642 exchange's send buffer (XPack), or nothing
 template <bool RK1, int NE2, bool SPLIT = false, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Config cf, DynTendScal s,
-                                                              int finalize) {
+                                                              int finalize, XPack tp = XPack{}) {
   constexpr bool PGF = RK1 && !SPLIT;
   const int eA = 2 * pair_wave();
   if (eA >= d.nEdges) return;
@@ -1861,6 +1902,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
     tu.y = tu.y + tue.y + tph.y;
   }
   if (solve) store(p.tend_u, tu);
+  if (finalize) pack_rec_edge(tp, d, eA, eB, hasB, h, lc, solve && stx, ODD ? sty : true, tu);
   if (PGF) del2(tue, dv1, dv2, vo1, vo2, kd1, kd2, invDv, msd2);
 }
 
@@ -2143,10 +2185,11 @@ __device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMa
 }
 
 // dl = 1: rtheta_pp_old holds rtheta_pp - rtheta_pp_old (k_acoustic_cells_r<ME, true> with dl)
+// rp: the stage's last damping also packs ru_p of the 876-887 exchange (XPack), or nothing
 template <bool REC = false, bool UP = false, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
                                                             int fresh, double invNs = 0.0, UnpackMap um = UnpackMap{},
-                                                            int dl = 0) {
+                                                            int dl = 0, XPack rp = XPack{}) {
   int eA, eB;
   bool hasB;
   if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
@@ -2188,6 +2231,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   d2 out;
   out.x = ru.x + coef_divdamp * (-(dd2.x) - -(dd1.x)) * (1.0 - mask) / (t1.x + t2.x);
   out.y = ru.y + coef_divdamp * (-(dd2.y) - -(dd1.y)) * (1.0 - mask) / (t1.y + t2.y);
+  pack_rec_edge(rp, d, eA, eB, hasB, h, lc, (h ? onB : onA) && 2 * l < K, two, out);
   if (!REC) {
     if ((h ? onB : onA) && 2 * l < K) {
       pst(p.ru_p + o, out, two);
@@ -2635,11 +2679,30 @@ __device__ __forceinline__ void pack_column(const PackMap& pk, int c, int k, boo
   }
 }
 
+// the column's new rw_p / rho_pp / rtheta_pp into its slots of the 876-887 exchange's send buffer
+// (XPack, fields 0 / 1 / 2), lane k = level k (rw_p: levels 0..K)
+__device__ __forceinline__ void pack_rec_cell(const XPack& pk, int c, int k, bool act, bool actw, double rw,
+                                              double rho, double rt) {
+  if (!pk.start) return;
+  const int s0 = __builtin_amdgcn_readfirstlane(pk.start[c]), s1 = __builtin_amdgcn_readfirstlane(pk.start[c + 1]);
+  for (int s = s0; s < s1; ++s) {
+    const int f = __builtin_amdgcn_readfirstlane(pk.fid[s]);
+    double* dst = pk.dst[s];
+    if (f == 0) {
+      if (actw) dst[k] = rw;
+    } else if (act) {
+      dst[k] = f == 1 ? rho : rt;
+    }
+  }
+}
+
+// rp: the stage's last sub-step (FIN) also packs the 876-887 exchange (XPack), or nothing
 template <int ME, bool FIN = false>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs p, double dts, int small_step,
                                                                     double epssm, double rdt = 0.0,
                                                                     double invNs = 0.0, int rk_step = 0,
-                                                                    int keep_pp = 1, PackMap pk = PackMap{}, int dl = 0) {
+                                                                    int keep_pp = 1, PackMap pk = PackMap{}, int dl = 0,
+                                                                    XPack rp = XPack{}) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
   const int k = lane_id(), K = d.K;
@@ -2743,6 +2806,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;  // levels 2..K: recover_cell_fused
     }
     pack_column(pk, c, k, act, rt_new, rho_new);
+    if (FIN) pack_rec_cell(rp, c, k, act, actw, rwp, rho_new, rt_new);
     if (FIN) ri = load_rec_in(d, p, o, rk_step);
     if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rho_new, rt_new, rwp, wwa, rdt, invNs, rk_step);
   } else {
@@ -2766,6 +2830,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
       else if (k == 0 || k == K) p.wwAvg[ow] = wwa;
     }
     pack_column(pk, c, k, act, rtpp, rhopp);
+    if (FIN) pack_rec_cell(rp, c, k, act, actw, rwp, rhopp, rtpp);
     if (FIN) ri = load_rec_in(d, p, o, rk_step);
     if (FIN) recover_cell_fused(d, p, c, k, zz, rws, fzm, fzp, ri, rhopp, rtpp, rwp, wwa, rdt, invNs, rk_step);
   }
@@ -2913,8 +2978,10 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_divdamp(Dims d, Ptrs p, doubl
 // two owned cells; owned cells whose edges all have two owned cells) and phase 2 the rest.
 // ============================================================================
 // cells (all, and the garbage slot): 2998-3040
+// ru: the 876-887 exchange's fused unpack (XUnpack, cell fields rw_p / rho_pp / rtheta_pp): a halo
+// cell reads its received columns from the receive buffer and writes them into the fields
 __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p, double dt, double invNs, int rk_step,
-                                                                  int phase, int c0) {
+                                                                  int phase, int c0, XUnpack ru = XUnpack{}) {
   const int c = wave_elem(c0);
   if (phase && ((c >= d.nCellsSolve) != (phase == 2))) return;
   const int k = lane_id(), K = d.K;
@@ -2926,10 +2993,15 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p
   if (c > d.nCells) return;
   const bool act = k < K;
   const size_t o = (size_t)c * K + k, ow = (size_t)c * K1 + k;
+  const int orw = rec_off(ru, 0, c, d.nCellsSolve), orho = rec_off(ru, 1, c, d.nCellsSolve),
+            ort = rec_off(ru, 2, c, d.nCellsSolve);
+  if (orw >= 0 && k <= K) p.rw_p[ow] = ru.recv[orw + k];
+  if (orho >= 0 && act) p.rho_pp[o] = ru.recv[orho + k];
+  if (ort >= 0 && act) p.rtheta_pp[o] = ru.recv[ort + k];
   const double rcv = RGAS / (CP - RGAS);
   double rz = 0.0;
   if (act) {
-    const double rho_p = p.rho_p_save[o] + p.rho_pp[o];
+    const double rho_p = p.rho_p_save[o] + (orho >= 0 ? ru.recv[orho + k] : p.rho_pp[o]);
     if (rk_step == 3) p.rho_p[o] = rho_p;  // stored at stage 3 only (recover_cell_fused)
     rz = rho_p + p.rho_base[o];
     p.rho_zz2[o] = rz;
@@ -2939,21 +3011,22 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p
   double w = 0.0;  // w(1) = w(nVertLevels+1) = 0
   if (act && k >= 1) {
     p.wwAvg[ow] = p.rw_save[ow] + (p.wwAvg[ow] * invNs);
-    const double rw = p.rw_save[ow] + p.rw_p[ow];
+    const double rw = p.rw_save[ow] + (orw >= 0 ? ru.recv[orw + k] : p.rw_p[ow]);
     p.rw[ow] = rw;
     w = rw / (fzm * zz + fzp * zzm);  // divided by density in k_recover_cells3
   }
   if (k <= K) p.w2[ow] = w;
   if (act) {
     if (rk_step == 3) {
-      const double rtp = p.rtheta_p_save[o] + p.rtheta_pp[o] - dt * rz * (d.diabatic ? p.rt_diabatic_tend[o] : 0.0);
+      const double rtpp = ort >= 0 ? ru.recv[ort + k] : p.rtheta_pp[o];
+      const double rtp = p.rtheta_p_save[o] + rtpp - dt * rz * (d.diabatic ? p.rt_diabatic_tend[o] : 0.0);
       p.rtheta_p[o] = rtp;
       p.theta_m2[o] = (rtp + p.rtheta_base[o]) / rz;
       const double ex = pow(zz * (RGAS / P0) * (rtp + p.rtheta_base[o]), rcv);
       p.exner[o] = ex;
       p.pressure_p[o] = zz * RGAS * (ex * rtp + p.rtheta_base[o] * (ex - p.exner_base[o]));
     } else {
-      const double rtp = p.rtheta_p_save[o] + p.rtheta_pp[o];
+      const double rtp = p.rtheta_p_save[o] + (ort >= 0 ? ru.recv[ort + k] : p.rtheta_pp[o]);
       p.rtheta_p[o] = rtp;
       p.theta_m2[o] = (rtp + p.rtheta_base[o]) / rz;
     }
@@ -2962,7 +3035,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p
 
 // edges (all): 3048-3059
 // phase 2 walks the compact bnd_edges list (the edges with edge_bnd set)
-__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs, int phase) {
+// ru: the 876-887 exchange's fused unpack (XUnpack, edge field ru_p), as in k_recover_cells1
+__global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs, int phase,
+                                                                 XUnpack ru = XUnpack{}) {
   int e = wave_elem(0);
   if (phase == 2) {
     if (e >= d.n_bnd_edges) return;
@@ -2974,10 +3049,18 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p,
   if (k >= K) return;
   const size_t o = (size_t)e * K + k;
   const int c1 = p.cellsOnEdge[2 * e], c2 = p.cellsOnEdge[2 * e + 1];
+  const int oru = rec_off(ru, 0, e, d.nEdgesSolve);
+  double rup;
+  if (oru >= 0) {
+    rup = ru.recv[oru + k];
+    p.ru_p[o] = rup;
+  } else {
+    rup = p.ru_p[o];
+  }
   p.ruAvg[o] = p.ru_save[o] + (p.ruAvg[o] * invNs);
-  const double ru = p.ru_save[o] + p.ru_p[o];
-  p.ru[o] = ru;
-  p.u2[o] = 2. * ru / (p.rho_zz2[(size_t)c1 * K + k] + p.rho_zz2[(size_t)c2 * K + k]);
+  const double ruv = p.ru_save[o] + rup;
+  p.ru[o] = ruv;
+  p.u2[o] = 2. * ruv / (p.rho_zz2[(size_t)c1 * K + k] + p.rho_zz2[(size_t)c2 * K + k]);
 }
 
 // cells (all): w from the flux-divergence operator, then divided by density (3063-3097)

@@ -137,3 +137,36 @@ def test_fused_pack_bitwise(small_case, overlap):
     for name in one:
         assert np.array_equal(runs[0][name], runs[1][name]), f"{name}: fused pack differs from the pack kernel"
         assert np.array_equal(runs[0][name], one[name]), f"{name}: fused-pack blocks differ from one block"
+
+
+def test_fused_exchanges_keep_halo_fields(small_case):
+    """The tend_u exchange (642) and the exchange before the recovery (876-887) packed by their
+    producing kernels and unpacked by their consumers (XPack / XUnpack: dyn_tend's final tend_u
+    kernel -> k_smlstep_pert_b; the stage's last cell phase and damping -> k_recover_cells1 /
+    k_recover_edges) leave every exchanged field, halo columns included, as the pack / unpack
+    kernels do (MPAS_DYCORE_FUSED_PACK=0); 4 RCCL blocks, split-phase exchanges, graph replay."""
+    import os
+    from mpas_dycore import Dycore, decomp
+    part = decomp.partition_sfc(small_case["nCells"], 4)
+    blocks = decomp.decompose(small_case, part)
+    names = [("diag", "rw_p"), ("diag", "ru_p"), ("diag", "rho_pp"), ("diag", "rtheta_pp"), ("tend", "u"),
+             ("state", "u"), ("state", "w")]
+    runs = []
+    for fused in ("1", "0"):
+        old = os.environ.get("MPAS_DYCORE_FUSED_PACK")
+        os.environ["MPAS_DYCORE_FUSED_PACK"] = fused
+        try:
+            dy = Dycore.from_blocks(blocks, device=0, comm_id=Dycore.comm_unique_id(), nranks=1, rank=0,
+                                    rccl_local=True)
+        finally:
+            if old is None:
+                os.environ.pop("MPAS_DYCORE_FUSED_PACK", None)
+            else:
+                os.environ["MPAS_DYCORE_FUSED_PACK"] = old
+        dy.set_overlap(True)
+        dy.use_graph(True)
+        _run(dy, 2)
+        runs.append({(p, n, i): dy.get(p, n, 1, block=i) for p, n in names for i in range(len(blocks))})
+        dy.close()
+    for key in runs[1]:
+        assert np.array_equal(runs[0][key], runs[1][key]), f"{key}: fused exchange differs from pack/unpack kernels"
