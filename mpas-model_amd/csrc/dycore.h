@@ -157,11 +157,17 @@ struct XPack {
 };
 // XUnpack: halo element i (i >= nSolve) has field f's received column at recv + off[f * nh + i -
 // nSolve] (-1: not in this exchange); the consumer reads it there and writes it into the field.
+// The u exchange after the recovery (988) is the third such point: packed where the recovery
+// computes u (k_divdamp_p<REC>, k_recover_edges), unpacked by the diagnostics' vertex kernel
+// (k_diag_vertices_p), the first reader of u's halo.
 // recv == nullptr: the fields hold the values.
 struct XUnpack {
   const double* recv;
   const int* off;
   int nh;
+  // wb (optional): the consumer element that writes halo element i's column back into the field
+  // (wb[i - nSolve]), when several of the consumer's elements read it
+  const int* wb;
 };
 
 }  // namespace mpas

@@ -69,6 +69,7 @@ struct Block {
   std::vector<XList> xl;
   int64_t nEdges_act = -1;             // edges with an owned cell (from cellsOnEdge), for B_ac
   std::vector<int32_t> h_coe, h_eoc, h_noc;  // host copies (0-based) for the halo-boundary flags
+  std::vector<int32_t> h_voe, h_eov;         // verticesOnEdge / edgesOnVertex (0-based): fused u unpack
   // summarize_timestep records (summary.hip): partials and one SUM_REC record per field
   double* sum_part = nullptr;
   double* sum_out = nullptr;
@@ -563,8 +564,11 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   } else if (!ctx->plain_exchange && fs.size() == 1 && std::string(fs[0].pool) == "tend" &&
              std::string(fs[0].name) == "u" && fs[0].layers == 0x1u) {
     fkind = 2;
+  } else if (!ctx->plain_exchange && !ctx->lbc && fs.size() == 1 && std::string(fs[0].pool) == "state" &&
+             std::string(fs[0].name) == "u" && fs[0].tl == 2 && fs[0].layers == ALL_LAYERS) {
+    fkind = 3;  // the u exchange after the recovery (988); regional runs overwrite u after the recovery
   }
-  if (fkind == 2) rec_fid = [](const XField&) -> int { return 0; };
+  if (fkind >= 2) rec_fid = [](const XField&) -> int { return 0; };
   bool recfuse = fkind != 0;
   struct RecSeg { int block, fid; Loc loc; const XList* x; size_t seg; };
   std::vector<RecSeg> rec_pack, rec_unpack;
@@ -863,15 +867,48 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
               any = true;
             }
           }
+          const int* d_wb = nullptr;
+          if (any && fkind == 3) {
+            // each received halo edge is written back by one vertex of the block that has it among its
+            // edgesOnVertex (the vertex kernel is its first reader); an edge without one: no fusion
+            const Block& b = ctx->blk[bi];
+            std::vector<int> wb(std::max(nh, 0), -1);
+            bool ok = (int64_t)b.h_voe.size() >= 2LL * d.nEdges && (int64_t)b.h_eov.size() >= 3LL * d.nVertices;
+            for (int i = 0; ok && i < nh; ++i) {
+              if (off[i] < 0) continue;
+              const int e = nsolve + i;
+              for (int j = 0; j < 2 && wb[i] < 0; ++j) {
+                const int v = b.h_voe[2 * (size_t)e + j];
+                if (v < 0 || v >= d.nVertices) continue;
+                for (int m = 0; m < 3; ++m)
+                  if (b.h_eov[3 * (size_t)v + m] == e) wb[i] = v;
+              }
+              ok = wb[i] >= 0;
+            }
+            if (!ok) {
+              recfuse = false;
+              break;
+            }
+            void* dwb = nullptr;
+            CHK(upload(wb.data(), wb.size() * sizeof(int), &dwb));
+            d_wb = (const int*)dwb;
+          }
           if (any) {
             void* doff = nullptr;
             CHK(upload(off.data(), off.size() * sizeof(int), &doff));
-            (loc == L_CELL ? pl.rup_cell : pl.rup_edge)[bi] = XUnpack{pl.recvbuf, (const int*)doff, nh};
+            (loc == L_CELL ? pl.rup_cell : pl.rup_edge)[bi] = XUnpack{pl.recvbuf, (const int*)doff, nh, d_wb};
           }
         }
       }
-      pl.fused_rec = fkind;
-      pl.fused_pack = pl.fused_unpack = true;
+      if (recfuse) {
+        pl.fused_rec = fkind;
+        pl.fused_pack = pl.fused_unpack = true;
+      } else {  // a write-back vertex is missing: the pack / unpack kernels run (maps unused)
+        pl.rpk_cell.clear();
+        pl.rpk_edge.clear();
+        pl.rup_cell.clear();
+        pl.rup_edge.clear();
+      }
     }
   }
   if (pl.npre) {
@@ -1356,15 +1393,17 @@ bool fused_recover_edges(const Dims& d) { return pair_layout(d) && fused_recover
 // invNs > 0: recover the edges with two owned cells too (fused_recover_edges)
 // dl: rtheta_pp_old holds the difference (acoustic_cells with dl); pair layout only
 // rp: the block's pack map of the 876-887 exchange (XPlan::fused_rec), or none
+// upk: the block's pack map of the u exchange (988, XPlan::fused_rec), used by the recovering variant
 void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int phase, int fresh = 0,
-                        double invNs = 0.0, UnpackMap um = UnpackMap{}, int dl = 0, XPack rp = XPack{}) {
+                        double invNs = 0.0, UnpackMap um = UnpackMap{}, int dl = 0, XPack rp = XPack{},
+                        XPack upk = XPack{}) {
   // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
   const bool up = um.recv != nullptr;
   const int64_t nw = ((phase == 2 ? d.n_bnd_pairs : d.nEdges) + 1) / 2;  // phase 2: the bnd_pairs list
   const double cd = coef_divdamp(ctx, dts);
   if (pair_layout(d) && invNs > 0.0 && fused_recover_edges(d)) {
-    if (up) LAUNCH_PE((k_divdamp_p<true, true, false>), (k_divdamp_p<true, true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl, rp);
-    else LAUNCH_PE((k_divdamp_p<true, false, false>), (k_divdamp_p<true, false, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl, rp);
+    if (up) LAUNCH_PE((k_divdamp_p<true, true, false>), (k_divdamp_p<true, true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl, rp, upk);
+    else LAUNCH_PE((k_divdamp_p<true, false, false>), (k_divdamp_p<true, false, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl, rp, upk);
   } else if (pair_layout(d)) {
     if (up) LAUNCH_PE((k_divdamp_p<false, true, false>), (k_divdamp_p<false, true, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl, rp);
     else LAUNCH_PE((k_divdamp_p<false, false, false>), (k_divdamp_p<false, false, true>), nw, d, p, cd, phase, dts, fresh, 0.0, um, dl, rp);
@@ -1377,8 +1416,9 @@ void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double 
 // the dycore, and no later phase of this one (pv_edge uses the values in registers).  Every call
 // overwrites them, so only the last call of a dt (and the model-init call) stores them: the pool
 // holds the same values after the step, at 2 x 8 B per edge-level less traffic in 8 of 9 calls.
+// uu_up: the block's fused-unpack map of the u exchange that precedes (988), or none
 void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt, int tl, int rk_step /*0 = absent*/,
-                       int store_grad = 1) {
+                       int store_grad = 1, XUnpack uu_up = XUnpack{}) {
   const double* u = (tl == 1) ? p.u1 : p.u2;
   const double* h = (tl == 1) ? p.rho_zz1 : p.rho_zz2;
   const int reconstruct_v = (rk_step == 0 || rk_step == 3) ? 1 : 0;
@@ -1392,7 +1432,8 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double d
     return;
   }
   if (pair_layout(d)) {
-    LAUNCH_PE((k_diag_vertices_p<false>), (k_diag_vertices_p<true>), (d.nVertices + 1) / 2, d, p, u, store_dv);
+    LAUNCH_PE((k_diag_vertices_p<false>), (k_diag_vertices_p<true>), (d.nVertices + 1) / 2, d, p, u, store_dv, uu_up,
+              (tl == 1) ? p.u1 : p.u2);
     // (a pair-layout k_diag_cells, two cells per wave, measured 18 % slower than the batched one)
     if (d.maxEdges == 6) LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     else LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
@@ -1731,6 +1772,12 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       auto rpe = [&](size_t ib) { return xr ? xr->rpk_edge[ib] : XPack{}; };
       auto ruc = [&](size_t ib) { return xr ? xr->rup_cell[ib] : XUnpack{}; };
       auto rue = [&](size_t ib) { return xr ? xr->rup_edge[ib] : XUnpack{}; };
+      // the u exchange after the recovery (988) packed where the recovery computes u and unpacked by
+      // the diagnostics' vertex kernel (XPlan::fused_rec), or nullptr
+      const std::vector<XField> xu = {{"state", "u", 2, ALL_LAYERS}};
+      const XPlan* xuu = fused_rec_plan(ctx, xu);
+      auto upk = [&](size_t ib) { return xuu ? xuu->rpk_edge[ib] : XPack{}; };
+      auto uup = [&](size_t ib) { return xuu ? xuu->rup_edge[ib] : XUnpack{}; };
       // the last Theta''/rho'' exchange whose unpack its consumer does (XPlan::fused_unpack): the
       // next edge phase, or the stage's last damping
       const XPlan* unpack_xp = nullptr;
@@ -1762,12 +1809,12 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         if (xp && xp->fused_unpack) unpack_xp = xp;
       }
       if (split) {  // the last sub-step's damping (849-869), interior edges overlapping the exchange
-        EACH(divergence_damping(ctx, d, p, dts, 1, nsub == 1, 1 / (double)nsub, UnpackMap{}, 0, rpe(ib_)));
+        EACH(divergence_damping(ctx, d, p, dts, 1, nsub == 1, 1 / (double)nsub, UnpackMap{}, 0, rpe(ib_), upk(ib_)));
         CHK(exchange_wait(ctx));
         EACH(divergence_damping(ctx, d, p, dts, 2, nsub == 1, 0.0, um_of(ib_), 0, rpe(ib_)));
       } else {
         EACH(divergence_damping(ctx, d, p, dts, 0, nsub == 1, 1 / (double)nsub, um_of(ib_),
-                                damping_delta(ctx, d, last_stage), rpe(ib_)));
+                                damping_delta(ctx, d, last_stage), rpe(ib_), upk(ib_)));
       }
       const double invNs = 1 / (double)number_sub_steps[rk_step - 1];
       const double rdt = rk_timestep[rk_step - 1];
@@ -1778,11 +1825,11 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         // owned cells: recovered by the last sub-step's cell phase (fused_recover) or here
         EACH(if (!fused_recover(d)) LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 1, 0));
         // edges with two owned cells: recovered by the last damping (fused_recover_edges) or here
-        EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1));
+        EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1, XUnpack{}, upk(ib_)));
         CHK(exchange_wait(ctx));
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2, d.nCellsSolve,
                     ruc(ib_)));
-        EACH(LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2, rue(ib_)));  // phase 2: the bnd_edges list
+        EACH(LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2, rue(ib_), upk(ib_)));  // phase 2: bnd_edges
         if (lbc) {  // the w recovery reads ru before the specified-zone overwrite (934-987)
           EACH(recover_cells3(ctx, d, p, 0));
           EACH(LAUNCH(k_lbc_u, d.nEdges, d, p, dt_dynamics * (double)(dynamics_substep - 1) + rk_timestep[rk_step - 1]));
@@ -1799,8 +1846,8 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
                                           d.nCellsSolve, ruc(ib_));
              else LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 0, 0, ruc(ib_)));
         // the edges with two owned cells were recovered by the last damping if fused_recover_edges
-        EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0, rue(ib_));
-             else LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2, rue(ib_)));
+        EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 0, rue(ib_), upk(ib_));
+             else LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2, rue(ib_), upk(ib_)));
         // stages 1 and 2: also the next stage's h_divergence (dyn_tend then skips k_dyn_cells1)
         EACH(recover_cells3(ctx, d, p, 0, hdiv_next));
         if (lbc)  // 934-987
@@ -1816,7 +1863,7 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         if (lbc) CHK(lbc_scalars(ctx, P, dt, rk_timestep[rk_step - 1]));  // 1109-1180
       }
       EACH(solve_diagnostics(ctx, d, p, dt, 2, rk_step,             // 1187-1228
-                             dynamics_substep == dynamics_split && rk_step == 3));
+                             dynamics_substep == dynamics_split && rk_step == 3, uup(ib_)));
       std::vector<XField> xd = {{"state", "w", 2, ALL_LAYERS}, {"diag", "pv_edge", 0, ALL_LAYERS},  // 1234-1249
                                 {"diag", "rho_edge", 0, ALL_LAYERS}};
       if (scalars_in_dynamics) xd.push_back({"state", "scalars", 2, ALL_LAYERS});
@@ -2258,6 +2305,10 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
     if (f->pool == "mesh" && f->name == "edgesOnCell") {
       b.h_eoc = tmp;
       ctx->bnd_ready = false;
+    }
+    if (f->pool == "mesh" && (f->name == "verticesOnEdge" || f->name == "edgesOnVertex")) {
+      (f->name == "verticesOnEdge" ? b.h_voe : b.h_eov) = tmp;
+      if (!ctx->plans.empty()) invalidate_plans(ctx);  // the fused u exchange's write-back vertices
     }
     HIPCHK(hipMemcpyAsync(f->buf[slot], tmp.data(), nb, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));

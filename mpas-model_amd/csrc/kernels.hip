@@ -2028,9 +2028,13 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
 
 // k_diag_vertices in the pair layout: two vertices per wavefront, two levels per lane (16-byte
 // gathers of u at the three edges); same expressions in the same order
+// uu_up: the u exchange's fused unpack (988, XUnpack with write-back vertices): a received halo edge's u
+// comes from the receive buffer for every vertex that reads it, and its write-back vertex (uu_up.wb)
+// stores it into uw (the field u names) for the later readers
 template <bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_diag_vertices_p(Dims d, Ptrs p, const double* __restrict__ u,
-                                                                  int store_dv) {
+                                                                  int store_dv, XUnpack uu_up = XUnpack{},
+                                                                  double* uw = nullptr) {
   const int vA = 2 * pair_wave();
   if (vA >= d.nVertices) return;
   const bool hasB = vA + 1 < d.nVertices;
@@ -2052,7 +2056,16 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_vertices_p(Dims d, Ptrs p
   }
   d2 uu[3];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) uu[i] = ld2(u + (size_t)ei[i] * K + 2 * lc);
+  for (int i = 0; i < 3; ++i) {
+    const int of = rec_off(uu_up, 0, ei[i], d.nEdgesSolve);
+    if (of >= 0) {
+      uu[i] = ld2(uu_up.recv + of + 2 * lc);
+      if (uu_up.wb[ei[i] - d.nEdgesSolve] == v && (h == 0 || hasB) && 2 * l < K)
+        pst(uw + (size_t)ei[i] * K + 2 * lc, uu[i], two);
+    } else {
+      uu[i] = ld2(u + (size_t)ei[i] * K + 2 * lc);
+    }
+  }
   const double iat = sel(h, ld_uniform_f64(p.invAreaTriangle + vA), ld_uniform_f64(p.invAreaTriangle + vB));
   const double fv = sel(h, ld_uniform_f64(p.fVertex + vA), ld_uniform_f64(p.fVertex + vB));
   d2 vort{0.0, 0.0};
@@ -2189,7 +2202,7 @@ __device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMa
 template <bool REC = false, bool UP = false, bool ODD = false>
 __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
                                                             int fresh, double invNs = 0.0, UnpackMap um = UnpackMap{},
-                                                            int dl = 0, XPack rp = XPack{}) {
+                                                            int dl = 0, XPack rp = XPack{}, XPack upk = XPack{}) {
   int eA, eB;
   bool hasB;
   if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
@@ -2244,6 +2257,8 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
   const d2 rs = ld2(p.ru_save + o);
   const d2 ra = fresh ? ru : ld2(p.ruAvg + o);  // fresh: sub-step 1 left ruAvg = dts * tend_u
   const d2 z1 = ld2(p.rho_zz2 + o1), z2 = ld2(p.rho_zz2 + o2);
+  const d2 rr{rs.x + out.x, rs.y + out.y};
+  const d2 un{2. * rr.x / (z1.x + z2.x), 2. * rr.y / (z1.y + z2.y)};
   if ((h ? onB : onA) && 2 * l < K) {
     // dl (one block, not the dt's last stage, see damping_delta): nothing reads ru_p of a
     // recovered edge before the next stage's sub-step 1 forms it again from tend_u, so only the
@@ -2251,13 +2266,14 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
     if (!(dl && (h ? rB : rA))) pst(p.ru_p + o, out, two);
     if (h ? rB : rA) {  // recover_edges (3048-3059), same expressions
       pst(p.ruAvg + o, d2{rs.x + (ra.x * invNs), rs.y + (ra.y * invNs)}, two);
-      const d2 rr{rs.x + out.x, rs.y + out.y};
       pst(p.ru + o, rr, two);
-      pst(p.u2 + o, d2{2. * rr.x / (z1.x + z2.x), 2. * rr.y / (z1.y + z2.y)}, two);
+      pst(p.u2 + o, un, two);
     } else if (fresh) {
       pst(p.ruAvg + o, ru, two);
     }
   }
+  // the recovered u of an owned edge into its slots of the u exchange (988) when fused
+  pack_rec_edge(upk, d, eA, eB, hasB, h, lc, (h ? onB : onA) && (h ? rB : rA) && 2 * l < K, two, un);
 }
 
 // k_scalars_edges in the pair layout (atm_advance_scalars_work, 3357-3426)
@@ -3036,8 +3052,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells1(Dims d, Ptrs p
 // edges (all): 3048-3059
 // phase 2 walks the compact bnd_edges list (the edges with edge_bnd set)
 // ru: the 876-887 exchange's fused unpack (XUnpack, edge field ru_p), as in k_recover_cells1
+// upk: the recovered u of an owned edge also goes to the u exchange's send buffer (988, XPack)
 __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p, double invNs, int phase,
-                                                                 XUnpack ru = XUnpack{}) {
+                                                                 XUnpack ru = XUnpack{}, XPack upk = XPack{}) {
   int e = wave_elem(0);
   if (phase == 2) {
     if (e >= d.n_bnd_edges) return;
@@ -3060,7 +3077,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_edges(Dims d, Ptrs p,
   p.ruAvg[o] = p.ru_save[o] + (p.ruAvg[o] * invNs);
   const double ruv = p.ru_save[o] + rup;
   p.ru[o] = ruv;
-  p.u2[o] = 2. * ruv / (p.rho_zz2[(size_t)c1 * K + k] + p.rho_zz2[(size_t)c2 * K + k]);
+  const double un = 2. * ruv / (p.rho_zz2[(size_t)c1 * K + k] + p.rho_zz2[(size_t)c2 * K + k]);
+  p.u2[o] = un;
+  if (upk.start && e < d.nEdgesSolve) {
+    const int s0 = __builtin_amdgcn_readfirstlane(upk.start[e]), s1 = __builtin_amdgcn_readfirstlane(upk.start[e + 1]);
+    for (int sl = s0; sl < s1; ++sl) upk.dst[sl][k] = un;
+  }
 }
 
 // cells (all): w from the flux-divergence operator, then divided by density (3063-3097)

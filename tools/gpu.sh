@@ -17,6 +17,7 @@
 #   prof8            rocprofv3 kernel trace of one rank's block of an 8-way split (rank emulation)
 #   blocks8          bench.py --blocks 8 --rccl-local (the 8-GPU decomposition on one device)
 #   prof8b           rocprofv3 kernel trace of blocks8 (gpurun_out/prof8b)
+#   ab8              blocks8 with the fused exchange packs / unpacks off and on (MPAS_DYCORE_FUSED_PACK), AB_ROUNDS rounds
 #   ab               same-box A/B of AB_LIBS (default exp/lib_base.so vs the in-tree library),
 #                    AB_ROUNDS rounds of tools/kbench.py (AB_ARGS extra arguments)
 #   kprof            rocprofv3 kernel stats of tools/kbench.py for each of AB_LIBS (gpurun_out/kprof_<i>)
@@ -42,6 +43,11 @@ step() {
     rank) timeout -k 10 400 python tools/rank_emulation.py --parts 1 2 4 8 > gpurun_out/rank.log 2>&1 && tail -4 gpurun_out/rank.log ;;
     prof8) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --steps 10 > gpurun_out/prof8.log 2>&1 && echo "prof8 done" ;;
     blocks8) timeout -k 10 400 python bench.py --blocks 8 --rccl-local --steps 5 --warmup 2 $B > gpurun_out/blocks8.log 2>&1 && last gpurun_out/blocks8.log 300 ;;
+    ab8) rm -f gpurun_out/ab8.log
+        for r in ${AB_ROUNDS:-1 2 3}; do for F in 0 1; do
+          echo "== MPAS_DYCORE_FUSED_PACK=$F" >> gpurun_out/ab8.log
+          MPAS_DYCORE_FUSED_PACK=$F timeout -k 10 300 python bench.py --blocks 8 --rccl-local --steps 5 --warmup 2 $B >> gpurun_out/ab8.log 2>&1 || return 1
+        done; done; grep -h "==\|ms_per_step" gpurun_out/ab8.log | sed 's/.*"ms_per_step": \([0-9.]*\).*/ms_per_step \1/' ;;
     prof8b) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8b -o run --output-format csv -- python3 bench.py --blocks 8 --rccl-local --steps 3 --warmup 1 $B > gpurun_out/prof8b.log 2>&1 && echo "prof8b done" ;;
     ab) rm -f gpurun_out/ab.log
         for r in ${AB_ROUNDS:-1 2 3}; do for L in ${AB_LIBS:-exp/lib_base.so mpas-model_amd/csrc/libmpas_dycore.so}; do
