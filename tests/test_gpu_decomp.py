@@ -140,17 +140,21 @@ def test_fused_pack_bitwise(small_case, overlap):
 
 
 def test_fused_exchanges_keep_halo_fields(small_case):
-    """The tend_u exchange (642) and the exchange before the recovery (876-887) packed by their
-    producing kernels and unpacked by their consumers (XPack / XUnpack: dyn_tend's final tend_u
-    kernel -> k_smlstep_pert_b; the stage's last cell phase and damping -> k_recover_cells1 /
-    k_recover_edges) leave every exchanged field, halo columns included, as the pack / unpack
-    kernels do (MPAS_DYCORE_FUSED_PACK=0); 4 RCCL blocks, split-phase exchanges, graph replay."""
+    """The tend_u exchange (642), the exchange before the recovery (876-887) and the u exchange
+    after it (988) packed by their producing kernels and unpacked by their consumers (XPack /
+    XUnpack: dyn_tend's final tend_u kernel -> k_smlstep_pert_b; the stage's last cell phase and
+    damping -> k_recover_cells1 / k_recover_edges; the recovery -> k_diag_vertices_p), and the
+    exchange after the diagnostics (1234-1249, with 1282-1297 at a substep's end) packed by the w
+    recovery and the diagnostics' edge kernel, leave every exchanged field, halo columns included,
+    as the pack / unpack kernels do (MPAS_DYCORE_FUSED_PACK=0); 4 RCCL blocks, split-phase
+    exchanges, graph replay."""
     import os
     from mpas_dycore import Dycore, decomp
     part = decomp.partition_sfc(small_case["nCells"], 4)
     blocks = decomp.decompose(small_case, part)
     names = [("diag", "rw_p"), ("diag", "ru_p"), ("diag", "rho_pp"), ("diag", "rtheta_pp"), ("tend", "u"),
-             ("state", "u"), ("state", "w")]
+             ("state", "u"), ("state", "w"), ("diag", "pv_edge"), ("diag", "rho_edge"), ("state", "theta_m"),
+             ("diag", "pressure_p"), ("diag", "rtheta_p"), ("diag", "exner")]
     runs = []
     for fused in ("1", "0"):
         old = os.environ.get("MPAS_DYCORE_FUSED_PACK")
