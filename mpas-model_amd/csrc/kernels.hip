@@ -25,7 +25,9 @@ namespace mpas {
 #define WAVES_PER_BLOCK 1
 #define BLOCK_THREADS WIDE_THREADS
 #else
-#define WAVES_PER_BLOCK 4
+#ifndef WAVES_PER_BLOCK
+#define WAVES_PER_BLOCK 4  // at most 4 (summary.hip's per-wave partials)
+#endif
 #define BLOCK_THREADS (64 * WAVES_PER_BLOCK)
 #endif
 
