@@ -15,7 +15,7 @@ def resources():
     src = os.path.join(ROOT, "mpas-model_amd", "csrc", "dycore.hip")
     r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                         "-ffp-contract=off", "-Wno-unused-result", "--cuda-device-only", "-c", src, "-o", "/dev/null",
-                        "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
+                        "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("KR_EXTRA", "").split(), capture_output=True, text=True)
     rows, cur = [], None
     for line in r.stderr.splitlines():
         m = re.search(r"Function Name: (\S+)", line)
