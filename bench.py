@@ -63,6 +63,48 @@ def cpu_baseline(case, dt, nthreads, steps, moist_end=1):
                        f"{len(use)} timed steps 2..{steps} ({t:.2f} s/step)")
 
 
+class Watchdog:
+    """Bounds every phase of a multi-rank run: a phase that does not finish in time (ncclCommInitRank,
+    a halo exchange's RCCL group, a captured step) makes this rank print one JSON line naming the
+    phase and the library's last enqueued exchange (mpas_dyc_last_exchange) and exit with status 3
+    (os._exit from this thread: the main thread may be blocked inside RCCL; nothing is re-executed)."""
+
+    def __init__(self, rank: int, enabled: bool):
+        import threading
+        self.rank, self.enabled = rank, enabled
+        self.name, self.deadline, self.t0 = None, None, time.time()
+        self.dy = None
+        self.lock = threading.Lock()
+        if enabled:
+            threading.Thread(target=self._run, daemon=True).start()
+
+    def phase(self, name: str, seconds: float):
+        with self.lock:
+            self.name, self.deadline, self.t0 = name, time.time() + seconds, time.time()
+
+    def done(self):
+        with self.lock:
+            self.name, self.deadline = None, None
+
+    def _run(self):
+        while True:
+            time.sleep(1.0)
+            with self.lock:
+                expired = self.deadline is not None and time.time() > self.deadline
+                name, t0 = self.name, self.t0
+            if expired:
+                last = ""
+                try:
+                    last = self.dy.last_exchange() if self.dy is not None else ""
+                except Exception:
+                    pass
+                msg = {"metric": METRIC, "value": None, "error": f"rank {self.rank}: phase '{name}' did not finish "
+                       f"within {time.time() - t0:.0f} s", "rank": self.rank, "phase": name, "last_exchange": last}
+                print(json.dumps(msg), flush=True)
+                print(json.dumps(msg), file=sys.stderr, flush=True)
+                os._exit(3)
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -126,6 +168,9 @@ def main():
                          "JW case; needs --dt and --len-disp (namelist config_dt / config_len_disp)")
     ap.add_argument("--dt", type=float, default=None)
     ap.add_argument("--len-disp", type=float, default=None)
+    ap.add_argument("--max-edges", default=None, metavar="ME[,ME2]",
+                    help="declare the mesh with maxEdges ME and maxEdges2 ME2 (default 2 ME), as MPAS mesh files "
+                         "do (10,20): the unused slots are padding the kernels never read")
     ap.add_argument("--moist", action="store_true",
                     help="BASELINE.json configs[3]: moist JW (qv) + tracer blobs, num_scalars=6, monotone transport")
     ap.add_argument("--no-graph", action="store_true")
@@ -139,6 +184,12 @@ def main():
     ap.add_argument("--rccl-local", action="store_true", help="route in-process block exchanges through RCCL")
     ap.add_argument("--no-configs1", action="store_true",
                     help="skip the secondary x1.10242 (BASELINE.json configs[1]) measurement")
+    ap.add_argument("--preflight-only", action="store_true",
+                    help="multi-rank: check on the host that every rank's RCCL plans pair up, print the result "
+                         "and exit before touching a GPU")
+    ap.add_argument("--phase-timeout", type=float, default=600.0,
+                    help="multi-rank watchdog: seconds any one phase (RCCL init, model init, first step with its "
+                         "capture, warmup, profile) may take; the timed loop gets this plus 10 s per step")
     args = ap.parse_args()
 
     world, rank, local = _dist()
@@ -158,6 +209,14 @@ def main():
     if args.num_scalars is None:
         args.num_scalars = 6 if args.moist else 1
     def make_case():
+        c = _make_case()
+        if args.max_edges:
+            from mpas_dycore.mesh import pad_max_edges
+            me = [int(x) for x in str(args.max_edges).split(",")]
+            c = pad_max_edges(c, me[0], me[1] if len(me) > 1 else 2 * me[0])
+        return c
+
+    def _make_case():
         if args.init:
             from mpas_dycore.mpas_files import read_init
             if args.dt is None or args.len_disp is None:
@@ -181,8 +240,33 @@ def main():
     # WSM6-like species set: every scalar is a moist species (moist_start..moist_end, qtot)
     moist_end = case["num_scalars"] if (args.moist or args.init) else 1
     nparts = world * args.blocks
+    wd = Watchdog(rank, world > 1)
+    preflight = None
     if nparts > 1:
         blocks, placement = decomp.rank_blocks(case, world, rank, args.blocks)
+        if world > 1 or args.preflight_only:
+            # every rank's RCCL plans, checked against each other on the host before any GPU call
+            from mpas_dycore.dycore import plan_exchanges
+            from mpas_dycore.preflight import PlanMismatch, check_plans
+            wd.phase("preflight", args.phase_timeout)
+            mine = plan_exchanges(blocks, placement, rank, world, float(dt), moist_end=moist_end)
+            allp = [None] * world
+            if dist:
+                dist.all_gather_object(allp, mine)
+            else:
+                allp = [mine]
+            try:
+                preflight = dict(check_plans(allp), ok=True)
+            except PlanMismatch as e:
+                preflight = {"ok": False, "error": str(e), "point": e.point, "key": e.key}
+            wd.done()
+            if not preflight["ok"] or args.preflight_only:
+                if rank == 0:
+                    print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "preflight": preflight,
+                                      "rccl_version": Dycore.rccl_version()}), flush=True)
+                if dist:
+                    dist.destroy_process_group()
+                raise SystemExit(0 if preflight["ok"] else 2)
         comm_id = None
         # --rccl-local: blocks of this process also exchange through RCCL (send to self), to
         # measure the cost of the RCCL path on one GPU
@@ -192,6 +276,7 @@ def main():
                 dist.broadcast_object_list(obj, src=0)
             comm_id = obj[0]
         torch.cuda.set_device(device)
+        wd.phase("rccl_init (ncclCommInitRank) and upload", args.phase_timeout)
         dy = Dycore.from_blocks(blocks, device=device, placement=placement, rank=rank, nranks=world,
                                 comm_id=comm_id, moist_end=moist_end, rccl_local=args.rccl_local)
         owned = sum(b.solve[0] for b in blocks)
@@ -199,7 +284,10 @@ def main():
     else:
         dy = Dycore(case, device=device, moist_end=moist_end)
         owned, halo = case["nCells"], 0
+    wd.dy = dy
+    wd.phase("model init (init_diagnostics)", args.phase_timeout)
     dy.init_diagnostics(dt)
+    dy.synchronize()
     if not args.no_graph:
         dy.use_graph(True)
 
@@ -208,11 +296,14 @@ def main():
         dy.shift_time_levels()
 
     for i in range(args.warmup):
+        wd.phase(f"warmup step {i + 1}" + (" (exchange plans, RCCL warm-up, hipGraph capture)" if i == 0 else ""),
+                 args.phase_timeout)
         step(i + 1)
-    dy.synchronize()
+        dy.synchronize()
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
+    wd.phase("timed loop", args.phase_timeout + 10.0 * args.steps)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i + 1)
@@ -221,8 +312,24 @@ def main():
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
+    wd.done()
     elapsed = t1 - t0
     graph = dy.graph_active()
+    layout = dy.layout()
+    ranks = None
+    if nparts > 1:
+        # one more step, eager, with HIP events around every exchange's exposed part (outside the
+        # timed region): where this rank's time goes
+        wd.phase("exchange profile step", args.phase_timeout)
+        prof = dict(dy.exchange_profile(dt, args.warmup + args.steps + 1), rank=rank, owned_cells=int(owned),
+                    halo_cells=int(halo))
+        dy.shift_time_levels()
+        wd.done()
+        ranks = [None] * world
+        if dist:
+            dist.all_gather_object(ranks, prof)
+        else:
+            ranks = [prof]
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -289,6 +396,8 @@ def main():
                             f"{args.blocks} per GPU, halo exchange over RCCL" if nparts > 1 else "single block"),
             "owned_cells_rank0": owned, "halo_cells_rank0": halo,
             "hip_graph": graph,
+            "maxEdges_declared": [case["maxEdges"], case["maxEdges2"]],
+            "kernel_layout": layout,
         },
         "roofline": {
             "kernel": "acoustic sub-step (k_acoustic_edges<damped> + k_acoustic_cells; per sub-step of an "
@@ -300,6 +409,10 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if nparts > 1:
+        out["ranks"] = ranks
+        out["preflight"] = preflight
+        out["rccl_version"] = Dycore.rccl_version()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             # the box's CPU share for one GPU (OMP_NUM_THREADS there), not the machine's nproc

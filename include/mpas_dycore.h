@@ -91,7 +91,19 @@ int mpas_dyc_get_field(mpas_dyc_ctx* ctx, const char* pool, const char* name, in
 int64_t mpas_dyc_field_bytes(const mpas_dyc_ctx* ctx, const char* pool, const char* name);
 /* Raw device pointer of a field (for zero-copy use from torch / RCCL); NULL if unknown.
  * Device layout = the Fortran image, except scalars / scalars_tend, which are
- * scalar-major [num_scalars][n+1][nVertLevels] in HBM (set/get transpose them). */
+ * scalar-major [num_scalars][n+1][nVertLevels] in HBM (set/get transpose them).
+ * A pointer is valid until the next mpas_dyc_timestep / mpas_dyc_shift_time_levels: the step
+ * rotates buffers instead of copying them, so re-query it after every step for
+ *   - diag.ru, ru_save, rw, rw_save, rtheta_p, rtheta_p_save, rho_p, rho_p_save (the _save
+ *     copies of atm_rk_integration_setup / atm_rk_dynamics_substep_finish, 1847-1850, 6051-6054,
+ *     are buffer trades),
+ *   - state.theta_m (theta_m_1 = theta_m_2 at every substep end, 6058, is a trade of its two
+ *     time levels), and every state field's time levels across mpas_dyc_shift_time_levels.
+ * The maxEdges / maxEdges2-strided mesh fields (edgesOnCell, cellsOnCell, verticesOnCell,
+ * kiteForCell, edgesOnCell_sign, defc_a, defc_b, coeffs_reconstruct, zb_cell, zb3_cell,
+ * edgesOnEdge, weightsOnEdge) return their image at the declared maxEdges; the kernels read a
+ * copy at the mesh's actual cell degree (mpas_dyc_block_layout), so change them through
+ * mpas_dyc_set_field, not through this pointer. */
 void* mpas_dyc_field_device_ptr(mpas_dyc_ctx* ctx, const char* pool, const char* name, int32_t time_level);
 
 /* atm_init_coupled_diagnostics + atm_compute_solve_diagnostics on time level 1
@@ -286,6 +298,28 @@ int mpas_dyc_time_acoustic_step(mpas_dyc_ctx* ctx, double dts, int32_t small_ste
 int mpas_dyc_use_graph(mpas_dyc_ctx* ctx, int32_t on);
 /* Algorithmic HBM bytes of one acoustic sub-step of block 0 (B_ac). */
 double mpas_dyc_acoustic_bytes(const mpas_dyc_ctx* ctx);
+/* Exchange profile of a multi-rank run (bench.py --gpus N): with on = 1 every following
+ * mpas_dyc_timestep runs eagerly (no hipGraph) with HIP events around the exposed part of each
+ * halo exchange -- a blocking exchange whole, a split-phase one from the moment the compute stream
+ * reaches the join until the exchange stream's work has completed -- and around each RCCL group.
+ * mpas_dyc_get_profile then returns, for the last such step: out[0] = exchanges waited on,
+ * out[1] = ms of the step (events on the compute stream), out[2] = ms of exposed exchange time,
+ * out[3] = RCCL groups issued, out[4] = ms inside them (mostly overlapped with compute). */
+int mpas_dyc_set_profile(mpas_dyc_ctx* ctx, int32_t on);
+int mpas_dyc_get_profile(mpas_dyc_ctx* ctx, double* out, int32_t n);
+/* The plan key of the exchange whose RCCL group was enqueued last ("warm_rccl <key>" while the
+ * connections are set up before graph capture, which synchronises after every group): what a
+ * watchdog reports when a rank hangs in RCCL.  Safe to read from another thread (a fixed buffer). */
+const char* mpas_dyc_last_exchange(const mpas_dyc_ctx* ctx);
+/* ncclGetVersion of the RCCL the library links (e.g. 22703 = 2.27.3), -1 on error. */
+int32_t mpas_dyc_rccl_version(void);
+/* How the kernels see a block, once its mesh is set (computed on the first call that needs it):
+ * out[0] = maxEdges the kernels index with (max(nEdgesOnCell), at least 6 -- mesh files may
+ * declare more, e.g. 10, Registry.xml:13-16), out[1] = maxEdges2 likewise, out[2] = kernel
+ * family (0 one column per element, 1 batched stencil records, 2 pair layout: two elements per
+ * wavefront, two levels per lane), out[3] = column shape (0 one wavefront, 1 one workgroup:
+ * nVertLevels > MPAS_DYC_MAX_LEVELS_WAVE). */
+int mpas_dyc_block_layout(mpas_dyc_ctx* ctx, int32_t block, int32_t* out /* [4] */);
 
 #ifdef __cplusplus
 }

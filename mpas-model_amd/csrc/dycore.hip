@@ -49,6 +49,12 @@ struct Field {
   // (X <-> X_save) whose buffer this field trades at every rotation, rot_pos counts the trades mod 2
   // (which of the two buffers it holds); flip = the time levels of a state field are swapped
   int rot = -1, rot_pos = 0, flip = 0;
+  // mesh fields strided by maxEdges (me = 1) or maxEdges2 (me = 2): buf holds the Fortran image at the
+  // declared size (what set/get_field and the device pointer see), `packed` the same array at the
+  // block's effective strides (pack_mesh), which is what the kernels read; nullptr: equal strides
+  int me = 0;
+  void* packed = nullptr;
+  int64_t packed_inner = 0;
 };
 
 // One entry of a block's multihalo exchange list (mpas_multihalo_exchange_list:
@@ -70,6 +76,11 @@ struct Block {
   int64_t nEdges_act = -1;             // edges with an owned cell (from cellsOnEdge), for B_ac
   std::vector<int32_t> h_coe, h_eoc, h_noc;  // host copies (0-based) for the halo-boundary flags
   std::vector<int32_t> h_voe, h_eov;         // verticesOnEdge / edgesOnVertex (0-based): fused u unpack
+  std::vector<int32_t> h_noe;                // nEdgesOnEdge (pack_mesh)
+  // maxEdges / maxEdges2 as the host declared them (the mesh file's dimensions; Fortran images and
+  // h_eoc use these strides).  d.maxEdges / d.maxEdges2 are the strides the kernels index with:
+  // max(nEdgesOnCell) and the edgesOnEdge slots the kernels need after pack_mesh
+  int me_decl = 0, me2_decl = 0;
   // summarize_timestep records (summary.hip): partials and one SUM_REC record per field
   double* sum_part = nullptr;
   double* sum_out = nullptr;
@@ -158,6 +169,17 @@ struct mpas_dyc_ctx {
   // default is config_print_global_minmax_vel = true, Registry.xml:339)
   int summary_flags = MPAS_DYC_PRINT_GLOBAL_MINMAX_VEL;
   int summary_tl = 0;                   // time level the records describe (0: none yet)
+  bool tail_pending = false;            // MPAS_DYC_PHYSICS_MICROPHYSICS: a step ran, mpas_dyc_finish_step not yet
+  // exchange profile (mpas_dyc_set_profile): eager steps with HIP events around the exposed part of
+  // every exchange (a blocking exchange whole; a split-phase one from the compute stream reaching
+  // the join to the join's completion) and around every RCCL group
+  bool profile = false;
+  bool in_async = false;                // exchange() issued by exchange_async (on the exchange stream)
+  std::vector<hipEvent_t> prof_exposed, prof_rccl;  // pairs (start, end)
+  hipEvent_t prof_step[2] = {};
+  double prof_out[5] = {};              // mpas_dyc_get_profile
+  // the exchange whose RCCL group was enqueued last (a watchdog's report when a group hangs)
+  char last_key[256] = {0};
   double* sum_gather = nullptr;         // RCCL all-gather buffer of the per-rank records
 };
 
@@ -340,6 +362,11 @@ void build_registry(Block& c) {
     c.fields[a].rot = b;
     c.fields[b].rot = a;
   }
+  // the maxEdges- and maxEdges2-strided mesh arrays (pack_mesh)
+  for (const char* n : {"edgesOnCell", "cellsOnCell", "verticesOnCell", "kiteForCell", "coeffs_reconstruct",
+                        "edgesOnCell_sign", "defc_a", "defc_b", "zb_cell", "zb3_cell"})
+    c.fields[c.by_name[std::string("mesh.") + n]].me = 1;
+  for (const char* n : {"edgesOnEdge", "weightsOnEdge"}) c.fields[c.by_name[std::string("mesh.") + n]].me = 2;
 }
 
 Field* find(Block& b, const char* pool, const char* name) {
@@ -361,7 +388,7 @@ T* P(mpas_dyc_ctx* c, Block& b, const char* pool, const char* name, int tl = 1) 
     fprintf(stderr, "mpas_dycore: internal: missing field %s.%s\n", pool, name);
     abort();
   }
-  return (T*)f->buf[slot_of(c, *f, tl)];
+  return (T*)(f->packed ? f->packed : f->buf[slot_of(c, *f, tl)]);
 }
 
 Ptrs make_ptrs(mpas_dyc_ctx* c, Block& b) {
@@ -922,6 +949,22 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   return MPAS_DYC_OK;
 }
 
+// a profile event pair's first half on `s` (the second is prof_mark_end); nothing unless profiling
+int prof_mark(mpas_dyc_ctx* ctx, std::vector<hipEvent_t>& v, hipStream_t s) {
+  if (!ctx->profile || ctx->planning) return MPAS_DYC_OK;
+  hipEvent_t e = nullptr;
+  HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventRecord(e, s));
+  v.push_back(e);
+  return MPAS_DYC_OK;
+}
+
+void set_last_key(mpas_dyc_ctx* ctx, const std::string& k) {
+  const size_t n = std::min(k.size(), sizeof(ctx->last_key) - 1);
+  memcpy(ctx->last_key, k.data(), n);
+  ctx->last_key[n] = 0;
+}
+
 int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   if (!needs_exchange(ctx)) return MPAS_DYC_OK;
   const std::string key = plan_key(ctx, fs);
@@ -944,18 +987,24 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   }
   if (ctx->planning) return MPAS_DYC_OK;
   XPlan& pl = it->second;
+  const bool whole = !ctx->in_async;  // a blocking exchange: all of it is exposed
+  if (whole) CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
   if (pl.npre && !pl.fused_pack)
     hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_pre + 3) / 4, pl.npre), dim3(256), 0, ctx->stream, pl.d_pre);
   if (!pl.rsend.empty() || !pl.rrecv.empty()) {
+    set_last_key(ctx, key);
+    CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
     NCCLCHK(ncclGroupStart());
     for (const XMsg& m : pl.rsend)
       NCCLCHK(ncclSend(pl.sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
     for (const XMsg& m : pl.rrecv)
       NCCLCHK(ncclRecv(pl.recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
     NCCLCHK(ncclGroupEnd());
+    CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
   }
   if (pl.npost && !pl.fused_unpack)
     hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_post + 3) / 4, pl.npost), dim3(256), 0, ctx->stream, pl.d_post);
+  if (whole) CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
   return MPAS_DYC_OK;
 }
 
@@ -998,16 +1047,95 @@ inline bool fuse_smlstep(const Dims& d) { return g_fuse_smlstep && batched(d); }
 // levels above K at an even K
 inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K <= 64; }
 
+// why a block cannot run regional LBCs (they need the pair layout), named by its actual cause
+std::string lbc_layout_error(const Dims& d) {
+#ifdef MPAS_WIDE
+  (void)d;
+  return "regional LBCs are not supported above " + std::to_string(MPAS_DYC_MAX_LEVELS_WAVE) + " vertical levels";
+#else
+  if (g_kernel_tier < 2) return "regional LBCs need the pair kernel family (MPAS_DYCORE_KERNELS=pair)";
+  return "regional LBCs need cells of at most 7 edges (max(nEdgesOnCell) = " + std::to_string(d.maxEdges) +
+         ") and maxEdges2 >= " + std::to_string(2 * d.maxEdges - 2);
+#endif
+}
+
+// The kernels index the maxEdges-strided mesh arrays with the mesh's actual cell degree, not with
+// the declared one.  maxEdges in a mesh file is "the largest number of neighbors that a primal mesh
+// cell *may* have" (core_atmosphere/Registry.xml:13-16) -- MPAS-distributed meshes declare 10 (and
+// maxEdges2 = 20) -- and the reference never reads a slot past nEdgesOnCell (its loops run to
+// nEdgesOnCell, and edgesOnCell_sign is 0 there, mpas_atm_core.F:1025-1050).  So the block keeps the
+// Fortran images at the declared strides (buf: set/get_field, the device pointers) and the kernels
+// read copies at
+//   maxEdges  = max(nEdgesOnCell) over the block, at least 6 (or the declared value, if smaller),
+//   maxEdges2 = max(max(nEdgesOnEdge), 2 * maxEdges - 2), at most the declared value
+// (2 maxEdges - 2 = the edgesOnEdge slots the batched kernels load, NE2).  The floor of 6 gives every
+// block of an SCVT mesh (pentagons..heptagons) the same kernel family whatever its cells, so the
+// blocks of different ranks make the same choices.  Every slot a kernel reads is a prefix of the
+// declared row, so the packed copy holds the same values at the same (element, slot).
+int pack_mesh(mpas_dyc_ctx* ctx, Block& b) {
+  Dims& d = b.d;
+  int me = std::min(6, b.me_decl), me2 = 0;
+  for (int c = 0; c < d.nCells; ++c) me = std::max(me, b.h_noc[c]);
+  if (me > b.me_decl) {
+    ctx->err = "nEdgesOnCell exceeds maxEdges (" + std::to_string(me) + " > " + std::to_string(b.me_decl) + ")";
+    return MPAS_DYC_EINVAL;
+  }
+  if ((int64_t)b.h_noe.size() >= d.nEdges) {
+    for (int e = 0; e < d.nEdges; ++e) me2 = std::max(me2, b.h_noe[e]);
+    if (me2 > b.me2_decl) {
+      ctx->err = "nEdgesOnEdge exceeds maxEdges2 (" + std::to_string(me2) + " > " + std::to_string(b.me2_decl) + ")";
+      return MPAS_DYC_EINVAL;
+    }
+    me2 = std::min(b.me2_decl, std::max(me2, 2 * me - 2));
+  } else {
+    me2 = b.me2_decl;  // nEdgesOnEdge not set: keep the declared stride
+  }
+  for (auto& f : b.fields) {
+    if (!f.me) continue;
+    const int64_t slot = f.inner / (f.me == 1 ? b.me_decl : b.me2_decl);
+    const int64_t inner = slot * (f.me == 1 ? me : me2);
+    const int64_t es = f.is_int ? 4 : 8, n = nloc(b, f.loc);
+    if (inner == f.inner) {
+      if (f.packed) (void)hipFree(f.packed);
+      f.packed = nullptr;
+      f.packed_inner = 0;
+      continue;
+    }
+    if (f.packed && f.packed_inner != inner) {
+      (void)hipFree(f.packed);
+      f.packed = nullptr;
+    }
+    if (!f.packed) {
+      HIPCHK(hipMalloc(&f.packed, n * inner * es + 256));
+      HIPCHK(hipMemsetAsync(f.packed, 0, n * inner * es + 256, ctx->stream));
+    }
+    f.packed_inner = inner;
+    HIPCHK(hipMemcpy2DAsync(f.packed, inner * es, f.buf[0], f.inner * es, inner * es, n, hipMemcpyDeviceToDevice,
+                            ctx->stream));
+  }
+  if (d.maxEdges != me || d.maxEdges2 != me2) {
+    d.maxEdges = me;
+    d.maxEdges2 = me2;
+    invalidate_plans(ctx);  // kernel families and the fused exchanges follow the strides
+  }
+  return MPAS_DYC_OK;
+}
+
 // Halo-boundary flags of the split-phase exchanges: an edge is "boundary" when one of its
 // cells is a halo cell (it reads exchanged cell data); an owned cell is "boundary" when
 // one of its edges is a halo edge (it reads exchanged edge data).
 int compute_bnd(mpas_dyc_ctx* ctx) {
   for (auto& b : ctx->blk) {
     const Dims& d = b.d;
-    if ((int64_t)b.h_coe.size() < 2LL * d.nEdges || (int64_t)b.h_eoc.size() < (int64_t)d.maxEdges * d.nCells ||
+    if ((int64_t)b.h_coe.size() < 2LL * d.nEdges || (int64_t)b.h_eoc.size() < (int64_t)b.me_decl * d.nCells ||
         (int64_t)b.h_noc.size() < d.nCells) {
       ctx->err = "mesh connectivity (cellsOnEdge, edgesOnCell, nEdgesOnCell) not set";
       return MPAS_DYC_ESTATE;
+    }
+    CHK(pack_mesh(ctx, b));
+    if (ctx->lbc && !pair_layout(d)) {
+      ctx->err = lbc_layout_error(d);
+      return MPAS_DYC_EINVAL;
     }
     std::vector<int32_t> eb(d.nEdges + 1, 1), cb(d.nCells + 1, 1);
     for (int e = 0; e < d.nEdges; ++e)
@@ -1015,7 +1143,7 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
     for (int c = 0; c < d.nCells; ++c) {
       int bnd = c >= d.nCellsSolve ? CELL_HALO_EDGE | CELL_BND_EDGE : 0;
       for (int i = 0; i < b.h_noc[c]; ++i) {
-        const int e = b.h_eoc[(size_t)c * d.maxEdges + i];
+        const int e = b.h_eoc[(size_t)c * b.me_decl + i];
         if (e >= d.nEdgesSolve) bnd |= CELL_HALO_EDGE;
         if (e >= d.nEdges || eb[e]) bnd |= CELL_BND_EDGE;
       }
@@ -1078,7 +1206,9 @@ int exchange_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   HIPCHK(hipStreamWaitEvent(ctx->xstream, ctx->xfork, 0));
   hipStream_t s = ctx->stream;
   ctx->stream = ctx->xstream;  // exchange() issues on ctx->stream
+  ctx->in_async = true;
   const int r = exchange(ctx, fs);
+  ctx->in_async = false;
   ctx->stream = s;
   if (r) return r;
   HIPCHK(hipEventRecord(ctx->xjoin, ctx->xstream));
@@ -1087,7 +1217,9 @@ int exchange_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
 
 int exchange_wait(mpas_dyc_ctx* ctx) {
   if (ctx->planning) return MPAS_DYC_OK;
+  CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));  // the compute stream's work before the join
   HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->xjoin, 0));
+  CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));  // ... completes once the join has
   return MPAS_DYC_OK;
 }
 
@@ -2080,16 +2212,55 @@ int warm_rccl(mpas_dyc_ctx* ctx) {
     if (pl.warmed) continue;
     pl.warmed = true;
     if (pl.rsend.empty() && pl.rrecv.empty()) continue;
+    set_last_key(ctx, "warm_rccl " + kv.first);
     NCCLCHK(ncclGroupStart());
     for (const XMsg& m : pl.rsend)
       NCCLCHK(ncclSend(pl.sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
     for (const XMsg& m : pl.rrecv)
       NCCLCHK(ncclRecv(pl.recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
     NCCLCHK(ncclGroupEnd());
+    // one group at a time: a group that never completes names its plan in last_key
+    HIPCHK(hipStreamSynchronize(ctx->stream));
     any = true;
   }
-  if (any) HIPCHK(hipStreamSynchronize(ctx->stream));
+  (void)any;
   return MPAS_DYC_OK;
+}
+
+// One eager step with the exchange profile's events (mpas_dyc_set_profile), read back at its end
+int profiled_step(mpas_dyc_ctx* ctx, double dt) {
+  auto clear = [&]() {
+    for (auto* v : {&ctx->prof_exposed, &ctx->prof_rccl}) {
+      for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+      v->clear();
+    }
+  };
+  clear();
+  for (auto& e : ctx->prof_step)
+    if (!e) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventRecord(ctx->prof_step[0], ctx->stream));
+  ctx->graph_ran = false;
+  const int r = srk3(ctx, dt);
+  HIPCHK(hipEventRecord(ctx->prof_step[1], ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->xstream));
+  auto sum = [&](const std::vector<hipEvent_t>& v) {
+    double ms = 0.0;
+    for (size_t i = 0; i + 1 < v.size(); i += 2) {
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, v[i], v[i + 1]) == hipSuccess) ms += t;
+    }
+    return ms;
+  };
+  float tot = 0.f;
+  (void)hipEventElapsedTime(&tot, ctx->prof_step[0], ctx->prof_step[1]);
+  ctx->prof_out[0] = (double)(ctx->prof_exposed.size() / 2);
+  ctx->prof_out[1] = tot;
+  ctx->prof_out[2] = sum(ctx->prof_exposed);
+  ctx->prof_out[3] = (double)(ctx->prof_rccl.size() / 2);
+  ctx->prof_out[4] = sum(ctx->prof_rccl);
+  clear();
+  return r;
 }
 
 int plan_all(mpas_dyc_ctx* ctx, double dt) {
@@ -2124,6 +2295,8 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
       delete ctx;
       return MPAS_DYC_EINVAL;
     }
+    ctx->blk[b].me_decl = dims[b].maxEdges;
+    ctx->blk[b].me2_decl = dims[b].maxEdges2;
   }
   ctx->index_qv = dims[0].index_qv - 1;
   fill_config(ctx->cf, cfg);
@@ -2206,6 +2379,7 @@ void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
     for (auto& f : b.fields) {
       for (int t = 0; t < f.ntl; ++t)
         if (f.buf[t]) (void)hipFree(f.buf[t]);
+      if (f.packed) (void)hipFree(f.packed);
       if (is_host_0d(f)) delete (double*)f.buf[1];
     }
     for (auto& x : b.xl)
@@ -2216,6 +2390,8 @@ void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
   if (ctx->sum_gather) (void)hipFree(ctx->sum_gather);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->prof_step)
     if (e) (void)hipEventDestroy(e);
   if (ctx->xfork) (void)hipEventDestroy(ctx->xfork);
   if (ctx->xjoin) (void)hipEventDestroy(ctx->xjoin);
@@ -2285,6 +2461,7 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
   }
   const int slot = slot_of(ctx, *f, time_level);
   HIPCHK(hipSetDevice(ctx->device));
+  if (f->me) ctx->bnd_ready = false;  // pack_mesh copies the new image for the kernels
   if (f->is_int && f->target != T_NONE) {
     // MPAS 1-based -> device 0-based; out-of-range / 0 -> garbage slot
     const int64_t n = field_elems(b, *f);
@@ -2327,6 +2504,10 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (f->pool == "mesh" && f->name == "nEdgesOnCell") {
       b.h_noc.assign((const int32_t*)host, (const int32_t*)host + nb / 4);
+      ctx->bnd_ready = false;
+    }
+    if (f->pool == "mesh" && f->name == "nEdgesOnEdge") {
+      b.h_noe.assign((const int32_t*)host, (const int32_t*)host + nb / 4);
       ctx->bnd_ready = false;
     }
     if (f->pool == "mesh" && (f->name == "zb_cell" || f->name == "zb3_cell")) ctx->bnd_ready = false;  // zb_p / zb_m
@@ -2500,6 +2681,10 @@ int mpas_dyc_halo_exchange(mpas_dyc_ctx* ctx, const char* pool, const char* name
   ctx->plain_exchange = false;
   if (r) return r;
   HIPCHK(hipGetLastError());
+  for (auto& b : ctx->blk) {
+    const Field* f = find(b, pool, name);
+    if (f && f->me) ctx->bnd_ready = false;  // a maxEdges-strided mesh field: pack_mesh copies it again
+  }
   return MPAS_DYC_OK;
 }
 
@@ -2524,6 +2709,10 @@ static int get_summary(mpas_dyc_ctx* ctx, int32_t blocks, mpas_dyc_summary* out,
   if (scalar_minmax && n < 2 * ns) return MPAS_DYC_EINVAL;
   if (!ctx->summary_flags || !ctx->summary_tl) {
     ctx->err = "no summary: no step has run with summary modes on (mpas_dyc_set_summary)";
+    return MPAS_DYC_ESTATE;
+  }
+  if (ctx->tail_pending) {  // the records would describe the step before
+    ctx->err = "no summary: with MPAS_DYC_PHYSICS_MICROPHYSICS, call mpas_dyc_finish_step after the step first";
     return MPAS_DYC_ESTATE;
   }
   HIPCHK(hipSetDevice(ctx->device));
@@ -2656,13 +2845,20 @@ int mpas_dyc_set_lbc(mpas_dyc_ctx* ctx, int32_t apply, double seconds_to_interva
   if (!ctx || (apply != 0 && apply != 1)) return MPAS_DYC_EINVAL;
   if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
-  if (apply) {
+  // the mesh decides the kernel layout (pack_mesh); before it is known, compute_bnd checks
+  if (apply && ctx->bnd_ready) {
     for (auto& b : ctx->blk)
       if (!pair_layout(b.d)) {
-        ctx->err = "regional LBCs need the pair kernel layout (maxEdges <= 7)";
+        ctx->err = lbc_layout_error(b.d);
         return MPAS_DYC_EINVAL;
       }
   }
+#ifdef MPAS_WIDE
+  if (apply) {
+    ctx->err = lbc_layout_error(ctx->blk[0].d);
+    return MPAS_DYC_EINVAL;
+  }
+#endif
   if ((apply != 0) != ctx->lbc) {  // other exchange points and kernels: re-plan, re-capture
     ctx->lbc = apply != 0;
     for (auto& b : ctx->blk) b.d.lbc = apply;
@@ -2708,6 +2904,8 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
   if (ctx->host_only) return MPAS_DYC_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   CHK(plan_all(ctx, dt));
+  ctx->tail_pending = (ctx->physics & MPAS_DYC_PHYSICS_MICROPHYSICS) != 0;
+  if (ctx->profile) return profiled_step(ctx, dt);
   if (ctx->use_graph) {
     // one captured graph per buffer layout the step starts from; capturing runs srk3, whose
     // rotations move the host's view of the buffers, and a replay repeats them
@@ -2722,7 +2920,12 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
       HIPCHK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
       int r = srk3(ctx, dt);
       hipError_t e = hipStreamEndCapture(ctx->stream, &g);
-      if (r && r != MPAS_DYC_ECOMM) return r;
+      if (r && r != MPAS_DYC_ECOMM) {  // nothing ran: undo the capture's rotations of the host view
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        restore_layout(l0);
+        return r;
+      }
       if (r == MPAS_DYC_ECOMM && e == hipSuccess) e = hipErrorUnknown;  // RCCL refused to be captured
       if (e == hipSuccess) e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
       if (g) (void)hipGraphDestroy(g);
@@ -2760,12 +2963,33 @@ int mpas_dyc_timestep(mpas_dyc_ctx* ctx, double dt, int32_t itimestep) {
   return r;
 }
 
+int mpas_dyc_set_profile(mpas_dyc_ctx* ctx, int32_t on) {
+  if (!ctx) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
+  ctx->profile = on != 0;
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_get_profile(mpas_dyc_ctx* ctx, double* out, int32_t n) {
+  if (!ctx || !out || n < 1) return MPAS_DYC_EINVAL;
+  for (int i = 0; i < n; ++i) out[i] = i < 5 ? ctx->prof_out[i] : 0.0;
+  return MPAS_DYC_OK;
+}
+
+const char* mpas_dyc_last_exchange(const mpas_dyc_ctx* ctx) { return ctx ? ctx->last_key : ""; }
+
+int32_t mpas_dyc_rccl_version(void) {
+  int v = 0;
+  return ncclGetVersion(&v) == ncclSuccess ? v : -1;
+}
+
 int mpas_dyc_finish_step(mpas_dyc_ctx* ctx, double dt) {
   if (!ctx || !(dt > 0.0)) return MPAS_DYC_EINVAL;
   if (ctx->host_only) return MPAS_DYC_ESTATE;
   if (!(ctx->physics & MPAS_DYC_PHYSICS_MICROPHYSICS)) return MPAS_DYC_OK;  // the step ran its own tail
   HIPCHK(hipSetDevice(ctx->device));
   const std::vector<Ptrs> P = block_ptrs(ctx);
+  ctx->tail_pending = false;
   int r = step_tail(ctx, P, dt);
   HIPCHK(hipGetLastError());
   return r;
@@ -2851,6 +3075,23 @@ int mpas_dyc_set_overlap(mpas_dyc_ctx* ctx, int32_t on) {
 int mpas_dyc_use_graph(mpas_dyc_ctx* ctx, int32_t on) {
   if (!ctx) return MPAS_DYC_EINVAL;
   ctx->use_graph = on != 0;
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_block_layout(mpas_dyc_ctx* ctx, int32_t block, int32_t* out) {
+  Block* b = get_block(ctx, block);
+  if (!b || !out) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (!ctx->bnd_ready) CHK(compute_bnd(ctx));
+  out[0] = b->d.maxEdges;
+  out[1] = b->d.maxEdges2;
+  out[2] = pair_layout(b->d) ? 2 : batched(b->d) ? 1 : 0;
+#ifdef MPAS_WIDE
+  out[3] = 1;
+#else
+  out[3] = 0;
+#endif
   return MPAS_DYC_OK;
 }
 

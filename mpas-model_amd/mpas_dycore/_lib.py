@@ -22,7 +22,8 @@ EXPORTS = (
     "mpas_dyc_set_transport", "mpas_dyc_halo_exchange", "mpas_dyc_set_overlap", "mpas_dyc_output_diagnostics",
     "mpas_dyc_set_physics", "mpas_dyc_set_summary", "mpas_dyc_get_summary", "mpas_dyc_plan_exchanges",
     "mpas_dyc_graph_active", "mpas_dyc_solve_diagnostics", "mpas_dyc_set_lbc", "mpas_dyc_finish_step",
-    "mpas_dyc_get_block_summary",
+    "mpas_dyc_get_block_summary", "mpas_dyc_block_layout", "mpas_dyc_set_profile", "mpas_dyc_get_profile",
+    "mpas_dyc_last_exchange", "mpas_dyc_rccl_version",
 )
 HOST_ONLY = -2  # MPAS_DYC_HOST_ONLY: planner-only context
 PRINT_GLOBAL_MINMAX_VEL, PRINT_DETAILED_MINMAX_VEL, PRINT_GLOBAL_MINMAX_SCA = 1, 2, 4
@@ -149,6 +150,13 @@ def load() -> C.CDLL:
     lib.mpas_dyc_plan_exchanges.argtypes = [vp, i32, i32, dbl, C.POINTER(PlanMsg), i64, C.POINTER(i64), C.c_char_p,
                                             i64, C.POINTER(i64)]
     lib.mpas_dyc_graph_active.argtypes = [vp]
+    lib.mpas_dyc_block_layout.argtypes = [vp, i32, C.POINTER(i32)]
+    lib.mpas_dyc_set_profile.argtypes = [vp, i32]
+    lib.mpas_dyc_get_profile.argtypes = [vp, C.POINTER(dbl), i32]
+    lib.mpas_dyc_last_exchange.argtypes = [vp]
+    lib.mpas_dyc_last_exchange.restype = C.c_char_p
+    lib.mpas_dyc_rccl_version.argtypes = []
+    lib.mpas_dyc_rccl_version.restype = i32
     if os.environ.get("MPAS_DYCORE_LIB"):
         lib = _real
     _lib = lib

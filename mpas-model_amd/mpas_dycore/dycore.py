@@ -334,6 +334,37 @@ class Dycore:
                                                          C.byref(ms), ks), "time_acoustic_step")
         return ms.value, list(ks)
 
+    def layout(self, block: int = 0) -> dict:
+        """How the kernels see a block (mpas_dyc_block_layout): the maxEdges / maxEdges2 they index
+        with, the kernel family and the column shape."""
+        out = (C.c_int32 * 4)()
+        self._check(self.lib.mpas_dyc_block_layout(self.h, int(block), out), "block_layout")
+        return {"maxEdges": out[0], "maxEdges2": out[1], "family": ("general", "batched", "pair")[out[2]],
+                "column": ("wavefront", "workgroup")[out[3]]}
+
+    def exchange_profile(self, dt: float, itimestep: int = 1) -> dict:
+        """One eager atm_timestep with HIP events around every exchange's exposed part and every
+        RCCL group (mpas_dyc_set_profile / mpas_dyc_get_profile); synchronous.  Shift the time
+        levels afterwards as after any step."""
+        self._check(self.lib.mpas_dyc_set_profile(self.h, 1), "set_profile")
+        try:
+            self.atm_timestep(dt, itimestep)
+        finally:
+            self._check(self.lib.mpas_dyc_set_profile(self.h, 0), "set_profile")
+        out = (C.c_double * 5)()
+        self._check(self.lib.mpas_dyc_get_profile(self.h, out, 5), "get_profile")
+        return {"exchanges": int(out[0]), "ms_step_eager": out[1], "ms_exchange_exposed": out[2],
+                "ms_compute": out[1] - out[2], "rccl_groups": int(out[3]), "ms_rccl_groups": out[4]}
+
+    def last_exchange(self) -> str:
+        """Plan key of the exchange whose RCCL group was enqueued last (thread-safe read)."""
+        k = self.lib.mpas_dyc_last_exchange(self.h) if self.h else None
+        return k.decode() if k else ""
+
+    @staticmethod
+    def rccl_version() -> int:
+        return int(_lib.load().mpas_dyc_rccl_version())
+
     def acoustic_bytes(self) -> float:
         return self.lib.mpas_dyc_acoustic_bytes(self.h)
 

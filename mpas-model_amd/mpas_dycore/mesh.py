@@ -543,3 +543,42 @@ def _trisk(m):
     m["edgesOnEdge"] = eoe
     m["weightsOnEdge"] = w
     m["nEdgesOnEdge"] = neoe
+
+
+# arrays of a mesh / case whose second axis is the maxEdges (maxEdges2) slot
+MAX_EDGES_ARRAYS = ("edgesOnCell", "cellsOnCell", "verticesOnCell", "kiteForCell", "edgesOnCell_sign", "defc_a",
+                    "defc_b", "coeffs_reconstruct", "zb_cell", "zb3_cell")
+MAX_EDGES2_ARRAYS = ("edgesOnEdge", "weightsOnEdge")
+
+
+def pad_max_edges(m: dict, max_edges: int = 10, max_edges2: int = 20, fill: str = "none") -> dict:
+    """The same mesh (or case) declared with larger maxEdges / maxEdges2, as MPAS-distributed mesh files
+    declare them (maxEdges = 10, maxEdges2 = 20: "the largest number of neighbors that a primal mesh
+    cell may have", core_atmosphere/Registry.xml:13-16).  Slots past nEdgesOnCell / nEdgesOnEdge are
+    never read by the reference; they hold ``fill``: "none" -- index -1 (0 in the 1-based file), real
+    0 -- or "repeat" -- the row's last used entry repeated (index arrays; reals stay 0), the two
+    conventions MPAS mesh tools have written."""
+    out = dict(m)
+    out["maxEdges"], out["maxEdges2"] = int(max_edges), int(max_edges2)
+    for names, n_new, cnt in ((MAX_EDGES_ARRAYS, max_edges, "nEdgesOnCell"),
+                              (MAX_EDGES2_ARRAYS, max_edges2, "nEdgesOnEdge")):
+        for n in names:
+            if n not in m:
+                continue
+            a = np.asarray(m[n])
+            if a.shape[1] > n_new:
+                raise ValueError(f"{n} has {a.shape[1]} slots, more than {n_new}")
+            pad_shape = (a.shape[0], n_new - a.shape[1]) + a.shape[2:]
+            is_index = np.issubdtype(a.dtype, np.integer) and n != "kiteForCell"
+            pad = np.full(pad_shape, -1 if is_index else 0, dtype=a.dtype)
+            b = np.concatenate([a, pad], axis=1)
+            if is_index or n == "kiteForCell":
+                used = np.asarray(m[cnt])
+                slot = np.arange(n_new)[None, :]
+                if fill == "repeat":
+                    last = b[np.arange(b.shape[0]), np.maximum(used - 1, 0)]
+                    b = np.where(slot < used[:, None], b, last[:, None])
+                elif n != "kiteForCell":
+                    b = np.where(slot < used[:, None], b, -1)
+            out[n] = b
+    return out

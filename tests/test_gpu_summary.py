@@ -137,3 +137,22 @@ def test_summary_detailed_nan_aborts(case):
     with pytest.raises(DycoreError, match="NaN detected"):
         _step(dy, case)
     dy.close()
+
+
+def test_summary_refused_until_finish_step(case):
+    """With MPAS_DYC_PHYSICS_MICROPHYSICS the summary belongs to mpas_dyc_finish_step (atm_srk3
+    reduces after the microphysics, 1650-1660 then 1794): between the step and finish_step
+    get_summary refuses instead of returning the previous step's records."""
+    from mpas_dycore import Dycore, DycoreError
+    dt = case["dt"]
+    dy = Dycore(case, device=0, moist_end=3)
+    dy.init_diagnostics(dt)
+    dy.set_physics(tendencies=False, microphysics=True)
+    dy.atm_timestep(dt, 1)
+    with pytest.raises(DycoreError, match="finish_step"):
+        dy.summarize_timestep()
+    dy.finish_step(dt)
+    s = dy.summarize_timestep()
+    dy.shift_time_levels()
+    dy.close()
+    assert np.isfinite(s["w_max"]) and np.isfinite(s["u_max"])

@@ -97,3 +97,31 @@ def test_init_file_gives_the_same_case(tmp_path, version):
     for n in names:
         a, b = np.asarray(case[n]), np.asarray(got[n])
         assert a.shape == b.shape and np.array_equal(a, b), n
+
+
+@pytest.mark.parametrize("fill", ["none", "repeat"])
+def test_init_file_declaring_max_edges_10(tmp_path, fill):
+    """MPAS-distributed meshes declare maxEdges = 10, maxEdges2 = 20 whatever their cells' degree
+    (core_atmosphere/Registry.xml:13-16).  A file written that way reads back as the same case at
+    those strides: every slot a cell or edge uses equals the maxEdges = 6 case's, the model-init
+    precompute leaves the unused slots at 0, and the index padding is whatever the file held."""
+    from mpas_dycore.mesh import MAX_EDGES2_ARRAYS, MAX_EDGES_ARRAYS, pad_max_edges
+    case = jw_case(642, K=8, ns=3, moist=True, cache=False)
+    p0, p1 = str(tmp_path / "me6.nc"), str(tmp_path / "me10.nc")
+    mpas_files.write_init(p0, case, version=5)
+    mpas_files.write_init(p1, pad_max_edges(case, 10, 20, fill), version=5)
+    r0 = mpas_files.read_init(p0, config=case["config"])
+    r1 = mpas_files.read_init(p1, config=case["config"])
+    assert (r0["maxEdges"], r0["maxEdges2"], r1["maxEdges"], r1["maxEdges2"]) == (6, 12, 10, 20)
+    noc, noe = r0["nEdgesOnCell"], r0["nEdgesOnEdge"]
+    for names, cnt in ((MAX_EDGES_ARRAYS, noc), (MAX_EDGES2_ARRAYS, noe)):
+        for n in names:
+            a, b = np.asarray(r0[n]), np.asarray(r1[n])
+            used = np.arange(b.shape[1])[None, :] < cnt[:, None]
+            assert b.shape[1] in (10, 20) and a.shape[2:] == b.shape[2:], n
+            assert np.array_equal(a[used[:, :a.shape[1]]], b[used]), n
+            if b.dtype.kind == "f":
+                assert not b[~used].any(), n
+    for n, v in r0.items():
+        if isinstance(v, np.ndarray) and n not in MAX_EDGES_ARRAYS + MAX_EDGES2_ARRAYS:
+            assert np.array_equal(v, r1[n]), n

@@ -17,6 +17,7 @@ import pytest
 
 from mpas_dycore import _lib, decomp
 from mpas_dycore.dycore import plan_exchanges
+from mpas_dycore.preflight import PlanMismatch, check_plans
 
 
 @pytest.fixture(scope="module")
@@ -35,25 +36,21 @@ def _plans(case, nranks, overlap=None):
 
 
 def _check_matching(plans, nranks):
-    keys0 = plans[0][1]
-    assert len(keys0) > 40
-    for r in range(nranks):
-        assert plans[r][1] == keys0, f"rank {r} issues a different exchange sequence"
-    npts = len(keys0)
-    nmsg = 0
-    for r in range(nranks):
-        sends = plans[r][0][plans[r][0]["direction"] == _lib.SEND]
-        for p in range(nranks):
-            recvs = plans[p][0][plans[p][0]["direction"] == _lib.RECV]
-            for i in range(npts):
-                s = sends[(sends["point"] == i) & (sends["peer_rank"] == p)]
-                v = recvs[(recvs["point"] == i) & (recvs["peer_rank"] == r)]
-                # the RCCL pairing: the k-th send r->p matches the k-th receive at p from r
-                assert len(s) == len(v), f"point {i} ({keys0[i]}): {len(s)} sends {r}->{p}, {len(v)} receives"
-                assert np.array_equal(s["count"], v["count"]), f"point {i}: message sizes {r}->{p} differ"
-                assert np.array_equal(s["peer_block"], v["block"]) and np.array_equal(s["block"], v["peer_block"])
-                nmsg += len(s)
-    return nmsg
+    assert len(plans) == nranks
+    got = check_plans(plans)
+    assert got["plan_keys"] > 40
+    return got["messages"]
+
+
+def test_mismatch_is_reported(case163842):
+    """A rank whose receive list differs is caught before any GPU call, naming the exchange."""
+    plans = _plans(case163842, 2)
+    msgs = plans[1][0].copy()
+    j = np.flatnonzero(msgs["direction"] == _lib.RECV)[3]
+    msgs["count"][j] += 1
+    with pytest.raises(PlanMismatch) as e:
+        check_plans([plans[0], (msgs, plans[1][1])])
+    assert e.value.key == plans[0][1][e.value.point]
 
 
 @pytest.mark.parametrize("nranks", [2, 4, 8])

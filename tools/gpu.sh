@@ -23,6 +23,8 @@
 #   kprof            rocprofv3 kernel stats of tools/kbench.py for each of AB_LIBS (gpurun_out/kprof_<i>)
 #   kpmc             two rocprofv3 --pmc passes (SQ wait/active cycles; TA/TCP/TCC traffic) of one
 #                    eager tools/kbench.py dt for each of AB_LIBS (gpurun_out/kpmc_<lib>_<set>)
+#   maxedges         bench.py with the mesh declared maxEdges 6 vs 10 (AB_ROUNDS rounds), and from an init file
+#                    declaring maxEdges 10 (tools/write_init.py)
 #   smoke            __graft_entry__.smoke()
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out || exit 1
 B="--no-cpu-baseline --no-configs1"
@@ -61,6 +63,15 @@ step() {
           for C in "${KPMC_SET1:-SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES}" "${KPMC_SET2:-TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum}"; do
             MPAS_DYCORE_LIB=$L timeout -s KILL 240 rocprofv3 --pmc $C -d gpurun_out/kpmc_${i}_$j -o pmc --output-format csv -- python3 tools/kbench.py --steps 1 --reps 1 --no-graph > gpurun_out/kpmc_${i}_$j.log 2>&1 || return 1
             j=$((j+1)); done; echo "kpmc_$i = $L"; i=$((i+1)); done ;;
+    maxedges) rm -f gpurun_out/maxedges.log
+        for r in ${AB_ROUNDS:-1 2}; do for M in "" "--max-edges 10,20"; do
+          echo "== bench $M" >> gpurun_out/maxedges.log
+          timeout -k 10 300 python bench.py --steps 10 --warmup 2 $B $M >> gpurun_out/maxedges.log 2>&1 || return 1
+        done; done
+        timeout -k 10 400 python tools/write_init.py --max-edges 10,20 /tmp/x1.163842.me10.init.nc >> gpurun_out/maxedges.log 2>&1 || return 1
+        echo "== bench --init (maxEdges 10)" >> gpurun_out/maxedges.log
+        timeout -k 10 400 python bench.py --steps 10 --warmup 2 $B --init /tmp/x1.163842.me10.init.nc --dt 360 --len-disp 60000 >> gpurun_out/maxedges.log 2>&1 || return 1
+        grep -h "==\|ms_per_step" gpurun_out/maxedges.log | sed 's/.*"ms_per_step": \([0-9.]*\).*"kernel_layout": \({[^}]*}\).*/ms_per_step \1 \2/' ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && last gpurun_out/smoke.log ;;
     *) echo "unknown step $1"; return 2 ;;
   esac
