@@ -1402,8 +1402,9 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
       LAUNCH(k_dyn_cells2, d.nCells, d, p);
     } else {
       if (s.h_mom_eddy_visc4 > 0.0) {
-        if (m6) LAUNCH(k_dyn_delsq_vc_b<6>, d.nVertices + d.nCells, d, p);
-        else LAUNCH(k_dyn_delsq_vc_b<7>, d.nVertices + d.nCells, d, p);
+        const int nvc = 3 * std::max((d.nVertices + 1) / 2, d.nCells);  // interleaved (k_dyn_delsq_vc_b)
+        if (m6) LAUNCH(k_dyn_delsq_vc_b<6>, nvc, d, p);
+        else LAUNCH(k_dyn_delsq_vc_b<7>, nvc, d, p);
       }
       LAUNCH(k_dyn_edges_rk1b_b, d.nEdgesSolve, d, p, cf, s, tp);
       if (m6) LAUNCH(k_dyn_cells2_b<6>, d.nCells, d, p);
@@ -2707,12 +2708,12 @@ static int get_summary(mpas_dyc_ctx* ctx, int32_t blocks, mpas_dyc_summary* out,
   if (ctx->host_only) return MPAS_DYC_ESTATE;
   const int ns = ctx->blk[0].d.ns;
   if (scalar_minmax && n < 2 * ns) return MPAS_DYC_EINVAL;
-  if (!ctx->summary_flags || !ctx->summary_tl) {
-    ctx->err = "no summary: no step has run with summary modes on (mpas_dyc_set_summary)";
+  if (ctx->tail_pending) {  // the records would describe the step before, if any
+    ctx->err = "no summary: with MPAS_DYC_PHYSICS_MICROPHYSICS, call mpas_dyc_finish_step after the step first";
     return MPAS_DYC_ESTATE;
   }
-  if (ctx->tail_pending) {  // the records would describe the step before
-    ctx->err = "no summary: with MPAS_DYC_PHYSICS_MICROPHYSICS, call mpas_dyc_finish_step after the step first";
+  if (!ctx->summary_flags || !ctx->summary_tl) {
+    ctx->err = "no summary: no step has run with summary modes on (mpas_dyc_set_summary)";
     return MPAS_DYC_ESTATE;
   }
   HIPCHK(hipSetDevice(ctx->device));

@@ -880,13 +880,20 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_cells2(Dims d, Ptrs p) {
   if (k <= K) p.tend_w_euler[(size_t)c * (K + 1) + k] = (act && k >= 1) ? tw : 0.0;
 }
 
+// Vertices and cells interleaved, two vertices then one cell per three waves: vertex 2j, 2j+1 and cell
+// j lie at the same place of the space-filling curve (vertices are numbered in cell order, nVertices
+// ~ 2 nCells), so one XCD's slab of waves reads delsq_u of one region once for both halves instead of
+// the vertex and cell halves each streaming all of delsq_u through different L2s.  Launch
+// 3 * max(ceil(nVertices / 2), nCells) waves.
 template <int ME>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_delsq_vc_b(Dims d, Ptrs p) {
   const int idx = wave_elem(0);
   const int k = lane_id(), K = d.K;
   if (k >= K) return;
-  if (idx < d.nVertices) {
-    const int v = idx;
+  const int j3 = idx / 3, t3 = idx - 3 * j3;
+  if (t3 < 2) {
+    const int v = 2 * j3 + t3;
+    if (v >= d.nVertices) return;
     int ei[3];
     double sg[3];
 #pragma unroll
@@ -907,7 +914,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_dyn_delsq_vc_b(Dims d, Ptrs p
     for (int i = 0; i < 3; ++i) dv = dv + (iat * dc[i] * sg[i]) * du[i];
     p.delsq_vorticity[(size_t)v * K + k] = dv;
   } else {
-    const int c = idx - d.nVertices;
+    const int c = j3;
     if (c >= d.nCells) return;
     const CellSten<ME> st = load_sten<ME>(p, c);
     double sdv[ME], du[ME];
@@ -2301,7 +2308,6 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
                ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
   }
   const d2 uh = ld2(p.ruAvg + o);
-  const double sgx = sgn1(uh.x), sgy = sgn1(uh.y);
   const bool hex = na == 10;  // the reference's unrolled hexagon form (3363-3390)
   bool st = (h == 0 || hasB) && 2 * l < K;
   // regional: edges of the two outer relaxation rows take a first-order upwind flux, and
@@ -2320,10 +2326,20 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
     }
     return;
   }
-  for (int is = 0; is < ns; ++is) {
-    d2 sv[NA];
+  // the first scalar's gathers go out before anything waits for uh (the sign of the flux): issued
+  // after the sign, they would start one memory round trip late (tools/gather_floor: 329 us against
+  // 246 us for the same loads alone).  The scheduling barrier keeps the compiler from pulling the
+  // sign's use back above them.
+  d2 sv[NA];
 #pragma unroll
-    for (int j = 0; j < NA; ++j) sv[j] = ld2(p.scalars2 + SIX(ic[j], 2 * lc, is));
+  for (int j = 0; j < NA; ++j) sv[j] = ld2(p.scalars2 + SIX(ic[j], 2 * lc, 0));
+  __builtin_amdgcn_sched_barrier(0);
+  const double sgx = sgn1(uh.x), sgy = sgn1(uh.y);
+  for (int is = 0; is < ns; ++is) {
+    if (is > 0) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) sv[j] = ld2(p.scalars2 + SIX(ic[j], 2 * lc, is));
+    }
     d2 acc{0.0, 0.0};
     if (hex) {
       acc.x = (a[0] + sgx * b[0]) * sv[0].x;
@@ -2383,6 +2399,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
 #pragma unroll
   for (int j = 0; j < NA; ++j) sv[j] = val(p.scalars2, ic[j]);
   const d2 so1 = val(p.scalars1, c1), so2 = val(p.scalars1, c2);
+  __builtin_amdgcn_sched_barrier(0);  // every gather issued before the first wait (see k_scalars_edges_p)
   auto flux = [&](double u, int lev) {
     double acc = 0.0;
     if (na == 10) {

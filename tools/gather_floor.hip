@@ -1,0 +1,307 @@
+// The floor of the gather kernels' access patterns on MI355X (VERDICT r03 "Next 2").
+//
+// Replays the real index streams of the x1.163842 mesh (dumped by tools/gather_floor.py) through
+// three of the library's own kernels, on the same device data layout:
+//   advflux   k_dyn_advflux_p<10>           10 stencil cells x (w, theta_m) per edge
+//   scalars   k_scalars_edges_p<10>         10 stencil cells x scalars per edge
+//   dynedges  k_dyn_edges_p<false, 10>      10 TRiSK edges x (u, pv_edge) + 2 cells x 4 fields
+// next to a "floor" twin of each: the same wave -> edge mapping (pair layout, XCD slabs), the same
+// index loads, the same 16-byte column gathers and own-column loads, the same stores, but a plain sum
+// instead of the flux arithmetic -- what that access pattern costs with nothing else in the way.  A
+// "stream" twin moves the same number of bytes per edge from contiguous per-edge columns (no index
+// indirection): the cost of the bytes alone.  Each variant is timed with HIP events over REPS
+// launches, in interleaved rounds; the median per launch is printed.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/gather_floor.hip -o tools/gather_floor
+//   tools/gather_floor DUMPDIR [reps] [rounds]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../mpas-model_amd/csrc/kernels.hip"
+
+using namespace mpas;
+
+#define CK(x)                                                                              \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) {                                                                \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));    \
+      exit(1);                                                                             \
+    }                                                                                      \
+  } while (0)
+
+template <class T>
+std::vector<T> load(const std::string& dir, const char* name, size_t n) {
+  std::vector<T> v(n);
+  FILE* f = fopen((dir + "/" + name).c_str(), "rb");
+  if (!f || fread(v.data(), sizeof(T), n, f) != n) {
+    fprintf(stderr, "cannot read %zu values from %s/%s\n", n, dir.c_str(), name);
+    exit(1);
+  }
+  fclose(f);
+  return v;
+}
+
+template <class T>
+T* dev(const std::vector<T>& h) {
+  T* d = nullptr;
+  CK(hipMalloc(&d, h.size() * sizeof(T) + 256));
+  CK(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+
+double* dev_field(size_t n, unsigned seed) {  // smooth positive values, 256 B of slack
+  std::vector<double> h(n);
+  for (size_t i = 0; i < n; ++i) h[i] = 1.0 + 1e-3 * (double)((i * 2654435761u + seed) % 1000);
+  return dev(h);
+}
+
+// ---- floor twins: the real kernel's loads and stores, a plain sum for the arithmetic --------------
+__global__ __launch_bounds__(EDGE_THREADS) void f_advflux(Dims d, Ptrs p) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  const size_t K1 = K + 1;
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  int ic[10];
+  double a[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
+    a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j)) +
+           sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
+               ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
+  }
+  const d2 rue = ld2(p.ru + o);
+  const bool onA = ceA.x < d.nCellsSolve || ceA.y < d.nCellsSolve;
+  const bool onB = hasB && (ceB.x < d.nCellsSolve || ceB.y < d.nCellsSolve);
+  if (!onA && !onB) return;
+  d2 fw = rue, ft = rue;
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const d2 w_ = ld2(p.w2 + (size_t)ic[j] * K1 + 2 * lw), t_ = ld2(p.theta_m2 + (size_t)ic[j] * K + 2 * lc);
+    fw.x += a[j] * w_.x;
+    fw.y += a[j] * w_.y;
+    ft.x += a[j] * t_.x;
+    ft.y += a[j] * t_.y;
+  }
+  if ((h ? onB : onA) && 2 * l < K) {
+    st2(p.advflux_w + o, fw);
+    st2(p.advflux_th + o, ft);
+  }
+}
+
+// the same bytes per edge from contiguous columns: edge e reads columns 10 e .. 10 e + 9 of two
+// (10 nE)-column arrays
+__global__ __launch_bounds__(EDGE_THREADS) void s_advflux(Dims d, Ptrs p, const double* __restrict__ W,
+                                                          const double* __restrict__ T) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  const size_t K1 = K + 1;
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const d2 rue = ld2(p.ru + o);
+  d2 fw = rue, ft = rue;
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const size_t c = (size_t)e * 10 + j;
+    const d2 w_ = ld2(W + c * K1 + 2 * lw), t_ = ld2(T + c * K + 2 * lc);
+    fw.x += w_.x;
+    fw.y += w_.y;
+    ft.x += t_.x;
+    ft.y += t_.y;
+  }
+  if ((h == 0 || hasB) && 2 * l < K) {
+    st2(p.advflux_w + o, fw);
+    st2(p.advflux_th + o, ft);
+  }
+}
+
+__global__ __launch_bounds__(EDGE_THREADS) void f_scalars(Dims d, Ptrs p) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31, ns = d.ns;
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  int ic[10];
+  double a[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
+    a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j)) +
+           sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
+               ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
+  }
+  const d2 uh = ld2(p.ruAvg + o);
+  const bool st = (h == 0 || hasB) && 2 * l < K;
+  for (int is = 0; is < ns; ++is) {
+    d2 acc = uh;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const d2 sv = ld2(p.scalars2 + SIX(ic[j], 2 * lc, is));
+      acc.x += a[j] * sv.x;
+      acc.y += a[j] * sv.y;
+    }
+    if (st) st2(p.horiz_flux_array + HIX(e, 2 * lc, is), acc);
+  }
+}
+
+__global__ __launch_bounds__(EDGE_THREADS) void f_dynedges(Dims d, Ptrs p) {
+  const int eA = 2 * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  const int e = sel(h, eA, eB);
+  const size_t K1 = K + 1;
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const double invDc = sel(h, ld_uniform_f64(p.invDcEdge + eA), ld_uniform_f64(p.invDcEdge + eB));
+  const d2 re = ld2(p.rho_edge + o);
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
+  const size_t o1 = (size_t)c1 * K + 2 * lc, o2 = (size_t)c2 * K + 2 * lc;
+  int eoe[10];
+  double wgt[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    eoe[j] = sel(h, p.edgesOnEdge[(size_t)eA * d.maxEdges2 + j], p.edgesOnEdge[(size_t)eB * d.maxEdges2 + j]);
+    wgt[j] = sel(h, ld_uniform_f64(p.weightsOnEdge + (size_t)eA * d.maxEdges2 + j),
+                 ld_uniform_f64(p.weightsOnEdge + (size_t)eB * d.maxEdges2 + j));
+  }
+  const d2 uk = ld2(p.u2 + o), pve = ld2(p.pv_edge + o), tue = ld2(p.tend_u_euler + o);
+  const d2 rw1 = ld2(p.rw + (size_t)c1 * K1 + 2 * lw), rw2 = ld2(p.rw + (size_t)c2 * K1 + 2 * lw);
+  const d2 ke1 = ld2(p.ke + o1), ke2 = ld2(p.ke + o2), hd1 = ld2(p.h_divergence + o1), hd2 = ld2(p.h_divergence + o2);
+  d2 q{invDc * re.x + uk.x + pve.x + tue.x + rw1.x + rw2.x + ke1.x + ke2.x + hd1.x + hd2.x,
+       re.y + uk.y + pve.y + tue.y + rw1.y + rw2.y + ke1.y + ke2.y + hd1.y + hd2.y};
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const size_t oj = (size_t)eoe[j] * K + 2 * lc;
+    const d2 pv = ld2(p.pv_edge + oj), uu = ld2(p.u2 + oj);
+    q.x += wgt[j] * uu.x * pv.x;
+    q.y += wgt[j] * uu.y * pv.y;
+  }
+  const bool solve = h ? (hasB && eB < d.nEdgesSolve) : (eA < d.nEdgesSolve);
+  if (solve && 2 * l < K) st2(p.tend_u + o, q);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    fprintf(stderr, "usage: %s DUMPDIR [reps] [rounds]\n", argv[0]);
+    return 2;
+  }
+  const std::string dir = argv[1];
+  const int reps = argc > 2 ? atoi(argv[2]) : 20, rounds = argc > 3 ? atoi(argv[3]) : 5;
+  int nC, nE, nV, K, ns;
+  {
+    FILE* f = fopen((dir + "/meta.txt").c_str(), "r");
+    if (!f || fscanf(f, "%d %d %d %d %d", &nC, &nE, &nV, &K, &ns) != 5) {
+      fprintf(stderr, "bad %s/meta.txt\n", dir.c_str());
+      return 1;
+    }
+    fclose(f);
+  }
+  if (K % 2 || K > 64) {
+    fprintf(stderr, "even K <= 64 only\n");
+    return 1;
+  }
+  Dims d{};
+  d.nCells = nC;
+  d.nEdges = nE;
+  d.nVertices = nV;
+  d.K = K;
+  d.maxEdges = 6;
+  d.maxEdges2 = 10;
+  d.ns = ns;
+  d.nCellsSolve = nC;
+  d.nEdgesSolve = nE;
+  d.nVerticesSolve = nV;
+  Ptrs p{};
+  p.advCellsForEdge = dev(load<int>(dir, "advCellsForEdge.i32", (size_t)(nE + 1) * 15));
+  p.nAdvCellsForEdge = dev(load<int>(dir, "nAdvCellsForEdge.i32", (size_t)nE + 1));
+  p.cellsOnEdge = dev(load<int>(dir, "cellsOnEdge.i32", (size_t)(nE + 1) * 2));
+  p.edgesOnEdge = dev(load<int>(dir, "edgesOnEdge.i32", (size_t)(nE + 1) * 10));
+  p.nEdgesOnEdge = dev(load<int>(dir, "nEdgesOnEdge.i32", (size_t)nE + 1));
+  p.adv_coefs = dev(load<double>(dir, "adv_coefs.f64", (size_t)(nE + 1) * 15));
+  p.adv_coefs_3rd = dev(load<double>(dir, "adv_coefs_3rd.f64", (size_t)(nE + 1) * 15));
+  p.weightsOnEdge = dev(load<double>(dir, "weightsOnEdge.f64", (size_t)(nE + 1) * 10));
+  const size_t cK = (size_t)(nC + 1) * K, cK1 = (size_t)(nC + 1) * (K + 1), eK = (size_t)(nE + 1) * K;
+  unsigned seed = 1;
+  p.invDcEdge = dev_field(nE + 1, seed++);
+  p.fzm = dev_field(K, seed++);
+  p.fzp = dev_field(K, seed++);
+  p.rdzw = dev_field(K, seed++);
+  p.w2 = dev_field(cK1, seed++);
+  p.rw = dev_field(cK1, seed++);
+  p.theta_m2 = dev_field(cK, seed++);
+  p.ke = dev_field(cK, seed++);
+  p.h_divergence = dev_field(cK, seed++);
+  p.scalars2 = dev_field(cK * ns, seed++);
+  for (double** f : {&p.ru, &p.ruAvg, &p.advflux_w, &p.advflux_th, &p.rho_edge, &p.u2, &p.pv_edge, &p.tend_u_euler,
+                     &p.tend_u})
+    *f = dev_field(eK, seed++);
+  p.horiz_flux_array = dev_field(eK * ns, seed++);
+  double* W10 = dev_field((size_t)nE * 10 * (K + 1), seed++);
+  double* T10 = dev_field((size_t)nE * 10 * K, seed++);
+  Config cf{};
+  DynTendScal s{};
+  s.rk_step = 2;
+  const dim3 blk(EDGE_THREADS), grid((unsigned)(((nE + 1) / 2 + EDGE_WPB - 1) / EDGE_WPB));
+  struct V {
+    const char* name;
+    std::function<void()> run;
+    std::vector<double> us;
+  };
+  std::vector<V> vs = {
+      {"advflux kernel", [&] { hipLaunchKernelGGL((k_dyn_advflux_p<10, false>), grid, blk, 0, 0, d, p); }, {}},
+      {"advflux floor", [&] { hipLaunchKernelGGL(f_advflux, grid, blk, 0, 0, d, p); }, {}},
+      {"advflux stream", [&] { hipLaunchKernelGGL(s_advflux, grid, blk, 0, 0, d, p, W10, T10); }, {}},
+      {"scalars kernel", [&] { hipLaunchKernelGGL((k_scalars_edges_p<10, false>), grid, blk, 0, 0, d, p); }, {}},
+      {"scalars floor", [&] { hipLaunchKernelGGL(f_scalars, grid, blk, 0, 0, d, p); }, {}},
+      {"dynedges kernel",
+       [&] { hipLaunchKernelGGL((k_dyn_edges_p<false, 10, false, false>), grid, blk, 0, 0, d, p, cf, s, 0, XPack{}); },
+       {}},
+      {"dynedges floor", [&] { hipLaunchKernelGGL(f_dynedges, grid, blk, 0, 0, d, p); }, {}},
+  };
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (auto& v : vs) v.run();  // warm
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < rounds; ++r)
+    for (auto& v : vs) {
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < reps; ++i) v.run();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.us.push_back(1e3 * ms / reps);
+    }
+  CK(hipGetLastError());
+  printf("x1.%d, K = %d, ns = %d, %d launches x %d rounds, median us per launch\n", nC, K, ns, reps, rounds);
+  for (auto& v : vs) {
+    std::sort(v.us.begin(), v.us.end());
+    printf("%-16s %8.1f   (min %.1f max %.1f)\n", v.name, v.us[v.us.size() / 2], v.us.front(), v.us.back());
+  }
+  return 0;
+}
