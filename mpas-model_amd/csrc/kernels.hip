@@ -2308,6 +2308,7 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
                ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
   }
   const d2 uh = ld2(p.ruAvg + o);
+  const double sgx = sgn1(uh.x), sgy = sgn1(uh.y);
   const bool hex = na == 10;  // the reference's unrolled hexagon form (3363-3390)
   bool st = (h == 0 || hasB) && 2 * l < K;
   // regional: edges of the two outer relaxation rows take a first-order upwind flux, and
@@ -2326,20 +2327,10 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
     }
     return;
   }
-  // the first scalar's gathers go out before anything waits for uh (the sign of the flux): issued
-  // after the sign, they would start one memory round trip late (tools/gather_floor: 329 us against
-  // 246 us for the same loads alone).  The scheduling barrier keeps the compiler from pulling the
-  // sign's use back above them.
-  d2 sv[NA];
-#pragma unroll
-  for (int j = 0; j < NA; ++j) sv[j] = ld2(p.scalars2 + SIX(ic[j], 2 * lc, 0));
-  __builtin_amdgcn_sched_barrier(0);
-  const double sgx = sgn1(uh.x), sgy = sgn1(uh.y);
   for (int is = 0; is < ns; ++is) {
-    if (is > 0) {
+    d2 sv[NA];
 #pragma unroll
-      for (int j = 0; j < NA; ++j) sv[j] = ld2(p.scalars2 + SIX(ic[j], 2 * lc, is));
-    }
+    for (int j = 0; j < NA; ++j) sv[j] = ld2(p.scalars2 + SIX(ic[j], 2 * lc, is));
     d2 acc{0.0, 0.0};
     if (hex) {
       acc.x = (a[0] + sgx * b[0]) * sv[0].x;
@@ -2399,7 +2390,6 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
 #pragma unroll
   for (int j = 0; j < NA; ++j) sv[j] = val(p.scalars2, ic[j]);
   const d2 so1 = val(p.scalars1, c1), so2 = val(p.scalars1, c2);
-  __builtin_amdgcn_sched_barrier(0);  // every gather issued before the first wait (see k_scalars_edges_p)
   auto flux = [&](double u, int lev) {
     double acc = 0.0;
     if (na == 10) {
