@@ -157,6 +157,19 @@ int mpas_dyc_finish_step(mpas_dyc_ctx* ctx, double dt);
  * seconds into the step is then state - (seconds_to_interval_end - delta) * tendency, as
  * mpas_atm_get_bdy_state (:337-409) computes it.  All scalars are driven. */
 int mpas_dyc_set_lbc(mpas_dyc_ctx* ctx, int32_t apply, double seconds_to_interval_end);
+/* The model-init precompute of atm_mpas_init_block (mpas_atm_core.F:311-358, 456-458; the routines at
+ * 927-1288), on the device, for every block: invAreaCell, invDvEdge, invDcEdge, invAreaTriangle;
+ * atm_compute_signs (edgesOnVertex_sign, edgesOnCell_sign, zb_cell, zb3_cell, kiteForCell);
+ * atm_adv_coef_compression (nAdvCellsForEdge, advCellsForEdge, adv_coefs, adv_coefs_3rd);
+ * atm_couple_coef_3rd_order (config_coef_3rd_order of the context's config);
+ * atm_compute_mesh_scaling (meshScalingDel2 / Del4, meshScalingRegionalCell / Edge,
+ * config_h_ScaleWithMesh) and atm_compute_damping_coefs (dss, config_zd, config_xnutr).
+ * It reads what the init file holds, set beforehand with mpas_dyc_set_field: the connectivity,
+ * dcEdge, dvEdge, zgrid and mesh.deriv_two (15, 2, nEdges+1), mesh.zb / zb3 (nVertLevels+1, 2,
+ * nEdges+1), mesh.meshDensity, mesh.areaCell (nCells+1), mesh.areaTriangle (nVertices+1).
+ * Bitwise the reference's arithmetic; x**0.25 and sin are correctly rounded (the reference's C library
+ * is 1 ulp away for ~0.1 % of arguments).  Synchronous. */
+int mpas_dyc_model_init(mpas_dyc_ctx* ctx, int32_t h_scale_with_mesh, double config_zd, double config_xnutr);
 /* atm_compute_output_diagnostics(state, time_level, diag, mesh) (mpas_atm_core.F:753, called
  * before history writes at :544 and :694): diag theta, rho and pressure from theta_m, rho_zz,
  * scalars(index_qv) of the time level, zz, pressure_base and pressure_p.  Asynchronous. */

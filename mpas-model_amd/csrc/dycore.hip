@@ -28,6 +28,7 @@
 #include "halo.hip"
 #include "summary.hip"
 #include "lbc.hip"
+#include "model_init.hip"
 
 using namespace mpas;
 
@@ -55,6 +56,9 @@ struct Field {
   int me = 0;
   void* packed = nullptr;
   int64_t packed_inner = 0;
+  // allocated at its first set_field: the inputs only the model-init precompute reads (deriv_two, zb,
+  // zb3, meshDensity, areaCell, areaTriangle -- mpas_dyc_model_init)
+  bool lazy = false;
 };
 
 // One entry of a block's multihalo exchange list (mpas_multihalo_exchange_list:
@@ -362,6 +366,15 @@ void build_registry(Block& c) {
     c.fields[a].rot = b;
     c.fields[b].rot = a;
   }
+  // inputs of the model-init precompute (mpas_dyc_model_init), allocated when set
+  add(c, "mesh", "deriv_two", L_EDGE, 30);
+  add(c, "mesh", "zb", L_EDGE, 2 * (int64_t)(K + 1));
+  add(c, "mesh", "zb3", L_EDGE, 2 * (int64_t)(K + 1));
+  add(c, "mesh", "meshDensity", L_CELL, 1);
+  add(c, "mesh", "areaCell", L_CELL, 1);
+  add(c, "mesh", "areaTriangle", L_VERTEX, 1);
+  for (const char* n : {"deriv_two", "zb", "zb3", "meshDensity", "areaCell", "areaTriangle"})
+    c.fields[c.by_name[std::string("mesh.") + n]].lazy = true;
   // the maxEdges- and maxEdges2-strided mesh arrays (pack_mesh)
   for (const char* n : {"edgesOnCell", "cellsOnCell", "verticesOnCell", "kiteForCell", "coeffs_reconstruct",
                         "edgesOnCell_sign", "defc_a", "defc_b", "zb_cell", "zb3_cell"})
@@ -601,7 +614,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   std::vector<RecSeg> rec_pack, rec_unpack;
   auto field_of = [&](Block& b, const XField& f) -> Field* {
     Field* F = find(b, f.pool, f.name);
-    if (!F || F->is_int || F->loc == L_NONE) {
+    if (!F || F->is_int || F->loc == L_NONE || !F->buf[0]) {
       ctx->err = std::string("halo exchange of unsupported field ") + f.pool + "." + f.name;
       return nullptr;
     }
@@ -2342,6 +2355,7 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   for (auto& b : ctx->blk) {
     build_registry(b);
     for (auto& f : b.fields) {
+      if (f.lazy) continue;
       // 256 B of slack: the two-levels-per-lane kernels read 16 B at the last level of the last column
       const int64_t nb = field_bytes(b, f) + 256;
       for (int t = 0; t < f.ntl; ++t) {
@@ -2462,6 +2476,7 @@ int mpas_dyc_set_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
   }
   const int slot = slot_of(ctx, *f, time_level);
   HIPCHK(hipSetDevice(ctx->device));
+  if (f->lazy && !f->buf[slot]) HIPCHK(hipMalloc(&f->buf[slot], nb + 256));
   if (f->me) ctx->bnd_ready = false;  // pack_mesh copies the new image for the kernels
   if (f->is_int && f->target != T_NONE) {
     // MPAS 1-based -> device 0-based; out-of-range / 0 -> garbage slot
@@ -2554,6 +2569,10 @@ int mpas_dyc_get_block_field(mpas_dyc_ctx* ctx, int32_t block, const char* pool,
   if (nbytes != nb) {
     ctx->err = "size mismatch for " + f->pool + "." + f->name;
     return MPAS_DYC_EINVAL;
+  }
+  if (!f->buf[slot_of(ctx, *f, time_level)]) {
+    ctx->err = f->pool + "." + f->name + " has not been set";
+    return MPAS_DYC_ESTATE;
   }
   HIPCHK(hipSetDevice(ctx->device));
   if (f->nsub > 1) {  // scalar-major -> Fortran (nsub, inner/nsub, n+1)
@@ -2883,6 +2902,83 @@ int mpas_dyc_set_physics(mpas_dyc_ctx* ctx, int32_t flags) {
   ctx->physics = flags;
   for (auto& b : ctx->blk) b.d.physics = (flags & MPAS_DYC_PHYSICS_TENDENCIES) ? 1 : 0;
   drop_graphs(ctx);  // captured steps bake the flags in
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_model_init(mpas_dyc_ctx* ctx, int32_t h_scale_with_mesh, double config_zd, double config_xnutr) {
+  if (!ctx) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
+  HIPCHK(hipSetDevice(ctx->device));
+  for (auto& b : ctx->blk) {
+    for (const char* n : {"deriv_two", "zb", "zb3", "meshDensity", "areaCell", "areaTriangle"})
+      if (!find(b, "mesh", n)->buf[0]) {
+        ctx->err = std::string("mpas_dyc_model_init needs mesh.") + n + " (set it first)";
+        return MPAS_DYC_ESTATE;
+      }
+    // the declared-stride images (buf), not the kernels' packed copies: pack_mesh redoes those after
+    auto I = [&](const char* n) { return (int*)find(b, "mesh", n)->buf[0]; };
+    auto R = [&](const char* n) { return (double*)find(b, "mesh", n)->buf[0]; };
+    MInit m{};
+    m.nEdgesOnCell = I("nEdgesOnCell");
+    m.edgesOnCell = I("edgesOnCell");
+    m.cellsOnCell = I("cellsOnCell");
+    m.verticesOnCell = I("verticesOnCell");
+    m.cellsOnEdge = I("cellsOnEdge");
+    m.verticesOnEdge = I("verticesOnEdge");
+    m.cellsOnVertex = I("cellsOnVertex");
+    m.edgesOnVertex = I("edgesOnVertex");
+    m.deriv_two = R("deriv_two");
+    m.zb = R("zb");
+    m.zb3 = R("zb3");
+    m.meshDensity = R("meshDensity");
+    m.areaCell = R("areaCell");
+    m.areaTriangle = R("areaTriangle");
+    m.dcEdge = R("dcEdge");
+    m.dvEdge = R("dvEdge");
+    m.zgrid = R("zgrid");
+    m.invAreaCell = R("invAreaCell");
+    m.invDvEdge = R("invDvEdge");
+    m.invDcEdge = R("invDcEdge");
+    m.invAreaTriangle = R("invAreaTriangle");
+    m.edgesOnVertex_sign = R("edgesOnVertex_sign");
+    m.edgesOnCell_sign = R("edgesOnCell_sign");
+    m.zb_cell = R("zb_cell");
+    m.zb3_cell = R("zb3_cell");
+    m.kiteForCell = I("kiteForCell");
+    m.nAdvCellsForEdge = I("nAdvCellsForEdge");
+    m.advCellsForEdge = I("advCellsForEdge");
+    m.adv_coefs = R("adv_coefs");
+    m.adv_coefs_3rd = R("adv_coefs_3rd");
+    m.meshScalingDel2 = R("meshScalingDel2");
+    m.meshScalingDel4 = R("meshScalingDel4");
+    m.meshScalingRegionalCell = R("meshScalingRegionalCell");
+    m.meshScalingRegionalEdge = R("meshScalingRegionalEdge");
+    m.dss = R("dss");
+    m.nCells = b.d.nCells;
+    m.nEdges = b.d.nEdges;
+    m.nVertices = b.d.nVertices;
+    m.K = b.d.K;
+    m.maxEdges = b.me_decl;
+    auto grid = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
+    const int nmax = std::max(b.d.nCells, std::max(b.d.nEdges, b.d.nVertices));
+    hipStream_t st = ctx->stream;
+    // atm_mpas_init_block's order (mpas_atm_core.F:311-458): signs, inverses, adv_coef compression,
+    // 3rd-order coupling, mesh scaling, damping coefficients
+    hipLaunchKernelGGL(k_mi_vertex_signs, grid(b.d.nVertices), dim3(256), 0, st, m);
+    hipLaunchKernelGGL(k_mi_cell_signs, grid((int64_t)b.d.nCells * b.me_decl), dim3(256), 0, st, m);
+    hipLaunchKernelGGL(k_mi_inverses, grid(nmax), dim3(256), 0, st, m);
+    hipLaunchKernelGGL(k_mi_adv_compression, grid(b.d.nEdges), dim3(256), 0, st, m);
+    const double c3 = ctx->cf.coef_3rd_order;
+    hipLaunchKernelGGL(k_mi_couple, dim3(1024), dim3(256), 0, st, m.adv_coefs_3rd, (int64_t)(b.d.nEdges + 1) * 15, c3);
+    hipLaunchKernelGGL(k_mi_couple, dim3(1024), dim3(256), 0, st, m.zb3_cell,
+                       (int64_t)(b.d.nCells + 1) * b.me_decl * (b.d.K + 1), c3);
+    hipLaunchKernelGGL(k_mi_mesh_scaling, grid(std::max(b.d.nCells, b.d.nEdges)), dim3(256), 0, st, m,
+                       (int)(h_scale_with_mesh != 0));
+    hipLaunchKernelGGL(k_mi_damping, grid((int64_t)b.d.nCells * b.d.K), dim3(256), 0, st, m, config_zd, config_xnutr);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->bnd_ready = false;  // signs, zb_cell, zb3_cell, kiteForCell changed: pack_mesh and the records again
   return MPAS_DYC_OK;
 }
 

@@ -1,0 +1,275 @@
+// The model-init precompute core_atmosphere runs on every start, on the device
+// (mpas_atm_core.F:311-358 and 927-1288, called from atm_mpas_init_block): the inverses of the cell /
+// triangle areas and edge lengths, atm_compute_signs (edge signs, zb_cell / zb3_cell, kiteForCell),
+// atm_adv_coef_compression, atm_couple_coef_3rd_order, atm_compute_mesh_scaling and
+// atm_compute_damping_coefs.  Inputs are the init file's fields (deriv_two, zb, zb3, meshDensity,
+// areaCell, areaTriangle, zgrid and the connectivity), as the reference reads them from its input
+// stream; outputs go to the mesh pool at the declared strides (maxEdges = the block's declared value).
+//
+// Arithmetic follows the Fortran statement by statement (same operands, same order, fp64, no
+// contraction).  Two functions go beyond + - * / sqrt: x**0.25 (a runtime pow in the compiled
+// reference) and sin.  Here they are correctly rounded (cr_root4, cr_sin below, both proved against a
+// 60-digit evaluation in tests/test_gpu_model_init.py); the reference's C library rounds them correctly for
+// all but ~0.1 % of arguments and is 1 ulp away there.  x**0.75 is sqrt(x) * sqrt(sqrt(x)), as the
+// reference build lowers it (init_atm._pow).
+// Included by dycore.hip.
+#pragma once
+#include "dycore.h"
+
+namespace mpas {
+
+// ---- double-double helpers (exact products with fma; fp-contract is off for the library) ----
+struct dd {
+  double hi, lo;
+};
+__device__ __forceinline__ dd two_sum(double a, double b) {
+  const double s = a + b, bb = s - a;
+  return dd{s, (a - (s - bb)) + (b - bb)};
+}
+__device__ __forceinline__ dd two_prod(double a, double b) {
+  const double p = a * b;
+  return dd{p, fma(a, b, -p)};
+}
+__device__ __forceinline__ dd dd_add(dd a, dd b) {
+  dd s = two_sum(a.hi, b.hi);
+  const double lo = s.lo + (a.lo + b.lo);
+  const double hi = s.hi + lo;
+  return dd{hi, lo - (hi - s.hi)};
+}
+__device__ __forceinline__ dd dd_mul(dd a, dd b) {
+  dd p = two_prod(a.hi, b.hi);
+  const double lo = p.lo + (a.hi * b.lo + a.lo * b.hi);
+  const double hi = p.hi + lo;
+  return dd{hi, lo - (hi - p.hi)};
+}
+// sign of (a - b) for double-doubles
+__device__ __forceinline__ int dd_cmp(dd a, dd b) {
+  const dd d = dd_add(a, dd{-b.hi, -b.lo});
+  return (d.hi > 0.0) - (d.hi < 0.0);
+}
+
+// x**0.25 correctly rounded, x > 0 finite: y = sqrt(sqrt(x)) is within an ulp or so; the correctly
+// rounded root is the double whose rounding interval [y - u/2, y + u/2] holds x**0.25, i.e. whose two
+// midpoints m satisfy m_lo**4 <= x < m_hi**4, decided exactly enough in double-double.
+__device__ double cr_root4(double x) {
+  double y = sqrt(sqrt(x));
+  for (int it = 0; it < 4; ++it) {
+    const double up = nextafter(y, INFINITY), dn = nextafter(y, 0.0);
+    // midpoints as double-doubles: y + (up - y) / 2 (the halves are exact)
+    const dd mh = two_sum(y, 0.5 * (up - y)), ml = two_sum(y, -0.5 * (y - dn));
+    const dd mh2 = dd_mul(mh, mh), ml2 = dd_mul(ml, ml);
+    const dd mh4 = dd_mul(mh2, mh2), ml4 = dd_mul(ml2, ml2);
+    const dd xx{x, 0.0};
+    if (dd_cmp(xx, mh4) >= 0) y = up;       // the root lies above the upper midpoint
+    else if (dd_cmp(xx, ml4) < 0) y = dn;   // below the lower one
+    else break;
+  }
+  return y;
+}
+
+// sin(x) correctly rounded for 0 <= x <= pi/2 (the damping layer's argument): the Taylor series in
+// double-double, Horner form, 1/(2k+1)! as (hi, lo) pairs.
+__constant__ double SIN_C[16][2] = {
+    {1.0, 0.0},
+    {-0.16666666666666666, -9.25185853854297e-18},
+    {0.008333333333333333, 1.1564823173178714e-19},
+    {-0.0001984126984126984, -1.7209558293420705e-22},
+    {2.7557319223985893e-06, -1.858393274046472e-22},
+    {-2.505210838544172e-08, 1.448814070935912e-24},
+    {1.6059043836821613e-10, 1.2585294588752098e-26},
+    {-7.647163731819816e-13, -7.03872877733453e-30},
+    {2.8114572543455206e-15, 1.6508842730861433e-31},
+    {-8.22063524662433e-18, -2.2141894119604265e-34},
+    {1.9572941063391263e-20, -1.3643503830087908e-36},
+    {-3.868170170630684e-23, 8.843177655482344e-40},
+    {6.446950284384474e-26, -1.9330404233703465e-42},
+    {-9.183689863795546e-29, -1.4303150396787322e-45},
+    {1.1309962886447716e-31, 1.0498015412959506e-47},
+    {-1.216125041553518e-34, -5.586290567888806e-51},
+};
+__device__ double cr_sin(double x) {
+  const dd x2 = two_prod(x, x);
+  dd s{SIN_C[15][0], SIN_C[15][1]};
+  for (int k = 14; k >= 0; --k) s = dd_add(dd_mul(s, x2), dd{SIN_C[k][0], SIN_C[k][1]});
+  s = dd_mul(s, dd{x, 0.0});
+  return s.hi + s.lo;
+}
+
+struct MInit {
+  // inputs (device, 0-based indices, missing -> the garbage element)
+  const int *nEdgesOnCell, *edgesOnCell, *cellsOnCell, *verticesOnCell, *cellsOnEdge, *verticesOnEdge;
+  const int *cellsOnVertex, *edgesOnVertex;
+  const double *deriv_two, *zb, *zb3, *meshDensity, *areaCell, *areaTriangle, *dcEdge, *dvEdge, *zgrid;
+  // outputs
+  double *invAreaCell, *invDvEdge, *invDcEdge, *invAreaTriangle;
+  double *edgesOnVertex_sign, *edgesOnCell_sign, *zb_cell, *zb3_cell;
+  int *kiteForCell, *nAdvCellsForEdge, *advCellsForEdge;
+  double *adv_coefs, *adv_coefs_3rd;
+  double *meshScalingDel2, *meshScalingDel4, *meshScalingRegionalCell, *meshScalingRegionalEdge, *dss;
+  int nCells, nEdges, nVertices, K, maxEdges;  // maxEdges: the declared stride
+};
+
+__device__ __forceinline__ int gtid() { return blockIdx.x * blockDim.x + threadIdx.x; }
+
+// 339-353
+__global__ void k_mi_inverses(MInit m) {
+  const int i = gtid();
+  if (i < m.nCells) m.invAreaCell[i] = 1.0 / m.areaCell[i];
+  if (i < m.nEdges) {
+    m.invDvEdge[i] = 1.0 / m.dvEdge[i];
+    m.invDcEdge[i] = 1.0 / m.dcEdge[i];
+  }
+  if (i < m.nVertices) m.invAreaTriangle[i] = 1.0 / m.areaTriangle[i];
+}
+
+// atm_compute_signs, 1023-1035 (vertexDegree 3)
+__global__ void k_mi_vertex_signs(MInit m) {
+  const int v = gtid();
+  if (v >= m.nVertices) return;
+  for (int i = 0; i < 3; ++i) {
+    const int e = m.edgesOnVertex[3 * v + i];
+    m.edgesOnVertex_sign[3 * v + i] = e < m.nEdges ? (v == m.verticesOnEdge[2 * e + 1] ? 1.0 : -1.0) : 0.0;
+  }
+}
+
+// 1037-1053: one thread per (cell, slot); the zb / zb3 column of the slot's edge side is copied
+__global__ void k_mi_cell_signs(MInit m) {
+  const int t = gtid();
+  if (t >= m.nCells * m.maxEdges) return;
+  const int c = t / m.maxEdges, i = t - c * m.maxEdges;
+  if (i >= m.nEdgesOnCell[c]) return;
+  const int e = m.edgesOnCell[(size_t)c * m.maxEdges + i];
+  const size_t K1 = m.K + 1, slot = (size_t)c * m.maxEdges + i;
+  if (e < m.nEdges) {
+    const int side = c == m.cellsOnEdge[2 * e] ? 0 : 1;
+    m.edgesOnCell_sign[slot] = side == 0 ? 1.0 : -1.0;
+    for (size_t k = 0; k < K1; ++k) {
+      m.zb_cell[slot * K1 + k] = m.zb[((size_t)e * 2 + side) * K1 + k];
+      m.zb3_cell[slot * K1 + k] = m.zb3[((size_t)e * 2 + side) * K1 + k];
+    }
+  } else {
+    m.edgesOnCell_sign[slot] = 0.0;
+  }
+  // 1055-1072: kiteForCell, the 1-based position of the cell among its vertex's cells (0-based here)
+  const int v = m.verticesOnCell[slot];
+  if (v < m.nVertices) {
+    for (int j = 0; j < 3; ++j)
+      if (c == m.cellsOnVertex[3 * v + j]) {
+        m.kiteForCell[slot] = j;
+        break;
+      }
+  } else {
+    m.kiteForCell[slot] = 0;
+  }
+}
+
+// atm_adv_coef_compression, 1154-1264, one thread per edge; the list and the sums in the reference's
+// order (j_in = the last list position holding the cell)
+__global__ void k_mi_adv_compression(MInit m) {
+  const int e = gtid();
+  if (e >= m.nEdges) return;
+  m.nAdvCellsForEdge[e] = 0;
+  const int c1 = m.cellsOnEdge[2 * e], c2 = m.cellsOnEdge[2 * e + 1];
+  if (!(c1 < m.nCells || c2 < m.nCells)) return;
+  int lst[20];
+  lst[0] = c1;
+  lst[1] = c2;
+  int n = 2;
+  const int ne1 = m.nEdgesOnCell[c1], ne2 = m.nEdgesOnCell[c2];
+  for (int i = 0; i < ne1; ++i) {
+    const int cc = m.cellsOnCell[(size_t)c1 * m.maxEdges + i];
+    if (cc != c2) lst[n++] = cc;
+  }
+  for (int i = 0; i < ne2; ++i) {
+    const int cc = m.cellsOnCell[(size_t)c2 * m.maxEdges + i];
+    bool add = true;
+    for (int j = 0; j < n; ++j)
+      if (lst[j] == cc) add = false;
+    if (add) lst[n++] = cc;
+  }
+  m.nAdvCellsForEdge[e] = n;
+  for (int j = 0; j < 15; ++j) m.advCellsForEdge[(size_t)e * 15 + j] = j < n ? lst[j] : m.nCells;  // unused: none
+  double a[20], b[20];
+  for (int j = 0; j < 20; ++j) a[j] = b[j] = 0.0;
+  auto jin = [&](int cell) {
+    int r = -1;
+    for (int j = 0; j < n; ++j)
+      if (lst[j] == cell) r = j;
+    return r;
+  };
+  const double* d2 = m.deriv_two + (size_t)e * 30;  // deriv_two(15, 2, nEdges+1)
+  // every cell looked up is in the list by construction (j >= 0)
+  int j = jin(c1);
+  a[j] = a[j] + d2[0];
+  b[j] = b[j] + d2[0];
+  for (int i = 0; i < ne1; ++i) {
+    j = jin(m.cellsOnCell[(size_t)c1 * m.maxEdges + i]);
+    a[j] = a[j] + d2[i + 1];
+    b[j] = b[j] + d2[i + 1];
+  }
+  j = jin(c2);
+  a[j] = a[j] + d2[15];
+  b[j] = b[j] - d2[15];
+  for (int i = 0; i < ne2; ++i) {
+    j = jin(m.cellsOnCell[(size_t)c2 * m.maxEdges + i]);
+    a[j] = a[j] + d2[15 + i + 1];
+    b[j] = b[j] - d2[15 + i + 1];
+  }
+  const double dc = m.dcEdge[e], dv = m.dvEdge[e];
+  for (j = 0; j < n; ++j) {
+    a[j] = -(dc * dc) * a[j] / 12.;
+    b[j] = -(dc * dc) * b[j] / 12.;
+  }
+  j = jin(c1);
+  a[j] = a[j] + 0.5;
+  j = jin(c2);
+  a[j] = a[j] + 0.5;
+  for (j = 0; j < 15; ++j) {  // adv_coefs(:, iEdge) = 0 first (1195-1196); 15 = the array's FIFTEEN
+    m.adv_coefs[(size_t)e * 15 + j] = j < n ? dv * a[j] : 0.0;
+    m.adv_coefs_3rd[(size_t)e * 15 + j] = j < n ? dv * b[j] : 0.0;
+  }
+}
+
+// atm_couple_coef_3rd_order, 1285-1286: every element of both arrays, garbage slot included
+__global__ void k_mi_couple(double* a, int64_t n, double coef) {
+  for (int64_t i = gtid(); i < n; i += (int64_t)gridDim.x * blockDim.x) a[i] = coef * a[i];
+}
+
+// atm_compute_mesh_scaling, 956-982 (config_h_ScaleWithMesh = scale)
+__global__ void k_mi_mesh_scaling(MInit m, int scale) {
+  const int i = gtid();
+  if (i < m.nEdges) {
+    double s2 = 1.0, s4 = 1.0, sr = 1.0;
+    if (scale) {
+      const int c1 = m.cellsOnEdge[2 * i], c2 = m.cellsOnEdge[2 * i + 1];
+      const double x = (m.meshDensity[c1] + m.meshDensity[c2]) / 2.0;
+      s2 = 1.0 / cr_root4(x);
+      s4 = 1.0 / (sqrt(x) * sqrt(sqrt(x)));
+      sr = s2;
+    }
+    m.meshScalingDel2[i] = s2;
+    m.meshScalingDel4[i] = s4;
+    m.meshScalingRegionalEdge[i] = sr;
+  }
+  if (i < m.nCells) m.meshScalingRegionalCell[i] = scale ? 1.0 / cr_root4(m.meshDensity[i]) : 1.0;
+}
+
+// atm_compute_damping_coefs, 1105-1116: one thread per (cell, level)
+__global__ void k_mi_damping(MInit m, double zd, double xnutr) {
+  const int t = gtid();
+  if (t >= m.nCells * m.K) return;
+  const int c = t / m.K, k = t - c * m.K;
+  const size_t K1 = m.K + 1;
+  const double pii = 3.141592653589793;  // acos(-1.0)
+  const double zt = m.zgrid[(size_t)c * K1 + m.K];
+  const double z = 0.5 * (m.zgrid[(size_t)c * K1 + k] + m.zgrid[(size_t)c * K1 + k + 1]);
+  double v = 0.0;
+  if (z > zd) {
+    const double s = cr_sin(0.5 * pii * (z - zd) / (zt - zd));
+    v = xnutr * (s * s);
+    v = v / cr_root4(m.meshDensity[c]);
+  }
+  m.dss[(size_t)c * m.K + k] = v;
+}
+
+}  // namespace mpas

@@ -22,6 +22,13 @@ from . import fields as F
 from .layout import LOC_N, to_fortran
 
 STATE_INPUTS = ("u", "w", "scalars")
+# what atm_mpas_init_block precomputes (mpas_atm_core.F:311-358, 927-1288; mpas_dyc_model_init) and what
+# it reads beyond the dycore's own mesh fields
+MODEL_INIT_OUT = ("invAreaCell", "invDvEdge", "invDcEdge", "invAreaTriangle", "edgesOnVertex_sign",
+                  "edgesOnCell_sign", "zb_cell", "zb3_cell", "kiteForCell", "nAdvCellsForEdge", "advCellsForEdge",
+                  "adv_coefs", "adv_coefs_3rd", "meshScalingDel2", "meshScalingDel4", "meshScalingRegionalCell",
+                  "meshScalingRegionalEdge", "dss")
+MODEL_INIT_IN = ("deriv_two", "zb", "zb3", "meshDensity", "areaCell", "areaTriangle")
 DIAG_INPUTS = ("theta", "rho", "rho_base", "theta_base")
 _SKIP = set(STATE_INPUTS) | set(DIAG_INPUTS) | {"xCell", "yCell", "zCell", "xEdge", "yEdge", "zEdge", "xVertex",
                                                 "yVertex", "zVertex",
@@ -104,7 +111,7 @@ class Dycore:
     (``mpas_dycore.decomp``) and installs their exchange lists."""
 
     def __init__(self, case: dict | None = None, device: int = 0, solve: tuple | None = None, moist_end: int = 1,
-                 _blocks: list | None = None):
+                 _blocks: list | None = None, model_init: str = "host"):
         self.lib = _lib.load()
         cases = [case] if _blocks is None else [b.case for b in _blocks]
         solves = [solve] if _blocks is None else [b.solve for b in _blocks]
@@ -122,8 +129,15 @@ class Dycore:
         if rc != 0 or not h.value:
             raise DycoreError(f"mpas_dyc_create_blocks failed ({rc})")
         self.h = h
+        if model_init not in ("host", "device"):
+            raise ValueError("model_init: 'host' (the case's precomputed arrays) or 'device' (mpas_dyc_model_init)")
         for ib, c in enumerate(cases):
-            self._upload_case(c, ib)
+            self._upload_case(c, ib, device_init=model_init == "device")
+        if model_init == "device":
+            cfg = self.case["config"]
+            self._check(self.lib.mpas_dyc_model_init(self.h, int(bool(cfg.get("config_h_ScaleWithMesh", True))),
+                                                     float(cfg["config_zd"]), float(cfg["config_xnutr"])),
+                        "model_init")
 
     @classmethod
     def from_blocks(cls, blocks: list, device: int = 0, moist_end: int = 1, placement: dict | None = None,
@@ -212,9 +226,15 @@ class Dycore:
         self._check(self.lib.mpas_dyc_halo_exchange(self.h, pool.encode(), name.encode(), time_level, mask),
                     f"halo_exchange {pool}.{name}")
 
-    def _upload_case(self, case: dict, block: int = 0):
+    def _upload_case(self, case: dict, block: int = 0, device_init: bool = False):
+        """device_init: leave atm_mpas_init_block's precompute to the device (mpas_dyc_model_init) --
+        upload its inputs (the init file's deriv_two, zb, zb3, meshDensity, areaCell, areaTriangle)
+        instead of the case's precomputed arrays."""
+        if device_init:
+            for name in MODEL_INIT_IN:
+                self.set_raw("mesh", name, to_fortran(case, name), block=block)
         for name in case:
-            if name in _SKIP:
+            if name in _SKIP or (device_init and name in MODEL_INIT_OUT):
                 continue
             if name in F.LOCATION or name in F.VERTICAL_1D:
                 if name in F.VERTICAL_1D:

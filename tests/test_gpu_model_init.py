@@ -1,0 +1,196 @@
+"""GPU: the model-init precompute on the device (mpas_dyc_model_init: atm_compute_signs,
+atm_adv_coef_compression, atm_couple_coef_3rd_order, atm_compute_mesh_scaling,
+atm_compute_damping_coefs and the inverses of atm_mpas_init_block, mpas_atm_core.F:311-358, 927-1288).
+
+Checked against the reference's own outputs on our meshes (tests/golden/init_*.npz, the unmodified
+mpas_atm_core.F run by the harness) and against init_atm.model_init (the host restatement):
+  * signs, kiteForCell, advCellsForEdge, nAdvCellsForEdge: bit for bit;
+  * adv_coefs / adv_coefs_3rd: bit for bit when the device is handed the reference's deriv_two (the
+    compression is pure arithmetic on it);
+  * zb_cell / zb3_cell (copies of zb / zb3 times config_coef_3rd_order), inverses: bit for bit vs host;
+  * meshScalingDel2 / Del4, dss: bit for bit, except where the reference's C library does not round
+    x**0.25 or sin correctly -- there the device value is the correctly rounded one (checked against a
+    60-digit evaluation here), 1 ulp from the reference's root / sine, so at most 2 ulp from its
+    meshScalingDel2 and 4 ulp from its dss.
+Then a model run from the device-initialised mesh equals the host-initialised one."""
+import math
+from decimal import Decimal, getcontext
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+getcontext().prec = 60
+
+
+def cr_root4(x: float) -> float:
+    """x**0.25, correctly rounded (Decimal's sqrt is exact to 60 digits; float() rounds to nearest)."""
+    return float(Decimal(x).sqrt().sqrt())
+
+
+def cr_sin(x: float) -> float:
+    x = Decimal(x)
+    s, term, k = Decimal(0), x, 1
+    while abs(term) > Decimal(10) ** -58:
+        s += term
+        term = -term * x * x / ((2 * k) * (2 * k + 1))
+        k += 1
+    return float(s)
+
+
+def _cases():
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools"))
+    import make_golden
+    return make_golden
+
+
+def _device(case, fields):
+    from mpas_dycore import Dycore
+    dy = Dycore(case, device=0, model_init="device")
+    out = {}
+    for n in fields:
+        nb = dy.lib.mpas_dyc_field_bytes(dy.h, b"mesh", n.encode())
+        if n in ("kiteForCell", "advCellsForEdge", "nAdvCellsForEdge"):
+            import ctypes as C
+            buf = np.empty(nb // 4, dtype=np.int32)
+            assert dy.lib.mpas_dyc_get_field(dy.h, b"mesh", n.encode(), 1, buf.ctypes.data_as(C.c_void_p), nb) == 0
+            out[n] = buf
+        else:
+            out[n] = dy.get_raw("mesh", n)
+    dy.close()
+    return out
+
+
+def _expected_scaling(case):
+    """meshScalingDel2 / Del4 / Regional and dss as the reference writes them, with correctly rounded
+    pow / sin, and a mask of where that differs from the C library's result."""
+    cfg = case["config"]
+    md = np.asarray(case["meshDensity"], dtype=np.float64)
+    coe = np.asarray(case["cellsOnEdge"])
+    x = (md[coe[:, 0]] + md[coe[:, 1]]) / 2.0
+    r4 = np.array([cr_root4(v) for v in x])
+    lib4 = np.array([math.pow(v, 0.25) for v in x])
+    d2 = 1.0 / r4
+    d4 = 1.0 / (np.sqrt(x) * np.sqrt(np.sqrt(x)))
+    zg = np.asarray(case["zgrid"])
+    K = zg.shape[1] - 1
+    zd, xn = float(cfg["config_zd"]), float(cfg["config_xnutr"])
+    pii = math.acos(-1.0)
+    dss = np.zeros((zg.shape[0], K))
+    dss_lib = np.zeros_like(dss)
+    for c in range(zg.shape[0]):
+        zt = zg[c, K]
+        mr, ml = cr_root4(md[c]), math.pow(md[c], 0.25)
+        for k in range(K):
+            z = 0.5 * (zg[c, k] + zg[c, k + 1])
+            if z > zd:
+                a = 0.5 * pii * (z - zd) / (zt - zd)
+                s, sl = cr_sin(a), math.sin(a)
+                dss[c, k] = xn * (s * s) / mr
+                dss_lib[c, k] = xn * (sl * sl) / ml
+    reg_c = 1.0 / np.array([cr_root4(v) for v in md])
+    return dict(meshScalingDel2=d2, meshScalingDel4=d4, meshScalingRegionalEdge=d2, meshScalingRegionalCell=reg_c,
+                dss=dss), dict(meshScalingDel2=r4 != lib4, dss=dss != dss_lib)
+
+
+@pytest.mark.parametrize("fixture", ["init_x1.642_K8.npz", "init_varres2562_K8.npz"])
+def test_model_init_matches_reference(fixture):
+    import os
+    from mpas_dycore.layout import to_fortran
+    mg = _cases()
+    case = mg.INIT_CASES[fixture]()
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", fixture))
+    assert str(z["checksum"]) == mg.init_inputs_checksum(case), "mesh generator changed: regenerate the fixture"
+    ref = {k: z[k] for k in z.files if k != "checksum"}
+    nC, nE, ME = case["nCells"], case["nEdges"], case["maxEdges"]
+    K = case["nVertLevels"]
+    # the reference's deriv_two: the compression is then pure arithmetic on identical operands
+    c = dict(case, deriv_two=ref["deriv_two"])
+    names = ("edgesOnCell_sign", "edgesOnVertex_sign", "kiteForCell", "advCellsForEdge", "nAdvCellsForEdge",
+             "adv_coefs", "adv_coefs_3rd", "meshScalingDel2", "meshScalingDel4", "meshScalingRegionalEdge",
+             "meshScalingRegionalCell", "dss", "zb_cell", "zb3_cell", "invAreaCell", "invDvEdge", "invDcEdge",
+             "invAreaTriangle")
+    got = _device(c, names)
+    noc = np.asarray(case["nEdgesOnCell"])
+    slot = np.arange(ME)[None, :] < noc[:, None]
+    nadv = np.asarray(ref["nAdvCellsForEdge"])
+    aslot = np.arange(15)[None, :] < nadv[:, None]
+    g = {k: v.reshape(-1) for k, v in got.items()}
+    # index / sign arrays
+    assert np.array_equal(g["nAdvCellsForEdge"][:nE], nadv)
+    adv = g["advCellsForEdge"].reshape(nE + 1, 15)[:nE] - 1
+    assert np.array_equal(np.where(aslot, adv, 0), np.where(aslot, ref["advCellsForEdge"], 0))
+    for n in ("edgesOnCell_sign", "kiteForCell"):
+        a = g[n].reshape(nC + 1, ME)[:nC]
+        if n == "kiteForCell":
+            a = a - 1  # Fortran 1-based -> the fixture's 0-based
+        assert np.array_equal(np.where(slot, a, 0), np.where(slot, ref[n], 0)), n
+    assert np.array_equal(g["edgesOnVertex_sign"].reshape(-1, 3)[:-1], ref["edgesOnVertex_sign"])
+    for n in ("adv_coefs", "adv_coefs_3rd"):
+        a = g[n].reshape(nE + 1, 15)[:nE]
+        assert np.array_equal(np.where(aslot, a, 0), np.where(aslot, ref[n], 0)), f"{n} not bit for bit"
+    # pow / sin outputs: the correctly rounded values; the reference's where its C library rounds right
+    want, lib_off = _expected_scaling(case)
+    for n in ("meshScalingDel2", "meshScalingDel4", "meshScalingRegionalEdge"):
+        assert np.array_equal(g[n][:nE], want[n]), n
+    assert np.array_equal(g["meshScalingRegionalCell"][:nC], want["meshScalingRegionalCell"])
+    dss = g["dss"].reshape(nC + 1, K)[:nC]
+    assert np.array_equal(dss, want["dss"])
+    for n, a in (("meshScalingDel2", g["meshScalingDel2"][:nE]), ("meshScalingDel4", g["meshScalingDel4"][:nE]),
+                 ("dss", dss)):
+        off = lib_off.get(n, np.zeros(a.shape, bool))
+        assert np.array_equal(a[~off], np.asarray(ref[n])[~off]), f"{n} differs from the reference where libm is exact"
+        if off.any():
+            # 1 ulp in the root: <= 2 ulp in its reciprocal; 1 ulp in the sine, squared, and the root:
+            # <= 4 ulp in dss = xnutr sin^2 / root
+            ulp = np.spacing(np.abs(np.asarray(ref[n])[off]))
+            assert np.all(np.abs(a[off] - np.asarray(ref[n])[off]) <= (4 if n == "dss" else 2) * ulp), n
+    # the copies and inverses: what the host restatement computes
+    zb = np.asarray(case["zb_cell"]).reshape(nC, ME, K + 1)
+    z3 = np.asarray(case["zb3_cell"]).reshape(nC, ME, K + 1)
+    s3 = slot[:, :, None]
+    assert np.array_equal(np.where(s3, g["zb_cell"].reshape(nC + 1, ME, K + 1)[:nC], 0), np.where(s3, zb, 0))
+    assert np.array_equal(np.where(s3, g["zb3_cell"].reshape(nC + 1, ME, K + 1)[:nC], 0), np.where(s3, z3, 0))
+    for n in ("invAreaCell", "invDvEdge", "invDcEdge", "invAreaTriangle"):
+        want_inv = np.asarray(to_fortran(case, n)).reshape(-1)
+        assert np.array_equal(g[n][:-1], want_inv[:-1]), n
+
+
+def test_model_run_from_device_init(moist_case):
+    """A moist run whose mesh precompute came from mpas_dyc_model_init: every precomputed array equals
+    the host-initialised one bit for bit except dss, which may differ by a few ulp (<= 4) where the C library's sin
+    is not correctly rounded; the run is bitwise equal when dss is, else within the parity tests' bars
+    (1e-13, w 1e-11)."""
+    from conftest import rel_linf
+    from mpas_dycore import Dycore
+    case = moist_case
+    dt = 2880.0
+    runs = []
+    for mode in ("host", "device"):
+        dy = Dycore(case, device=0, moist_end=3, model_init=mode)
+        mesh = {n: dy.get_raw("mesh", n) for n in ("adv_coefs", "adv_coefs_3rd", "zb3_cell", "dss", "meshScalingDel2",
+                                                    "meshScalingDel4", "edgesOnCell_sign", "invDcEdge")}
+        dy.init_diagnostics(dt)
+        dy.use_graph(True)
+        for it in range(3):
+            dy.atm_timestep(dt, it + 1)
+            dy.shift_time_levels()
+        dy.synchronize()
+        runs.append((mesh, {n: dy.get("state", n, 1) for n in ("u", "w", "theta_m", "rho_zz", "scalars")}))
+        dy.close()
+    (m0, s0), (m1, s1) = runs
+    for n in m0:
+        if n == "dss":
+            off = m0[n] != m1[n]
+            assert np.all(np.abs(m0[n][off] - m1[n][off]) <= 4 * np.spacing(np.abs(m0[n][off]))), "dss beyond 4 ulp"
+            continue
+        assert np.array_equal(m0[n], m1[n]), f"{n}: device model init differs from the host's"
+    exact = np.array_equal(m0["dss"], m1["dss"])
+    for n in s0:
+        if exact:
+            assert np.array_equal(s0[n], s1[n]), n
+        else:  # the parity tests' 1-step bars: w amplifies a last-bit change of dss the most
+            assert rel_linf(s1[n], s0[n]) <= (1e-11 if n == "w" else 1e-13), n

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Build the generators of the BASELINE.json configs[4] mesh: a 60-3 km variable-resolution spherical
+centroidal Voronoi tessellation with 835586 cells (the MPAS x20.835586 mesh's size and range), and
+store them quantised to int32 per coordinate (mpas_dycore/data/x20.835586_generators.npz) so the GPU
+box only triangulates (mesh.varres_from_generators).
+
+Density (MPAS convention, cell spacing ~ rho^-1/4): rho = (1-g)/2 (tanh((beta-d)/alpha) + 1) + g,
+g = 20^-4, beta = 9 deg, alpha = 3 deg, centred at (30N, 90W): integrating sqrt(rho) over the sphere
+with 3 km hexagons in the refined disc gives 835714 cells, i.e. 3 km there and 60 km far away.
+
+Start: a Fibonacci lattice remapped radially so that the point density is ~ sqrt(rho) (the areal
+density of a CVT), then density-weighted Lloyd iterations on the spherical Delaunay triangulation,
+rebuilt every step, until the mesh is well shaped (progress and quality every --report steps).
+
+    python tools/make_varres_mesh.py [--iters 300] [--out mpas-model_amd/mpas_dycore/data/...]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpas-model_amd"))
+
+from mpas_dycore import mesh as M  # noqa: E402
+
+NCELLS, CENTER, RADIUS_DEG, WIDTH_DEG, RATIO = 835586, (30.0, -90.0), 9.0, 3.0, 20.0
+
+
+def radial_start(n):
+    """Fibonacci points, each moved along its great circle from the centre so that the cumulative
+    count inside distance d follows the integral of sqrt(rho) (point density ~ sqrt(rho))."""
+    p = M._fibonacci_sphere(n)
+    lat, lon = np.radians(CENTER[0]), np.radians(CENTER[1])
+    zc = np.array([np.cos(lat) * np.cos(lon), np.cos(lat) * np.sin(lon), np.sin(lat)])
+    rho = M.varres_density(CENTER, RADIUS_DEG, WIDTH_DEG, RATIO)
+    d = np.linspace(0.0, np.pi, 400001)
+    ray = np.cos(d)[:, None] * zc + np.sin(d)[:, None] * np.cross(zc, [0.0, 0.0, 1.0]) / np.linalg.norm(
+        np.cross(zc, [0.0, 0.0, 1.0]))
+    w = np.sqrt(rho(ray)) * np.sin(d)
+    cdf = np.concatenate([[0.0], np.cumsum(0.5 * (w[1:] + w[:-1]) * np.diff(d))])
+    cdf /= cdf[-1]
+    d0 = np.arccos(np.clip(p @ zc, -1.0, 1.0))
+    d1 = np.interp((1.0 - np.cos(d0)) / 2.0, cdf, d)
+    t = p - (p @ zc)[:, None] * zc  # direction away from the centre
+    t /= np.maximum(np.linalg.norm(t, axis=1), 1e-300)[:, None]
+    return M._normalize(np.cos(d1)[:, None] * zc + np.sin(d1)[:, None] * t)
+
+
+def quality(p):
+    f = M._delaunay(p)
+    vc = M._circumcenters(p, f)
+    pairs = np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]])
+    face = np.concatenate([np.arange(len(f))] * 3)
+    s = np.sort(pairs, axis=1)
+    o = np.lexsort((s[:, 1], s[:, 0]))
+    s, face = s[o], face[o]
+    a, fa, fb = s[0::2], face[0::2], face[1::2]
+    dv = np.linalg.norm(vc[fa] - vc[fb], axis=1)
+    dc = np.linalg.norm(p[a[:, 0]] - p[a[:, 1]], axis=1)
+    deg = np.bincount(f.ravel(), minlength=len(p))
+    R = M.SPHERE_RADIUS / 1e3
+    return dict(dc_min_km=float(dc.min() * R), dc_max_km=float(dc.max() * R), dv_over_dc_min=float((dv / dc).min()),
+                n_small_dv=int((dv < 0.2 * dc).sum()), deg={int(k): int((deg == k).sum()) for k in np.unique(deg)})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=300)
+    ap.add_argument("--report", type=int, default=10)
+    ap.add_argument("--resume", default=None, help="continue from a checkpoint .npy")
+    ap.add_argument("--checkpoint", default="/tmp/varres_gen.npy")
+    ap.add_argument("--out", default=os.path.join(ROOT, "mpas-model_amd", "mpas_dycore", "data",
+                                                  "x20.835586_generators.npz"))
+    a = ap.parse_args()
+    rho = M.varres_density(CENTER, RADIUS_DEG, WIDTH_DEG, RATIO)
+    p = np.load(a.resume) if a.resume else radial_start(NCELLS)
+    t0 = time.time()
+    for it in range(a.iters):
+        p = M._lloyd_step(p, M._delaunay(p), rho)
+        if (it + 1) % a.report == 0 or it + 1 == a.iters:
+            np.save(a.checkpoint, p)
+            print(f"iter {it + 1}: {time.time() - t0:.0f} s {quality(p)}", flush=True)
+    q = np.round(p * 2.0 ** 30).astype(np.int32)  # |x| <= 1: int32 with 2^-30 steps (~6 mm on Earth)
+    np.savez_compressed(a.out, xyz_q30=q, center=np.array(CENTER), radius_deg=RADIUS_DEG, width_deg=WIDTH_DEG,
+                        ratio=RATIO)
+    print(f"wrote {a.out}: {quality(M._normalize(q / 2.0 ** 30))}")
+
+
+if __name__ == "__main__":
+    main()
