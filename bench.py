@@ -221,10 +221,12 @@ def main():
             from mpas_dycore.mpas_files import read_init
             if args.dt is None or args.len_disp is None:
                 raise SystemExit("--init needs --dt and --len-disp")
-            return read_init(args.init, config=dict(config_dt=args.dt, config_len_disp=args.len_disp))
+            return read_init(args.init, config=dict(config_dt=args.dt, config_len_disp=args.len_disp,
+                                                    config_time_integration_order=args.order))
         if args.varres:
             from mpas_dycore.cases import varres_case
-            return varres_case(args.varres, ratio=20.0, K=args.levels, ns=args.num_scalars, moist=args.moist)
+            return varres_case(args.varres, ratio=20.0, K=args.levels, ns=args.num_scalars, moist=args.moist,
+                               order=args.order)
         return jw_case(args.ncells, K=args.levels, ns=args.num_scalars, moist=args.moist, order=args.order)
 
     t_build = time.time()
@@ -382,8 +384,9 @@ def main():
                          f"(one full atm_srk3 per step)" if args.init else
                          f"variable-resolution SCVT, {case['nCells']} cells (20x refinement, "
                          f"{case['dcEdge'].min() / 1e3:.1f}-{case['dcEdge'].max() / 1e3:.0f} km, maxEdges="
-                         f"{case['maxEdges']}), {case['nVertLevels']} levels, dt={dt:g}s (BASELINE.json configs[4] "
-                         f"analogue; one full atm_srk3 per step)" if args.varres else
+                         f"{case['maxEdges']}, {int((case['nEdgesOnCell'] == 5).sum())} pentagons / "
+                         f"{int((case['nEdgesOnCell'] == 7).sum())} heptagons), {case['nVertLevels']} levels, "
+                         f"dt={dt:g}s (BASELINE.json configs[4]; one full atm_srk3 per step)" if args.varres else
                          f"x1.{case['nCells']} moist dycore + scalar transport (num_scalars={case['num_scalars']}, "
                          f"monotone), {case['nVertLevels']} levels, dt={dt:g}s (BASELINE.json configs[3]; one full "
                          f"atm_srk3 per step)" if args.moist else

@@ -246,6 +246,17 @@ void* mpas_dyc_block_field_device_ptr(mpas_dyc_ctx* ctx, int32_t block, const ch
 int mpas_dyc_set_exchange_list(mpas_dyc_ctx* ctx, int32_t block, int32_t location, int32_t halo_layer,
                                int32_t direction, int32_t peer_rank, int32_t peer_block, const int32_t* local_index,
                                int32_t n);
+/* A list of another task as mpas_dmpar keeps it when tasks hold several blocks (parinfo xToSend /
+ * xToRecv: endPointID = the task, the other list = buffer positions; mpas_dmpar.F:5448-5535): this
+ * block's elements local_index[i] (1-based; owned to send, halo to receive) take 1-based slot
+ * position[i] of the (location, halo_layer) region of the one message between this task and task
+ * peer_rank, whose slots all blocks of this task fill together.  The message is laid out as
+ * mpas_dmpar lays out its buffer -- per field of the exchange, per halo layer a region as long as its
+ * largest position -- so a task need not know which block of the peer receives an element.  A peer
+ * rank takes either positional lists or block-pair lists (mpas_dyc_set_exchange_list), not both. */
+int mpas_dyc_set_exchange_positions(mpas_dyc_ctx* ctx, int32_t block, int32_t location, int32_t halo_layer,
+                                    int32_t direction, int32_t peer_rank, const int32_t* local_index,
+                                    const int32_t* position, int32_t n);
 /* RCCL communicator for exchanges between processes (one rank per GPU): rank 0 creates the
  * id (ncclGetUniqueId), every rank passes it to mpas_dyc_comm_init (ncclCommInitRank). */
 int64_t mpas_dyc_comm_unique_id_bytes(void);

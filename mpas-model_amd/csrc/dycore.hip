@@ -69,6 +69,11 @@ struct XList {
   int n = 0;
   int* d_idx = nullptr;  // 0-based local element indices, message order
   std::vector<int32_t> h_idx;  // the same on the host (fused-pack maps)
+  // a positional list (mpas_dyc_set_exchange_positions, peer_block -1): element i takes slot
+  // d_pos[i] (0-based) of the (loc, layer) region of the message to / from rank peer_rank, whose
+  // slots all blocks of this process fill together -- mpas_dmpar's per-task buffers
+  int* d_pos = nullptr;
+  std::vector<int32_t> h_pos;
 };
 
 // A block: MPAS block_type -- dims, fields and exchange lists of one patch.
@@ -561,7 +566,7 @@ bool is_local(const mpas_dyc_ctx* ctx, int peer_rank) { return peer_rank == ctx-
 std::vector<std::pair<int, int>> peers_of(const Block& b, int dir) {
   std::vector<std::pair<int, int>> peers;
   for (const auto& x : b.xl)
-    if (x.dir == dir && x.n > 0) peers.emplace_back(x.peer_rank, x.peer_block);
+    if (x.dir == dir && x.n > 0 && x.peer_block >= 0) peers.emplace_back(x.peer_rank, x.peer_block);
   std::sort(peers.begin(), peers.end());
   peers.erase(std::unique(peers.begin(), peers.end()), peers.end());
   return peers;
@@ -614,7 +619,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   std::vector<RecSeg> rec_pack, rec_unpack;
   auto field_of = [&](Block& b, const XField& f) -> Field* {
     Field* F = find(b, f.pool, f.name);
-    if (!F || F->is_int || F->loc == L_NONE || !F->buf[0]) {
+    if (!F || F->is_int || F->loc == L_NONE || (!F->buf[0] && !ctx->host_only)) {
       ctx->err = std::string("halo exchange of unsupported field ") + f.pool + "." + f.name;
       return nullptr;
     }
@@ -715,6 +720,79 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
         }
       }
       if (!local && rtotal > start) pl.rrecv.push_back(XMsg{bi, pr.first, pr.second, start, rtotal - start});
+    }
+  }
+  // positional lists (mpas_dyc_set_exchange_positions): per peer rank one message, laid out as
+  // mpas_dmpar lays out its buffer (mpas_dmpar.F:5448-5535): per field, per halo layer a region whose
+  // slots the blocks of this process fill at their positions; the receiver reads its blocks' slots
+  // at theirs.  Region sizes are the largest position over the blocks (both sides agree: it is one
+  // buffer).  No fused pack / unpack for them.
+  {
+    std::set<int> pos_ranks;
+    for (const auto& b : ctx->blk)
+      for (const auto& x : b.xl)
+        if (x.peer_block < 0 && x.n > 0) pos_ranks.insert(x.peer_rank);
+    for (int dir = MPAS_DYC_SEND; dir <= MPAS_DYC_RECV; ++dir)
+      for (int pr : pos_ranks) {
+        int64_t& total = dir == MPAS_DYC_SEND ? stotal : rtotal;
+        const int64_t start = total;
+        for (const auto& f : fs) {
+          Field* F0 = field_of(ctx->blk[0], f);
+          if (!F0) return MPAS_DYC_EINVAL;
+          for (int layer = 1; layer <= 3; ++layer) {
+            if (!((f.layers >> (layer - 1)) & 1u)) continue;
+            std::vector<const XList*> lx(nb, nullptr);
+            int64_t npos = 0;
+            for (int bi = 0; bi < nb; ++bi)
+              for (const auto& x : ctx->blk[bi].xl)
+                if (x.peer_block < 0 && x.n > 0 && x.peer_rank == pr && x.dir == dir && x.loc == (int)F0->loc &&
+                    x.layer == layer) {
+                  lx[bi] = &x;
+                  for (int32_t q : x.h_pos) npos = std::max<int64_t>(npos, (int64_t)q + 1);
+                }
+            if (!npos) continue;
+            const int64_t sub_inner = F0->inner / F0->nsub;
+            for (int is = 0; is < F0->nsub; ++is) {
+              for (int bi = 0; bi < nb; ++bi) {
+                if (!lx[bi]) continue;
+                Block& b = ctx->blk[bi];
+                Field* F = field_of(b, f);
+                if (!F) return MPAS_DYC_EINVAL;
+                double* fld = (double*)F->buf[slot_of(ctx, *F, f.tl)] + (size_t)is * nloc(b, F->loc) * sub_inner;
+                XSeg sg{};
+                sg.n = lx[bi]->n;
+                sg.inner = (int)sub_inner;
+                if (dir == MPAS_DYC_SEND) {
+                  sg.src = fld;
+                  sg.sidx = lx[bi]->d_idx;
+                  sg.didx = lx[bi]->d_pos;
+                  pre.push_back(sg);
+                  pre_off.push_back(total);
+                  pl.maxn_pre = std::max(pl.maxn_pre, sg.n);
+                } else {
+                  sg.sidx = lx[bi]->d_pos;
+                  sg.dst = fld;
+                  sg.didx = lx[bi]->d_idx;
+                  post.push_back(sg);
+                  post_off.push_back(total);
+                  pl.maxn_post = std::max(pl.maxn_post, sg.n);
+                }
+              }
+              total += npos * sub_inner;
+            }
+          }
+        }
+        if (total > start) (dir == MPAS_DYC_SEND ? pl.rsend : pl.rrecv).push_back(XMsg{-1, pr, -1, start, total - start});
+      }
+    if (!pos_ranks.empty()) {
+      fusable = false;
+      recfuse = false;
+      for (const auto& m : pl.rsend)
+        for (const auto& m2 : pl.rsend)
+          if (m.peer_rank == m2.peer_rank && (m.block < 0) != (m2.block < 0)) {
+            ctx->err = "rank " + std::to_string(m.peer_rank) + " has both positional and block-pair exchange lists";
+            return MPAS_DYC_EINVAL;
+          }
     }
   }
   if ((!pl.rsend.empty() || !pl.rrecv.empty()) && !ctx->comm && !ctx->host_only) {
@@ -2397,8 +2475,10 @@ void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
       if (f.packed) (void)hipFree(f.packed);
       if (is_host_0d(f)) delete (double*)f.buf[1];
     }
-    for (auto& x : b.xl)
+    for (auto& x : b.xl) {
       if (x.d_idx) (void)hipFree(x.d_idx);
+      if (x.d_pos) (void)hipFree(x.d_pos);
+    }
     if (b.sum_part) (void)hipFree(b.sum_part);
     if (b.sum_out) (void)hipFree(b.sum_out);
   }
@@ -2650,6 +2730,69 @@ int mpas_dyc_set_exchange_list(mpas_dyc_ctx* ctx, int32_t block, int32_t locatio
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipMalloc(&x->d_idx, n * sizeof(int32_t)));
     HIPCHK(hipMemcpy(x->d_idx, idx.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
+  return MPAS_DYC_OK;
+}
+
+int mpas_dyc_set_exchange_positions(mpas_dyc_ctx* ctx, int32_t block, int32_t location, int32_t halo_layer,
+                                    int32_t direction, int32_t peer_rank, const int32_t* local_index,
+                                    const int32_t* position, int32_t n) {
+  Block* bp = get_block(ctx, block);
+  if (!bp) {
+    if (ctx) ctx->err = "no block " + std::to_string(block);
+    return MPAS_DYC_EINVAL;
+  }
+  if (location < MPAS_DYC_CELL || location > MPAS_DYC_VERTEX || halo_layer < 1 || halo_layer > 3 ||
+      (location == MPAS_DYC_CELL && halo_layer > 2) || (direction != MPAS_DYC_SEND && direction != MPAS_DYC_RECV) ||
+      peer_rank < 0 || n < 0 || (n > 0 && (!local_index || !position))) {
+    ctx->err = "invalid exchange list arguments";
+    return MPAS_DYC_EINVAL;
+  }
+  if (peer_rank == ctx->rank && !ctx->host_only && ctx->nranks > 1) {
+    ctx->err = "positional lists are for other ranks (mpas_dyc_set_exchange_list copies within a process)";
+    return MPAS_DYC_EINVAL;
+  }
+  Block& b = *bp;
+  const int64_t nl = location == MPAS_DYC_CELL ? b.d.nCells : location == MPAS_DYC_EDGE ? b.d.nEdges : b.d.nVertices;
+  const int64_t nown = location == MPAS_DYC_CELL ? b.d.nCellsSolve
+                       : location == MPAS_DYC_EDGE ? b.d.nEdgesSolve : b.d.nVerticesSolve;
+  std::vector<int32_t> idx(n), pos(n);
+  std::set<int32_t> seen;
+  for (int i = 0; i < n; ++i) {
+    const int32_t v = local_index[i] - 1;
+    const bool ok = direction == MPAS_DYC_SEND ? (v >= 0 && v < nown) : (v >= nown && v < nl);
+    if (!ok || position[i] < 1 || !seen.insert(position[i]).second) {
+      ctx->err = "exchange list entry " + std::to_string(i + 1) + " (index " + std::to_string(local_index[i]) +
+                 ", position " + std::to_string(position[i]) + ") out of range or repeated";
+      return MPAS_DYC_EINVAL;
+    }
+    idx[i] = v;
+    pos[i] = position[i] - 1;
+  }
+  invalidate_plans(ctx);
+  XList* x = nullptr;
+  for (auto& e : b.xl)
+    if (e.loc == location && e.layer == halo_layer && e.dir == direction && e.peer_rank == peer_rank &&
+        e.peer_block < 0)
+      x = &e;
+  if (!x) {
+    b.xl.push_back(XList{location, halo_layer, direction, peer_rank, -1});
+    x = &b.xl.back();
+  }
+  if (!ctx->host_only) {
+    if (x->d_idx) HIPCHK(hipFree(x->d_idx));
+    if (x->d_pos) HIPCHK(hipFree(x->d_pos));
+    x->d_idx = x->d_pos = nullptr;
+  }
+  x->n = n;
+  x->h_idx = idx;
+  x->h_pos = pos;
+  if (n > 0 && !ctx->host_only) {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMalloc(&x->d_idx, n * sizeof(int32_t)));
+    HIPCHK(hipMemcpy(x->d_idx, idx.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&x->d_pos, n * sizeof(int32_t)));
+    HIPCHK(hipMemcpy(x->d_pos, pos.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
   }
   return MPAS_DYC_OK;
 }

@@ -146,6 +146,14 @@ module atm_time_integration
          integer(c_int32_t), dimension(*), intent(in) :: local_index
          integer(c_int32_t), value :: n
       end function
+      integer(c_int) function mpas_dyc_set_exchange_positions(ctx, block, location, halo_layer, direction, &
+            peer_rank, local_index, position, n) bind(C, name='mpas_dyc_set_exchange_positions')
+         import :: c_int, c_ptr, c_int32_t
+         type(c_ptr), value :: ctx
+         integer(c_int32_t), value :: block, location, halo_layer, direction, peer_rank
+         integer(c_int32_t), dimension(*), intent(in) :: local_index, position
+         integer(c_int32_t), value :: n
+      end function
       integer(c_int64_t) function mpas_dyc_comm_unique_id_bytes() bind(C, name='mpas_dyc_comm_unique_id_bytes')
          import :: c_int64_t
       end function
@@ -492,8 +500,6 @@ module atm_time_integration
       nb = count_blocks(domain)
       nprocs = domain % dminfo % nprocs
       myrank = domain % dminfo % my_proc_id
-      if (nprocs > 1 .and. nb > 1) &
-         call fatal(c_null_ptr, 'with several MPI tasks the MI355X dycore takes one block per task')
       if (nb == 1 .and. nprocs == 1 .and. c_associated(dyc_init)) then
          dyc = dyc_init
          dyc_init = c_null_ptr
@@ -528,7 +534,7 @@ module atm_time_integration
             call mpas_pool_get_subpool(block % structs, 'mesh', mesh)
             call mpas_pool_get_subpool(block % structs, 'state', state)
             call mpas_pool_get_subpool(block % structs, 'diag', diag)
-            call set_block_lists(block, ib, myrank, nprocs > 1)
+            call set_block_lists(block, ib, myrank, nprocs > 1, nb > 1)
             call upload_block(dyc, ib, mesh, state, diag)
             ib = ib + 1
             block => block % next
@@ -597,13 +603,16 @@ module atm_time_integration
    ! The block's parinfo lists (mpas_multihalo_exchange_list, built by mpas_block_creator):
    !  * xToCopy: endPointID = the local block receiving, srcList = owned elements here, destList
    !    = its halo elements, element i of one to element i of the other (mpas_dmpar.F:5480-5502);
-   !  * xToSend / xToRecv (other tasks, one block each): endPointID = the task, and the other list
-   !    holds buffer positions; sorted by position they give the order the two sides exchange
-   !    (mpas_dmpar.F:5440-5470, 5510-5540).
-   subroutine set_block_lists(block, ib, myrank, remote)
+   !  * xToSend / xToRecv (other tasks): endPointID = the task, and the other list holds buffer
+   !    positions (mpas_dmpar.F:5440-5470, 5510-5540).  One block per task: sorted by position they
+   !    give the order the two sides exchange (a block-pair list with the peer's block 0).  Several
+   !    blocks per task (positional): the lists go in as they are, element and position, and the
+   !    library lays the message out as mpas_dmpar lays out its buffer, which the task's blocks fill
+   !    together (mpas_dyc_set_exchange_positions).
+   subroutine set_block_lists(block, ib, myrank, remote, positional)
       type (block_type), pointer :: block
       integer, intent(in) :: ib, myrank
-      logical, intent(in) :: remote
+      logical, intent(in) :: remote, positional
       type (mpas_multihalo_exchange_list), pointer :: ml
       type (mpas_exchange_list), pointer :: node
       integer :: il, kind, layer
@@ -639,6 +648,18 @@ module atm_time_integration
                                    int(layer, c_int32_t), DYC_RECV, int(myrank, c_int32_t), int(ib, c_int32_t), &
                                    int(node % destList(1:node % nList), c_int32_t), int(node % nList, c_int32_t)), &
                                    'mpas_dyc_set_exchange_list')
+                     else if (positional .and. kind == 2) then
+                        call check(dyc, mpas_dyc_set_exchange_positions(dyc, int(ib, c_int32_t), loc, &
+                                   int(layer, c_int32_t), DYC_SEND, int(node % endPointID, c_int32_t), &
+                                   int(node % srcList(1:node % nList), c_int32_t), &
+                                   int(node % destList(1:node % nList), c_int32_t), int(node % nList, c_int32_t)), &
+                                   'mpas_dyc_set_exchange_positions')
+                     else if (positional) then
+                        call check(dyc, mpas_dyc_set_exchange_positions(dyc, int(ib, c_int32_t), loc, &
+                                   int(layer, c_int32_t), DYC_RECV, int(node % endPointID, c_int32_t), &
+                                   int(node % destList(1:node % nList), c_int32_t), &
+                                   int(node % srcList(1:node % nList), c_int32_t), int(node % nList, c_int32_t)), &
+                                   'mpas_dyc_set_exchange_positions')
                      else if (kind == 2) then
                         idx = sorted_by(node % srcList(1:node % nList), node % destList(1:node % nList))
                         call check(dyc, mpas_dyc_set_exchange_list(dyc, int(ib, c_int32_t), loc, int(layer, c_int32_t), &

@@ -66,22 +66,29 @@ def jw_case(ncells: int, K: int = 56, ns: int = 1, moist: bool = False, order: i
 
 
 def varres_case(ncells: int, ratio: float = 20.0, K: int = 56, ns: int = 1, moist: bool = False,
-                lloyd_iters: int | None = None, cache: bool = True) -> dict:
-    """JW state on a variable-resolution SCVT (BASELINE.json configs[4] analogue).
+                lloyd_iters: int | None = None, cache: bool = True, order: int = 2) -> dict:
+    """JW state on a variable-resolution SCVT (BASELINE.json configs[4]).
 
-    dt and config_len_disp follow the finest spacing, as MPAS variable-resolution runs do
-    (dt ~ 5 s per km of the finest cells, len_disp = finest spacing)."""
+    ncells = 835586 with ratio 20: the 60-3 km mesh of configs[4] from its stored generators
+    (mesh.varres_from_generators, Lloyd-relaxed offline by tools/make_varres_mesh.py); other sizes
+    are generated here (mesh.build_varres_mesh).  dt and config_len_disp follow the finest spacing,
+    as MPAS variable-resolution runs do (dt ~ 5 s per km of the finest cells, len_disp = finest
+    spacing); ``order`` = config_time_integration_order (3 for the BASELINE runs)."""
+    from .mesh import X20_835586, varres_from_generators
+    stored = ncells == 835586 and ratio == 20.0 and os.path.isfile(X20_835586)
     if lloyd_iters is None:
         lloyd_iters = 40 if ncells <= 200000 else 6
-    key = f"vr_n{ncells}_r{ratio:g}_K{K}_ns{ns}_m{int(moist)}_ll{lloyd_iters}_v6"
+    key = (f"vr_x20.835586_K{K}_ns{ns}_m{int(moist)}_o{order}_v7" if stored else
+           f"vr_n{ncells}_r{ratio:g}_K{K}_ns{ns}_m{int(moist)}_ll{lloyd_iters}_o{order}_v6")
     path = os.path.join(CACHE, key + ".pkl")
     if cache and os.path.isfile(path):
         with open(path, "rb") as f:  # our own cache file, written below
             return pickle.load(f)
-    m = build_varres_mesh(ncells, ratio=ratio, lloyd_iters=lloyd_iters)
+    m = varres_from_generators(X20_835586) if stored else build_varres_mesh(ncells, ratio=ratio,
+                                                                               lloyd_iters=lloyd_iters)
     dx_min = float(m["dcEdge"].min())
     dt = float(max(1.0, round(5.0 * dx_min / 1000.0)))
-    cfg = dict(config_len_disp=dx_min, config_dt=dt)
+    cfg = dict(config_len_disp=dx_min, config_dt=dt, config_time_integration_order=order)
     if ncells > 200000:
         print(f"varres case: mesh done ({m['nCells']} cells), building the JW state", file=sys.__stderr__, flush=True)
     case = build_case(m, K=K, ns=ns, moist=moist, config=cfg)

@@ -280,3 +280,46 @@ def rank_blocks(case: dict, nranks: int, rank: int, blocks_per_rank: int = 1, ce
     placement = {p: (p // blocks_per_rank, p % blocks_per_rank) for p in range(nparts)}
     blocks = decompose(case, cell_part, parts=mine, placement=placement)
     return blocks, placement
+
+
+def positional_lists(blocks: list[Block], placement: dict, rank: int, include_self: bool = False) -> list:
+    """The exchange lists of this rank's blocks as mpas_dmpar holds them when tasks own several blocks
+    (parinfo xToSend / xToRecv: endPointID = the task, the other list = buffer positions,
+    mpas_dmpar.F:5448-5535): for each (peer rank, location, halo layer) one buffer whose slots are the
+    distinct elements the two tasks exchange there, in ascending global index -- a set both sides
+    know, so both number it alike without knowing the other side's blocks.  Returns, per block, a
+    list of (direction "send" / "recv", loc, layer, peer_rank, local 0-based indices, 1-based
+    positions) for mpas_dyc_set_exchange_positions.  include_self: also the lists between blocks of
+    this rank (a one-process test of the positional path over RCCL)."""
+    def peer_ok(pr):
+        return pr != rank or include_self
+    union = {}   # (dir, loc, layer, peer_rank) -> global ids of this rank's side
+    per = []     # per block: {(dir, loc, layer, peer_rank): (local idx, gids)}
+    for b in blocks:
+        mine = {}
+        for dname, lists in (("send", b.send), ("recv", b.recv)):
+            for loc, layer, peer, idx in lists:
+                pr = placement[peer][0]
+                if not peer_ok(pr):
+                    continue
+                key = (dname, loc, layer, pr)
+                idx = np.asarray(idx, dtype=np.int64)
+                mine.setdefault(key, []).append(idx)
+        out = {}
+        for key, parts in mine.items():
+            idx = np.concatenate(parts)
+            gids = b.glob[key[1]][idx]
+            gids, first = np.unique(gids, return_index=True)   # an element goes once per buffer
+            out[key] = (idx[first], gids)
+            union.setdefault(key, []).append(gids)
+        per.append(out)
+    union = {k: np.unique(np.concatenate(v)) for k, v in union.items()}
+    res = []
+    for out in per:
+        lst = []
+        for key in sorted(out):
+            idx, gids = out[key]
+            pos = np.searchsorted(union[key], gids) + 1
+            lst.append((key[0], key[1], key[2], key[3], idx.astype(np.int32), pos.astype(np.int32)))
+        res.append(lst)
+    return res

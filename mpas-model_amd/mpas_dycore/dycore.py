@@ -53,9 +53,32 @@ def _make_dims(cases, solves, moist_end):
     return dims
 
 
-def _install_lists(lib, h, blocks, placement, check):
-    """Every block's send / receive lists (mpas_multihalo_exchange_list) into the context."""
+def _install_lists(lib, h, blocks, placement, check, positional_rank=None, include_self=False):
+    """Every block's send / receive lists (mpas_multihalo_exchange_list) into the context.
+    positional_rank (this process's rank): the lists with other ranks go in as mpas_dmpar keeps them
+    for tasks of several blocks -- positions in one buffer per task pair (decomp.positional_lists,
+    mpas_dyc_set_exchange_positions); include_self: this rank's own block pairs too."""
     code = {"cell": _lib.CELL, "edge": _lib.EDGE, "vertex": _lib.VERTEX}
+    if positional_rank is not None:
+        from .decomp import positional_lists
+        pos = positional_lists(blocks, placement, positional_rank, include_self=include_self)
+        for ib, (b, lst) in enumerate(zip(blocks, pos)):
+            for dname, loc, layer, pr, idx, p in lst:
+                a = np.ascontiguousarray(idx + 1, dtype=np.int32)
+                p = np.ascontiguousarray(p, dtype=np.int32)
+                check(lib.mpas_dyc_set_exchange_positions(h, ib, code[loc], int(layer),
+                                                          _lib.SEND if dname == "send" else _lib.RECV, int(pr),
+                                                          a.ctypes.data_as(C.c_void_p), p.ctypes.data_as(C.c_void_p),
+                                                          int(a.size)), "set_exchange_positions")
+            for direction, lists in ((_lib.SEND, b.send), (_lib.RECV, b.recv)):
+                for loc, layer, peer, idx in lists:
+                    pr, pb = placement[peer]
+                    if pr != positional_rank or include_self:
+                        continue
+                    a = np.ascontiguousarray(np.asarray(idx, dtype=np.int32) + 1)
+                    check(lib.mpas_dyc_set_exchange_list(h, ib, code[loc], int(layer), direction, int(pr), int(pb),
+                                                         a.ctypes.data_as(C.c_void_p), int(a.size)), "set_exchange_list")
+        return
     for ib, b in enumerate(blocks):
         for direction, lists in ((_lib.SEND, b.send), (_lib.RECV, b.recv)):
             for loc, layer, peer, idx in lists:
@@ -66,7 +89,7 @@ def _install_lists(lib, h, blocks, placement, check):
 
 
 def plan_exchanges(blocks: list, placement: dict, rank: int, nranks: int, dt: float, moist_end: int = 1,
-                   overlap: bool | None = None) -> tuple[np.ndarray, list[str]]:
+                   overlap: bool | None = None, positional: bool = False) -> tuple[np.ndarray, list[str]]:
     """Dry run of the exchange planner for one rank, on the host (no GPU): the RCCL messages
     this rank posts over model init and one step on each time-level parity, and the plan key of
     every exchange call in issue order (mpas_dyc_plan_exchanges).  Messages are a structured array
@@ -85,7 +108,7 @@ def plan_exchanges(blocks: list, placement: dict, rank: int, nranks: int, dt: fl
             msg = lib.mpas_dyc_last_error(h)
             raise DycoreError(f"{what} failed ({r}): {msg.decode() if msg else ''}")
     try:
-        _install_lists(lib, h, blocks, placement, check)
+        _install_lists(lib, h, blocks, placement, check, positional_rank=rank if positional else None)
         check(lib.mpas_dyc_set_overlap(h, -1 if overlap is None else int(bool(overlap))), "set_overlap")
         nm, kl = C.c_int64(), C.c_int64()
         lib.mpas_dyc_plan_exchanges(h, int(nranks), int(rank), float(dt), None, 0, C.byref(nm), None, 0,
@@ -141,7 +164,8 @@ class Dycore:
 
     @classmethod
     def from_blocks(cls, blocks: list, device: int = 0, moist_end: int = 1, placement: dict | None = None,
-                    rank: int = 0, nranks: int = 1, comm_id: bytes | None = None, rccl_local: bool = False):
+                    rank: int = 0, nranks: int = 1, comm_id: bytes | None = None, rccl_local: bool = False,
+                    positional: bool = False):
         """Blocks of this process (``decomp.decompose(..., parts=...)``) on one GPU.
 
         ``placement`` maps every block (part) id to (rank, local block index); by
@@ -155,7 +179,10 @@ class Dycore:
             self._check(self.lib.mpas_dyc_comm_init(self.h, idb, len(comm_id), int(nranks), int(rank)), "comm_init")
         if rccl_local:
             self._check(self.lib.mpas_dyc_set_transport(self.h, 1), "set_transport")
-        _install_lists(self.lib, self.h, blocks, placement, self._check)
+        # positional: the lists with other ranks as mpas_dmpar keeps them for tasks of several blocks (with
+        # rccl_local, this process's block pairs too) -- the Fortran drop-in's path
+        _install_lists(self.lib, self.h, blocks, placement, self._check, positional_rank=rank if positional else None,
+                       include_self=positional and rccl_local)
         return self
 
     def graph_active(self) -> bool:

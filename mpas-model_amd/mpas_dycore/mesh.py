@@ -26,6 +26,7 @@ are local in memory (north_star: "index arrays reordered by SFC").
 """
 from __future__ import annotations
 
+import os
 import sys
 
 import numpy as np
@@ -271,6 +272,31 @@ def build_varres_mesh(ncells: int, ratio: float = 20.0, lloyd_iters: int = 10, s
             print(f"varres mesh: Lloyd iteration {it + 1}/{lloyd_iters}", file=sys.__stderr__, flush=True)
     if start == "icosahedral":  # a safety net: the stretched lattice relaxes without such quads
         p = _untangle_cocircular(p)
+    f = _delaunay(p)
+    if sfc:
+        order = np.argsort(_hilbert3d_keys(p), kind="stable")
+        rank = np.empty_like(order)
+        rank[order] = np.arange(len(order))
+        p = p[order]
+        f = rank[f]
+    m = _topology_and_geometry(p, f, radius)
+    m["meshDensity"] = rho(p)
+    return m
+
+
+DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+X20_835586 = os.path.join(DATA, "x20.835586_generators.npz")
+
+
+def varres_from_generators(path: str = X20_835586, radius: float = SPHERE_RADIUS, sfc: bool = True) -> dict:
+    """A variable-resolution mesh from stored generators (tools/make_varres_mesh.py: the BASELINE.json
+    configs[4] 60-3 km SCVT of 835586 cells, Lloyd-relaxed offline): the spherical Delaunay
+    triangulation of the generators, Hilbert-ordered, with the MPAS topology and geometry, and the
+    meshDensity of the density it was relaxed for."""
+    z = np.load(path, allow_pickle=False)
+    p = _normalize(z["xyz_q30"].astype(np.float64) / 2.0 ** 30)
+    rho = varres_density(tuple(float(x) for x in z["center"]), float(z["radius_deg"]), float(z["width_deg"]),
+                         float(z["ratio"]))
     f = _delaunay(p)
     if sfc:
         order = np.argsort(_hilbert3d_keys(p), kind="stable")

@@ -37,12 +37,13 @@ def _single(case, nsteps, graph=False):
     return out
 
 
-def _blocks(case, nblocks, nsteps, graph=False, rccl_local=False, overlap=True):
+def _blocks(case, nblocks, nsteps, graph=False, rccl_local=False, overlap=True, positional=False, moist_end=1):
     from mpas_dycore import Dycore, decomp
     part = decomp.partition_sfc(case["nCells"], nblocks)
     blocks = decomp.decompose(case, part)
     comm_id = Dycore.comm_unique_id() if rccl_local else None
-    dy = Dycore.from_blocks(blocks, device=0, comm_id=comm_id, nranks=1, rank=0, rccl_local=rccl_local)
+    dy = Dycore.from_blocks(blocks, device=0, comm_id=comm_id, nranks=1, rank=0, rccl_local=rccl_local,
+                            positional=positional, moist_end=moist_end)
     dy.set_overlap(overlap)
     dy.use_graph(graph)
     _run(dy, nsteps)
@@ -112,6 +113,20 @@ def test_rccl_transport_matches_device_copies(small_case):
     b = _blocks(small_case, 2, 2, graph=True, rccl_local=True)
     for name in a:
         assert np.array_equal(a[name], b[name]), name
+
+
+@pytest.mark.parametrize("which", ["small_case", "moist_case"])
+def test_positional_lists_bitwise(which, request):
+    """The lists of a task that holds several blocks, as mpas_dmpar keeps them and the Fortran drop-in
+    hands them over (one buffer per task pair and halo layer, positions filled by all the task's
+    blocks; mpas_dyc_set_exchange_positions): 4 blocks exchanging through RCCL by positions equal the
+    block-pair lists and one block bit for bit, graph replay, split-phase exchanges."""
+    case = request.getfixturevalue(which)
+    me = case["num_scalars"]
+    a = _blocks(case, 4, 3, graph=True, rccl_local=True, moist_end=me)
+    b = _blocks(case, 4, 3, graph=True, rccl_local=True, positional=True, moist_end=me)
+    for name in a:
+        assert np.array_equal(a[name], b[name]), f"{name}: positional lists differ from block-pair lists"
 
 
 @pytest.mark.parametrize("overlap", [True, False])

@@ -12,9 +12,11 @@ box as a binary) run on the GPU box's host cores, 16 OpenMP threads.
     to the one-block run;
   * configs[3]: the same mesh, num_scalars = 6 (all moist species), monotone split transport,
     10 steps vs the reference;
-  * configs[4]: variable-resolution mesh of ~835586 cells (835212: a Schmidt-stretched, Lloyd-relaxed
-    icosahedral mesh, 4.5-129 km, mesh.build_varres_mesh), 56 levels: 10 steps vs the reference, and
-    8 RCCL blocks (cells of very different sizes per block) bitwise equal to one block.
+  * configs[4]: the 60-3 km variable-resolution SCVT of 835586 cells (x20.835586's size and range:
+    generators relaxed offline by tools/make_varres_mesh.py, triangulated on the box by
+    mesh.varres_from_generators; pentagons, hexagons and heptagons, maxEdges = 7), 56 levels,
+    config_time_integration_order = 3: 10 steps vs the reference, and 8 RCCL blocks (cells of very
+    different sizes per block) bitwise equal to one block.
 
 Cases are built on the box (about a minute at 163842, a few at 835586) and cached under
 $MPAS_DYCORE_CACHE (default /tmp/mpas_dycore_cache), where bench.py finds them too.
@@ -171,9 +173,14 @@ def test_configs3_x1_163842_L56_moist_ns6_mono_10_steps_matches_reference():
 @pytest.fixture(scope="module")
 def varres835586():
     from mpas_dycore.cases import varres_case
-    with heartbeat("building the ~835586-cell variable-resolution case (20x)"):
-        c = varres_case(835586, ratio=20.0, K=56, ns=1)
-    assert c["nCells"] > 800000 and c["dcEdge"].max() / c["dcEdge"].min() > 10.0
+    with heartbeat("building the 835586-cell 60-3 km variable-resolution case (order 3)"):
+        c = varres_case(835586, ratio=20.0, K=56, ns=1, order=3)
+    noc = np.asarray(c["nEdgesOnCell"])
+    assert c["nCells"] == 835586 and c["maxEdges"] == 7 and (noc == 7).sum() > 0 and (noc == 5).sum() > 0
+    assert 2.0e3 < c["dcEdge"].min() < 3.6e3 and 50e3 < c["dcEdge"].max() < 75e3, "not a 60-3 km mesh"
+    assert c["config"]["config_time_integration_order"] == 3
+    progress(f"x20.835586: dcEdge {c['dcEdge'].min() / 1e3:.2f}-{c['dcEdge'].max() / 1e3:.1f} km, "
+             f"{int((noc == 5).sum())} pentagons, {int((noc == 7).sum())} heptagons, dt {c['dt']:g} s")
     return c
 
 

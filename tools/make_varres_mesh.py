@@ -8,9 +8,12 @@ Density (MPAS convention, cell spacing ~ rho^-1/4): rho = (1-g)/2 (tanh((beta-d)
 g = 20^-4, beta = 9 deg, alpha = 3 deg, centred at (30N, 90W): integrating sqrt(rho) over the sphere
 with 3 km hexagons in the refined disc gives 835714 cells, i.e. 3 km there and 60 km far away.
 
-Start: a Fibonacci lattice remapped radially so that the point density is ~ sqrt(rho) (the areal
-density of a CVT), then density-weighted Lloyd iterations on the spherical Delaunay triangulation,
-rebuilt every step, until the mesh is well shaped (progress and quality every --report steps).
+Construction (multilevel Lloyd): a 3266-generator SCVT of the same density (a Fibonacci lattice
+remapped radially so that the point density is ~ sqrt(rho), relaxed by many Lloyd iterations), then
+four refinements, each adding the midpoint of every Delaunay edge (N -> 4 N - 6: 3266 -> 13058 ->
+52226 -> 208898 -> 835586) and relaxing again with density-weighted Lloyd iterations on the spherical
+Delaunay triangulation, rebuilt every step.  Refinement keeps the coarse mesh's few pentagon /
+heptagon defects, and each level only has to relax what the new points change.
 
     python tools/make_varres_mesh.py [--iters 300] [--out mpas-model_amd/mpas_dycore/data/...]
 """
@@ -66,27 +69,42 @@ def quality(p):
                 n_small_dv=int((dv < 0.2 * dc).sum()), deg={int(k): int((deg == k).sum()) for k in np.unique(deg)})
 
 
+def refine(p):
+    """Add the normalised midpoint of every Delaunay edge: N -> 4 N - 6 generators."""
+    f = M._delaunay(p)
+    e = np.sort(np.concatenate([f[:, [0, 1]], f[:, [1, 2]], f[:, [2, 0]]]), axis=1)
+    e = np.unique(e, axis=0)
+    return np.concatenate([p, M._normalize(p[e[:, 0]] + p[e[:, 1]])])
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=300)
-    ap.add_argument("--report", type=int, default=10)
-    ap.add_argument("--resume", default=None, help="continue from a checkpoint .npy")
-    ap.add_argument("--checkpoint", default="/tmp/varres_gen.npy")
+    ap.add_argument("--iters", default="600,200,80,40,30", help="Lloyd iterations per level, coarse to fine")
+    ap.add_argument("--checkpoint", default="/tmp/varres_gen")
     ap.add_argument("--out", default=os.path.join(ROOT, "mpas-model_amd", "mpas_dycore", "data",
                                                   "x20.835586_generators.npz"))
     a = ap.parse_args()
+    iters = [int(x) for x in a.iters.split(",")]
     rho = M.varres_density(CENTER, RADIUS_DEG, WIDTH_DEG, RATIO)
-    p = np.load(a.resume) if a.resume else radial_start(NCELLS)
+    n0 = (NCELLS + 510) // 256
+    assert 256 * n0 - 510 == NCELLS
+    p = radial_start(n0)
     t0 = time.time()
-    for it in range(a.iters):
-        p = M._lloyd_step(p, M._delaunay(p), rho)
-        if (it + 1) % a.report == 0 or it + 1 == a.iters:
-            np.save(a.checkpoint, p)
-            print(f"iter {it + 1}: {time.time() - t0:.0f} s {quality(p)}", flush=True)
+    for level, nit in enumerate(iters):
+        if level:
+            p = refine(p)
+        for it in range(nit):
+            p = M._lloyd_step(p, M._delaunay(p), rho)
+            if len(p) > 200000 and (it + 1) % 10 == 0:
+                print(f"level {level} ({len(p)}): iter {it + 1} {time.time() - t0:.0f} s", flush=True)
+        np.save(f"{a.checkpoint}_{level}.npy", p)
+        print(f"level {level}: {len(p)} generators, {nit} iterations, {time.time() - t0:.0f} s {quality(p)}",
+              flush=True)
+    assert len(p) == NCELLS
     q = np.round(p * 2.0 ** 30).astype(np.int32)  # |x| <= 1: int32 with 2^-30 steps (~6 mm on Earth)
     np.savez_compressed(a.out, xyz_q30=q, center=np.array(CENTER), radius_deg=RADIUS_DEG, width_deg=WIDTH_DEG,
                         ratio=RATIO)
-    print(f"wrote {a.out}: {quality(M._normalize(q / 2.0 ** 30))}")
+    print(f"wrote {a.out}: {quality(M._normalize(q / 2.0 ** 30))}", flush=True)
 
 
 if __name__ == "__main__":
