@@ -53,7 +53,15 @@ def cpu_baseline(case, dt, nthreads, steps, moist_end=1):
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = None
-    return dict(value=case["nCells"] * case["nVertLevels"] / t, unit="cell-updates/s", cores=nthreads,
+    value = case["nCells"] * case["nVertLevels"] / t
+    # the whole host as context: the pool's rules give one GPU's job 16 host threads (OMP_NUM_THREADS on
+    # the box), so the reference is not run on every core of the shared host; at ideal (linear) OpenMP
+    # scaling over `affinity` cores it could reach at most this
+    whole = None
+    if affinity and affinity > nthreads:
+        whole = dict(value=value * affinity / nthreads, cores=affinity, kind="upper bound, linear scaling of the "
+                     f"{nthreads}-thread measurement (not run: the box's CPU share is {nthreads} threads)")
+    return dict(value=value, unit="cell-updates/s", cores=nthreads, whole_host=whole,
                 kind="reference", cpu_model=_cpu_model(), host_nproc=os.cpu_count(), affinity=affinity,
                 omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
                 cores_note="threads = the host-CPU share the GPU pool gives one GPU (OMP_NUM_THREADS on the box); "

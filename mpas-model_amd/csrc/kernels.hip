@@ -165,6 +165,49 @@ __device__ __forceinline__ double ld_uniform_f64(const double* a) {
 }
 
 #ifdef MPAS_WIDE
+// The column's sequential recurrences in the wide build: one lane walks the column in LDS, the
+// reference's loop exactly (two barriers in all, instead of two per level through readlane_d).
+// Forward x(k) = (x(k) - a(k) x(k-1)) alpha(k) for k = 1..K-1, then backward x(k) = x(k) - gamma(k)
+// x(k+1) for k = K-1..0 (mpas_atm_time_integration.F:2675-2682); x(K) is read, never written.
+__device__ __forceinline__ double column_solve(double x, double a, double alpha, double gamma, int k, int K) {
+  __shared__ double sx[WIDE_THREADS], sa[WIDE_THREADS], sal[WIDE_THREADS], sg[WIDE_THREADS];
+  __syncthreads();
+  sx[threadIdx.x] = x;
+  sa[threadIdx.x] = a;
+  sal[threadIdx.x] = alpha;
+  sg[threadIdx.x] = gamma;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int kk = 1; kk < K; ++kk) sx[kk] = (sx[kk] - sa[kk] * sx[kk - 1]) * sal[kk];
+    for (int kk = K - 1; kk >= 0; --kk) sx[kk] = sx[kk] - sg[kk] * sx[kk + 1];
+  }
+  __syncthreads();
+  return sx[k];
+}
+// the LU factors of the implicit w solve (2124-2127): alpha(k) = 1 / (b(k) - a(k) gamma(k-1)),
+// gamma(k) = c(k) alpha(k) for k = 1..K-1; lane 0 keeps alpha = gamma = 0
+__device__ __forceinline__ void column_lu(double a, double b, double c, int k, int K, double& alpha, double& gamma) {
+  __shared__ double sa[WIDE_THREADS], sb[WIDE_THREADS], sc[WIDE_THREADS], sal[WIDE_THREADS], sg[WIDE_THREADS];
+  __syncthreads();
+  sa[threadIdx.x] = a;
+  sb[threadIdx.x] = b;
+  sc[threadIdx.x] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double g = 0.0;
+    sal[0] = 0.0;
+    sg[0] = 0.0;
+    for (int kk = 1; kk < K; ++kk) {
+      const double al = 1. / (sb[kk] - sa[kk] * g);
+      g = sc[kk] * al;
+      sal[kk] = al;
+      sg[kk] = g;
+    }
+  }
+  __syncthreads();
+  alpha = k < K ? sal[k] : 0.0;
+  gamma = k < K ? sg[k] : 0.0;
+}
 __device__ __forceinline__ double readlane_d(double v, int l) {
   __shared__ double rl_buf[WIDE_THREADS];
   __syncthreads();
@@ -360,6 +403,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_vert_imp_coefs(Dims d, Ptrs p
   }
   // sequential LU recurrence in the reference order (2124-2127)
   double alpha = 0.0, gamma = 0.0;
+#ifdef MPAS_WIDE
+  column_lu(a, b, cc, k, K, alpha, gamma);
+#else
   for (int kk = 1; kk < K; ++kk) {
     const double gp = readlane_d(gamma, kk - 1);
     if (k == kk) {
@@ -367,6 +413,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_vert_imp_coefs(Dims d, Ptrs p
       gamma = cc * alpha;
     }
   }
+#endif
   if (act) {
     if (k >= 1) {
       p.cofwr[o] = cofwr;
@@ -2915,6 +2962,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p
     }
     // tridiagonal solve sweeping up and then down the column (2675-2682), reference order
     const double a_tri = LD(p.a_tri, o), alpha_tri = LD(p.alpha_tri, o), gamma_tri = LD(p.gamma_tri, o);
+#ifdef MPAS_WIDE
+    rwp = column_solve(rwp, a_tri, alpha_tri, gamma_tri, k, K);
+#else
     for (int kk = 1; kk < K; ++kk) {
       const double xm = readlane_d(rwp, kk - 1);
       if (k == kk) rwp = (rwp - a_tri * xm) * alpha_tri;
@@ -2923,6 +2973,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells(Dims d, Ptrs p
       const double xp = readlane_d(rwp, kk + 1);
       if (k == kk) rwp = rwp - gamma_tri * xp;
     }
+#endif
     // implicit Rayleigh damping of w (2687-2693)
     if (act && k >= 1) {
       const double fzm = p.fzm[k], fzp = p.fzp[k];

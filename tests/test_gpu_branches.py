@@ -14,7 +14,8 @@ They also run the dynamics/transport split with 1, 2 and 4 dynamics substeps
 (5993-6081) and the exchanges at a substep boundary (1282-1297).  Then scalar advection
 switched off (config_scalar_advection, 1355).  Then the reference's default 55 levels
 (core_init_atmosphere/Registry.xml:100), moist with num_scalars = 6 and the monotone limiter.
-At that odd K the pair-layout edge kernels give way to the one-column ones.
+At that odd K the pair-layout kernels run their odd-K instantiations (ODD = true: the last lane pair
+holds level K-1 and a masked level past the column).
 
 Each variant runs 10 atm_timestep calls on x1.2562 with the captured hipGraph (the product
 path).  It is compared with the unmodified reference atm_srk3 (oracle/_ref) on the same mesh
