@@ -44,9 +44,11 @@ extern "C" {
 #define MPAS_DYC_ESTATE -3    /* call out of sequence */
 #define MPAS_DYC_ECOMM -4     /* halo exchange failure */
 
-/* nVertLevels: 4..MPAS_DYC_MAX_LEVELS.  Up to MPAS_DYC_MAX_LEVELS_WAVE a column is one 64-lane
- * wavefront (lane = level, every kernel family); above, one 128-lane workgroup whose cross-level
- * moves go through LDS (the one-column-per-element kernels, no regional LBCs). */
+/* nVertLevels: 4..MPAS_DYC_MAX_LEVELS, every kernel family and regional LBCs at any of them.  Up to
+ * MPAS_DYC_MAX_LEVELS_WAVE a column is one 64-lane wavefront (lane = level), or half of one in the
+ * pair layout (two levels per lane); above, the pair-layout kernels give a whole wavefront to one
+ * column (two levels per lane) and the per-cell kernels one 128-lane workgroup, whose cross-level
+ * moves go through LDS. */
 #define MPAS_DYC_MAX_LEVELS_WAVE 63
 #define MPAS_DYC_MAX_LEVELS 127
 
@@ -341,8 +343,9 @@ int32_t mpas_dyc_rccl_version(void);
  * out[0] = maxEdges the kernels index with (max(nEdgesOnCell), at least 6 -- mesh files may
  * declare more, e.g. 10, Registry.xml:13-16), out[1] = maxEdges2 likewise, out[2] = kernel
  * family (0 one column per element, 1 batched stencil records, 2 pair layout: two elements per
- * wavefront, two levels per lane), out[3] = column shape (0 one wavefront, 1 one workgroup:
- * nVertLevels > MPAS_DYC_MAX_LEVELS_WAVE). */
+ * wavefront, two levels per lane -- one element per wavefront above MPAS_DYC_MAX_LEVELS_WAVE),
+ * out[3] = column shape (0 one wavefront, 1 nVertLevels > MPAS_DYC_MAX_LEVELS_WAVE: one 128-lane
+ * workgroup per column in the per-cell kernels, one wavefront per column in the pair layout). */
 int mpas_dyc_block_layout(mpas_dyc_ctx* ctx, int32_t block, int32_t* out /* [4] */);
 
 #ifdef __cplusplus

@@ -502,10 +502,18 @@ inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + WAVES_PER_BLOCK - 
                          ctx->stream, __VA_ARGS__);                                                        \
   } while (0)
 // a pair-layout kernel in its even-K or odd-K instance (its last template parameter, ODD)
+// over n elements (PAIR_EPW per wavefront, PAIR_WPB wavefronts per workgroup)
+#define LAUNCH_P(kern, n, ...)                                                                             \
+  do {                                                                                                     \
+    const int64_t nw_ = ((int64_t)(n) + PAIR_EPW - 1) / PAIR_EPW;                                           \
+    if (nw_ > 0 && !ctx->planning)                                                                         \
+      hipLaunchKernelGGL(kern, dim3((unsigned)((nw_ + PAIR_WPB - 1) / PAIR_WPB)), dim3(PAIR_THREADS), 0,    \
+                         ctx->stream, __VA_ARGS__);                                                        \
+  } while (0)
 #define LAUNCH_PE(kern_even, kern_odd, n, ...)        \
   do {                                               \
-    if (d.K & 1) LAUNCH_E(kern_odd, n, __VA_ARGS__);   \
-    else LAUNCH_E(kern_even, n, __VA_ARGS__);          \
+    if (d.K & 1) LAUNCH_P(kern_odd, n, __VA_ARGS__);   \
+    else LAUNCH_P(kern_even, n, __VA_ARGS__);          \
   } while (0)
 #define LAUNCH(kern, n, ...)                                                                               \
   do {                                                                                                     \
@@ -1136,18 +1144,14 @@ inline bool fuse_smlstep(const Dims& d) { return g_fuse_smlstep && batched(d); }
 // pair's second level is past the column: loaded (the 256 B of slack behind every field covers the
 // last column), never stored, and every level-dependent expression masks it as it masks the
 // levels above K at an even K
-inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K <= 64; }
+// (the wide build: one column per wavefront, K <= 2 x 64 - 1 levels, same kernels)
+inline bool pair_layout(const Dims& d) { return g_kernel_tier >= 2 && batched(d) && d.K <= 64 * (3 - PAIR_EPW) - 1; }
 
 // why a block cannot run regional LBCs (they need the pair layout), named by its actual cause
 std::string lbc_layout_error(const Dims& d) {
-#ifdef MPAS_WIDE
-  (void)d;
-  return "regional LBCs are not supported above " + std::to_string(MPAS_DYC_MAX_LEVELS_WAVE) + " vertical levels";
-#else
   if (g_kernel_tier < 2) return "regional LBCs need the pair kernel family (MPAS_DYCORE_KERNELS=pair)";
   return "regional LBCs need cells of at most 7 edges (max(nEdgesOnCell) = " + std::to_string(d.maxEdges) +
          ") and maxEdges2 >= " + std::to_string(2 * d.maxEdges - 2);
-#endif
 }
 
 // The kernels index the maxEdges-strided mesh arrays with the mesh's actual cell degree, not with
@@ -1433,7 +1437,7 @@ void rk_integration_setup(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p) {
 
 void vert_imp_coefs(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts) {
   if (pair_layout(d))
-    LAUNCH_PE((k_vert_imp_coefs_p<false>), (k_vert_imp_coefs_p<true>), std::max((d.nCellsSolve + 1) / 2, 1), d, p, dts, ctx->cf.epssm);
+    LAUNCH_PE((k_vert_imp_coefs_p<false>), (k_vert_imp_coefs_p<true>), std::max(d.nCellsSolve, 1), d, p, dts, ctx->cf.epssm);
   else
     LAUNCH(k_vert_imp_coefs, std::max(d.nCellsSolve, 1), d, p, dts, ctx->cf.epssm);
 }
@@ -1471,7 +1475,7 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   }
   if (part == 1) return;
   if (pair_layout(d)) {
-    const int64_t nw = (d.nEdges + 1) / 2;
+    const int64_t nw = d.nEdges;
     if (rk_step == 1) LAUNCH_PE((k_dyn_edges_pgf_p<false>), (k_dyn_edges_pgf_p<true>), nw, d, p);
     if (d.maxEdges == 6 && rk_step == 1) LAUNCH_PE((k_dyn_edges_p<true, 10, true, false>), (k_dyn_edges_p<true, 10, true, true>), nw, d, p, cf, s, 0);
     if (d.maxEdges == 6 && rk_step != 1) LAUNCH_PE((k_dyn_edges_p<false, 10, false, false>), (k_dyn_edges_p<false, 10, false, true>), nw, d, p, cf, s, 1, tp);
@@ -1503,8 +1507,8 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
     }
   }
   if (!batched(d)) LAUNCH(k_dyn_advflux, d.nEdges, d, p);
-  else if (pair_layout(d) && d.maxEdges == 6) LAUNCH_PE((k_dyn_advflux_p<10, false>), (k_dyn_advflux_p<10, true>), (d.nEdges + 1) / 2, d, p);
-  else if (pair_layout(d)) LAUNCH_PE((k_dyn_advflux_p<12, false>), (k_dyn_advflux_p<12, true>), (d.nEdges + 1) / 2, d, p);
+  else if (pair_layout(d) && d.maxEdges == 6) LAUNCH_PE((k_dyn_advflux_p<10, false>), (k_dyn_advflux_p<10, true>), d.nEdges, d, p);
+  else if (pair_layout(d)) LAUNCH_PE((k_dyn_advflux_p<12, false>), (k_dyn_advflux_p<12, true>), d.nEdges, d, p);
   else if (d.maxEdges == 6) LAUNCH_E(k_dyn_advflux_b<10>, d.nEdges, d, p);
   else LAUNCH_E(k_dyn_advflux_b<12>, d.nEdges, d, p);
   if (batched(d)) {
@@ -1553,7 +1557,7 @@ double coef_divdamp(const mpas_dyc_ctx* ctx, double dts) {  // 2761-2763
 void acoustic_edges(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dts, int small_step, int damp,
                     int phase, int fresh = 0, UnpackMap um = UnpackMap{}) {
   if (pair_layout(d)) {
-    const int64_t nw = ((phase == 2 ? d.n_bnd_pairs : d.nEdges) + 1) / 2;  // phase 2: the bnd_pairs list
+    const int64_t nw = phase == 2 ? d.n_bnd_pairs : d.nEdges;  // phase 2: the bnd_pairs list
     const bool up = um.recv != nullptr;
     if (damp && up)
       LAUNCH_PE((k_acoustic_edges_p<true, true, false>), (k_acoustic_edges_p<true, true, true>), nw, d, p, dts, small_step, coef_divdamp(ctx, dts), phase, fresh, um);
@@ -1623,7 +1627,7 @@ void divergence_damping(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double 
                         XPack upk = XPack{}) {
   // (k_divdamp_b, one edge per wave with batched loads, measured 6 % slower than this)
   const bool up = um.recv != nullptr;
-  const int64_t nw = ((phase == 2 ? d.n_bnd_pairs : d.nEdges) + 1) / 2;  // phase 2: the bnd_pairs list
+  const int64_t nw = phase == 2 ? d.n_bnd_pairs : d.nEdges;  // phase 2: the bnd_pairs list
   const double cd = coef_divdamp(ctx, dts);
   if (pair_layout(d) && invNs > 0.0 && fused_recover_edges(d)) {
     if (up) LAUNCH_PE((k_divdamp_p<true, true, false>), (k_divdamp_p<true, true, true>), nw, d, p, cd, phase, dts, fresh, invNs, um, dl, rp, upk);
@@ -1656,12 +1660,12 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double d
     return;
   }
   if (pair_layout(d)) {
-    LAUNCH_PE((k_diag_vertices_p<false>), (k_diag_vertices_p<true>), (d.nVertices + 1) / 2, d, p, u, store_dv, uu_up,
+    LAUNCH_PE((k_diag_vertices_p<false>), (k_diag_vertices_p<true>), d.nVertices, d, p, u, store_dv, uu_up,
               (tl == 1) ? p.u1 : p.u2);
     // (a pair-layout k_diag_cells, two cells per wave, measured 18 % slower than the batched one)
     if (d.maxEdges == 6) LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     else LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
-    const int64_t nw = (d.nEdges + 1) / 2;
+    const int64_t nw = d.nEdges;
     if (d.maxEdges == 6) LAUNCH_PE((k_diag_edges_p<10, false>), (k_diag_edges_p<10, true>), nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
     else LAUNCH_PE((k_diag_edges_p<12, false>), (k_diag_edges_p<12, true>), nw, d, p, u, h, reconstruct_v, ctx->cf.apvm_upwinding, dt, store_grad);
   } else if (d.maxEdges == 6) {
@@ -1684,8 +1688,8 @@ void advance_scalars(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt,
     if (rk_step == 3) wt_new = 1.;
   }
   if (batched(d) && pair_layout(d)) {
-    if (d.maxEdges == 6) LAUNCH_PE((k_scalars_edges_p<10, false>), (k_scalars_edges_p<10, true>), (d.nEdges + 1) / 2, d, p);
-    else LAUNCH_PE((k_scalars_edges_p<12, false>), (k_scalars_edges_p<12, true>), (d.nEdges + 1) / 2, d, p);
+    if (d.maxEdges == 6) LAUNCH_PE((k_scalars_edges_p<10, false>), (k_scalars_edges_p<10, true>), d.nEdges, d, p);
+    else LAUNCH_PE((k_scalars_edges_p<12, false>), (k_scalars_edges_p<12, true>), d.nEdges, d, p);
   } else {
     LAUNCH(k_scalars_edges, d.nEdges, d, p);
   }
@@ -1723,8 +1727,8 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
       else if (m6) LAUNCH(k_mono_bounds_b<6>, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
       else LAUNCH(k_mono_bounds_b<7>, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
       if (batched(d) && pair_layout(d)) {
-        if (d.maxEdges == 6) LAUNCH_PE((k_mono_edges1_p<10, false>), (k_mono_edges1_p<10, true>), (d.nEdges + 1) / 2, d, P[b], is, dt);
-        else LAUNCH_PE((k_mono_edges1_p<12, false>), (k_mono_edges1_p<12, true>), (d.nEdges + 1) / 2, d, P[b], is, dt);
+        if (d.maxEdges == 6) LAUNCH_PE((k_mono_edges1_p<10, false>), (k_mono_edges1_p<10, true>), d.nEdges, d, P[b], is, dt);
+        else LAUNCH_PE((k_mono_edges1_p<12, false>), (k_mono_edges1_p<12, true>), d.nEdges, d, P[b], is, dt);
       } else {
         LAUNCH(k_mono_edges1, d.nEdges, d, P[b], is, dt);
       }
@@ -1740,7 +1744,7 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
         LAUNCH(k_mono_cells2, d.nCells, d, P[b], is, ad);
         continue;
       }
-      if (pair_layout(d)) LAUNCH_PE((k_mono_edges2_p<false>), (k_mono_edges2_p<true>), (d.nEdges + 1) / 2, d, P[b], dt);
+      if (pair_layout(d)) LAUNCH_PE((k_mono_edges2_p<false>), (k_mono_edges2_p<true>), d.nEdges, d, P[b], dt);
       else LAUNCH(k_mono_edges2, d.nEdges, d, P[b], dt);
       if (d.maxEdges == 6) LAUNCH(k_mono_cells2_b<6>, d.nCells, d, P[b], is, ad);
       else LAUNCH(k_mono_cells2_b<7>, d.nCells, d, P[b], is, ad);
@@ -2424,9 +2428,6 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   } else {
     g_kernel_tier = 2;
   }
-#ifdef MPAS_WIDE
-  g_kernel_tier = 0;  // the wide build runs the one-column-per-element kernels only
-#endif
   g_fuse_smlstep = 1;
   if (const char* fs = getenv("MPAS_DYCORE_FUSE_SMLSTEP")) g_fuse_smlstep = std::string(fs) != "0";
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
@@ -3016,12 +3017,6 @@ int mpas_dyc_set_lbc(mpas_dyc_ctx* ctx, int32_t apply, double seconds_to_interva
         return MPAS_DYC_EINVAL;
       }
   }
-#ifdef MPAS_WIDE
-  if (apply) {
-    ctx->err = lbc_layout_error(ctx->blk[0].d);
-    return MPAS_DYC_EINVAL;
-  }
-#endif
   if ((apply != 0) != ctx->lbc) {  // other exchange points and kernels: re-plan, re-capture
     ctx->lbc = apply != 0;
     for (auto& b : ctx->blk) b.d.lbc = apply;

@@ -223,6 +223,28 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 }
 #endif
 
+// the value of lane-1 (own at lane 0) and of lanes 0, 1, 2 (the bottom-boundary extrapolation of
+// the w recovery, 3077-3078): one LDS round trip in the wide build instead of four
+#ifdef MPAS_WIDE
+__device__ __forceinline__ void up1_first3(double x, double& m, double& f0, double& f1, double& f2) {
+  __shared__ double b3[WIDE_THREADS];
+  __syncthreads();
+  b3[threadIdx.x] = x;
+  __syncthreads();
+  m = threadIdx.x ? b3[threadIdx.x - 1] : x;
+  f0 = b3[0];
+  f1 = b3[1];
+  f2 = b3[2];
+}
+#else
+__device__ __forceinline__ void up1_first3(double x, double& m, double& f0, double& f1, double& f2) {
+  m = up1(x);
+  f0 = readlane_d(x, 0);
+  f1 = readlane_d(x, 1);
+  f2 = readlane_d(x, 2);
+}
+#endif
+
 // Fortran sign(1.0_RKIND, x): IEEE copysign semantics
 __device__ __forceinline__ double sgn1(double x) { return copysign(1.0, x); }
 
@@ -1740,23 +1762,36 @@ __device__ __forceinline__ void pst(double* a, d2 v, bool two) {
   if (two) st2(a, v);
   else a[0] = v.x;
 }
+// PAIR_EPW elements per wavefront: 2 in the K <= 63 build (lanes 0..31 and 32..63, levels 2l, 2l+1
+// of lane l of each half), 1 in the wide build (lanes 0..63 of one column: K <= 127 with the same
+// two levels per lane, the same DPP moves and 16-byte accesses, no LDS).  PAIR_WPB wavefronts of
+// consecutive elements per workgroup.
+#ifdef MPAS_WIDE
+#define PAIR_EPW 1
+#define PAIR_WPB 4
+#else
+#define PAIR_EPW 2
+#define PAIR_WPB EDGE_WPB
+#endif
+#define PAIR_THREADS (64 * PAIR_WPB)
 __device__ __forceinline__ int pair_wave() {
-  return __builtin_amdgcn_readfirstlane(xcd_block() * EDGE_WPB + (threadIdx.x >> 6));
+  return __builtin_amdgcn_readfirstlane(xcd_block() * PAIR_WPB + (threadIdx.x >> 6));
 }
-__device__ __forceinline__ int pair_half() { return (threadIdx.x >> 5) & 1; }
+__device__ __forceinline__ int pair_half() { return PAIR_EPW == 2 ? (threadIdx.x >> 5) & 1 : 0; }
+__device__ __forceinline__ int pair_lane() { return PAIR_EPW == 2 ? threadIdx.x & 31 : threadIdx.x & 63; }
 // the two edges of this wavefront: consecutive edges, or in phase 2 of a split kernel consecutive
 // entries of the compact bnd_pairs list (halo-boundary edges with an owned cell); false: none
 __device__ __forceinline__ bool pair_edges(const Dims& d, const Ptrs& p, int phase, int& eA, int& eB, bool& hasB) {
-  const int i = 2 * pair_wave();
+  const int i = PAIR_EPW * pair_wave();
   if (phase == 2) {
     if (i >= d.n_bnd_pairs) return false;
-    hasB = i + 1 < d.n_bnd_pairs;
+    hasB = PAIR_EPW == 2 && i + 1 < d.n_bnd_pairs;
     eA = __builtin_amdgcn_readfirstlane(p.bnd_pairs[i]);
     eB = hasB ? __builtin_amdgcn_readfirstlane(p.bnd_pairs[i + 1]) : eA;
     return true;
   }
   if (i >= d.nEdges) return false;
-  hasB = i + 1 < d.nEdges;
+  hasB = PAIR_EPW == 2 && i + 1 < d.nEdges;
   eA = i;
   eB = hasB ? i + 1 : i;
   return true;
@@ -1810,14 +1845,14 @@ __device__ __forceinline__ void pack_rec_edge(const XPack& pk, const Dims& d, in
 // at rk1 the two are independent (no finalize), and together they need 244 VGPRs (2 waves/SIMD).
 // tp: with finalize, the final tend_u also goes to the 642 exchange's send buffer (XPack), or nothing
 template <bool RK1, int NE2, bool SPLIT = false, bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Config cf, DynTendScal s,
+__global__ __launch_bounds__(PAIR_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Config cf, DynTendScal s,
                                                               int finalize, XPack tp = XPack{}) {
   constexpr bool PGF = RK1 && !SPLIT;
-  const int eA = 2 * pair_wave();
+  const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
-  const bool hasB = eA + 1 < d.nEdges;
+  const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int K = d.K, h = pair_half(), l = pair_lane();
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1), lw = min(l, K / 2);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
@@ -1965,12 +2000,12 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
 // rk1, all edges: the PGF part of tend_u_euler (4781-4788, edges 1..nEdgesSolve) and the del2 of u
 // (4856-4883) -- the half of k_dyn_edges_p<true> that SPLIT leaves out
 template <bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_pgf_p(Dims d, Ptrs p) {
-  const int eA = 2 * pair_wave();
+__global__ __launch_bounds__(PAIR_THREADS) void k_dyn_edges_pgf_p(Dims d, Ptrs p) {
+  const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
-  const bool hasB = eA + 1 < d.nEdges;
+  const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int K = d.K, h = pair_half(), l = pair_lane();
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
@@ -2012,12 +2047,12 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_edges_pgf_p(Dims d, Ptrs p
 
 // k_dyn_advflux_b in the pair layout
 template <int NA, bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) {
-  const int eA = 2 * pair_wave();
+__global__ __launch_bounds__(PAIR_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) {
+  const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
-  const bool hasB = eA + 1 < d.nEdges;
+  const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int K = d.K, h = pair_half(), l = pair_lane();
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1), lw = min(l, K / 2);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const size_t K1 = K + 1;
@@ -2088,14 +2123,14 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
 // comes from the receive buffer for every vertex that reads it, and its write-back vertex (uu_up.wb)
 // stores it into uw (the field u names) for the later readers
 template <bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_diag_vertices_p(Dims d, Ptrs p, const double* __restrict__ u,
+__global__ __launch_bounds__(PAIR_THREADS) void k_diag_vertices_p(Dims d, Ptrs p, const double* __restrict__ u,
                                                                   int store_dv, XUnpack uu_up = XUnpack{},
                                                                   double* uw = nullptr) {
-  const int vA = 2 * pair_wave();
+  const int vA = PAIR_EPW * pair_wave();
   if (vA >= d.nVertices) return;
-  const bool hasB = vA + 1 < d.nVertices;
+  const bool hasB = PAIR_EPW == 2 && vA + 1 < d.nVertices;
   const int vB = hasB ? vA + 1 : vA;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int K = d.K, h = pair_half(), l = pair_lane();
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int v = sel(h, vA, vB);
@@ -2146,14 +2181,14 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_diag_vertices_p(Dims d, Ptrs p
 
 // k_diag_edges_b in the pair layout
 template <int NE2, bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_diag_edges_p(Dims d, Ptrs p, const double* __restrict__ u,
+__global__ __launch_bounds__(PAIR_THREADS) void k_diag_edges_p(Dims d, Ptrs p, const double* __restrict__ u,
                                                                const double* __restrict__ hh, int reconstruct_v,
                                                                double apvm, double dt, int store_grad) {
-  const int eA = 2 * pair_wave();
+  const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
-  const bool hasB = eA + 1 < d.nEdges;
+  const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int K = d.K, h = pair_half(), l = pair_lane();
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
@@ -2256,13 +2291,13 @@ __device__ __forceinline__ d2 ld_pp(const Dims& d, const Ptrs& p, const UnpackMa
 // dl = 1: rtheta_pp_old holds rtheta_pp - rtheta_pp_old (k_acoustic_cells_r<ME, true> with dl)
 // rp: the stage's last damping also packs ru_p of the 876-887 exchange (XPack), or nothing
 template <bool REC = false, bool UP = false, bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
+__global__ __launch_bounds__(PAIR_THREADS) void k_divdamp_p(Dims d, Ptrs p, double coef_divdamp, int phase, double dts,
                                                             int fresh, double invNs = 0.0, UnpackMap um = UnpackMap{},
                                                             int dl = 0, XPack rp = XPack{}, XPack upk = XPack{}) {
   int eA, eB;
   bool hasB;
   if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int K = d.K, h = pair_half(), l = pair_lane();
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
@@ -2334,12 +2369,12 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
 
 // k_scalars_edges in the pair layout (atm_advance_scalars_work, 3357-3426)
 template <int NA, bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p) {
-  const int eA = 2 * pair_wave();
+__global__ __launch_bounds__(PAIR_THREADS) void k_scalars_edges_p(Dims d, Ptrs p) {
+  const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
-  const bool hasB = eA + 1 < d.nEdges;
+  const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31, ns = d.ns;
+  const int K = d.K, h = pair_half(), l = pair_lane(), ns = d.ns;
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
@@ -2402,12 +2437,12 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
 
 // k_mono_edges1 in the pair layout (atm_advance_scalars_mono_work, 3916-3961, 4007-4022)
 template <int NA, bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, int is, double dt) {
-  const int eA = 2 * pair_wave();
+__global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, int is, double dt) {
+  const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
-  const bool hasB = eA + 1 < d.nEdges;
+  const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31, ns = d.ns;
+  const int K = d.K, h = pair_half(), l = pair_lane(), ns = d.ns;
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);
@@ -2481,15 +2516,15 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
 // the first in registers), K/2 iterations instead of K-1, each from exactly the operands of the
 // sequential recurrence -- and a wave now carries two columns, halving the DP work per column.
 template <bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs p, double dts, double epssm) {
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+__global__ __launch_bounds__(PAIR_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs p, double dts, double epssm) {
+  const int K = d.K, h = pair_half(), l = pair_lane();
   const double dtseps = .5 * dts * (1. + epssm);
   const double rcv = RGAS / (CP - RGAS);
   const double c2 = CP * rcv;
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)K) p.cofrz[threadIdx.x] = dtseps * p.rdzw[threadIdx.x];
-  const int cA = 2 * pair_wave();
+  const int cA = PAIR_EPW * pair_wave();
   if (cA >= d.nCellsSolve) return;
-  const bool hasB = cA + 1 < d.nCellsSolve;
+  const bool hasB = PAIR_EPW == 2 && cA + 1 < d.nCellsSolve;
   const int c = sel(h, cA, hasB ? cA + 1 : cA);
   const bool mine = h == 0 || hasB;
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
@@ -2581,13 +2616,13 @@ __global__ __launch_bounds__(EDGE_THREADS) void k_vert_imp_coefs_p(Dims d, Ptrs 
 // k_acoustic_edges in the pair layout (same expressions, per level)
 // UP: the Theta''/rho'' halo comes from the exchange's receive buffer (fused unpack, UnpackMap)
 template <bool DD, bool UP = false, bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,
+__global__ __launch_bounds__(PAIR_THREADS) void k_acoustic_edges_p(Dims d, Ptrs p, double dts, int small_step,
                                                                    double coef_divdamp, int phase, int fresh,
                                                                    UnpackMap um = UnpackMap{}) {
   int eA, eB;
   bool hasB;
   if (!pair_edges(d, p, phase, eA, eB, hasB)) return;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int K = d.K, h = pair_half(), l = pair_lane();
   const bool lev = 2 * l < K;                     // this lane holds levels 2l, 2l+1
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
@@ -2852,7 +2887,11 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
             cofwtm * (tsm + resm * rtppm);
     }
     // tridiagonal solve sweeping up and then down the column (2675-2682), reference order
+#ifdef MPAS_WIDE
+    rwp = column_solve(rwp, a_tri, alpha_tri, gamma_tri, k, K);
+#else
     rwp = thomas_column(rwp, a_tri, alpha_tri, gamma_tri, k, K);
+#endif
     // implicit Rayleigh damping of w (2687-2693)
     const double rzm = up1(rz);
     if (act && k >= 1) {
@@ -3161,8 +3200,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3(Dims d, Ptrs p
     const int e = uni(p.edgesOnCell[c * d.maxEdges + i]);
     const double sg = p.edgesOnCell_sign[c * d.maxEdges + i];
     const double ruk = act ? p.ru[(size_t)e * K + k] : 0.0;
-    const double rum = up1(ruk);
-    const double ru1 = readlane_d(ruk, 0), ru2 = readlane_d(ruk, 1), ru3 = readlane_d(ruk, 2);
+    double rum, ru1, ru2, ru3;
+    up1_first3(ruk, rum, ru1, ru2, ru3);
     const size_t zo = ((size_t)c * d.maxEdges + i) * K1 + k;
     if (k == 0) {
       const double flux = (p.cf1 * ru1 + p.cf2 * ru2 + p.cf3 * ru3);
@@ -3173,8 +3212,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3(Dims d, Ptrs p
     }
   }
   const double rz = act ? p.rho_zz2[o] : 0.0;
-  const double rzm = up1(rz);
-  const double r1 = readlane_d(rz, 0), r2 = readlane_d(rz, 1), r3 = readlane_d(rz, 2);
+  double rzm, r1, r2, r3;
+  up1_first3(rz, rzm, r1, r2, r3);
   if (k == 0) w = w / (p.cf1 * r1 + p.cf2 * r2 + p.cf3 * r3);
   else if (act) w = w / (fzm * rz + fzp * rzm);
   if (act) p.w2[ow] = w;  // w(K+1) stays 0
@@ -3334,8 +3373,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs
 #pragma unroll
   for (int i = 0; i < ME; ++i) {
     const double ruk = ru[i];
-    const double rum = up1(ruk);
-    const double ru1 = readlane_d(ruk, 0), ru2 = readlane_d(ruk, 1), ru3 = readlane_d(ruk, 2);
+    double rum, ru1, ru2, ru3;
+    up1_first3(ruk, rum, ru1, ru2, ru3);
     fl[i] = (k == 0) ? (p.cf1 * ru1 + p.cf2 * ru2 + p.cf3 * ru3) : (fzm * ruk + fzp * rum);
   }
 #pragma unroll
@@ -3352,8 +3391,8 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_recover_cells3_b(Dims d, Ptrs
     hd = hd * ld_uniform_f64(p.invAreaCell + c);
     if (act) p.h_divergence[o] = hd;
   }
-  const double rzm = up1(rz);
-  const double r1 = readlane_d(rz, 0), r2 = readlane_d(rz, 1), r3 = readlane_d(rz, 2);
+  double rzm, r1, r2, r3;
+  up1_first3(rz, rzm, r1, r2, r3);
   if (k == 0) w = w / (p.cf1 * r1 + p.cf2 * r2 + p.cf3 * r3);
   else if (act) w = w / (fzm * rz + fzp * rzm);
   if (act) p.w2[ow] = w;  // w(K+1) stays 0
@@ -4177,12 +4216,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2_b(Dims d, Ptrs p,
 }
 
 template <bool ODD = false>
-__global__ __launch_bounds__(EDGE_THREADS) void k_mono_edges2_p(Dims d, Ptrs p, double dt) {
-  const int eA = 2 * pair_wave();
+__global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges2_p(Dims d, Ptrs p, double dt) {
+  const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
-  const bool hasB = eA + 1 < d.nEdges;
+  const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
   const int eB = hasB ? eA + 1 : eA;
-  const int K = d.K, h = pair_half(), l = threadIdx.x & 31;
+  const int K = d.K, h = pair_half(), l = pair_lane();
   const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
   const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
   const int e = sel(h, eA, eB);

@@ -29,17 +29,18 @@ KEYS = [("state", "u", "state.u.tl1"), ("state", "theta_m", "state.theta_m.tl1")
 NSTEPS = 6
 
 
-@pytest.mark.parametrize("variant", ["dry", "moist_split_transport", "moist_in_dynamics", "moist_L55"])
+@pytest.mark.parametrize("variant", ["dry", "moist_split_transport", "moist_in_dynamics", "moist_L55", "moist_L80"])
 def test_lbc_matches_reference(variant):
     """moist_L55: the reference's default 55 levels (core_init_atmosphere/Registry.xml:100), an odd
-    K, in the pair kernel layout the regional updates need."""
+    K, in the pair kernel layout the regional updates need; moist_L80: above 63 levels, the wide
+    build (pair-layout kernels with one column per wavefront)."""
     from mpas_dycore import Dycore
     from mpas_dycore.cases import jw_case, regional_lbc
     from oracle import ref_runner
     if not ref_runner.available():
         pytest.skip("oracle/_ref not built")
     moist = variant != "dry"
-    case = jw_case(2562, K=55 if variant == "moist_L55" else 26, ns=6 if moist else 1, moist=moist, cache=False)
+    case = jw_case(2562, {"moist_L55": 55, "moist_L80": 80}.get(variant, 26), ns=6 if moist else 1, moist=moist, cache=False)
     if variant == "moist_in_dynamics":
         case["config"] = dict(case["config"], config_split_dynamics_transport=False)
     case, lbc = regional_lbc(case)

@@ -1,14 +1,21 @@
-"""GPU parity above 63 vertical levels: the library's wide build (one workgroup of 128 lanes per
-column, lane = level, cross-level moves through LDS; dycore.hip / kernels.hip with MPAS_WIDE),
-which api_dispatch.cpp selects for nVertLevels 64..127.  nVertLevels is a namelist dimension of
-the reference (core_init_atmosphere/Registry.xml:31,100), which has no limit of its own.
+"""GPU parity above 63 vertical levels: the library's wide build (dycore.hip / kernels.hip with
+MPAS_WIDE), which api_dispatch.cpp selects for nVertLevels 64..127.  Its pair-layout kernels give
+one wavefront to a column, two levels per lane (the K <= 63 build's lane map and DPP moves, one
+element per wavefront instead of two); its per-cell kernels one workgroup of 128 lanes, lane =
+level, cross-level moves through LDS.  nVertLevels is a namelist dimension of the reference
+(core_init_atmosphere/Registry.xml:31,100), which has no limit of its own.
 
   * K = 80 dry and K = 100 moist (num_scalars = 3, monotone transport) on x1.2562, 10 steps with
     the captured hipGraph, against the unmodified reference atm_srk3 (oracle/_ref):
     relative L-infinity <= 1e-10 on u, theta_m, rho_zz; <= 1e-9 on w and the mixing ratios;
   * K = 80 on 4 MPAS blocks, every halo message through RCCL with split-phase exchanges: equal
-    to the one-block run bit for bit.
+    to the one-block run bit for bit;
+  * the three kernel families (general, batched, pair) give the same bits at K = 80 and at the
+    largest, odd K = 127, moist monotone, as they do below 64 levels (test_gpu_kernels.py), and the
+    default family there is the pair layout.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -85,3 +92,42 @@ def test_wide_columns_four_rccl_blocks_bitwise(cases):
         got = decomp.gather_owned(blocks, per, loc, n_glob[loc])
         assert np.array_equal(got, single[key]), f"{key}: 4 RCCL blocks (K=80) differ from one block"
     dy.close()
+
+
+def _steps_with_kernels(case, family, nsteps=2):
+    from mpas_dycore import Dycore
+    saved = os.environ.get("MPAS_DYCORE_KERNELS")
+    os.environ["MPAS_DYCORE_KERNELS"] = family
+    try:
+        dy = Dycore(case, device=0, moist_end=case["num_scalars"])
+    finally:
+        if saved is None:
+            os.environ.pop("MPAS_DYCORE_KERNELS")
+        else:
+            os.environ["MPAS_DYCORE_KERNELS"] = saved
+    lay = dy.layout()
+    dt = float(case["dt"])
+    dy.init_diagnostics(dt)
+    dy.use_graph(True)
+    for i in range(nsteps):
+        dy.atm_timestep(dt, i + 1)
+        dy.shift_time_levels()
+    dy.synchronize()
+    out = {n: dy.get("state", n, 1) for n in ("u", "w", "theta_m", "rho_zz", "scalars")}
+    out.update({n: dy.get("diag", n) for n in ("pv_edge", "rho_edge", "exner", "ru", "rw", "uReconstructZonal")})
+    dy.close()
+    return lay, out
+
+
+@pytest.mark.parametrize("K", [80, 127])
+def test_wide_kernel_families_give_identical_bits(K):
+    from mpas_dycore.cases import jw_case
+    with heartbeat(f"x1.642 K={K} moist, three kernel families"):
+        case = jw_case(642, K=K, ns=2, moist=True, cache=False)
+        lay, ref = _steps_with_kernels(case, "general")
+        assert lay["family"] == "general" and lay["column"] == "wide"
+        for fam in ("batched", "pair"):
+            lay, got = _steps_with_kernels(case, fam)
+            assert lay["family"] == fam and lay["column"] == "wide"
+            for n in ref:
+                assert np.array_equal(got[n], ref[n]), f"K={K} {fam}: {n}"
