@@ -93,15 +93,32 @@ __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlan
 // the column spans several wavefronts: every move is a store to LDS, a barrier and a load.  Every
 // call site is reached by all lanes of the workgroup (the kernels keep these moves out of
 // lane-dependent branches, which the wavefront DPP forms need as well); the first barrier keeps a
-// move from overwriting the previous one's values before every lane has read them.
+// move from overwriting the previous one's values before every lane has read them -- which also
+// lets every helper below use the same LDS rows.
+#define WIDE_LDS_ROWS 8
+__shared__ double wide_lds[WIDE_LDS_ROWS][WIDE_THREADS];
 __device__ __forceinline__ double col_move(double x, int delta, bool zero_end) {
-  __shared__ double col_buf[WIDE_THREADS];
   __syncthreads();
-  col_buf[threadIdx.x] = x;
+  wide_lds[0][threadIdx.x] = x;
   __syncthreads();
   const int s = (int)threadIdx.x + delta;
   if (s < 0 || s >= WIDE_THREADS) return zero_end ? 0.0 : x;
-  return col_buf[s];
+  return wide_lds[0][s];
+}
+// N values moved by delta = -1 (up1: value of level k-1) or +1 (dn1: level k+1) in one LDS round
+// trip; the end lanes keep their own value
+template <int N>
+__device__ __forceinline__ void col_shift(double (&v)[N], int delta) {
+  static_assert(N <= WIDE_LDS_ROWS, "LDS rows");
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) wide_lds[i][threadIdx.x] = v[i];
+  __syncthreads();
+  const int s = (int)threadIdx.x + delta;
+  if (s >= 0 && s < WIDE_THREADS) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = wide_lds[i][s];
+  }
 }
 __device__ __forceinline__ double up1(double x) { return col_move(x, -1, false); }
 __device__ __forceinline__ double dn1(double x) { return col_move(x, 1, false); }
@@ -122,6 +139,13 @@ __device__ __forceinline__ double dn1(double x) {
 #else
 __device__ __forceinline__ double up1(double x) { return __shfl_up(x, 1, 64); }
 __device__ __forceinline__ double dn1(double x) { return __shfl_down(x, 1, 64); }
+#endif
+#ifndef MPAS_WIDE
+template <int N>
+__device__ __forceinline__ void col_shift(double (&v)[N], int delta) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = delta < 0 ? up1(v[i]) : dn1(v[i]);
+}
 #endif
 #ifndef MPAS_WIDE
 __device__ __forceinline__ double up2(double x) { return __shfl_up(x, 2, 64); }
@@ -165,55 +189,83 @@ __device__ __forceinline__ double ld_uniform_f64(const double* a) {
 }
 
 #ifdef MPAS_WIDE
-// The column's sequential recurrences in the wide build: one lane walks the column in LDS, the
-// reference's loop exactly (two barriers in all, instead of two per level through readlane_d).
-// Forward x(k) = (x(k) - a(k) x(k-1)) alpha(k) for k = 1..K-1, then backward x(k) = x(k) - gamma(k)
-// x(k+1) for k = K-1..0 (mpas_atm_time_integration.F:2675-2682); x(K) is read, never written.
+// DPP wavefront shifts (as up1 / dn1 of the one-wavefront build): value of lane-1 / lane+1, own at
+// the end lane
+__device__ __forceinline__ double wave_shr1(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x138, 0xf, 0xf, false),
+                          __builtin_amdgcn_update_dpp(lo, lo, 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double wave_shl1(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(hi, hi, 0x130, 0xf, 0xf, false),
+                          __builtin_amdgcn_update_dpp(lo, lo, 0x130, 0xf, 0xf, false));
+}
+// The column's tridiagonal sweeps (2675-2682) in the wide build: forward x(k) = (x(k) - a(k) x(k-1))
+// alpha(k) for k = 1..K-1, then backward x(k) = x(k) - gamma(k) x(k+1) for k = K-1..0; x(K) is read,
+// never written.  The column goes through LDS to the first wavefront, which holds levels 2l, 2l+1
+// on lane l and runs thomas_column's lane sweep over the lane pairs: every iteration each lane
+// re-evaluates its two updates from its neighbour's current value, so after (K+1)/2 iterations each
+// level holds what the sequential loop computes, from the same operands, bit for bit.
 __device__ __forceinline__ double column_solve(double x, double a, double alpha, double gamma, int k, int K) {
-  __shared__ double sx[WIDE_THREADS], sa[WIDE_THREADS], sal[WIDE_THREADS], sg[WIDE_THREADS];
   __syncthreads();
-  sx[threadIdx.x] = x;
-  sa[threadIdx.x] = a;
-  sal[threadIdx.x] = alpha;
-  sg[threadIdx.x] = gamma;
+  wide_lds[0][threadIdx.x] = x;
+  wide_lds[1][threadIdx.x] = a;
+  wide_lds[2][threadIdx.x] = alpha;
+  wide_lds[3][threadIdx.x] = gamma;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int kk = 1; kk < K; ++kk) sx[kk] = (sx[kk] - sa[kk] * sx[kk - 1]) * sal[kk];
-    for (int kk = K - 1; kk >= 0; --kk) sx[kk] = sx[kk] - sg[kk] * sx[kk + 1];
+  if (threadIdx.x < 64) {
+    const int kx = 2 * threadIdx.x, ky = kx + 1;
+    const double rx = wide_lds[0][kx], ry = wide_lds[0][ky];
+    const double ax = wide_lds[1][kx], ay = wide_lds[1][ky], alx = wide_lds[2][kx], aly = wide_lds[2][ky];
+    const double gx = wide_lds[3][kx], gy = wide_lds[3][ky];
+    const bool fx = kx >= 1 && kx < K, fy = ky < K;
+    double xx = rx, xy = ry;
+    for (int it = 0; it < (K + 1) / 2; ++it) {
+      const double m = wave_shr1(xy);  // level kx - 1
+      if (fx) xx = (rx - ax * m) * alx;
+      if (fy) xy = (ry - ay * xx) * aly;
+    }
+    const double fxx = xx, fxy = xy;
+    for (int it = 0; it < (K + 1) / 2; ++it) {
+      const double q = wave_shl1(xx);  // level ky + 1
+      if (fy) xy = fxy - gy * q;
+      if (kx < K) xx = fxx - gx * xy;
+    }
+    wide_lds[0][kx] = xx;
+    wide_lds[0][ky] = xy;
   }
   __syncthreads();
-  return sx[k];
+  return wide_lds[0][k];
 }
 // the LU factors of the implicit w solve (2124-2127): alpha(k) = 1 / (b(k) - a(k) gamma(k-1)),
 // gamma(k) = c(k) alpha(k) for k = 1..K-1; lane 0 keeps alpha = gamma = 0
 __device__ __forceinline__ void column_lu(double a, double b, double c, int k, int K, double& alpha, double& gamma) {
-  __shared__ double sa[WIDE_THREADS], sb[WIDE_THREADS], sc[WIDE_THREADS], sal[WIDE_THREADS], sg[WIDE_THREADS];
   __syncthreads();
-  sa[threadIdx.x] = a;
-  sb[threadIdx.x] = b;
-  sc[threadIdx.x] = c;
+  wide_lds[0][threadIdx.x] = a;
+  wide_lds[1][threadIdx.x] = b;
+  wide_lds[2][threadIdx.x] = c;
   __syncthreads();
   if (threadIdx.x == 0) {
     double g = 0.0;
-    sal[0] = 0.0;
-    sg[0] = 0.0;
+    wide_lds[3][0] = 0.0;
+    wide_lds[4][0] = 0.0;
     for (int kk = 1; kk < K; ++kk) {
-      const double al = 1. / (sb[kk] - sa[kk] * g);
-      g = sc[kk] * al;
-      sal[kk] = al;
-      sg[kk] = g;
+      const double al = 1. / (wide_lds[1][kk] - wide_lds[0][kk] * g);
+      g = wide_lds[2][kk] * al;
+      wide_lds[3][kk] = al;
+      wide_lds[4][kk] = g;
     }
   }
   __syncthreads();
-  alpha = k < K ? sal[k] : 0.0;
-  gamma = k < K ? sg[k] : 0.0;
+  alpha = k < K ? wide_lds[3][k] : 0.0;
+  gamma = k < K ? wide_lds[4][k] : 0.0;
 }
 __device__ __forceinline__ double readlane_d(double v, int l) {
-  __shared__ double rl_buf[WIDE_THREADS];
   __syncthreads();
-  rl_buf[threadIdx.x] = v;
+  wide_lds[0][threadIdx.x] = v;
   __syncthreads();
-  return rl_buf[l];
+  return wide_lds[0][l];
 }
 #else
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -227,14 +279,13 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // the w recovery, 3077-3078): one LDS round trip in the wide build instead of four
 #ifdef MPAS_WIDE
 __device__ __forceinline__ void up1_first3(double x, double& m, double& f0, double& f1, double& f2) {
-  __shared__ double b3[WIDE_THREADS];
   __syncthreads();
-  b3[threadIdx.x] = x;
+  wide_lds[0][threadIdx.x] = x;
   __syncthreads();
-  m = threadIdx.x ? b3[threadIdx.x - 1] : x;
-  f0 = b3[0];
-  f1 = b3[1];
-  f2 = b3[2];
+  m = threadIdx.x ? wide_lds[0][threadIdx.x - 1] : x;
+  f0 = wide_lds[0][0];
+  f1 = wide_lds[0][1];
+  f2 = wide_lds[0][2];
 }
 #else
 __device__ __forceinline__ void up1_first3(double x, double& m, double& f0, double& f1, double& f2) {
@@ -2870,17 +2921,18 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
         ts = ts - flux * 0.5 * (th[i] + thc);  // (th2 + th1): the sum commutes exactly
       }
     }
-    const double coftz_p = dn1(coftz);
-    const double rwp_p = dn1(rwp);
+    double dn2[2] = {coftz, rwp};  // levels k+1 (one LDS round trip in the wide build)
+    col_shift(dn2, 1);
+    const double coftz_p = dn2[0], rwp_p = dn2[1];
     if (act) {
       rs = rhopp + dts * trho + rs - cofrz * resm * (rwp_p - rwp);
       ts = rtpp + dts * tth + ts - resm * rdzw * (coftz_p * rwp_p - coftz * rwp);
     }
     if (act && k >= 1) wwa = wwa + 0.5 * (1.0 - epssm) * rwp;
     // rw_p right-hand side (2660-2670)
-    const double zzm = up1(zz);
-    const double tsm = up1(ts), rsm = up1(rs), rtppm = up1(rtpp), rhoppm = up1(rhopp);
-    const double cofwtm = up1(cofwt);
+    double up7[7] = {zz, ts, rs, rtpp, rhopp, cofwt, rz};  // levels k-1
+    col_shift(up7, -1);
+    const double zzm = up7[0], tsm = up7[1], rsm = up7[2], rtppm = up7[3], rhoppm = up7[4], cofwtm = up7[5];
     if (act && k >= 1) {
       rwp = rwp + dts * tw - cofwz * ((zz * ts - zzm * tsm) + resm * (zz * rtpp - zzm * rtppm)) -
             cofwr * ((rs + rsm) + resm * (rhopp + rhoppm)) + cofwt * (ts + resm * rtpp) +
@@ -2893,7 +2945,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_acoustic_cells_r(Dims d, Ptrs
     rwp = thomas_column(rwp, a_tri, alpha_tri, gamma_tri, k, K);
 #endif
     // implicit Rayleigh damping of w (2687-2693)
-    const double rzm = up1(rz);
+    const double rzm = up7[6];
     if (act && k >= 1) {
       const double dd = rws - rw;
       rwp = (rwp + dd - dts * dss * (fzm * zz + fzp * zzm) * (fzm * rz + fzp * rzm) * w2) / (1.0 + dts * dss) - dd;
