@@ -1,0 +1,26 @@
+/* The C library's pow / exp / asin / acos / tan over arrays, for the host-side case builder
+ * (mpas_dycore/init_atm.py).  The reference's initialisation calls these functions of the C
+ * library element by element; init_atm reproduces its arithmetic with the same library, and this
+ * loop does in C what np.frompyfunc(math.pow, ...) does one Python call at a time.  Built without
+ * -ffast-math, so every element is one scalar call of the library function (no vector variants). */
+#include <math.h>
+#include <stdint.h>
+
+void hl_pow_s(const double* x, double y, double* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = pow(x[i], y);
+}
+void hl_pow_v(const double* x, const double* y, double* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = pow(x[i], y[i]);
+}
+void hl_exp(const double* x, double* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = exp(x[i]);
+}
+void hl_asin(const double* x, double* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = asin(x[i]);
+}
+void hl_acos(const double* x, double* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = acos(x[i]);
+}
+void hl_tan(const double* x, double* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = tan(x[i]);
+}

@@ -112,6 +112,27 @@ _LIBM_POW = np.frompyfunc(math.pow, 2, 1)
 _LIBM_EXP = np.frompyfunc(math.exp, 1, 1)
 _LIBM_TAN = np.frompyfunc(math.tan, 1, 1)
 
+# The same C library functions looped in C (csrc/host_libm.c -> csrc/libmpas_host.so, built with
+# the dycore): the math.* calls above one element per Python call take minutes at 835586 cells.
+# Same library, same results; without the built helper the math.* loops run.
+_HOST = None
+try:
+    import ctypes as _C
+    _HOST = _C.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc",
+                                 "libmpas_host.so"))
+    for _f in ("hl_exp", "hl_asin", "hl_acos", "hl_tan"):
+        getattr(_HOST, _f).argtypes = [_C.c_void_p, _C.c_void_p, _C.c_int64]
+    _HOST.hl_pow_s.argtypes = [_C.c_void_p, _C.c_double, _C.c_void_p, _C.c_int64]
+except OSError:
+    _HOST = None
+
+
+def _host1(fn, x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    fn(x.ctypes.data, out.ctypes.data, x.size)
+    return out
+
 
 # The JW initial state follows the compiled reference's arithmetic (checked against amdflang's
 # lowering): x**n with an integer n is the product x*x*...*x from the left, x**r with a real r and
@@ -125,10 +146,14 @@ def _ipow(x, n):
 
 
 def _exp(x):
+    if _HOST is not None:
+        return _host1(_HOST.hl_exp, x)
     return np.asarray(_LIBM_EXP(np.asarray(x, dtype=np.float64)), dtype=np.float64)
 
 
 def _tan(x):
+    if _HOST is not None:
+        return _host1(_HOST.hl_tan, x)
     return np.asarray(_LIBM_TAN(np.asarray(x, dtype=np.float64)), dtype=np.float64)
 
 
@@ -140,14 +165,23 @@ def _pow(x, y):
     x = np.asarray(x, dtype=np.float64)
     if y == 0.75:
         return np.sqrt(x) * np.sqrt(np.sqrt(x))
+    if _HOST is not None:
+        x = np.ascontiguousarray(x)
+        out = np.empty_like(x)
+        _HOST.hl_pow_s(x.ctypes.data, float(y), out.ctypes.data, x.size)
+        return out
     return np.asarray(_LIBM_POW(x, float(y)), dtype=np.float64)
 
 
 def _asin(x):
+    if _HOST is not None:
+        return _host1(_HOST.hl_asin, x)
     return np.asarray(_LIBM_ASIN(np.asarray(x, dtype=np.float64)), dtype=np.float64)
 
 
 def _acos(x):
+    if _HOST is not None:
+        return _host1(_HOST.hl_acos, x)
     return np.asarray(_LIBM_ACOS(np.asarray(x, dtype=np.float64)), dtype=np.float64)
 
 def _ref_arc_length(a, b):
@@ -197,6 +231,8 @@ def _ref_arc_bisect(a, b):
 def _ref_migs(a):
     """MIGS / ELGS (642-740): inverse by partial-pivoting Gaussian elimination, batched over the
     leading axis; same pivot choice (first largest scaled element) and update order."""
+    if a.shape[0] > 8192:  # independent systems: batches that stay in cache
+        return np.concatenate([_ref_migs(a[i:i + 8192]) for i in range(0, a.shape[0], 8192)])
     a = a.copy()
     nb, n, _ = a.shape
     rows = np.arange(nb)
@@ -488,13 +524,20 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
     # ---- deriv_two, zb/zb3 (mpas_init_atm_cases.F:1045-1093, theta_adv_order = 3)
     d2 = m["deriv_two"] if "deriv_two" in m else compute_deriv_two(m)  # an init file may carry it
     nEoC, coc, eoc = m["nEdgesOnCell"], m["cellsOnCell"], m["edgesOnCell"]
-    d2c1 = d2[:, 0, 0][:, None] * zgrid[c1]
-    d2c2 = d2[:, 1, 0][:, None] * zgrid[c2]
-    for i in range(m["maxEdges"]):
-        v1 = (i < nEoC[c1])[:, None]
-        v2 = (i < nEoC[c2])[:, None]
-        d2c1 = d2c1 + np.where(v1, d2[:, 0, i + 1][:, None] * zgrid[coc[c1, i]], 0.0)
-        d2c2 = d2c2 + np.where(v2, d2[:, 1, i + 1][:, None] * zgrid[coc[c2, i]], 0.0)
+    d2c1 = np.empty((nE, nz))
+    d2c2 = np.empty((nE, nz))
+    for e0 in range(0, nE, 32768):  # edge batches that stay in cache; per element the same sums
+        s_ = slice(e0, min(nE, e0 + 32768))
+        a1_, a2_ = c1[s_], c2[s_]
+        x1 = d2[s_, 0, 0][:, None] * zgrid[a1_]
+        x2 = d2[s_, 1, 0][:, None] * zgrid[a2_]
+        for i in range(m["maxEdges"]):
+            v1 = (i < nEoC[a1_])[:, None]
+            v2 = (i < nEoC[a2_])[:, None]
+            x1 = x1 + np.where(v1, d2[s_, 0, i + 1][:, None] * zgrid[coc[a1_, i]], 0.0)
+            x2 = x2 + np.where(v2, d2[s_, 1, i + 1][:, None] * zgrid[coc[a2_, i]], 0.0)
+        d2c1[s_] = x1
+        d2c2[s_] = x2
     dcE = m["dcEdge"][:, None]
     z_edge = 0.5 * (zgrid[c1] + zgrid[c2]) - dcE ** 2 * (d2c1 + d2c2) / 12.0
     z_edge3 = -dcE ** 2 * (d2c1 - d2c2) / 12.0
@@ -513,21 +556,23 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
     # the reference adds the edges' contributions in edge order (1103-1118): per cell, its edges in
     # ascending order, as cellsOnEdge(2) +A -B or as cellsOnEdge(1) -C +D
     eoc_sorted = np.sort(np.where(np.arange(m["maxEdges"])[None, :] < nEoC[:, None], eoc, nE), axis=1)
-    for k in range(1, nz1):
-        fl = fzm[k] * ru[:, k] + fzp[k] * ru[:, k - 1]
-        z2 = fzm[k] * zz[c2, k] + fzp[k] * zz[c2, k - 1]
-        z1 = fzm[k] * zz[c1, k] + fzp[k] * zz[c1, k - 1]
-        sg = np.copysign(1.0, ru[:, k])
-        a2, b2 = z2 * zb[:, 1, k] * fl, sg * coef3 * z2 * zb3[:, 1, k] * fl
-        a1, b1 = z1 * zb[:, 0, k] * fl, sg * coef3 * z1 * zb3[:, 0, k] * fl
-        x = np.zeros(nC)
+    for k0 in range(1, nz1, 8):  # 8 levels at a time, each level's expressions as written per k
+        ks = np.arange(k0, min(nz1, k0 + 8))
+        fl = fzm[ks] * ru[:, ks] + fzp[ks] * ru[:, ks - 1]
+        z2 = fzm[ks] * zz[c2[:, None], ks] + fzp[ks] * zz[c2[:, None], ks - 1]
+        z1 = fzm[ks] * zz[c1[:, None], ks] + fzp[ks] * zz[c1[:, None], ks - 1]
+        sg = np.copysign(1.0, ru[:, ks])
+        a2, b2 = z2 * zb[:, 1, ks] * fl, sg * coef3 * z2 * zb3[:, 1, ks] * fl
+        a1, b1 = z1 * zb[:, 0, ks] * fl, sg * coef3 * z1 * zb3[:, 0, ks] * fl
+        x = np.zeros((nC, len(ks)))
         for j in range(m["maxEdges"]):
             e = eoc_sorted[:, j]
             ok = e < nE
             ee = np.where(ok, e, 0)
-            second = c2[ee] == np.arange(nC)
-            x = np.where(ok & second, (x + a2[ee]) - b2[ee], np.where(ok, (x - a1[ee]) + b1[ee], x))
-        rw[:, k] = x
+            second = (c2[ee] == np.arange(nC))[:, None]
+            okc = ok[:, None]
+            x = np.where(okc & second, (x + a2[ee]) - b2[ee], np.where(okc, (x - a1[ee]) + b1[ee], x))
+        rw[:, ks] = x
     w = np.zeros((nC, nz))
     w[:, 1:nz1] = rw[:, 1:nz1] / (fzp[1:] * rho_zz[:, :-1] + fzm[1:] * rho_zz[:, 1:])
 
@@ -745,16 +790,24 @@ def _jw_flux_zonal(lat1_in, lat2_in, dvEdge, R, vg, moist):
     i1 = np.minimum(np.ceil(hi / dlat).astype(np.int64) + 1, NLAT - 2)
     acc = np.zeros((lo.shape[0], nz1))
     dl_last = np.zeros(lo.shape[0])
-    for j in range(int((i1 - i0).max()) + 1):
-        i = np.minimum(i0 + j, NLAT - 2)
-        ok = (i0 + j <= i1) & (lo <= lat_2d[i + 1]) & (hi >= lat_2d[i])
-        dl = lat_2d[i + 1] - lat_2d[i]
-        da = (np.maximum(lo, lat_2d[i]) - lat_2d[i]) / dl
-        db = (np.minimum(hi, lat_2d[i + 1]) - lat_2d[i]) / dl
-        w1 = (db - da) - 0.5 * (db - da) ** 2
-        w2 = 0.5 * (db - da) ** 2
-        acc = np.where(ok[:, None], acc + w1[:, None] * u_2d[:, i].T + w2[:, None] * u_2d[:, i + 1].T, acc)
-        dl_last = np.where(ok, dl, dl_last)
+    u_2dT = np.ascontiguousarray(u_2d.T)  # (nlat, K)
+    for e0 in range(0, lo.shape[0], 32768):  # edge batches that stay in cache
+        s_ = slice(e0, min(lo.shape[0], e0 + 32768))
+        lo_, hi_, i0_, i1_ = lo[s_], hi[s_], i0[s_], i1[s_]
+        ac = np.zeros((lo_.shape[0], nz1))
+        dll = np.zeros(lo_.shape[0])
+        for j in range(int((i1_ - i0_).max()) + 1):
+            i = np.minimum(i0_ + j, NLAT - 2)
+            ok = (i0_ + j <= i1_) & (lo_ <= lat_2d[i + 1]) & (hi_ >= lat_2d[i])
+            dl = lat_2d[i + 1] - lat_2d[i]
+            da = (np.maximum(lo_, lat_2d[i]) - lat_2d[i]) / dl
+            db = (np.minimum(hi_, lat_2d[i + 1]) - lat_2d[i]) / dl
+            w1 = (db - da) - 0.5 * (db - da) ** 2
+            w2 = 0.5 * (db - da) ** 2
+            ac = np.where(ok[:, None], ac + w1[:, None] * u_2dT[i] + w2[:, None] * u_2dT[i + 1], ac)
+            dll = np.where(ok, dl, dll)
+        acc[s_] = ac
+        dl_last[s_] = dll
     sgn = np.copysign(1.0, lat2_in - lat1_in)
     # the reference scales by its loop variable dlat: the width of the last interval it summed
     return sgn[:, None] * acc * dl_last[:, None] * R / dvEdge[:, None] / u0

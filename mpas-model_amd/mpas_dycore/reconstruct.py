@@ -54,8 +54,15 @@ def initialize_vectors(case: dict) -> dict:
     return dict(edgeNormalVectors=n, cellTangentPlane=np.stack([xhat, yhat], axis=1), localVerticalUnitVectors=vert)
 
 
+CHUNK = 8192  # systems per batch: the batch's arrays stay in cache (each system is independent)
+
+
 def _legs_batched(A: np.ndarray, B: np.ndarray) -> np.ndarray:
-    """elgs + mpas_legs for a batch of systems A (m,N,N), B (m,N); returns X (m,N)."""
+    """elgs + mpas_legs for a batch of systems A (m,N,N) and right-hand sides B (m,N,R); returns
+    X (m,N,R).  The elimination (elgs) depends on A only, so it runs once for the R right-hand
+    sides that the reference solves one call each -- same operations on each, same bits."""
+    if A.shape[0] > CHUNK:
+        return np.concatenate([_legs_batched(A[i:i + CHUNK], B[i:i + CHUNK]) for i in range(0, A.shape[0], CHUNK)])
     A = A.copy()
     B = B.copy()
     m, N, _ = A.shape
@@ -88,14 +95,14 @@ def _legs_batched(A: np.ndarray, B: np.ndarray) -> np.ndarray:
                 A[rows, ii, kk] = A[rows, ii, kk] - pj * A[rows, jj, kk]
     for i in range(N - 1):
         for j in range(i + 1, N):
-            B[rows, indx[:, j]] = B[rows, indx[:, j]] - A[rows, indx[:, j], i] * B[rows, indx[:, i]]
-    X = np.zeros((m, N))
-    X[:, N - 1] = B[rows, indx[:, N - 1]] / A[rows, indx[:, N - 1], N - 1]
+            B[rows, indx[:, j]] = B[rows, indx[:, j]] - A[rows, indx[:, j], i][:, None] * B[rows, indx[:, i]]
+    X = np.zeros((m, N, B.shape[2]))
+    X[:, N - 1] = B[rows, indx[:, N - 1]] / A[rows, indx[:, N - 1], N - 1][:, None]
     for i in range(N - 2, -1, -1):
         xi = B[rows, indx[:, i]]
         for j in range(i + 1, N):
-            xi = xi - A[rows, indx[:, i], j] * X[:, j]
-        X[:, i] = xi / A[rows, indx[:, i], i]
+            xi = xi - A[rows, indx[:, i], j][:, None] * X[:, j]
+        X[:, i] = xi / A[rows, indx[:, i], i][:, None]
     return X
 
 
@@ -155,8 +162,8 @@ def init_reconstruct(case: dict, vectors: dict | None = None) -> np.ndarray:
             M[:, pc:pc + 2, i] = pu[:, i, :]
         rhs[:, pc, 0] = 1.0
         rhs[:, pc + 1, 1] = 1.0
-        c1 = _legs_batched(M, rhs[:, :, 0])
-        c2 = _legs_batched(M, rhs[:, :, 1])
+        cc = _legs_batched(M, rhs)
+        c1, c2 = cc[:, :, 0], cc[:, :, 1]
         for i in range(3):  # coefficients(:,i) = b1(i) c1 + b2(i) c2 (:1131-1134)
             out[cells, :pc, i] = b1[:, i][:, None] * c1[:, :pc] + b2[:, i][:, None] * c2[:, :pc]
     return out

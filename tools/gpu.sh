@@ -33,7 +33,7 @@ last() { tail -1 "$1" | cut -c1-${2:-400}; }
 step() {
   case "$1" in
     tests) timeout -k 10 1000 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m "gpu and not slow" ${TESTS:-tests} > gpurun_out/tests.log 2>&1; r=$?; tail -2 gpurun_out/tests.log; return $r ;;
-    tests_full) timeout -k 10 1100 python -u -m pytest -x -v --timeout 900 --timeout-method thread -m gpu ${TESTS:-tests} > gpurun_out/tests_full.log 2>&1; r=$?; tail -2 gpurun_out/tests_full.log; return $r ;;
+    tests_full) timeout -k 10 1100 python -u -m pytest -x -v --durations=30 --timeout 900 --timeout-method thread -m gpu ${TESTS:-tests} > gpurun_out/tests_full.log 2>&1; r=$?; tail -2 gpurun_out/tests_full.log; return $r ;;
     bench) timeout -k 10 400 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1 && last gpurun_out/bench.log 700 ;;
     bench_fast) timeout -k 10 300 python bench.py --steps 10 --warmup 2 $B ${BENCH_ARGS} > gpurun_out/bench_fast.log 2>&1 && last gpurun_out/bench_fast.log ;;
     bench55) timeout -k 10 300 python bench.py --steps 10 --warmup 2 $B --levels 55 > gpurun_out/bench55.log 2>&1 && last gpurun_out/bench55.log ;;
