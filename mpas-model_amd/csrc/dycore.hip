@@ -356,6 +356,12 @@ void build_registry(Block& c) {
   c.fields.back().nsub = ns;
   add(c, "scratch", "scale_arr", L_CELL, 2 * (int64_t)K);
   add(c, "scratch", "wdtn", L_CELL, K + 1);
+  if (ns >= 2) {  // the second scalar of a pair in the monotone transport (advance_scalars_mono)
+    for (const char* n : {"s_max_1", "s_min_1", "scalar_old_copy_1"}) add(c, "scratch", n, L_CELL, K);
+    for (const char* n : {"flux_arr_1", "flux_upwind_tmp_1", "flux_tmp_1"}) add(c, "scratch", n, L_EDGE, K);
+    add(c, "scratch", "scale_arr_1", L_CELL, 2 * (int64_t)K);
+    add(c, "scratch", "wdtn_1", L_CELL, K + 1);
+  }
   add(c, "scratch", "edge_bnd", L_EDGE, 1, 1, true);
   add(c, "scratch", "cell_bnd", L_CELL, 1, 1, true);
   add(c, "scratch", "bnd_edges", L_EDGE, 1, 1, true);
@@ -1709,6 +1715,29 @@ void mono_prep(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt, bool ad
   }
 }
 
+// The block's pointers with the monotone transport's per-scalar scratch (s_max, s_min, wdtn,
+// flux_arr, flux_upwind_tmp, flux_tmp, scalar_old_copy, scale_arr) switched to its second set, which
+// the second scalar of a pair uses
+Ptrs mono_slot1(mpas_dyc_ctx* c, Block& b, Ptrs p) {
+  p.s_max = P<double>(c, b, "scratch", "s_max_1");
+  p.s_min = P<double>(c, b, "scratch", "s_min_1");
+  p.scalar_old_copy = P<double>(c, b, "scratch", "scalar_old_copy_1");
+  p.flux_arr = P<double>(c, b, "scratch", "flux_arr_1");
+  p.flux_upwind_tmp = P<double>(c, b, "scratch", "flux_upwind_tmp_1");
+  p.flux_tmp = P<double>(c, b, "scratch", "flux_tmp_1");
+  p.scale_arr = P<double>(c, b, "scratch", "scale_arr_1");
+  p.wdtn = P<double>(c, b, "scratch", "wdtn_1");
+  return p;
+}
+
+// MPAS_DYCORE_MONO_PAIRS=0 (read when a context is created): one scalar at a time
+int g_mono_pairs = 1;
+
+// The reference's per-scalar loop (3798-4210): bounds, fluxes, limiter factors, the scale_arr
+// exchange (4098), rescale and update, one scalar after the other.  Each scalar's pipeline reads and
+// writes only its own scalar and its own scratch, so two scalars run it side by side here with two
+// sets of scratch and one scale_arr exchange for both (half the exchanges, and half the RCCL groups
+// between GPUs) -- the same operations on the same operands, bit for bit.
 // prepared = true: mono_prep ran and its exchange was merged into the caller's
 int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt, bool advance_density,
                          bool prepared = false) {
@@ -1719,35 +1748,52 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
     CHK(exchange(ctx, {{"state", "scalars", 1, ALL_LAYERS}}));
   }
   const int ns = ctx->blk[0].d.ns;
-  for (int is = 0; is < ns; ++is) {
+  std::vector<Ptrs> P1;
+  if (ns >= 2 && g_mono_pairs)
+    for (int b = 0; b < nb; ++b) P1.push_back(mono_slot1(ctx, ctx->blk[b], P[b]));
+  for (int is = 0; is < ns; is += (P1.empty() ? 1 : 2)) {
+    const int nq = (!P1.empty() && is + 1 < ns) ? 2 : 1;  // scalars in this pass
     for (int b = 0; b < nb; ++b) {
       const Dims& d = ctx->blk[b].d;
       const bool bt = batched(d), m6 = d.maxEdges == 6;
-      if (!bt) LAUNCH(k_mono_bounds, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
-      else if (m6) LAUNCH(k_mono_bounds_b<6>, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
-      else LAUNCH(k_mono_bounds_b<7>, d.nCellsSolve, d, P[b], is, ctx->cf.coef_3rd_order);
-      if (batched(d) && pair_layout(d)) {
-        if (d.maxEdges == 6) LAUNCH_PE((k_mono_edges1_p<10, false>), (k_mono_edges1_p<10, true>), d.nEdges, d, P[b], is, dt);
-        else LAUNCH_PE((k_mono_edges1_p<12, false>), (k_mono_edges1_p<12, true>), d.nEdges, d, P[b], is, dt);
-      } else {
-        LAUNCH(k_mono_edges1, d.nEdges, d, P[b], is, dt);
+      for (int q = 0; q < nq; ++q) {
+        const Ptrs& pq = q ? P1[b] : P[b];
+        if (!bt) LAUNCH(k_mono_bounds, d.nCellsSolve, d, pq, is + q, ctx->cf.coef_3rd_order);
+        else if (m6) LAUNCH(k_mono_bounds_b<6>, d.nCellsSolve, d, pq, is + q, ctx->cf.coef_3rd_order);
+        else LAUNCH(k_mono_bounds_b<7>, d.nCellsSolve, d, pq, is + q, ctx->cf.coef_3rd_order);
       }
-      if (!bt) LAUNCH(k_mono_cells1, d.nCellsSolve, d, P[b], is, dt, ad);
-      else if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, P[b], is, dt, ad);
-      else LAUNCH(k_mono_cells1_b<7>, d.nCellsSolve, d, P[b], is, dt, ad);
+      for (int q = 0; q < nq; ++q) {
+        const Ptrs& pq = q ? P1[b] : P[b];
+        if (batched(d) && pair_layout(d)) {
+          if (m6) LAUNCH_PE((k_mono_edges1_p<10, false>), (k_mono_edges1_p<10, true>), d.nEdges, d, pq, is + q, dt);
+          else LAUNCH_PE((k_mono_edges1_p<12, false>), (k_mono_edges1_p<12, true>), d.nEdges, d, pq, is + q, dt);
+        } else {
+          LAUNCH(k_mono_edges1, d.nEdges, d, pq, is + q, dt);
+        }
+      }
+      for (int q = 0; q < nq; ++q) {
+        const Ptrs& pq = q ? P1[b] : P[b];
+        if (!bt) LAUNCH(k_mono_cells1, d.nCellsSolve, d, pq, is + q, dt, ad);
+        else if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, pq, is + q, dt, ad);
+        else LAUNCH(k_mono_cells1_b<7>, d.nCellsSolve, d, pq, is + q, dt, ad);
+      }
     }
-    CHK(exchange(ctx, {{"scratch", "scale_arr", 1, 0x1u}}));
+    if (nq == 2) CHK(exchange(ctx, {{"scratch", "scale_arr", 1, 0x1u}, {"scratch", "scale_arr_1", 1, 0x1u}}));
+    else CHK(exchange(ctx, {{"scratch", "scale_arr", 1, 0x1u}}));
     for (int b = 0; b < nb; ++b) {
       const Dims& d = ctx->blk[b].d;
-      if (!batched(d)) {
-        LAUNCH(k_mono_edges2, d.nEdges, d, P[b], dt);
-        LAUNCH(k_mono_cells2, d.nCells, d, P[b], is, ad);
-        continue;
+      for (int q = 0; q < nq; ++q) {
+        const Ptrs& pq = q ? P1[b] : P[b];
+        if (!batched(d)) {
+          LAUNCH(k_mono_edges2, d.nEdges, d, pq, dt);
+          LAUNCH(k_mono_cells2, d.nCells, d, pq, is + q, ad);
+          continue;
+        }
+        if (pair_layout(d)) LAUNCH_PE((k_mono_edges2_p<false>), (k_mono_edges2_p<true>), d.nEdges, d, pq, dt);
+        else LAUNCH(k_mono_edges2, d.nEdges, d, pq, dt);
+        if (d.maxEdges == 6) LAUNCH(k_mono_cells2_b<6>, d.nCells, d, pq, is + q, ad);
+        else LAUNCH(k_mono_cells2_b<7>, d.nCells, d, pq, is + q, ad);
       }
-      if (pair_layout(d)) LAUNCH_PE((k_mono_edges2_p<false>), (k_mono_edges2_p<true>), d.nEdges, d, P[b], dt);
-      else LAUNCH(k_mono_edges2, d.nEdges, d, P[b], dt);
-      if (d.maxEdges == 6) LAUNCH(k_mono_cells2_b<6>, d.nCells, d, P[b], is, ad);
-      else LAUNCH(k_mono_cells2_b<7>, d.nCells, d, P[b], is, ad);
     }
   }
   return MPAS_DYC_OK;
@@ -2430,6 +2476,8 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   }
   g_fuse_smlstep = 1;
   if (const char* fs = getenv("MPAS_DYCORE_FUSE_SMLSTEP")) g_fuse_smlstep = std::string(fs) != "0";
+  g_mono_pairs = 1;
+  if (const char* mp = getenv("MPAS_DYCORE_MONO_PAIRS")) g_mono_pairs = std::string(mp) != "0";
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
   for (auto& b : ctx->blk) {
     build_registry(b);

@@ -2486,6 +2486,9 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
   }
 }
 
+// (a two-scalar variant -- both scalars' gathers from one pass over the stencil indices and
+// coefficients -- needs 197 VGPRs, runs 2 waves per SIMD instead of 4 and took exactly the time
+// of two launches: the in-flight gathers per SIMD, not the index loads, bound this kernel)
 // k_mono_edges1 in the pair layout (atm_advance_scalars_mono_work, 3916-3961, 4007-4022)
 template <int NA, bool ODD = false>
 __global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, int is, double dt) {

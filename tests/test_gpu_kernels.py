@@ -136,3 +136,55 @@ def test_odd_level_count_pair_layout_matches_general():
     got = _steps_with_kernels(case, "pair", nsteps=2)
     for n in ref:
         assert np.array_equal(got[n], ref[n]), n
+
+
+def _steps_env(case, env, nsteps=3, dt=None, blocks=0):
+    """nsteps moist monotone steps with the environment variables env set while the context is
+    created (the library reads its switches then); blocks > 0: that many MPAS blocks on the device,
+    exchanging through RCCL."""
+    from mpas_dycore import Dycore, decomp
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        if blocks:
+            bl = decomp.decompose(case, decomp.partition_sfc(case["nCells"], blocks))
+            dy = Dycore.from_blocks(bl, device=0, comm_id=Dycore.comm_unique_id(), nranks=1, rank=0,
+                                    rccl_local=True, moist_end=case["num_scalars"])
+        else:
+            dy = Dycore(case, device=0, moist_end=case["num_scalars"])
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+    dt = dt or 2880.0
+    dy.init_diagnostics(dt)
+    dy.use_graph(True)
+    for i in range(nsteps):
+        dy.atm_timestep(dt, i + 1)
+        dy.shift_time_levels()
+    dy.synchronize()
+    if blocks:
+        n_glob = {"cell": case["nCells"], "edge": case["nEdges"]}
+        out = {n: decomp.gather_owned(bl, [dy.get("state", n, 1, block=i) for i in range(len(bl))],
+                                      "edge" if n == "u" else "cell", n_glob["edge" if n == "u" else "cell"])
+               for n in ("u", "w", "theta_m", "rho_zz", "scalars")}
+    else:
+        out = {n: dy.get("state", n, 1) for n in ("u", "w", "theta_m", "rho_zz", "scalars")}
+    dy.close()
+    return out
+
+
+@pytest.mark.parametrize("ns,blocks", [(3, 0), (6, 0), (5, 4)])
+def test_mono_scalar_pairs_bitwise(ns, blocks):
+    """The monotone transport's per-scalar pipeline (3798-4210) runs two scalars side by side with
+    two sets of scratch and one scale_arr exchange per pair (dycore.hip, advance_scalars_mono):
+    equal bit for bit to one scalar at a time (MPAS_DYCORE_MONO_PAIRS=0), odd and even scalar
+    counts, and on 4 RCCL blocks."""
+    from mpas_dycore.cases import jw_case
+    case = jw_case(642, K=26, ns=ns, moist=True, cache=False)
+    ref = _steps_env(case, {"MPAS_DYCORE_MONO_PAIRS": "0"}, blocks=blocks)
+    got = _steps_env(case, {"MPAS_DYCORE_MONO_PAIRS": "1"}, blocks=blocks)
+    for n in ref:
+        assert np.array_equal(got[n], ref[n]), n
