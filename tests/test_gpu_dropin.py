@@ -81,6 +81,22 @@ def test_dropin_harness_matches_reference(small_case, moist_case, moist):
         assert np.array_equal(a, py[k].reshape(a.shape)), f"{k}: drop-in differs from the Python host"
 
 
+def test_dropin_wide_columns_match_reference():
+    """80 levels (the library's wide build, picked by nVertLevels behind the same Fortran API),
+    moist ns = 3 with the monotone transport: the drop-in under the reference's driver against the
+    reference, and bit for bit against the Python host."""
+    from mpas_dycore.cases import jw_case
+    case = jw_case(642, K=80, ns=3, moist=True, cache=False)
+    ref, got = _runs(case, moist_end=3)
+    errs = {k: rel_linf(got[NSTEPS][k], ref[NSTEPS][k]) for k in PROG + RECON}
+    bad = {k: v for k, v in errs.items() if not v <= (1e-11 if k in LOOSE else 1e-12)}
+    assert not bad, f"drop-in (K = 80) vs reference: {bad} (all {errs})"
+    py = _python_host(case, moist_end=3)
+    for k in PROG + RECON:
+        a = got[NSTEPS][k]
+        assert np.array_equal(a, py[k].reshape(a.shape)), f"{k}: drop-in differs from the Python host"
+
+
 def test_dropin_sync_every_step_same_bits(small_case):
     """MPAS_DYCORE_SYNC_EVERY_STEP=1 (copy-back after every step) == on-demand atm_dycore_to_host."""
     from oracle import ref_runner
