@@ -93,10 +93,11 @@ def _jw_hx(phi, r_earth):
     u0 = 35.0
     etavs = (1.0 - 0.252) * PII / 2.0
     ce15 = _pow(np.cos(etavs), 1.5)
+    sp, cp = _sincos(phi)  # one sincos(phi) for the statement (606-611)
     return (u0 / GRAVITY * ce15
-            * ((-2.0 * _ipow(np.sin(phi), 6) * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0)
+            * ((-2.0 * _ipow(sp, 6) * (cp ** 2 + 1.0 / 3.0) + 10.0 / 63.0)
                * u0 * ce15
-               + (1.6 * _ipow(np.cos(phi), 3) * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * r_earth * OMEGA))
+               + (1.6 * _ipow(cp, 3) * (sp ** 2 + 2.0 / 3.0) - PII / 4.0) * r_earth * OMEGA))
 
 
 # ---- the reference's spherical geometry (core_init_atmosphere/mpas_atm_advection.F:397-537),
@@ -123,8 +124,22 @@ try:
     for _f in ("hl_exp", "hl_asin", "hl_acos", "hl_tan"):
         getattr(_HOST, _f).argtypes = [_C.c_void_p, _C.c_void_p, _C.c_int64]
     _HOST.hl_pow_s.argtypes = [_C.c_void_p, _C.c_double, _C.c_void_p, _C.c_int64]
+    _HOST.hl_sincos.argtypes = [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_int64]
 except OSError:
     _HOST = None
+
+
+def _sincos(x):
+    """(sin x, cos x) as the compiled reference gets them where it evaluates both of one argument in
+    one place: amdflang -O2 merges the pair into one call of the C library's sincos(), which differs
+    from separate sin / cos in the last bit for ~0.06 % of arguments (measured with the same
+    compiler here).  Without the built helper, numpy's sin / cos (the separate functions' values)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    if _HOST is None:
+        return np.sin(x), np.cos(x)
+    sn, cs = np.empty_like(x), np.empty_like(x)
+    _HOST.hl_sincos(x.ctypes.data, sn.ctypes.data, cs.ctypes.data, x.size)
+    return sn, cs
 
 
 def _host1(fn, x):
@@ -318,7 +333,8 @@ def compute_deriv_two(m):
         thetat[:, 0] = theta_abs                      # x direction along the longitude line (176)
         for i in range(1, ne):
             thetat[:, i] = thetat[:, i - 1] + thetav[:, i - 1]
-        xp, yp = np.cos(thetat) * dl, np.sin(thetat) * dl
+        st_, ct_ = _sincos(thetat)  # 180-181: cos and sin of thetat(i) in one loop body
+        xp, yp = ct_ * dl, st_ * dl
         a = np.zeros((len(cells), n, 6))
         a[:, 0, 0] = 1.0
         a[:, 1:, 0] = 1.0
@@ -334,7 +350,7 @@ def compute_deriv_two(m):
             e = eoc[cells, i]
             mid = _ref_arc_bisect(xv[voe[e, 0]], xv[voe[e, 1]])
             the = _ref_sphere_angle(c, nb[:, i], mid) + thetat[:, i]
-            cos2t, sin2t = np.cos(the), np.sin(the)
+            sin2t, cos2t = _sincos(the)  # 334-335 / 347-348
             costsint = cos2t * sin2t
             cos2t, sin2t = cos2t * cos2t, sin2t * sin2t
             val = 2. * cos2t[:, None] * b[:, 3, :] + 2. * costsint[:, None] * b[:, 4, :] \
@@ -363,7 +379,8 @@ def compute_defc(m):
         th[:, 0] = 0.0                                # 872: x direction towards the first vertex
         for i in range(1, ne):
             th[:, i] = th[:, i - 1] + thetav[:, i - 1]
-        xp, yp = np.cos(th) * dl, np.sin(th) * dl
+        sth, cth = _sincos(th)  # 877-880: one sincos per thetat(i)
+        xp, yp = cth * dl, sth * dl
         ip1 = (np.arange(ne) + 1) % ne
         thetat = np.empty((len(cells), ne))
         thetat[:, 0] = theta_abs                      # 894
@@ -379,7 +396,7 @@ def compute_defc(m):
         for i in range(ne):
             j = ip1[i]
             dls = np.sqrt((xp[:, j] - xp[:, i]) ** 2 + (yp[:, j] - yp[:, i]) ** 2)
-            st, ct = np.sin(thetat[:, i]), np.cos(thetat[:, i])
+            st, ct = _sincos(thetat[:, i])  # 923-925
             sint2, cost2, sint_cost = st * st, ct * ct, st * ct
             a = dls * (cost2 - sint2) / area
             b = dls * 2. * sint_cost / area
@@ -697,15 +714,16 @@ def _jw_columns(lat, zgrid, zz, vg, R, moist):
     qv = np.zeros_like(ppb)
     phi = lat[None, :]
     dzw, dzu, fzp, fzm = vg["dzw"], vg["dzu"], vg["fzp"], vg["fzm"]
-    geo = ((-2.0 * _ipow(np.sin(phi), 6) * (np.cos(phi) ** 2 + 1.0 / 3.0) + 10.0 / 63.0),
-           (1.6 * _ipow(np.cos(phi), 3) * (np.sin(phi) ** 2 + 2.0 / 3.0) - PII / 4.0) * R * OMEGA)
+    sp, cp = _sincos(phi)  # one sincos(phi) per column (875-881)
+    geo = ((-2.0 * _ipow(sp, 6) * (cp ** 2 + 1.0 / 3.0) + 10.0 / 63.0),
+           (1.6 * _ipow(cp, 3) * (sp ** 2 + 2.0 / 3.0) - PII / 4.0) * R * OMEGA)
     for _ in range(10):
         eta = (ppb + pp) / P0
         etav = (eta - 0.252) * PII / 2.0
         dlt = znut - eta
         teta = t0 * _pow(eta, RGAS * dtdz / GRAVITY) + np.where(eta >= znut, 0.0, delta_t * (dlt * dlt * dlt * dlt * dlt))
-        ce = np.cos(etav)
-        temperature = teta + 0.75 * eta * PII * u0 / RGAS * np.sin(etav) * np.sqrt(ce) * (
+        se, ce = _sincos(etav)  # sin(etav(k)) and cos(etav(k)) of one statement: one sincos
+        temperature = teta + 0.75 * eta * PII * u0 / RGAS * se * np.sqrt(ce) * (
             geo[0] * 2.0 * u0 * _pow(ce, 1.5) + geo[1]) / (1.0 + 0.61 * qv)
         if moist:
             ptemp = ppb + pp

@@ -5,8 +5,8 @@ atm_compute_damping_coefs and the inverses of atm_mpas_init_block, mpas_atm_core
 Checked against the reference's own outputs on our meshes (tests/golden/init_*.npz, the unmodified
 mpas_atm_core.F run by the harness) and against init_atm.model_init (the host restatement):
   * signs, kiteForCell, advCellsForEdge, nAdvCellsForEdge: bit for bit;
-  * adv_coefs / adv_coefs_3rd: bit for bit when the device is handed the reference's deriv_two (the
-    compression is pure arithmetic on it);
+  * adv_coefs / adv_coefs_3rd: bit for bit (the compression is pure arithmetic on deriv_two, which
+    init_atm computes to the reference's bits, tests/test_init_pinned.py);
   * zb_cell / zb3_cell (copies of zb / zb3 times config_coef_3rd_order), inverses: bit for bit vs host;
   * meshScalingDel2 / Del4, dss: bit for bit, except where the reference's C library does not round
     x**0.25 or sin correctly -- there the device value is the correctly rounded one (checked against a
@@ -107,8 +107,9 @@ def test_model_init_matches_reference(fixture):
     ref = {k: z[k] for k in z.files if k != "checksum"}
     nC, nE, ME = case["nCells"], case["nEdges"], case["maxEdges"]
     K = case["nVertLevels"]
-    # the reference's deriv_two: the compression is then pure arithmetic on identical operands
-    c = dict(case, deriv_two=ref["deriv_two"])
+    # init_atm's deriv_two is the reference's, bit for bit (test_init_pinned.py)
+    assert np.array_equal(np.asarray(case["deriv_two"]).reshape(ref["deriv_two"].shape), ref["deriv_two"])
+    c = case
     names = ("edgesOnCell_sign", "edgesOnVertex_sign", "kiteForCell", "advCellsForEdge", "nAdvCellsForEdge",
              "adv_coefs", "adv_coefs_3rd", "meshScalingDel2", "meshScalingDel4", "meshScalingRegionalEdge",
              "meshScalingRegionalCell", "dss", "zb_cell", "zb3_cell", "invAreaCell", "invDvEdge", "invDcEdge",

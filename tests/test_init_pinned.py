@@ -7,15 +7,18 @@ mode 'init', tools/make_golden.py init): the unmodified core_init_atmosphere/mpa
 adv_coefs compression, 3rd-order coupling, mesh scaling, dss).  Both the oracle and the product
 consume init_atm's arrays, so without this pin a wrong restatement would pass every parity test.
 
-Bars: index arrays and sign codes bit for bit; zb_cell / zb3_cell (copies), mesh scaling and dss
-bit for bit; the least-squares / trigonometric weights (deriv_two, defc_a/b, adv_coefs,
-adv_coefs_3rd) to 1e-14 relative to each array's largest entry -- they reach the reference's bits
-except for last-place differences of sin/cos (numpy vs the Fortran runtime) that the ill-conditioned
-fits carry to ~1e-15.
+Bars: every array bit for bit -- index arrays, sign codes, zb_cell / zb3_cell, mesh scaling, dss and
+the least-squares / trigonometric weights (deriv_two, defc_a/b, adv_coefs, adv_coefs_3rd).  The
+weights reach the reference's bits because init_atm calls the C library's sincos() wherever the
+compiled reference evaluates sin and cos of one argument in one place (amdflang -O2 merges the pair
+into one sincos call, which differs from separate sin / cos in the last bit for ~0.06 % of
+arguments, and the ill-conditioned fits of deriv_two carried that to ~1e-13 before).
 
-The JW initial state (tests/golden/jw_x1.642_K26.npz and a live run on x1.2562 x 55): the
-reference's init_atm_case_jw (core_init_atmosphere/mpas_init_atm_cases.F:367-1312, with env_qv and
-sphere_distance, harness mode 'jw') on the same grid given on the unit sphere.  Bars in _jw_compare.
+The JW initial state (tests/golden/jw_x1.642_K26.npz and live runs on x1.2562 x 55 and x1.10242 x 26):
+the reference's init_atm_case_jw (core_init_atmosphere/mpas_init_atm_cases.F:367-1312, with env_qv and
+sphere_distance, harness mode 'jw') on the same grid given on the unit sphere: bit for bit, the
+rebalanced wind, w, zb / zb3 and deriv_two included (the same sincos pairs: sin / cos of the latitude
+and of eta_v in the temperature and terrain expressions).
 The reference's JW is dry (its parameter moisture = .false., :454): init_atm's moist profile
 (build_case(moist=True), the compiled-out branch restated) has no reference run to pin it.
 """
@@ -25,10 +28,9 @@ import numpy as np
 import pytest
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-EXACT = ("edgesOnCell_sign", "edgesOnVertex_sign", "advCellsForEdge", "nAdvCellsForEdge", "kiteForCell",
-         "meshScalingDel2", "meshScalingDel4", "dss", "zb_cell", "zb3_cell")
 WEIGHTS = ("deriv_two", "defc_a", "defc_b", "adv_coefs", "adv_coefs_3rd")
-TOL = 1e-14
+EXACT = ("edgesOnCell_sign", "edgesOnVertex_sign", "advCellsForEdge", "nAdvCellsForEdge", "kiteForCell",
+         "meshScalingDel2", "meshScalingDel4", "dss", "zb_cell", "zb3_cell") + WEIGHTS
 
 
 def _cases():
@@ -55,11 +57,6 @@ def _compare(case, ref):
         if k in EXACT:
             assert np.array_equal(a, b), f"{k}: {int((a != b).sum())} entries differ from the reference"
             errs[k] = 0.0
-        else:
-            den = np.max(np.abs(b))
-            errs[k] = float(np.max(np.abs(a - b)) / den) if den else float(np.max(np.abs(a - b)))
-    bad = {k: v for k, v in errs.items() if k in WEIGHTS and not v <= TOL}
-    assert not bad, f"above {TOL}: {bad}"
     assert set(WEIGHTS) <= set(errs)
     return errs
 
@@ -84,38 +81,18 @@ def test_init_matches_live_reference_x1_2562():
 
 
 # ---- the JW initial state: core_init_atmosphere/mpas_init_atm_cases.F:367-1312 (init_atm_case_jw) ----
-def _jw_compare(case, ref, ref_d2_case):
-    """init_atm's JW state vs the reference's.  Bit for bit: the vertical grid and metrics and the
-    base state; theta and rho to the last bit except at <= 0.02 % of the points (1 ulp).  u (the rebalanced wind) to 5e-14.  zb / zb3 bit for bit and w to 1e-13
-    given the reference's deriv_two (ref_d2_case), since deriv_two's least-squares fits differ from
-    the reference's in the last bit for ~0.2 % of the weights (test_init_matches_reference_fixture)
-    and zb3 = dcEdge**2 * (d2 sum 1 - d2 sum 2) / 12 cancels."""
-    from conftest import rel_linf
+def _jw_compare(case, ref):
+    """init_atm's JW state vs the reference's, bit for bit: the vertical grid and metrics, the base
+    state, theta and rho, the rebalanced wind u, w, zb / zb3 and deriv_two."""
     own = {"mesh.zgrid": "zgrid", "mesh.zz": "zz", "mesh.zxu": "zxu", "mesh.rdzw": "rdzw", "mesh.rdzu": "rdzu",
            "mesh.fzm": "fzm", "mesh.fzp": "fzp", "mesh.cf1": "cf1", "mesh.cf2": "cf2", "mesh.cf3": "cf3",
-           "diag.theta": "theta", "diag.rho": "rho", "diag.rho_base": "rho_base", "diag.theta_base": "theta_base"}
+           "diag.theta": "theta", "diag.rho": "rho", "diag.rho_base": "rho_base", "diag.theta_base": "theta_base",
+           "state.u.tl1": "u", "state.w.tl1": "w", "mesh.zb": "zb", "mesh.zb3": "zb3", "mesh.deriv_two": "deriv_two"}
     for key, name in own.items():
         r = np.asarray(ref[key]).ravel()
         a = np.asarray(case[name], dtype=np.float64).ravel()[:r.size]
-        if name in ("theta", "rho"):
-            # the column iteration (mpas_init_atm_cases.F:862-950) reproduces the reference bit for
-            # bit except at a few (latitude, level) points (theta 9, rho 19 of 140910 on x1.2562 x 55, 1 ulp)
-            # whose cause is not located: every transcendental is the C library's there
-            nd = int((a != r).sum())
-            assert nd <= max(1, r.size // 5000), f"JW {name}: {nd} of {r.size} values differ"
-            assert rel_linf(a, r) <= 1e-15, f"JW {name}: rel Linf {rel_linf(a, r):.3e}"
-            continue
+        assert a.size == r.size, f"JW {name}: {a.size} values vs the reference's {r.size}"
         assert np.array_equal(a, r), f"JW {name}: {int((a != r).sum())} of {r.size} values differ from the reference"
-    u = rel_linf(np.asarray(case["u"]).reshape(ref["state.u.tl1"].shape), ref["state.u.tl1"])
-    assert u <= 5e-14, f"JW u (rebalanced wind): rel Linf {u:.3e}"
-    for name in ("zb", "zb3"):
-        a = np.asarray(ref_d2_case[name]).reshape(ref["mesh." + name].shape)
-        assert np.array_equal(a, ref["mesh." + name]), f"JW {name} (reference deriv_two) differs"
-    w = rel_linf(np.asarray(ref_d2_case["w"]).reshape(ref["state.w.tl1"].shape), ref["state.w.tl1"])
-    assert w <= 1e-13, f"JW w: rel Linf {w:.3e}"
-    d2 = rel_linf(np.asarray(case["deriv_two"]).reshape(ref["mesh.deriv_two"].shape), ref["mesh.deriv_two"])
-    assert d2 <= 1e-14
-    return u, w
 
 
 def test_jw_state_matches_reference_fixture():
@@ -126,16 +103,15 @@ def test_jw_state_matches_reference_fixture():
     assert str(z["checksum"]) == mg.case_checksum(
         {**{k: v for k, v in m.items() if isinstance(v, np.ndarray)}, **unit}), "mesh generator changed: regenerate"
     ref = {k: z[k] for k in z.files if k != "checksum"}
-    case = build_case({**m, **scaled}, K=26, ns=1)
-    _jw_compare(case, ref, build_case({**m, **scaled, "deriv_two": ref["mesh.deriv_two"]}, K=26, ns=1))
+    _jw_compare(build_case({**m, **scaled}, K=26, ns=1), ref)
 
 
-def test_jw_state_matches_live_reference_x1_2562():
+@pytest.mark.parametrize("level,K", [(4, 55), (5, 26)])
+def test_jw_state_matches_live_reference(level, K):
     from oracle import ref_runner
     if not ref_runner.available():
         pytest.skip("oracle/_ref not built")
     from mpas_dycore.init_atm import build_case
-    m, unit, scaled = _cases().jw_inputs(level=4, K=55)
-    case = build_case({**m, **scaled}, K=55, ns=1)
-    ref = ref_runner.run_reference_jw(case, unit)
-    _jw_compare(case, ref, build_case({**m, **scaled, "deriv_two": ref["mesh.deriv_two"]}, K=55, ns=1))
+    m, unit, scaled = _cases().jw_inputs(level=level, K=K)
+    case = build_case({**m, **scaled}, K=K, ns=1)
+    _jw_compare(case, ref_runner.run_reference_jw(case, unit))
