@@ -535,8 +535,10 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
         u = u0 * flux[:, None] * _pow(np.cos(etavs), 1.5) + u_pert[:, None]
     ru = 0.5 * (rho_zz[c1] + rho_zz[c2]) * u
 
-    fEdge = 2.0 * OMEGA * np.sin(m["latEdge"])
-    fVertex = 2.0 * OMEGA * np.sin(m["latVertex"])
+    # 1024-1036: 2 omega (-cos(lon) cos(lat) sin(alpha) + sin(lat) cos(alpha)) with alpha_grid = 0 is
+    # 2 omega sin(lat), the sine from the statement's one sincos(lat)
+    fEdge = 2.0 * OMEGA * _sincos(m["latEdge"])[0]
+    fVertex = 2.0 * OMEGA * _sincos(m["latVertex"])[0]
 
     # ---- deriv_two, zb/zb3 (mpas_init_atm_cases.F:1045-1093, theta_adv_order = 3)
     d2 = m["deriv_two"] if "deriv_two" in m else compute_deriv_two(m)  # an init file may carry it

@@ -102,7 +102,7 @@ def srk3_fixture():
 
 JW_EXACT = ("mesh.zgrid", "mesh.zz", "mesh.zxu", "mesh.rdzw", "mesh.rdzu", "mesh.fzm", "mesh.fzp", "mesh.cf1",
             "mesh.cf2", "mesh.cf3", "diag.theta", "diag.rho", "diag.rho_base", "diag.theta_base")
-JW_CLOSE = ("state.u.tl1", "state.w.tl1", "mesh.zb", "mesh.zb3", "mesh.deriv_two")
+JW_CLOSE = ("state.u.tl1", "state.w.tl1", "mesh.zb", "mesh.zb3", "mesh.deriv_two", "mesh.fEdge", "mesh.fVertex")
 
 
 def jw_inputs(level: int = 3, K: int = 26):
