@@ -46,9 +46,9 @@ def _reference_nearest(case):
     return near
 
 
-def _case(moist):
+def _case(moist, K=26):
     from mpas_dycore.cases import jw_case, regional_lbc
-    case = jw_case(2562, K=26, ns=6 if moist else 1, moist=moist, cache=False)
+    case = jw_case(2562, K=K, ns=6 if moist else 1, moist=moist, cache=False)
     case, lbc = regional_lbc(case, interior_deg=150.0)
     assert (np.asarray(case["bdyMaskCell"]) == 7).sum() > 0
     case["nearestRelaxationCell"] = _reference_nearest(case)
@@ -66,13 +66,14 @@ def _run(dy, case, lbc, set_lbc_pool):
     dy.synchronize()
 
 
-@pytest.mark.parametrize("moist,rccl", [(False, False), (True, False), (True, True)])
-def test_regional_blocks_bitwise_equal_single_block(moist, rccl):
+@pytest.mark.parametrize("moist,rccl,K", [(False, False, 26), (True, False, 26), (True, True, 26), (True, True, 80)])
+def test_regional_blocks_bitwise_equal_single_block(moist, rccl, K):
     """rccl: the blocks exchange through RCCL (send to self) with split-phase exchanges and graph
-    replay, as ranks of a multi-GPU run do."""
+    replay, as ranks of a multi-GPU run do.  K = 80: the wide build (one column per wavefront in the
+    pair-layout kernels)."""
     from mpas_dycore import Dycore, decomp
     from oracle import ref_runner
-    case, lbc = _case(moist)
+    case, lbc = _case(moist, K)
     me = 6 if moist else 1
     images = ref_runner.lbc_images(case, lbc)  # element-major, garbage row last
 

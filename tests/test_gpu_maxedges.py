@@ -65,6 +65,18 @@ def test_declared_max_edges_10_bitwise(moist_case, fill):
     assert a["graph"] and b["graph"]
 
 
+def test_declared_max_edges_10_wide_columns():
+    """80 levels (the wide build) on a mesh declaring maxEdges 10: the same bits and the same pair
+    layout as the maxEdges 6 declaration."""
+    from mpas_dycore.cases import jw_case
+    from mpas_dycore.mesh import pad_max_edges
+    c = jw_case(642, K=80, ns=3, moist=True, cache=False)
+    a = _run(c)
+    b = _run(pad_max_edges(c, 10, 20, "none"))
+    _same(a, b, "K = 80, maxEdges 10 / maxEdges2 20")
+    assert a["layout"] == b["layout"] == {"maxEdges": 6, "maxEdges2": 10, "family": "pair", "column": "wide"}
+
+
 def test_declared_max_edges_heptagons(varres_case_small):
     """The var-res SCVT holds pentagons to heptagons: its blocks run maxEdges 7 (the <7> / NE2 12
     instantiations), declared 10 or not."""
