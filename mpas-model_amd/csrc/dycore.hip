@@ -1694,7 +1694,10 @@ void advance_scalars(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt,
     if (rk_step == 3) wt_new = 1.;
   }
   if (batched(d) && pair_layout(d)) {
-    if (d.maxEdges == 6) LAUNCH_PE((k_scalars_edges_p<10, false>), (k_scalars_edges_p<10, true>), d.nEdges, d, p);
+    if (d.maxEdges == 6 && d.ns == 1)
+      LAUNCH_PE((k_scalars_edges_p<10, false, true>), (k_scalars_edges_p<10, true, true>), d.nEdges, d, p);
+    else if (d.maxEdges == 6) LAUNCH_PE((k_scalars_edges_p<10, false>), (k_scalars_edges_p<10, true>), d.nEdges, d, p);
+    else if (d.ns == 1) LAUNCH_PE((k_scalars_edges_p<12, false, true>), (k_scalars_edges_p<12, true, true>), d.nEdges, d, p);
     else LAUNCH_PE((k_scalars_edges_p<12, false>), (k_scalars_edges_p<12, true>), d.nEdges, d, p);
   } else {
     LAUNCH(k_scalars_edges, d.nEdges, d, p);

@@ -1807,6 +1807,36 @@ __device__ __forceinline__ d2 ld2(const double* __restrict__ a) {
   return r;
 }
 __device__ __forceinline__ void st2(double* a, d2 v) { __builtin_memcpy(a, &v, 16); }
+
+// The first N entries of one edge's row of the 15-wide stencil tables (advCellsForEdge, adv_coefs,
+// adv_coefs_3rd), each half-wave its own edge's row, as 16-byte vector loads: both halves' rows
+// come in the same few instructions and one wait.  Through the scalar cache the two edges' rows
+// need ~100 SGPRs, so they arrive in dependent batches, a memory round trip each, before the
+// first gather can issue.
+template <int N>
+__device__ __forceinline__ void ld_row(const double* __restrict__ src, double (&dst)[N]) {
+#pragma unroll
+  for (int j = 0; j + 1 < N; j += 2) {
+    const d2 v = ld2(src + j);
+    dst[j] = v.x;
+    dst[j + 1] = v.y;
+  }
+  if (N & 1) dst[N - 1] = src[N - 1];
+}
+template <int N>
+__device__ __forceinline__ void ld_row(const int* __restrict__ src, int (&dst)[N]) {
+#pragma unroll
+  for (int j = 0; j + 3 < N; j += 4) {
+    int4 v;
+    __builtin_memcpy(&v, src + j, 16);
+    dst[j] = v.x;
+    dst[j + 1] = v.y;
+    dst[j + 2] = v.z;
+    dst[j + 3] = v.w;
+  }
+#pragma unroll
+  for (int j = N & ~3; j < N; ++j) dst[j] = src[j];
+}
 // store of a lane's two levels; two = false (odd K, last pair): its second level is level K, past
 // the column, so only the first is stored
 __device__ __forceinline__ void pst(double* a, d2 v, bool two) {
@@ -1955,6 +1985,7 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   const int neoe = sel(h, p.nEdgesOnEdge[eA], p.nEdgesOnEdge[eB]);
   int eoe[NE2];
   double wgt[NE2];
+  // (through the scalar cache: as vector loads, ld_row, 413 -> 426 us per call)
 #pragma unroll
   for (int j = 0; j < NE2; ++j) {
     eoe[j] = sel(h, p.edgesOnEdge[(size_t)eA * d.maxEdges2 + j], p.edgesOnEdge[(size_t)eB * d.maxEdges2 + j]);
@@ -2114,6 +2145,8 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
   const int naA = p.nAdvCellsForEdge[eA], naB = p.nAdvCellsForEdge[eB];
   int ic[NA];
   double a[NA], b[NA];
+  // (the rows through the scalar cache: as vector loads, ld_row, this kernel measured 368 -> 407 us
+  // per call -- its 20 gathers per wave already fill the vector memory pipe)
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
     ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
@@ -2253,6 +2286,7 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_diag_edges_p(Dims d, Ptrs p, c
   double wgt[NE2];
   if (reconstruct_v) {
     neoe = sel(h, p.nEdgesOnEdge[eA], p.nEdgesOnEdge[eB]);
+    // (through the scalar cache: as vector loads, ld_row, 285 -> 288-294 us per call)
 #pragma unroll
     for (int j = 0; j < NE2; ++j) {
       eoe[j] = sel(h, p.edgesOnEdge[(size_t)eA * d.maxEdges2 + j], p.edgesOnEdge[(size_t)eB * d.maxEdges2 + j]);
@@ -2419,7 +2453,9 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_divdamp_p(Dims d, Ptrs p, doub
 }
 
 // k_scalars_edges in the pair layout (atm_advance_scalars_work, 3357-3426)
-template <int NA, bool ODD = false>
+// VROW: the stencil rows as vector loads (ld_row) -- one scalar: 338 -> 278 us per call; with the
+// six moist species in the scalar loop the scalar-cache rows are faster (854 vs 944 us)
+template <int NA, bool ODD = false, bool VROW = false>
 __global__ __launch_bounds__(PAIR_THREADS) void k_scalars_edges_p(Dims d, Ptrs p) {
   const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
@@ -2433,12 +2469,18 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
   const int na = sel(h, p.nAdvCellsForEdge[eA], p.nAdvCellsForEdge[eB]);
   int ic[NA];
   double a[NA], b[NA];
+  if (VROW) {
+    ld_row(p.advCellsForEdge + (size_t)e * 15, ic);
+    ld_row(p.adv_coefs + (size_t)e * 15, a);
+    ld_row(p.adv_coefs_3rd + (size_t)e * 15, b);
+  } else {
 #pragma unroll
-  for (int j = 0; j < NA; ++j) {
-    ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
-    a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j));
-    b[j] = sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
-               ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
+    for (int j = 0; j < NA; ++j) {
+      ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
+      a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j));
+      b[j] = sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
+                 ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
+    }
   }
   const d2 uh = ld2(p.ruAvg + o);
   const double sgx = sgn1(uh.x), sgy = sgn1(uh.y);
@@ -2506,13 +2548,10 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
   const int na = sel(h, p.nAdvCellsForEdge[eA], p.nAdvCellsForEdge[eB]);
   int ic[NA];
   double a[NA], b[NA];
-#pragma unroll
-  for (int j = 0; j < NA; ++j) {
-    ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
-    a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j));
-    b[j] = sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
-               ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
-  }
+  // the stencil rows as vector loads: 394-404 -> 364-368 us per call
+  ld_row(p.advCellsForEdge + (size_t)e * 15, ic);
+  ld_row(p.adv_coefs + (size_t)e * 15, a);
+  ld_row(p.adv_coefs_3rd + (size_t)e * 15, b);
   const double dv = sel(h, ld_uniform_f64(p.dvEdge + eA), ld_uniform_f64(p.dvEdge + eB));
   const d2 uh = ld2(p.ruAvg + o);
   const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);

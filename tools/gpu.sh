@@ -56,7 +56,7 @@ step() {
         for r in ${AB_ROUNDS:-1 2 3}; do for L in ${AB_LIBS:-exp/lib_base.so mpas-model_amd/csrc/libmpas_dycore.so}; do
           echo "== $L" >> gpurun_out/ab.log
           MPAS_DYCORE_LIB=$L timeout -k 10 250 python tools/kbench.py --steps ${AB_STEPS:-10} ${AB_ARGS} >> gpurun_out/ab.log 2>&1 || return 1
-        done; done; grep -h "==\|ms_dt" gpurun_out/ab.log | cut -c1-200 ;;
+        done; done; grep -h "==\|ms_dt" gpurun_out/ab.log | cut -c1-130 ;;
     kprof) i=0; for L in ${AB_LIBS:-exp/lib_base.so mpas-model_amd/csrc/libmpas_dycore.so}; do
           MPAS_DYCORE_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof_$i -o run --output-format csv -- python3 tools/kbench.py --steps ${AB_STEPS:-10} ${AB_ARGS} > gpurun_out/kprof_$i.log 2>&1 || return 1
           echo "kprof_$i = $L"; i=$((i+1)); done ;;

@@ -41,10 +41,16 @@ def main():
         dy.shift_time_levels()
     dy.synchronize()
     ms_dt = (time.perf_counter() - t0) / a.steps * 1e3
+    # the prognostic state after the timed steps: equal digests = the two libraries' steps agree bit for bit
+    import hashlib
+    hsh = hashlib.sha256()
+    for name in ("u", "w", "theta_m", "rho_zz", "scalars"):
+        hsh.update(dy.get("state", name).tobytes())
+    digest = hsh.hexdigest()[:16]
     dts = dt / case["config"]["config_dynamics_split_steps"] / case["config"]["config_number_of_sub_steps"]
     ms, ks = dy.time_acoustic_step(dts, 2, a.reps)
     b = dy.acoustic_bytes()
-    print(json.dumps(dict(lib=os.environ.get("MPAS_DYCORE_LIB", "in-tree"), ms_dt=ms_dt, ms_sub=sum(ks),
+    print(json.dumps(dict(lib=os.environ.get("MPAS_DYCORE_LIB", "in-tree"), state=digest, ms_dt=ms_dt, ms_sub=sum(ks),
                           edges=ks[0], cells=ks[1], divdamp=ks[2], frac=b / (sum(ks) / 1e3) / 8e12)))
 
 
