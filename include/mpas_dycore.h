@@ -172,6 +172,20 @@ int mpas_dyc_set_lbc(mpas_dyc_ctx* ctx, int32_t apply, double seconds_to_interva
  * Bitwise the reference's arithmetic; x**0.25 and sin are correctly rounded (the reference's C library
  * is 1 ulp away for ~0.1 % of arguments).  Synchronous. */
 int mpas_dyc_model_init(mpas_dyc_ctx* ctx, int32_t h_scale_with_mesh, double config_zd, double config_xnutr);
+/* deriv_two as core_init_atmosphere computes it (mpas_atm_advection.F:21-394,
+ * atm_initialize_advection_rk, polynomial_order = 2, on a sphere), into mesh.deriv_two (15, 2, nEdges+1)
+ * of one block (allocated if not yet set), on the device.  The transcendental half comes from the
+ * caller, per cell and edgesOnCell slot (nCells x maxEdges at the declared stride, slots beyond
+ * nEdgesOnCell ignored): xp / yp, the tangent-plane coordinates of cellsOnCell(i) (132-181: cos / sin
+ * of thetat(i) times the arc length), and sin_the / cos_the of edgesOnCell(i)'s normal angle thetae
+ * (303-315, 334-335 / 347-348).  The least-squares fit -- amatrix, poly_fit_2 with MIGS / ELGS
+ * (215-226, 567-741) -- and the weights 2 cos^2 b(4,j) + 2 cos sin b(5,j) + 2 sin^2 b(6,j) (327-358)
+ * run here, one thread per cell, in the Fortran's operand order: bit for bit the reference's deriv_two
+ * when the inputs are its values (they are the C library's sin / cos / asin, which no device library
+ * reproduces; init_atm.deriv_two_inputs computes them that way).  Uses the block's nEdgesOnCell,
+ * edgesOnCell and cellsOnEdge.  Cells with more than 14 edges: MPAS_DYC_EINVAL.  Synchronous. */
+int mpas_dyc_init_deriv_two(mpas_dyc_ctx* ctx, int32_t block, const double* xp, const double* yp,
+                            const double* sin_the, const double* cos_the);
 /* atm_compute_output_diagnostics(state, time_level, diag, mesh) (mpas_atm_core.F:753, called
  * before history writes at :544 and :694): diag theta, rho and pressure from theta_m, rho_zz,
  * scalars(index_qv) of the time level, zz, pressure_base and pressure_p.  Asynchronous. */

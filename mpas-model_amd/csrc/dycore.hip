@@ -3171,6 +3171,65 @@ int mpas_dyc_model_init(mpas_dyc_ctx* ctx, int32_t h_scale_with_mesh, double con
   return MPAS_DYC_OK;
 }
 
+int mpas_dyc_init_deriv_two(mpas_dyc_ctx* ctx, int32_t block, const double* xp, const double* yp,
+                            const double* sin_the, const double* cos_the) {
+  if (!ctx || !xp || !yp || !sin_the || !cos_the) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
+  if (block < 0 || block >= (int)ctx->blk.size()) {
+    ctx->err = "mpas_dyc_init_deriv_two: no block " + std::to_string(block);
+    return MPAS_DYC_EINVAL;
+  }
+  Block& b = ctx->blk[block];
+  HIPCHK(hipSetDevice(ctx->device));
+  Field* f = find(b, "mesh", "deriv_two");
+  const int64_t nb = field_bytes(b, *f);
+  if (!f->buf[0]) HIPCHK(hipMalloc(&f->buf[0], nb + 256));
+  const size_t n = (size_t)b.d.nCells * b.me_decl;
+  double* in = nullptr;
+  int* bad = nullptr;
+  HIPCHK(hipMalloc(&in, 4 * n * sizeof(double) + 256));
+  auto run = [&]() -> hipError_t {
+    hipError_t e = hipMalloc(&bad, sizeof(int));
+    const double* src[4] = {xp, yp, sin_the, cos_the};
+    for (int i = 0; i < 4 && e == hipSuccess; ++i)
+      e = hipMemcpyAsync(in + i * n, src[i], n * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(f->buf[0], 0, nb, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(bad, 0, sizeof(int), ctx->stream);
+    if (e != hipSuccess) return e;
+    D2Fit q{};
+    q.nEdgesOnCell = (const int*)find(b, "mesh", "nEdgesOnCell")->buf[0];
+    q.edgesOnCell = (const int*)find(b, "mesh", "edgesOnCell")->buf[0];
+    q.cellsOnEdge = (const int*)find(b, "mesh", "cellsOnEdge")->buf[0];
+    q.xp = in;
+    q.yp = in + n;
+    q.sin_the = in + 2 * n;
+    q.cos_the = in + 3 * n;
+    q.deriv_two = (double*)f->buf[0];
+    q.bad = bad;
+    q.nCells = b.d.nCells;
+    q.nEdges = b.d.nEdges;
+    q.maxEdges = b.me_decl;
+    hipLaunchKernelGGL(k_mi_deriv_two, dim3((unsigned)((b.d.nCells + 127) / 128)), dim3(128), 0, ctx->stream, q);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e;
+  };
+  const hipError_t e = run();
+  int hbad = 0;
+  if (e == hipSuccess && bad) (void)hipMemcpy(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost);
+  (void)hipFree(in);
+  if (bad) (void)hipFree(bad);
+  if (e != hipSuccess) {
+    ctx->err = std::string("mpas_dyc_init_deriv_two: ") + hipGetErrorString(e);
+    return MPAS_DYC_EHIP;
+  }
+  if (hbad) {
+    ctx->err = "mpas_dyc_init_deriv_two: a cell has more than 14 edges (deriv_two holds 15 weights per side)";
+    return MPAS_DYC_EINVAL;
+  }
+  return MPAS_DYC_OK;
+}
+
 int mpas_dyc_output_diagnostics(mpas_dyc_ctx* ctx, int32_t time_level) {
   if (!ctx || (time_level != 1 && time_level != 2)) return MPAS_DYC_EINVAL;
   if (ctx->host_only) return MPAS_DYC_ESTATE;

@@ -272,4 +272,120 @@ __global__ void k_mi_damping(MInit m, double zd, double xnutr) {
   m.dss[(size_t)c * m.K + k] = v;
 }
 
+// ---- deriv_two (core_init_atmosphere/mpas_atm_advection.F:21-394, atm_initialize_advection_rk,
+// polynomial_order = 2, on a sphere): the arithmetic half, one thread per cell.  The caller hands in
+// the transcendental half per cell and edgesOnCell slot (stride maxEdges): xp / yp of the neighbour
+// cellsOnCell(i) in the cell's tangent plane (132-181) and sin / cos of the edge's normal angle thetae
+// (303-315, 334-335 / 347-348).  Here: amatrix (215-226), poly_fit_2 (567-614) with h = wt w the
+// identity, MIGS / ELGS (633-741) and the weights 2 cos^2 b(4,j) + 2 cos sin b(5,j) + 2 sin^2 b(6,j)
+// (336-357) for each edge, on the side the cell takes in cellsOnEdge.  Matrix products sum their inner
+// index from the first term up, starting from 0.0, as the compiled matmul does (init_atm._matmul_seq).
+struct D2Fit {
+  const int *nEdgesOnCell, *edgesOnCell, *cellsOnEdge;  // device, 0-based
+  const double *xp, *yp, *sin_the, *cos_the;              // (nCells, maxEdges)
+  double* deriv_two;                                      // (nEdges + 1, 2, 15)
+  int* bad;                                               // set when a cell has more than 14 edges
+  int nCells, nEdges, maxEdges;
+};
+constexpr int D2_MAXM = 15;  // the cell and up to 14 neighbours (deriv_two holds 15 weights per side)
+
+__global__ void k_mi_deriv_two(D2Fit q) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= q.nCells) return;
+  const int ne = q.nEdgesOnCell[c];
+  if (ne < 1 || ne > q.maxEdges || ne + 1 > D2_MAXM) {
+    if (ne + 1 > D2_MAXM) *q.bad = 1;
+    return;
+  }
+  const int m = ne + 1;  // ma
+  double a[D2_MAXM][6];
+  a[0][0] = 1.;
+  for (int j = 1; j < 6; ++j) a[0][j] = 0.;
+  for (int i = 1; i < m; ++i) {
+    const double x = q.xp[(size_t)c * q.maxEdges + i - 1], y = q.yp[(size_t)c * q.maxEdges + i - 1];
+    a[i][0] = 1.;
+    a[i][1] = x;
+    a[i][2] = y;
+    a[i][3] = x * x;
+    a[i][4] = x * y;
+    a[i][5] = y * y;
+  }
+  // ath = matmul(transpose(a), h), h the m x m identity
+  double ath[6][D2_MAXM];
+  for (int r = 0; r < 6; ++r)
+    for (int col = 0; col < m; ++col) {
+      double s = 0.0;
+      for (int k = 0; k < m; ++k) s = s + a[k][r] * (k == col ? 1.0 : 0.0);
+      ath[r][col] = s;
+    }
+  // atha = matmul(ath, a)
+  double A[6][6];
+  for (int r = 0; r < 6; ++r)
+    for (int col = 0; col < 6; ++col) {
+      double s = 0.0;
+      for (int k = 0; k < m; ++k) s = s + ath[r][k] * a[k][col];
+      A[r][col] = s;
+    }
+  // ELGS (678-741): partial-pivoting elimination, pivot order in indx
+  int indx[6];
+  double cs[6];
+  for (int i = 0; i < 6; ++i) {
+    indx[i] = i;
+    double c1 = 0.0;
+    for (int j = 0; j < 6; ++j) c1 = fmax(c1, fabs(A[i][j]));
+    cs[i] = c1;
+  }
+  for (int j = 0; j < 5; ++j) {
+    double pi1 = 0.0;
+    int k = j;
+    for (int i = j; i < 6; ++i) {
+      const double pi = fabs(A[indx[i]][j]) / cs[indx[i]];
+      if (pi > pi1) {
+        pi1 = pi;
+        k = i;
+      }
+    }
+    const int t = indx[j];
+    indx[j] = indx[k];
+    indx[k] = t;
+    for (int i = j + 1; i < 6; ++i) {
+      const double pj = A[indx[i]][j] / A[indx[j]][j];
+      A[indx[i]][j] = pj;
+      for (int kk = j + 1; kk < 6; ++kk) A[indx[i]][kk] = A[indx[i]][kk] - pj * A[indx[j]][kk];
+    }
+  }
+  // MIGS (633-675)
+  double B[6][6], X[6][6];
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) B[i][j] = i == j ? 1.0 : 0.0;
+  for (int i = 0; i < 5; ++i)
+    for (int j = i + 1; j < 6; ++j)
+      for (int k = 0; k < 6; ++k) B[indx[j]][k] = B[indx[j]][k] - A[indx[j]][i] * B[indx[i]][k];
+  for (int i = 0; i < 6; ++i) {
+    X[5][i] = B[indx[5]][i] / A[indx[5]][5];
+    for (int j = 4; j >= 0; --j) {
+      double v = B[indx[j]][i];
+      for (int k = j + 1; k < 6; ++k) v = v - A[indx[j]][k] * X[k][i];
+      X[j][i] = v / A[indx[j]][j];
+    }
+  }
+  // b = matmul(atha_inv, ath): only rows 4..6 (the second-derivative terms) are used
+  double b[3][D2_MAXM];
+  for (int r = 3; r < 6; ++r)
+    for (int col = 0; col < m; ++col) {
+      double s = 0.0;
+      for (int k = 0; k < 6; ++k) s = s + X[r][k] * ath[k][col];
+      b[r - 3][col] = s;
+    }
+  for (int i = 0; i < ne; ++i) {
+    const int e = q.edgesOnCell[(size_t)c * q.maxEdges + i];
+    if (e < 0 || e >= q.nEdges) continue;
+    const double cs_ = q.cos_the[(size_t)c * q.maxEdges + i], sn_ = q.sin_the[(size_t)c * q.maxEdges + i];
+    const double costsint = cs_ * sn_, cos2t = cs_ * cs_, sin2t = sn_ * sn_;
+    const int side = q.cellsOnEdge[2 * e] == c ? 0 : 1;
+    double* out = q.deriv_two + ((size_t)e * 2 + side) * 15;
+    for (int j = 0; j < m; ++j) out[j] = 2. * cos2t * b[0][j] + 2. * costsint * b[1][j] + 2. * sin2t * b[2][j];
+  }
+}
+
 }  // namespace mpas

@@ -198,6 +198,17 @@ class Dycore:
             raise DycoreError("mpas_dyc_comm_unique_id failed")
         return buf.raw
 
+    def init_deriv_two(self, inputs, block: int = 0):
+        """mpas_dyc_init_deriv_two: deriv_two's least-squares fits on the device into mesh.deriv_two,
+        from the transcendental inputs init_atm.deriv_two_inputs(mesh) returns (xp, yp, sin_the,
+        cos_the, each (nCells, maxEdges))."""
+        nC, me = self.cases[block]["nCells"], self.cases[block]["maxEdges"]
+        arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in inputs]
+        if len(arrs) != 4 or any(a.shape != (nC, me) for a in arrs):
+            raise ValueError(f"deriv_two inputs: four ({nC}, {me}) arrays")
+        self._check(self.lib.mpas_dyc_init_deriv_two(self.h, block, *[a.ctypes.data_as(C.c_void_p) for a in arrs]),
+                    "init_deriv_two")
+
     # -------------------------------------------------------------- fields
     def _check(self, rc, what):
         if rc != 0:

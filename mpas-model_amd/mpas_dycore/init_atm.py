@@ -312,20 +312,21 @@ def _ref_local_polygon(c, pts, R):
     return theta_abs, thetav, dl
 
 
-def compute_deriv_two(m):
-    """deriv_two, as atm_initialize_advection_rk computes it (mpas_atm_advection.F:21-394,
-    polynomial_order = 2, on a sphere): per cell a weighted least-squares quadratic through the
-    cell and its neighbours (poly_fit_2 with MIGS), the fit's second derivative along each edge's
-    normal direction.  deriv_two[e, side, j]: side 0 when the cell is cellsOnEdge(1, e); j = 0 the
-    cell itself, j = i + 1 its neighbour cellsOnCell(i)."""
-    nE, R = m["nEdges"], m["sphere_radius"]
+def deriv_two_inputs(m):
+    """The transcendental half of atm_initialize_advection_rk (mpas_atm_advection.F:21-394,
+    polynomial_order = 2, on a sphere), per cell and edgesOnCell slot: the tangent-plane coordinates
+    xp / yp of the neighbour cellsOnCell(i) (132-181) and sin / cos of the angle thetae of the edge's
+    normal direction (303-315, 334-335 / 347-348), from the C library's asin / sin / cos / sincos as the
+    compiled reference takes them.  Returns (xp, yp, sin_the, cos_the), each (nCells, maxEdges), zero
+    beyond nEdgesOnCell: what deriv_two_fit (host) or mpas_dyc_init_deriv_two (device) turn into
+    deriv_two."""
+    nC, R = m["nCells"], m["sphere_radius"]
     xc = np.stack([m["xCell"], m["yCell"], m["zCell"]], 1) / R
     xv = np.stack([m["xVertex"], m["yVertex"], m["zVertex"]], 1) / R
-    nEoC, coc, eoc, coe, voe = m["nEdgesOnCell"], m["cellsOnCell"], m["edgesOnCell"], m["cellsOnEdge"], m["verticesOnEdge"]
-    d2 = np.zeros((nE, 2, 15))
+    nEoC, coc, eoc, voe = m["nEdgesOnCell"], m["cellsOnCell"], m["edgesOnCell"], m["verticesOnEdge"]
+    out = [np.zeros((nC, m["maxEdges"])) for _ in range(4)]
     for ne in np.unique(nEoC):
         cells = np.nonzero(nEoC == ne)[0]
-        n = ne + 1
         c = xc[cells]
         nb = xc[coc[cells, :ne]]
         theta_abs, thetav, dl = _ref_local_polygon(c, nb, R)
@@ -334,7 +335,28 @@ def compute_deriv_two(m):
         for i in range(1, ne):
             thetat[:, i] = thetat[:, i - 1] + thetav[:, i - 1]
         st_, ct_ = _sincos(thetat)  # 180-181: cos and sin of thetat(i) in one loop body
-        xp, yp = ct_ * dl, st_ * dl
+        out[0][cells, :ne] = ct_ * dl
+        out[1][cells, :ne] = st_ * dl
+        for i in range(ne):
+            e = eoc[cells, i]
+            mid = _ref_arc_bisect(xv[voe[e, 0]], xv[voe[e, 1]])
+            the = _ref_sphere_angle(c, nb[:, i], mid) + thetat[:, i]
+            out[2][cells, i], out[3][cells, i] = _sincos(the)  # 334-335 / 347-348
+    return tuple(out)
+
+
+def deriv_two_fit(m, xp_all, yp_all, sin_all, cos_all):
+    """The arithmetic half (the host path; csrc/model_init.hip k_mi_deriv_two is the device one): per
+    cell the weighted least-squares quadratic through the cell and its neighbours (amatrix 215-226,
+    poly_fit_2 with MIGS, 567-741), and its second derivative along each edge's normal direction
+    (327-358)."""
+    nE = m["nEdges"]
+    nEoC, eoc, coe = m["nEdgesOnCell"], m["edgesOnCell"], m["cellsOnEdge"]
+    d2 = np.zeros((nE, 2, 15))
+    for ne in np.unique(nEoC):
+        cells = np.nonzero(nEoC == ne)[0]
+        n = ne + 1
+        xp, yp = xp_all[cells, :ne], yp_all[cells, :ne]
         a = np.zeros((len(cells), n, 6))
         a[:, 0, 0] = 1.0
         a[:, 1:, 0] = 1.0
@@ -348,9 +370,7 @@ def compute_deriv_two(m):
         b = _matmul_seq(_ref_migs(_matmul_seq(ath, a)), ath)   # (nc, 6, n)
         for i in range(ne):
             e = eoc[cells, i]
-            mid = _ref_arc_bisect(xv[voe[e, 0]], xv[voe[e, 1]])
-            the = _ref_sphere_angle(c, nb[:, i], mid) + thetat[:, i]
-            sin2t, cos2t = _sincos(the)  # 334-335 / 347-348
+            sin2t, cos2t = sin_all[cells, i], cos_all[cells, i]
             costsint = cos2t * sin2t
             cos2t, sin2t = cos2t * cos2t, sin2t * sin2t
             val = 2. * cos2t[:, None] * b[:, 3, :] + 2. * costsint[:, None] * b[:, 4, :] \
@@ -358,6 +378,15 @@ def compute_deriv_two(m):
             side = np.where(coe[e, 0] == cells, 0, 1)
             d2[e, side, :n] = val
     return d2
+
+
+def compute_deriv_two(m):
+    """deriv_two, as atm_initialize_advection_rk computes it (mpas_atm_advection.F:21-394,
+    polynomial_order = 2, on a sphere): per cell a weighted least-squares quadratic through the
+    cell and its neighbours (poly_fit_2 with MIGS), the fit's second derivative along each edge's
+    normal direction.  deriv_two[e, side, j]: side 0 when the cell is cellsOnEdge(1, e); j = 0 the
+    cell itself, j = i + 1 its neighbour cellsOnCell(i)."""
+    return deriv_two_fit(m, *deriv_two_inputs(m))
 
 
 def compute_defc(m):

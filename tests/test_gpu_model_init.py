@@ -195,3 +195,47 @@ def test_model_run_from_device_init(moist_case):
             assert np.array_equal(s0[n], s1[n]), n
         else:  # the parity tests' 1-step bars: w amplifies a last-bit change of dss the most
             assert rel_linf(s1[n], s0[n]) <= (1e-11 if n == "w" else 1e-13), n
+
+
+@pytest.mark.parametrize("fixture", ["init_x1.642_K8.npz", "init_varres2562_K8.npz"])
+def test_deriv_two_on_device_matches_reference(fixture):
+    """deriv_two's least-squares fits on the device (mpas_dyc_init_deriv_two: amatrix, poly_fit_2 with
+    MIGS / ELGS and the edge weights of mpas_atm_advection.F:215-358, 567-741), from the C library's
+    tangent-plane coordinates and edge angles (init_atm.deriv_two_inputs): bit for bit the reference's
+    deriv_two; and the device model init run on it gives the reference's adv_coefs bit for bit."""
+    import os
+    from mpas_dycore import Dycore, init_atm
+    mg = _cases()
+    case = mg.INIT_CASES[fixture]()
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", fixture))
+    assert str(z["checksum"]) == mg.init_inputs_checksum(case), "mesh generator changed: regenerate the fixture"
+    nE = case["nEdges"]
+    dy = Dycore(case, device=0, model_init="device")
+    try:
+        dy.init_deriv_two(init_atm.deriv_two_inputs(case))
+        got = dy.get_raw("mesh", "deriv_two").reshape(nE + 1, 2, 15)
+        assert np.array_equal(got[:nE], z["deriv_two"]), \
+            f"{int((got[:nE] != z['deriv_two']).sum())} deriv_two weights differ from the reference"
+        assert not got[nE].any()
+        cfg = case["config"]
+        dy._check(dy.lib.mpas_dyc_model_init(dy.h, int(bool(cfg.get("config_h_ScaleWithMesh", True))),
+                                             float(cfg["config_zd"]), float(cfg["config_xnutr"])), "model_init")
+        aslot = np.arange(15)[None, :] < np.asarray(z["nAdvCellsForEdge"])[:, None]
+        for n in ("adv_coefs", "adv_coefs_3rd"):
+            a = dy.get_raw("mesh", n).reshape(nE + 1, 15)[:nE]
+            assert np.array_equal(np.where(aslot, a, 0), np.where(aslot, z[n], 0)), n
+    finally:
+        dy.close()
+
+
+def test_deriv_two_on_device_refuses_bad_inputs(moist_case):
+    import ctypes as C
+    from mpas_dycore import Dycore
+    dy = Dycore(moist_case, device=0)
+    try:
+        with pytest.raises(ValueError):
+            dy.init_deriv_two([np.zeros((3, 3))] * 4)
+        assert dy.lib.mpas_dyc_init_deriv_two(dy.h, 5, *[C.c_void_p(1)] * 4) == -1  # no block 5
+        assert dy.lib.mpas_dyc_init_deriv_two(dy.h, 0, None, None, None, None) == -1
+    finally:
+        dy.close()
