@@ -186,6 +186,12 @@ int mpas_dyc_model_init(mpas_dyc_ctx* ctx, int32_t h_scale_with_mesh, double con
  * edgesOnCell and cellsOnEdge.  Cells with more than 14 edges: MPAS_DYC_EINVAL.  Synchronous. */
 int mpas_dyc_init_deriv_two(mpas_dyc_ctx* ctx, int32_t block, const double* xp, const double* yp,
                             const double* sin_the, const double* cos_the);
+/* zb / zb3, the z-metric terms of the omega equation, as core_init_atmosphere computes them
+ * (mpas_init_atm_cases.F:1045-1093) for config_theta_adv_order 2, 3 or 4, into mesh.zb / mesh.zb3
+ * (nVertLevels+1, 2, nEdges+1) of one block (allocated if not yet set), on the device, from the block's
+ * mesh.deriv_two, zgrid, dcEdge, dvEdge, areaCell and connectivity.  Edges with no owned cell and
+ * level nVertLevels+1 are 0.  Bit for bit the reference's arithmetic.  Synchronous. */
+int mpas_dyc_init_zb(mpas_dyc_ctx* ctx, int32_t block, int32_t theta_adv_order);
 /* atm_compute_output_diagnostics(state, time_level, diag, mesh) (mpas_atm_core.F:753, called
  * before history writes at :544 and :694): diag theta, rho and pressure from theta_m, rho_zz,
  * scalars(index_qv) of the time level, zz, pressure_base and pressure_p.  Asynchronous. */

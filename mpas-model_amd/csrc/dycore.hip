@@ -3230,6 +3230,50 @@ int mpas_dyc_init_deriv_two(mpas_dyc_ctx* ctx, int32_t block, const double* xp, 
   return MPAS_DYC_OK;
 }
 
+int mpas_dyc_init_zb(mpas_dyc_ctx* ctx, int32_t block, int32_t theta_adv_order) {
+  if (!ctx || theta_adv_order < 2 || theta_adv_order > 4) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
+  if (block < 0 || block >= (int)ctx->blk.size()) {
+    ctx->err = "mpas_dyc_init_zb: no block " + std::to_string(block);
+    return MPAS_DYC_EINVAL;
+  }
+  Block& b = ctx->blk[block];
+  for (const char* n : {"deriv_two", "areaCell"})
+    if (!find(b, "mesh", n)->buf[0]) {
+      ctx->err = std::string("mpas_dyc_init_zb needs mesh.") + n + " (set it or compute it first)";
+      return MPAS_DYC_ESTATE;
+    }
+  HIPCHK(hipSetDevice(ctx->device));
+  ZbFit q{};
+  for (const char* n : {"zb", "zb3"}) {
+    Field* f = find(b, "mesh", n);
+    const int64_t nb = field_bytes(b, *f);
+    if (!f->buf[0]) HIPCHK(hipMalloc(&f->buf[0], nb + 256));
+    HIPCHK(hipMemsetAsync(f->buf[0], 0, nb, ctx->stream));
+    (n[2] ? q.zb3 : q.zb) = (double*)f->buf[0];
+  }
+  q.nEdgesOnCell = (const int*)find(b, "mesh", "nEdgesOnCell")->buf[0];
+  q.cellsOnCell = (const int*)find(b, "mesh", "cellsOnCell")->buf[0];
+  q.cellsOnEdge = (const int*)find(b, "mesh", "cellsOnEdge")->buf[0];
+  q.deriv_two = (const double*)find(b, "mesh", "deriv_two")->buf[0];
+  q.zgrid = (const double*)find(b, "mesh", "zgrid")->buf[0];
+  q.dcEdge = (const double*)find(b, "mesh", "dcEdge")->buf[0];
+  q.dvEdge = (const double*)find(b, "mesh", "dvEdge")->buf[0];
+  q.areaCell = (const double*)find(b, "mesh", "areaCell")->buf[0];
+  q.nCells = b.d.nCells;
+  q.nCellsSolve = b.d.nCellsSolve;
+  q.nEdges = b.d.nEdges;
+  q.K = b.d.K;
+  q.maxEdges = b.me_decl;
+  q.order = theta_adv_order;
+  const int64_t n = (int64_t)b.d.nEdges * b.d.K;
+  hipLaunchKernelGGL(k_mi_zb, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, q);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  ctx->bnd_ready = false;  // zb / zb3 feed model_init's zb_cell copies
+  return MPAS_DYC_OK;
+}
+
 int mpas_dyc_output_diagnostics(mpas_dyc_ctx* ctx, int32_t time_level) {
   if (!ctx || (time_level != 1 && time_level != 2)) return MPAS_DYC_EINVAL;
   if (ctx->host_only) return MPAS_DYC_ESTATE;

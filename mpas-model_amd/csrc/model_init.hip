@@ -388,4 +388,47 @@ __global__ void k_mi_deriv_two(D2Fit q) {
   }
 }
 
+// ---- zb / zb3, the z-metric terms of the omega equation (core_init_atmosphere/
+// mpas_init_atm_cases.F:1045-1093), one thread per edge and level: the second derivative of zgrid
+// across the edge from deriv_two (each side's sum from the cell itself, then cellsOnCell in order),
+// z_edge and z_edge3 for config_theta_adv_order 2 / 3 / 4, over dvEdge / areaCell of each side.
+// Edges without an owned cell keep 0, as does level nVertLevels+1.
+struct ZbFit {
+  const int *nEdgesOnCell, *cellsOnCell, *cellsOnEdge;
+  const double *deriv_two, *zgrid, *dcEdge, *dvEdge, *areaCell;
+  double *zb, *zb3;
+  int nCells, nCellsSolve, nEdges, K, maxEdges, order;
+};
+
+__global__ void k_mi_zb(ZbFit q) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)q.nEdges * q.K) return;
+  const int e = (int)(t / q.K), k = (int)(t % q.K);
+  const int c1 = q.cellsOnEdge[2 * e], c2 = q.cellsOnEdge[2 * e + 1];
+  if (!(c1 < q.nCellsSolve || c2 < q.nCellsSolve)) return;
+  const size_t K1 = (size_t)q.K + 1;
+  const double z1 = q.zgrid[(size_t)c1 * K1 + k], z2 = q.zgrid[(size_t)c2 * K1 + k];
+  double z_edge, z_edge3 = 0.;
+  if (q.order == 2) {
+    z_edge = (z1 + z2) / 2.;
+  } else {
+    const double* d1 = q.deriv_two + ((size_t)e * 2 + 0) * 15;
+    const double* d2 = q.deriv_two + ((size_t)e * 2 + 1) * 15;
+    double f1 = d1[0] * z1, f2 = d2[0] * z2;
+    const int n1 = q.nEdgesOnCell[c1], n2 = q.nEdgesOnCell[c2];
+    for (int i = 0; i < n1 && i < q.maxEdges; ++i)
+      f1 = f1 + d1[i + 1] * q.zgrid[(size_t)q.cellsOnCell[(size_t)c1 * q.maxEdges + i] * K1 + k];
+    for (int i = 0; i < n2 && i < q.maxEdges; ++i)
+      f2 = f2 + d2[i + 1] * q.zgrid[(size_t)q.cellsOnCell[(size_t)c2 * q.maxEdges + i] * K1 + k];
+    const double dc = q.dcEdge[e];
+    z_edge = 0.5 * (z1 + z2) - (dc * dc) * (f1 + f2) / 12.;
+    if (q.order == 3) z_edge3 = -((dc * dc) * (f1 - f2) / 12.);
+  }
+  const double dv = q.dvEdge[e];
+  q.zb[((size_t)e * 2 + 0) * K1 + k] = (z_edge - z1) * dv / q.areaCell[c1];
+  q.zb[((size_t)e * 2 + 1) * K1 + k] = (z_edge - z2) * dv / q.areaCell[c2];
+  q.zb3[((size_t)e * 2 + 0) * K1 + k] = z_edge3 * dv / q.areaCell[c1];
+  q.zb3[((size_t)e * 2 + 1) * K1 + k] = z_edge3 * dv / q.areaCell[c2];
+}
+
 }  // namespace mpas

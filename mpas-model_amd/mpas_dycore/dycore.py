@@ -209,6 +209,10 @@ class Dycore:
         self._check(self.lib.mpas_dyc_init_deriv_two(self.h, block, *[a.ctypes.data_as(C.c_void_p) for a in arrs]),
                     "init_deriv_two")
 
+    def init_zb(self, theta_adv_order: int = 3, block: int = 0):
+        """mpas_dyc_init_zb: zb / zb3 on the device from the block's deriv_two and zgrid."""
+        self._check(self.lib.mpas_dyc_init_zb(self.h, block, int(theta_adv_order)), "init_zb")
+
     # -------------------------------------------------------------- fields
     def _check(self, rc, what):
         if rc != 0:

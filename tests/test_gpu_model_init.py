@@ -239,3 +239,31 @@ def test_deriv_two_on_device_refuses_bad_inputs(moist_case):
         assert dy.lib.mpas_dyc_init_deriv_two(dy.h, 0, None, None, None, None) == -1
     finally:
         dy.close()
+
+
+def test_init_chain_on_device_matches_reference_jw():
+    """The init core's arithmetic on the device, chained: deriv_two's fits (mpas_dyc_init_deriv_two) and
+    zb / zb3 (mpas_dyc_init_zb, mpas_init_atm_cases.F:1045-1093) from the C library's angles and the JW
+    vertical grid, against the reference's init_atm_case_jw on x1.642 x 26 (tests/golden/jw_x1.642_K26.npz):
+    bit for bit."""
+    import os
+    from mpas_dycore import Dycore, init_atm
+    mg = _cases()
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "jw_x1.642_K26.npz"))
+    m, unit, scaled = mg.jw_inputs()
+    assert str(z["checksum"]) == mg.case_checksum(
+        {**{k: v for k, v in m.items() if isinstance(v, np.ndarray)}, **unit}), "mesh generator changed: regenerate"
+    case = init_atm.build_case({**m, **scaled}, K=26, ns=1)
+    nE, K = case["nEdges"], case["nVertLevels"]
+    dy = Dycore(case, device=0, model_init="device")
+    try:
+        dy.init_deriv_two(init_atm.deriv_two_inputs(case))
+        dy.init_zb(3)
+        for name, n_per in (("deriv_two", 30), ("zb", 2 * (K + 1)), ("zb3", 2 * (K + 1))):
+            got = dy.get_raw("mesh", name)[:nE * n_per]
+            ref = np.asarray(z["mesh." + name]).ravel()[:nE * n_per]
+            assert np.array_equal(got, ref), f"{name}: {int((got != ref).sum())} of {got.size} differ from the reference"
+        with pytest.raises(Exception):
+            dy.init_zb(5)
+    finally:
+        dy.close()
