@@ -192,6 +192,15 @@ int mpas_dyc_init_deriv_two(mpas_dyc_ctx* ctx, int32_t block, const double* xp, 
  * mesh.deriv_two, zgrid, dcEdge, dvEdge, areaCell and connectivity.  Edges with no owned cell and
  * level nVertLevels+1 are 0.  Bit for bit the reference's arithmetic.  Synchronous. */
 int mpas_dyc_init_zb(mpas_dyc_ctx* ctx, int32_t block, int32_t theta_adv_order);
+/* The reconstruction coefficients of every block on the device: mpas_rbf_interp_initialize's vectors
+ * (operators/mpas_vector_operations.F:697-769: edge normals, each cell's tangent plane) and
+ * mpas_init_reconstruct (operators/mpas_vector_reconstruction.F:112-177: the inverse-multiquadric RBF
+ * system of each cell's edges with a constant vector in the plane, solved by elgs + mpas_legs), what
+ * mpas_atm_core.F:408-409 runs at model init, into mesh.coeffs_reconstruct.  Reads mesh.xCell, yCell,
+ * zCell (nCells+1), xEdge, yEdge, zEdge (nEdges+1), set beforehand, and the connectivity.  + - * / sqrt
+ * only, in the Fortran's order: bit for bit the reference's coefficients.  Cells with more than 14
+ * edges: MPAS_DYC_EINVAL.  Synchronous. */
+int mpas_dyc_init_reconstruct(mpas_dyc_ctx* ctx);
 /* atm_compute_output_diagnostics(state, time_level, diag, mesh) (mpas_atm_core.F:753, called
  * before history writes at :544 and :694): diag theta, rho and pressure from theta_m, rho_zz,
  * scalars(index_qv) of the time level, zz, pressure_base and pressure_p.  Asynchronous. */

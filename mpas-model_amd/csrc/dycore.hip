@@ -384,7 +384,11 @@ void build_registry(Block& c) {
   add(c, "mesh", "meshDensity", L_CELL, 1);
   add(c, "mesh", "areaCell", L_CELL, 1);
   add(c, "mesh", "areaTriangle", L_VERTEX, 1);
-  for (const char* n : {"deriv_two", "zb", "zb3", "meshDensity", "areaCell", "areaTriangle"})
+  // inputs of the reconstruction coefficients (mpas_dyc_init_reconstruct), allocated when set
+  for (const char* n : {"xCell", "yCell", "zCell"}) add(c, "mesh", n, L_CELL, 1);
+  for (const char* n : {"xEdge", "yEdge", "zEdge"}) add(c, "mesh", n, L_EDGE, 1);
+  for (const char* n : {"deriv_two", "zb", "zb3", "meshDensity", "areaCell", "areaTriangle", "xCell", "yCell", "zCell",
+                        "xEdge", "yEdge", "zEdge"})
     c.fields[c.by_name[std::string("mesh.") + n]].lazy = true;
   // the maxEdges- and maxEdges2-strided mesh arrays (pack_mesh)
   for (const char* n : {"edgesOnCell", "cellsOnCell", "verticesOnCell", "kiteForCell", "coeffs_reconstruct",
@@ -3272,6 +3276,62 @@ int mpas_dyc_init_zb(mpas_dyc_ctx* ctx, int32_t block, int32_t theta_adv_order) 
   HIPCHK(hipStreamSynchronize(ctx->stream));
   ctx->bnd_ready = false;  // zb / zb3 feed model_init's zb_cell copies
   return MPAS_DYC_OK;
+}
+
+int mpas_dyc_init_reconstruct(mpas_dyc_ctx* ctx) {
+  if (!ctx) return MPAS_DYC_EINVAL;
+  if (ctx->host_only) return MPAS_DYC_ESTATE;
+  HIPCHK(hipSetDevice(ctx->device));
+  int* bad = nullptr;
+  HIPCHK(hipMalloc(&bad, sizeof(int)));
+  int rc = MPAS_DYC_OK;
+  for (auto& b : ctx->blk) {
+    RecInit q{};
+    const double* xyz[6];
+    const char* names[6] = {"xCell", "yCell", "zCell", "xEdge", "yEdge", "zEdge"};
+    for (int i = 0; i < 6; ++i) {
+      xyz[i] = (const double*)find(b, "mesh", names[i])->buf[0];
+      if (!xyz[i]) {
+        ctx->err = std::string("mpas_dyc_init_reconstruct needs mesh.") + names[i] + " (set it first)";
+        rc = MPAS_DYC_ESTATE;
+      }
+    }
+    if (rc != MPAS_DYC_OK) break;
+    q.nEdgesOnCell = (const int*)find(b, "mesh", "nEdgesOnCell")->buf[0];
+    q.edgesOnCell = (const int*)find(b, "mesh", "edgesOnCell")->buf[0];
+    q.cellsOnEdge = (const int*)find(b, "mesh", "cellsOnEdge")->buf[0];
+    q.xCell = xyz[0];
+    q.yCell = xyz[1];
+    q.zCell = xyz[2];
+    q.xEdge = xyz[3];
+    q.yEdge = xyz[4];
+    q.zEdge = xyz[5];
+    Field* f = find(b, "mesh", "coeffs_reconstruct");
+    q.coeffs = (double*)f->buf[0];
+    q.bad = bad;
+    q.nCells = b.d.nCells;
+    q.maxEdges = b.me_decl;
+    if (hipMemsetAsync(f->buf[0], 0, field_bytes(b, *f), ctx->stream) != hipSuccess ||
+        hipMemsetAsync(bad, 0, sizeof(int), ctx->stream) != hipSuccess) {
+      rc = MPAS_DYC_EHIP;
+      break;
+    }
+    hipLaunchKernelGGL(k_mi_reconstruct, dim3((unsigned)((b.d.nCells + 127) / 128)), dim3(128), 0, ctx->stream, q);
+    int hbad = 0;
+    if (hipGetLastError() != hipSuccess || hipMemcpy(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = MPAS_DYC_EHIP;
+      break;
+    }
+    if (hbad) {
+      ctx->err = "mpas_dyc_init_reconstruct: a cell has more than 14 edges";
+      rc = MPAS_DYC_EINVAL;
+      break;
+    }
+  }
+  if (rc == MPAS_DYC_EHIP) ctx->err = "mpas_dyc_init_reconstruct: HIP error";
+  (void)hipFree(bad);
+  ctx->bnd_ready = false;  // pack_mesh copies coeffs_reconstruct for the kernels
+  return rc;
 }
 
 int mpas_dyc_output_diagnostics(mpas_dyc_ctx* ctx, int32_t time_level) {

@@ -431,4 +431,145 @@ __global__ void k_mi_zb(ZbFit q) {
   q.zb3[((size_t)e * 2 + 1) * K1 + k] = z_edge3 * dv / q.areaCell[c2];
 }
 
+// ---- coeffs_reconstruct (mpas_rbf_interp_initialize -> mpas_initialize_vectors,
+// operators/mpas_vector_operations.F:697-769, then mpas_init_reconstruct,
+// operators/mpas_vector_reconstruction.F:112-177 with mpas_rbf_interp_func_3D_plane_vec_const_dir_comp_coeffs,
+// mpas_rbf_interpolation.F:1079-1145), what mpas_atm_core.F:408-409 runs at model init, one thread per
+// cell: the edge normals (unit(x(cell2) - x(cell1))), the cell's tangent plane, and the RBF system of
+// its edges (inverse multiquadric, a constant vector in the plane) solved by elgs + mpas_legs
+// (:1670-1846).  + - * / sqrt only, each in the Fortran's order (sum() over R3 as (a1 + a2) + a3, **2 as
+// x * x): bit for bit the reference's coefficients (reconstruct.py is the host restatement).
+struct RecInit {
+  const int *nEdgesOnCell, *edgesOnCell, *cellsOnEdge;
+  const double *xCell, *yCell, *zCell, *xEdge, *yEdge, *zEdge;
+  double* coeffs;  // (nCells + 1, maxEdges, 3)
+  int* bad;
+  int nCells, maxEdges;
+};
+constexpr int REC_MAXE = 14, REC_MAXN = REC_MAXE + 2;
+
+struct v3 {
+  double x, y, z;
+};
+__device__ __forceinline__ double sum3(v3 a) { return (a.x + a.y) + a.z; }
+__device__ __forceinline__ v3 unit3(v3 v) {
+  const double mag = sqrt((v.x * v.x + v.y * v.y) + v.z * v.z);
+  return v3{v.x / mag, v.y / mag, v.z / mag};
+}
+__device__ __forceinline__ double rbf_imq(double r2) { return 1 / sqrt(1 + r2); }
+
+__global__ void k_mi_reconstruct(RecInit q) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= q.nCells) return;
+  const int pc = q.nEdgesOnCell[c];
+  if (pc < 1 || pc > q.maxEdges || pc > REC_MAXE) {
+    if (pc > REC_MAXE) *q.bad = 1;
+    return;
+  }
+  auto xc = [&](int i) { return v3{q.xCell[i], q.yCell[i], q.zCell[i]}; };
+  auto normal = [&](int e) {  // edgeNormalVectors(:, e)
+    const v3 a = xc(q.cellsOnEdge[2 * e]), b = xc(q.cellsOnEdge[2 * e + 1]);
+    return unit3(v3{b.x - a.x, b.y - a.y, b.z - a.z});
+  };
+  const v3 center = xc(c);
+  const v3 rhat = unit3(center);  // localVerticalUnitVectors
+  // cellTangentPlane: the first edge's normal with its radial part removed, and rhat x xhat
+  const v3 n1 = normal(q.edgesOnCell[(size_t)c * q.maxEdges]);
+  const double ndr = sum3(v3{n1.x * rhat.x, n1.y * rhat.y, n1.z * rhat.z});
+  const v3 b1 = unit3(v3{n1.x - ndr * rhat.x, n1.y - ndr * rhat.y, n1.z - ndr * rhat.z});
+  const v3 b2 = unit3(v3{rhat.y * b1.z - rhat.z * b1.y, rhat.z * b1.x - rhat.x * b1.z, rhat.x * b1.y - rhat.y * b1.x});
+  double ps[REC_MAXE][2], pu[REC_MAXE][2];
+  double alpha = 0.0;
+  for (int i = 0; i < pc; ++i) {
+    const int e = q.edgesOnCell[(size_t)c * q.maxEdges + i];
+    const v3 loc{q.xEdge[e], q.yEdge[e], q.zEdge[e]};
+    const v3 d{center.x - loc.x, center.y - loc.y, center.z - loc.z};
+    alpha = alpha + sqrt(sum3(v3{d.x * d.x, d.y * d.y, d.z * d.z}));
+    const v3 nor = normal(e);
+    ps[i][0] = sum3(v3{loc.x * b1.x, loc.y * b1.y, loc.z * b1.z});
+    ps[i][1] = sum3(v3{loc.x * b2.x, loc.y * b2.y, loc.z * b2.z});
+    pu[i][0] = sum3(v3{nor.x * b1.x, nor.y * b1.y, nor.z * b1.z});
+    pu[i][1] = sum3(v3{nor.x * b2.x, nor.y * b2.y, nor.z * b2.z});
+  }
+  alpha = alpha / pc;
+  const double pd0 = sum3(v3{center.x * b1.x, center.y * b1.y, center.z * b1.z});
+  const double pd1 = sum3(v3{center.x * b2.x, center.y * b2.y, center.z * b2.z});
+  const double a2 = alpha * alpha;
+  const int N = pc + 2;
+  double M[REC_MAXN][REC_MAXN], R[REC_MAXN][2];
+  for (int i = 0; i < N; ++i) {
+    for (int j = 0; j < N; ++j) M[i][j] = 0.0;
+    R[i][0] = R[i][1] = 0.0;
+  }
+  for (int j = 0; j < pc; ++j)
+    for (int i = j; i < pc; ++i) {
+      const double d0 = ps[i][0] - ps[j][0], d1 = ps[i][1] - ps[j][1];
+      const double r2 = (d0 * d0 + d1 * d1) / a2;
+      const double dot = pu[i][0] * pu[j][0] + pu[i][1] * pu[j][1];
+      M[i][j] = rbf_imq(r2) * dot;
+      M[j][i] = M[i][j];
+    }
+  for (int j = 0; j < pc; ++j) {
+    const double d0 = pd0 - ps[j][0], d1 = pd1 - ps[j][1];
+    const double f = rbf_imq((d0 * d0 + d1 * d1) / a2);
+    R[j][0] = f * pu[j][0];
+    R[j][1] = f * pu[j][1];
+  }
+  for (int i = 0; i < pc; ++i) {
+    M[i][pc] = pu[i][0];
+    M[i][pc + 1] = pu[i][1];
+    M[pc][i] = pu[i][0];
+    M[pc + 1][i] = pu[i][1];
+  }
+  R[pc][0] = 1.0;
+  R[pc + 1][1] = 1.0;
+  // elgs: scaled partial pivoting
+  int indx[REC_MAXN];
+  double C[REC_MAXN];
+  for (int i = 0; i < N; ++i) {
+    indx[i] = i;
+    double c1 = 0.0;
+    for (int j = 0; j < N; ++j) c1 = fmax(c1, fabs(M[i][j]));
+    C[i] = c1;
+  }
+  for (int j = 0; j < N - 1; ++j) {
+    double pi1 = 0.0;
+    int k = j;
+    for (int i = j; i < N; ++i) {
+      const double pi = fabs(M[indx[i]][j]) / C[indx[i]];
+      if (pi > pi1) {
+        pi1 = pi;
+        k = i;
+      }
+    }
+    const int t = indx[j];
+    indx[j] = indx[k];
+    indx[k] = t;
+    for (int i = j + 1; i < N; ++i) {
+      const double pj = M[indx[i]][j] / M[indx[j]][j];
+      M[indx[i]][j] = pj;
+      for (int kk = j + 1; kk < N; ++kk) M[indx[i]][kk] = M[indx[i]][kk] - pj * M[indx[j]][kk];
+    }
+  }
+  // mpas_legs: forward elimination of both right-hand sides, back substitution
+  for (int i = 0; i < N - 1; ++i)
+    for (int j = i + 1; j < N; ++j)
+      for (int r = 0; r < 2; ++r) R[indx[j]][r] = R[indx[j]][r] - M[indx[j]][i] * R[indx[i]][r];
+  double X[REC_MAXN][2];
+  for (int r = 0; r < 2; ++r) X[N - 1][r] = R[indx[N - 1]][r] / M[indx[N - 1]][N - 1];
+  for (int i = N - 2; i >= 0; --i)
+    for (int r = 0; r < 2; ++r) {
+      double xi = R[indx[i]][r];
+      for (int j = i + 1; j < N; ++j) xi = xi - M[indx[i]][j] * X[j][r];
+      X[i][r] = xi / M[indx[i]][i];
+    }
+  double* out = q.coeffs + (size_t)c * q.maxEdges * 3;
+  for (int i = 0; i < q.maxEdges; ++i) {
+    const bool on = i < pc;
+    out[i * 3 + 0] = on ? b1.x * X[i][0] + b2.x * X[i][1] : 0.0;
+    out[i * 3 + 1] = on ? b1.y * X[i][0] + b2.y * X[i][1] : 0.0;
+    out[i * 3 + 2] = on ? b1.z * X[i][0] + b2.z * X[i][1] : 0.0;
+  }
+}
+
 }  // namespace mpas

@@ -24,7 +24,7 @@ EXPORTS = (
     "mpas_dyc_graph_active", "mpas_dyc_solve_diagnostics", "mpas_dyc_set_lbc", "mpas_dyc_finish_step",
     "mpas_dyc_get_block_summary", "mpas_dyc_block_layout", "mpas_dyc_set_profile", "mpas_dyc_get_profile",
     "mpas_dyc_last_exchange", "mpas_dyc_rccl_version", "mpas_dyc_model_init", "mpas_dyc_set_exchange_positions",
-    "mpas_dyc_init_deriv_two", "mpas_dyc_init_zb",
+    "mpas_dyc_init_deriv_two", "mpas_dyc_init_zb", "mpas_dyc_init_reconstruct",
 )
 HOST_ONLY = -2  # MPAS_DYC_HOST_ONLY: planner-only context
 PRINT_GLOBAL_MINMAX_VEL, PRINT_DETAILED_MINMAX_VEL, PRINT_GLOBAL_MINMAX_SCA = 1, 2, 4
@@ -161,6 +161,7 @@ def load() -> C.CDLL:
     lib.mpas_dyc_model_init.argtypes = [vp, i32, dbl, dbl]
     lib.mpas_dyc_init_deriv_two.argtypes = [vp, i32, vp, vp, vp, vp]
     lib.mpas_dyc_init_zb.argtypes = [vp, i32, i32]
+    lib.mpas_dyc_init_reconstruct.argtypes = [vp]
     lib.mpas_dyc_set_exchange_positions.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, i32]
     if os.environ.get("MPAS_DYCORE_LIB"):
         lib = _real

@@ -29,6 +29,8 @@ MODEL_INIT_OUT = ("invAreaCell", "invDvEdge", "invDcEdge", "invAreaTriangle", "e
                   "adv_coefs", "adv_coefs_3rd", "meshScalingDel2", "meshScalingDel4", "meshScalingRegionalCell",
                   "meshScalingRegionalEdge", "dss")
 MODEL_INIT_IN = ("deriv_two", "zb", "zb3", "meshDensity", "areaCell", "areaTriangle")
+# and mpas_rbf_interp_initialize + mpas_init_reconstruct (mpas_atm_core.F:408-409; mpas_dyc_init_reconstruct)
+RECONSTRUCT_IN = ("xCell", "yCell", "zCell", "xEdge", "yEdge", "zEdge")
 DIAG_INPUTS = ("theta", "rho", "rho_base", "theta_base")
 _SKIP = set(STATE_INPUTS) | set(DIAG_INPUTS) | {"xCell", "yCell", "zCell", "xEdge", "yEdge", "zEdge", "xVertex",
                                                 "yVertex", "zVertex",
@@ -161,6 +163,8 @@ class Dycore:
             self._check(self.lib.mpas_dyc_model_init(self.h, int(bool(cfg.get("config_h_ScaleWithMesh", True))),
                                                      float(cfg["config_zd"]), float(cfg["config_xnutr"])),
                         "model_init")
+            if all(n in c for c in cases for n in RECONSTRUCT_IN):
+                self._check(self.lib.mpas_dyc_init_reconstruct(self.h), "init_reconstruct")
 
     @classmethod
     def from_blocks(cls, blocks: list, device: int = 0, moist_end: int = 1, placement: dict | None = None,
@@ -272,11 +276,12 @@ class Dycore:
         """device_init: leave atm_mpas_init_block's precompute to the device (mpas_dyc_model_init) --
         upload its inputs (the init file's deriv_two, zb, zb3, meshDensity, areaCell, areaTriangle)
         instead of the case's precomputed arrays."""
+        device_rec = device_init and all(n in case for n in RECONSTRUCT_IN)  # else the case's coefficients
         if device_init:
-            for name in MODEL_INIT_IN:
+            for name in MODEL_INIT_IN + (RECONSTRUCT_IN if device_rec else ()):
                 self.set_raw("mesh", name, to_fortran(case, name), block=block)
         for name in case:
-            if name in _SKIP or (device_init and name in MODEL_INIT_OUT):
+            if name in _SKIP or (device_init and name in MODEL_INIT_OUT) or (device_rec and name == "coeffs_reconstruct"):
                 continue
             if name in F.LOCATION or name in F.VERTICAL_1D:
                 if name in F.VERTICAL_1D:

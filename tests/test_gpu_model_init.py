@@ -173,7 +173,8 @@ def test_model_run_from_device_init(moist_case):
     for mode in ("host", "device"):
         dy = Dycore(case, device=0, moist_end=3, model_init=mode)
         mesh = {n: dy.get_raw("mesh", n) for n in ("adv_coefs", "adv_coefs_3rd", "zb3_cell", "dss", "meshScalingDel2",
-                                                    "meshScalingDel4", "edgesOnCell_sign", "invDcEdge")}
+                                                    "meshScalingDel4", "edgesOnCell_sign", "invDcEdge",
+                                                    "coeffs_reconstruct")}
         dy.init_diagnostics(dt)
         dy.use_graph(True)
         for it in range(3):
@@ -267,3 +268,29 @@ def test_init_chain_on_device_matches_reference_jw():
             dy.init_zb(5)
     finally:
         dy.close()
+
+
+def test_reconstruct_coefficients_on_device_match_reference():
+    """mpas_dyc_init_reconstruct (mpas_rbf_interp_initialize's vectors + mpas_init_reconstruct,
+    mpas_atm_core.F:408-409, run by Dycore(model_init="device")): coeffs_reconstruct bit for bit the
+    reference's on x1.642 (tests/golden/reconstruct_x1.642.npz), and equal to the host restatement
+    (reconstruct.py) on the var-res mesh with pentagons and heptagons."""
+    import os
+    from mpas_dycore import Dycore, reconstruct
+    from mpas_dycore.cases import jw_case
+    mg = _cases()
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "reconstruct_x1.642.npz"))
+    case = jw_case(642, K=8, ns=1, cache=False)
+    assert str(z["checksum"]) == mg.case_checksum(case), "mesh generator changed: regenerate the fixture"
+    cases = [(case, z["coeffs_reconstruct"]), (mg.INIT_CASES["init_varres2562_K8.npz"](), None)]
+    for c, ref in cases:
+        nC, ME = c["nCells"], c["maxEdges"]
+        if ref is None:
+            ref = reconstruct.init_reconstruct(c)
+            assert (np.asarray(c["nEdgesOnCell"]) != 6).any()
+        dy = Dycore(c, device=0, model_init="device")
+        try:
+            got = dy.get_raw("mesh", "coeffs_reconstruct").reshape(nC + 1, ME, 3)[:nC]
+        finally:
+            dy.close()
+        assert np.array_equal(got, ref), f"{int((got != ref).sum())} coefficients differ"
