@@ -1986,9 +1986,9 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_dyn_edges_p(Dims d, Ptrs p, Co
   int eoe[NE2];
   double wgt[NE2];
   // (through the scalar cache: as vector loads, ld_row, 413 -> 426 us per call)
+  ld_row(p.edgesOnEdge + (size_t)e * d.maxEdges2, eoe);
 #pragma unroll
   for (int j = 0; j < NE2; ++j) {
-    eoe[j] = sel(h, p.edgesOnEdge[(size_t)eA * d.maxEdges2 + j], p.edgesOnEdge[(size_t)eB * d.maxEdges2 + j]);
     wgt[j] = sel(h, ld_uniform_f64(p.weightsOnEdge + (size_t)eA * d.maxEdges2 + j),
                  ld_uniform_f64(p.weightsOnEdge + (size_t)eB * d.maxEdges2 + j));
   }
@@ -2147,9 +2147,9 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_dyn_advflux_p(Dims d, Ptrs p) 
   double a[NA], b[NA];
   // (the rows through the scalar cache: as vector loads, ld_row, this kernel measured 368 -> 407 us
   // per call -- its 20 gathers per wave already fill the vector memory pipe)
+  ld_row(p.advCellsForEdge + (size_t)e * 15, ic);
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    ic[j] = sel(h, p.advCellsForEdge[(size_t)eA * 15 + j], p.advCellsForEdge[(size_t)eB * 15 + j]);
     a[j] = sel(h, ld_uniform_f64(p.adv_coefs + (size_t)eA * 15 + j), ld_uniform_f64(p.adv_coefs + (size_t)eB * 15 + j));
     b[j] = sel(h, ld_uniform_f64(p.adv_coefs_3rd + (size_t)eA * 15 + j),
                ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
