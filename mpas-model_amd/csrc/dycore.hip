@@ -1769,14 +1769,12 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
         else if (m6) LAUNCH(k_mono_bounds_b<6>, d.nCellsSolve, d, pq, is + q, ctx->cf.coef_3rd_order);
         else LAUNCH(k_mono_bounds_b<7>, d.nCellsSolve, d, pq, is + q, ctx->cf.coef_3rd_order);
       }
-      for (int q = 0; q < nq; ++q) {
-        const Ptrs& pq = q ? P1[b] : P[b];
-        if (batched(d) && pair_layout(d)) {
-          if (m6) LAUNCH_PE((k_mono_edges1_p<10, false>), (k_mono_edges1_p<10, true>), d.nEdges, d, pq, is + q, dt);
-          else LAUNCH_PE((k_mono_edges1_p<12, false>), (k_mono_edges1_p<12, true>), d.nEdges, d, pq, is + q, dt);
-        } else {
-          LAUNCH(k_mono_edges1, d.nEdges, d, pq, is + q, dt);
-        }
+      if (batched(d) && pair_layout(d)) {  // both scalars of the pair in one launch (the rows read once)
+        const MonoFlux2 f2 = nq == 2 ? MonoFlux2{P1[b].flux_arr, P1[b].flux_upwind_tmp, P1[b].flux_tmp} : MonoFlux2{};
+        if (m6) LAUNCH_PE((k_mono_edges1_p<10, false>), (k_mono_edges1_p<10, true>), d.nEdges, d, P[b], is, dt, nq, f2);
+        else LAUNCH_PE((k_mono_edges1_p<12, false>), (k_mono_edges1_p<12, true>), d.nEdges, d, P[b], is, dt, nq, f2);
+      } else {
+        for (int q = 0; q < nq; ++q) LAUNCH(k_mono_edges1, d.nEdges, d, q ? P1[b] : P[b], is + q, dt);
       }
       for (int q = 0; q < nq; ++q) {
         const Ptrs& pq = q ? P1[b] : P[b];

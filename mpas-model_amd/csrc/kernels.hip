@@ -2532,8 +2532,13 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
 // coefficients -- needs 197 VGPRs, runs 2 waves per SIMD instead of 4 and took exactly the time
 // of two launches: the in-flight gathers per SIMD, not the index loads, bound this kernel)
 // k_mono_edges1 in the pair layout (atm_advance_scalars_mono_work, 3916-3961, 4007-4022)
+// the second scratch set's edge fluxes (mono_slot1) for the pair's second scalar
+struct MonoFlux2 {
+  double *flux_arr, *flux_upwind_tmp, *flux_tmp;
+};
 template <int NA, bool ODD = false>
-__global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, int is, double dt) {
+__global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, int is, double dt, int nq = 1,
+                                                                MonoFlux2 f2 = MonoFlux2{}) {
   const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
@@ -2556,50 +2561,60 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
   const d2 uh = ld2(p.ruAvg + o);
   const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
   const bool on = c1 < d.nCellsSolve || c2 < d.nCellsSolve;
-  // scalars outside the block (the garbage slot) read as 0, as the reference's halo loops see them
-  auto val = [&](const double* arr, int cc) {
-    const d2 v = ld2(arr + SIX(cc, 2 * lc, is));
-    return cc < d.nCells ? v : d2{0.0, 0.0};
-  };
-  d2 sv[NA];
-#pragma unroll
-  for (int j = 0; j < NA; ++j) sv[j] = val(p.scalars2, ic[j]);
-  const d2 so1 = val(p.scalars1, c1), so2 = val(p.scalars1, c2);
-  auto flux = [&](double u, int lev) {
-    double acc = 0.0;
-    if (na == 10) {
-      const bool up = u > 0;
-#pragma unroll
-      for (int j = 0; j < 10 && j < NA; ++j) {
-        const double swa = up ? (a[j] + b[j]) : (a[j] - b[j]);
-        const double term = swa * (lev ? sv[j].y : sv[j].x);
-        acc = (j == 0) ? term : acc + term;
-      }
-      return u * (acc);
-    }
-    double fa = 0.0;
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-      if (j < na) fa = fa + (u * (a[j] + sgn1(u) * b[j])) * (lev ? sv[j].y : sv[j].x);
-    }
-    return fa;
-  };
-  d2 fa{0.0, 0.0};
-  if (on) {
-    fa.x = flux(uh.x, 0);
-    fa.y = flux(uh.y, 1);
-  }
-  d2 fu;
-  fu.x = dv * dt * (fmax(0.0, uh.x) * so1.x + fmin(0.0, uh.x) * so2.x);
-  fu.y = dv * dt * (fmax(0.0, uh.y) * so1.y + fmin(0.0, uh.y) * so2.y);
   // 4017-4020 (operator precedence as written: (apply_lbcs .and. mask == 5) .or. mask == 4): the
   // two outer relaxation rows keep only the upwind flux
   const int bm = sel(h, p.bdyMaskEdge[eA], p.bdyMaskEdge[eB]);
   const bool upw = (d.lbc && bm == N_RELAX_ZONE) || bm == N_RELAX_ZONE - 1;
-  if ((h == 0 || hasB) && 2 * l < K) {
-    pst(p.flux_arr + o, upw ? fu : fa, two);
-    pst(p.flux_upwind_tmp + o, fu, two);
-    pst(p.flux_tmp + o, upw ? d2{0.0, 0.0} : d2{dt * fa.x - fu.x, dt * fa.y - fu.y}, two);
+  // nq = 2: the pair's second scalar (is + 1) from the same rows, into the second scratch set
+  // (f2), one after the other -- each scalar's operations as in its own launch
+#pragma unroll 1
+  for (int q = 0; q < nq; ++q) {
+    const int iq = is + q;
+    // the weights a +- b formed per scalar, not hoisted out of the loop (hoisted, they stay live
+    // across it: 180 VGPRs, half the occupancy)
+#pragma unroll
+    for (int j = 0; j < NA; ++j) asm volatile("" : "+v"(a[j]), "+v"(b[j]));
+    // scalars outside the block (the garbage slot) read as 0, as the reference's halo loops see them
+    auto val = [&](const double* arr, int cc) {
+      const d2 v = ld2(arr + SIX(cc, 2 * lc, iq));
+      return cc < d.nCells ? v : d2{0.0, 0.0};
+    };
+    d2 sv[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) sv[j] = val(p.scalars2, ic[j]);
+    const d2 so1 = val(p.scalars1, c1), so2 = val(p.scalars1, c2);
+    auto flux = [&](double u, int lev) {
+      double acc = 0.0;
+      if (na == 10) {
+        const bool up = u > 0;
+#pragma unroll
+        for (int j = 0; j < 10 && j < NA; ++j) {
+          const double swa = up ? (a[j] + b[j]) : (a[j] - b[j]);
+          const double term = swa * (lev ? sv[j].y : sv[j].x);
+          acc = (j == 0) ? term : acc + term;
+        }
+        return u * (acc);
+      }
+      double fa = 0.0;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        if (j < na) fa = fa + (u * (a[j] + sgn1(u) * b[j])) * (lev ? sv[j].y : sv[j].x);
+      }
+      return fa;
+    };
+    d2 fa{0.0, 0.0};
+    if (on) {
+      fa.x = flux(uh.x, 0);
+      fa.y = flux(uh.y, 1);
+    }
+    d2 fu;
+    fu.x = dv * dt * (fmax(0.0, uh.x) * so1.x + fmin(0.0, uh.x) * so2.x);
+    fu.y = dv * dt * (fmax(0.0, uh.y) * so1.y + fmin(0.0, uh.y) * so2.y);
+    if ((h == 0 || hasB) && 2 * l < K) {
+      pst((q ? f2.flux_arr : p.flux_arr) + o, upw ? fu : fa, two);
+      pst((q ? f2.flux_upwind_tmp : p.flux_upwind_tmp) + o, fu, two);
+      pst((q ? f2.flux_tmp : p.flux_tmp) + o, upw ? d2{0.0, 0.0} : d2{dt * fa.x - fu.x, dt * fa.y - fu.y}, two);
+    }
   }
 }
 
