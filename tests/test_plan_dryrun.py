@@ -102,5 +102,14 @@ def test_host_only_context_refuses_device_calls(case163842):
         assert lib.mpas_dyc_init_diagnostics(h, 1.0) == -3
         buf = np.zeros(8)
         assert lib.mpas_dyc_set_field(h, b"mesh", b"cf1", 1, buf.ctypes.data_as(C.c_void_p), 8) == -3
+        # the device model-init entry points: ESTATE without a device, EINVAL for bad arguments
+        assert lib.mpas_dyc_model_init(h, 1, 22000.0, 0.2) == -3
+        x = buf.ctypes.data_as(C.c_void_p)
+        assert lib.mpas_dyc_init_deriv_two(h, 0, x, x, x, x) == -3
+        assert lib.mpas_dyc_init_deriv_two(h, 0, None, x, x, x) == -1
+        assert lib.mpas_dyc_init_zb(h, 0, 3) == -3
+        assert lib.mpas_dyc_init_zb(h, 0, 5) == -1
+        assert lib.mpas_dyc_init_reconstruct(h) == -3
+        assert lib.mpas_dyc_init_reconstruct(None) == -1
     finally:
         lib.mpas_dyc_destroy(h)
