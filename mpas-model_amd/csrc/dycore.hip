@@ -1776,11 +1776,14 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
       } else {
         for (int q = 0; q < nq; ++q) LAUNCH(k_mono_edges1, d.nEdges, d, q ? P1[b] : P[b], is + q, dt);
       }
-      for (int q = 0; q < nq; ++q) {
-        const Ptrs& pq = q ? P1[b] : P[b];
-        if (!bt) LAUNCH(k_mono_cells1, d.nCellsSolve, d, pq, is + q, dt, ad);
-        else if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, pq, is + q, dt, ad);
-        else LAUNCH(k_mono_cells1_b<7>, d.nCellsSolve, d, pq, is + q, dt, ad);
+      if (bt) {  // both scalars of the pair in one launch (the cell's own columns read once)
+        const MonoCell2 s2 = nq == 2 ? MonoCell2{P1[b].wdtn, P1[b].s_max, P1[b].s_min, P1[b].flux_tmp,
+                                                 P1[b].flux_upwind_tmp, P1[b].scalar_old_copy, P1[b].scale_arr}
+                                     : MonoCell2{};
+        if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2);
+        else LAUNCH(k_mono_cells1_b<7>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2);
+      } else {
+        for (int q = 0; q < nq; ++q) LAUNCH(k_mono_cells1, d.nCellsSolve, d, q ? P1[b] : P[b], is + q, dt, ad);
       }
     }
     if (nq == 2) CHK(exchange(ctx, {{"scratch", "scale_arr", 1, 0x1u}, {"scratch", "scale_arr_1", 1, 0x1u}}));

@@ -4213,8 +4213,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds_b(Dims d, Ptrs p,
   p.s_min[o] = smin;
 }
 
+// the second scratch set (mono_slot1) of k_mono_cells1_b for the pair's second scalar
+struct MonoCell2 {
+  double *wdtn, *s_max, *s_min, *flux_tmp, *flux_upwind_tmp, *scalar_old_copy, *scale_arr;
+};
 template <int ME>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p, int is, double dt, int advance_density) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p, int is, double dt, int advance_density,
+                                                                  int nq = 1, MonoCell2 s2 = MonoCell2{}) {
   const int c = wave_elem(0);
   if (c >= d.nCellsSolve) return;
   const int k = lane_id(), K = d.K, ns = d.ns;
@@ -4225,57 +4230,69 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p,
   const double eps = 1.e-20;
   const CellSten<ME> st = load_sten<ME>(p, c);
   const double invA = ld_uniform_f64(p.invAreaCell + c);
-  double so = p.scalars1[SIX(c, kc, is)];
-  double rzo = p.rho_zz1[o];
+  const double rzo_l = p.rho_zz1[o];
   const double wwa = p.wwAvg[ow], rdnw = p.rdzw[kc];
-  double wd = p.wdtn[ow];
   const double rhoref = advance_density ? p.rho_zz_int[o] : p.rho_zz2[o];
-  const double smx = p.s_max[o], smn = p.s_min[o];
-  double ft[ME], fu[ME];
+  // nq = 2: the pair's second scalar (is + 1) with the second scratch set (s2), after the first --
+  // the cell's own columns and stencil read once
+#pragma unroll 1
+  for (int q = 0; q < nq; ++q) {
+    const int iq = is + q;
+    double* wdtn = q ? s2.wdtn : p.wdtn;
+    const double* ftmp = q ? s2.flux_tmp : p.flux_tmp;
+    const double* fup = q ? s2.flux_upwind_tmp : p.flux_upwind_tmp;
+    double so = p.scalars1[SIX(c, kc, iq)];
+    double rzo = rzo_l;
+    double wd = wdtn[ow];
+    const double smx = (q ? s2.s_max : p.s_max)[o], smn = (q ? s2.s_min : p.s_min)[o];
+    double ft[ME], fu[ME];
 #pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    ft[i] = p.flux_tmp[(size_t)st.e[i] * K + kc];
-    fu[i] = p.flux_upwind_tmp[(size_t)st.e[i] * K + kc];
-  }
-  if (!act) {
-    so = 0.0;
-    rzo = 0.0;
-  }
-  const double som = up1(so);
-  double snew = so * rzo;
-  double fua = 0.0;  // flux_upwind_arr(k), k >= 2
-  if (act && k >= 1) fua = dt * (fmax(0.0, wwa) * som + fmin(0.0, wwa) * so);
-  const double fua_p = dn1(fua);
-  if (act && k <= K - 2) snew = snew - fua_p * rdnw;
-  if (k > K) wd = 0.0;
-  if (act && k >= 1) {
-    snew = snew + fua * rdnw;
-    wd = dt * wd - fua;
-  }
-  if (k <= K) p.wdtn[ow] = wd;
-  const double wdp = dn1(wd);
-  double sin_ = 0.0, sout = 0.0;
-  if (act) {
-    sin_ = -rdnw * (fmin(0.0, wdp) - fmax(0.0, wd));
-    sout = -rdnw * (fmax(0.0, wdp) - fmin(0.0, wd));
-  }
+    for (int i = 0; i < ME; ++i) {
+      ft[i] = ftmp[(size_t)st.e[i] * K + kc];
+      fu[i] = fup[(size_t)st.e[i] * K + kc];
+    }
+    if (!act) {
+      so = 0.0;
+      rzo = 0.0;
+    }
+    const double som = up1(so);
+    double snew = so * rzo;
+    double fua = 0.0;  // flux_upwind_arr(k), k >= 2
+    if (act && k >= 1) fua = dt * (fmax(0.0, wwa) * som + fmin(0.0, wwa) * so);
+    const double fua_p = dn1(fua);
+    if (act && k <= K - 2) snew = snew - fua_p * rdnw;
+    if (k > K) wd = 0.0;
+    if (act && k >= 1) {
+      snew = snew + fua * rdnw;
+      wd = dt * wd - fua;
+    }
+    if (k <= K) wdtn[ow] = wd;
+    const double wdp = dn1(wd);
+    double sin_ = 0.0, sout = 0.0;
+    if (act) {
+      sin_ = -rdnw * (fmin(0.0, wdp) - fmax(0.0, wd));
+      sout = -rdnw * (fmax(0.0, wdp) - fmin(0.0, wd));
+    }
 #pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    if (i < st.ne && act) {
-      const double sg = st.sg(i);
-      snew = snew - sg * fu[i] * invA;
-      sout = sout - fmax(0.0, sg * ft[i]) * invA;
-      sin_ = sin_ - fmin(0.0, sg * ft[i]) * invA;
+    for (int i = 0; i < ME; ++i) {
+      if (i < st.ne && act) {
+        const double sg = st.sg(i);
+        snew = snew - sg * fu[i] * invA;
+        sout = sout - fmax(0.0, sg * ft[i]) * invA;
+        sin_ = sin_ - fmin(0.0, sg * ft[i]) * invA;
+      }
+    }
+    if (act) {
+      double scale_factor = (smx * rhoref - snew) / (sin_ + eps);
+      const double scale_in = fmin(1.0, fmax(0.0, scale_factor));
+      scale_factor = (smn * rhoref - snew) / (sout - eps);
+      const double scale_out = fmin(1.0, fmax(0.0, scale_factor));
+      double* sa = q ? s2.scale_arr : p.scale_arr;
+      (q ? s2.scalar_old_copy : p.scalar_old_copy)[o] = snew;  // upwind solution (the reference's scalar_new)
+      sa[((size_t)c * 2 + 0) * K + k] = scale_in;
+      sa[((size_t)c * 2 + 1) * K + k] = scale_out;
     }
   }
-  if (!act) return;
-  double scale_factor = (smx * rhoref - snew) / (sin_ + eps);
-  const double scale_in = fmin(1.0, fmax(0.0, scale_factor));
-  scale_factor = (smn * rhoref - snew) / (sout - eps);
-  const double scale_out = fmin(1.0, fmax(0.0, scale_factor));
-  p.scalar_old_copy[o] = snew;  // upwind solution (the reference's scratch scalar_new)
-  p.scale_arr[((size_t)c * 2 + 0) * K + k] = scale_in;
-  p.scale_arr[((size_t)c * 2 + 1) * K + k] = scale_out;
 }
 
 template <int ME>
