@@ -1763,11 +1763,17 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
     for (int b = 0; b < nb; ++b) {
       const Dims& d = ctx->blk[b].d;
       const bool bt = batched(d), m6 = d.maxEdges == 6;
-      for (int q = 0; q < nq; ++q) {
-        const Ptrs& pq = q ? P1[b] : P[b];
-        if (!bt) LAUNCH(k_mono_bounds, d.nCellsSolve, d, pq, is + q, ctx->cf.coef_3rd_order);
-        else if (m6) LAUNCH(k_mono_bounds_b<6>, d.nCellsSolve, d, pq, is + q, ctx->cf.coef_3rd_order);
-        else LAUNCH(k_mono_bounds_b<7>, d.nCellsSolve, d, pq, is + q, ctx->cf.coef_3rd_order);
+      // the pair's second scratch set for the kernels that take both scalars in one launch
+      const MonoCell2 s2 = nq == 2 ? MonoCell2{P1[b].wdtn, P1[b].s_max, P1[b].s_min, P1[b].flux_tmp,
+                                               P1[b].flux_upwind_tmp, P1[b].scalar_old_copy, P1[b].scale_arr}
+                                   : MonoCell2{};
+      const double c3 = ctx->cf.coef_3rd_order;
+      if (!bt) {
+        for (int q = 0; q < nq; ++q) LAUNCH(k_mono_bounds, d.nCellsSolve, d, q ? P1[b] : P[b], is + q, c3);
+      } else if (m6) {
+        LAUNCH(k_mono_bounds_b<6>, d.nCellsSolve, d, P[b], is, c3, nq, s2);
+      } else {
+        LAUNCH(k_mono_bounds_b<7>, d.nCellsSolve, d, P[b], is, c3, nq, s2);
       }
       if (batched(d) && pair_layout(d)) {  // both scalars of the pair in one launch (the rows read once)
         const MonoFlux2 f2 = nq == 2 ? MonoFlux2{P1[b].flux_arr, P1[b].flux_upwind_tmp, P1[b].flux_tmp} : MonoFlux2{};
@@ -1777,9 +1783,6 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
         for (int q = 0; q < nq; ++q) LAUNCH(k_mono_edges1, d.nEdges, d, q ? P1[b] : P[b], is + q, dt);
       }
       if (bt) {  // both scalars of the pair in one launch (the cell's own columns read once)
-        const MonoCell2 s2 = nq == 2 ? MonoCell2{P1[b].wdtn, P1[b].s_max, P1[b].s_min, P1[b].flux_tmp,
-                                                 P1[b].flux_upwind_tmp, P1[b].scalar_old_copy, P1[b].scale_arr}
-                                     : MonoCell2{};
         if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2);
         else LAUNCH(k_mono_cells1_b<7>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2);
       } else {
@@ -1790,18 +1793,27 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
     else CHK(exchange(ctx, {{"scratch", "scale_arr", 1, 0x1u}}));
     for (int b = 0; b < nb; ++b) {
       const Dims& d = ctx->blk[b].d;
-      for (int q = 0; q < nq; ++q) {
-        const Ptrs& pq = q ? P1[b] : P[b];
-        if (!batched(d)) {
+      if (!batched(d)) {
+        for (int q = 0; q < nq; ++q) {
+          const Ptrs& pq = q ? P1[b] : P[b];
           LAUNCH(k_mono_edges2, d.nEdges, d, pq, dt);
           LAUNCH(k_mono_cells2, d.nCells, d, pq, is + q, ad);
-          continue;
         }
+        continue;
+      }
+      // each scalar's edge pass, then both scalars' cell pass in one launch (each scalar's pipeline
+      // touches only its own scalar and scratch set: the order between the two does not matter)
+      for (int q = 0; q < nq; ++q) {
+        const Ptrs& pq = q ? P1[b] : P[b];
         if (pair_layout(d)) LAUNCH_PE((k_mono_edges2_p<false>), (k_mono_edges2_p<true>), d.nEdges, d, pq, dt);
         else LAUNCH(k_mono_edges2, d.nEdges, d, pq, dt);
-        if (d.maxEdges == 6) LAUNCH(k_mono_cells2_b<6>, d.nCells, d, pq, is + q, ad);
-        else LAUNCH(k_mono_cells2_b<7>, d.nCells, d, pq, is + q, ad);
       }
+      const MonoCell2 s2 = nq == 2 ? MonoCell2{P1[b].wdtn, P1[b].s_max, P1[b].s_min, P1[b].flux_tmp,
+                                               P1[b].flux_upwind_tmp, P1[b].scalar_old_copy, P1[b].scale_arr}
+                                   : MonoCell2{};
+      double* fa2 = nq == 2 ? P1[b].flux_arr : nullptr;
+      if (d.maxEdges == 6) LAUNCH(k_mono_cells2_b<6>, d.nCells, d, P[b], is, ad, nq, s2, fa2);
+      else LAUNCH(k_mono_cells2_b<7>, d.nCells, d, P[b], is, ad, nq, s2, fa2);
     }
   }
   return MPAS_DYC_OK;

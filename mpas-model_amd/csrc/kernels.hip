@@ -4158,8 +4158,13 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_cells_b(Dims d, Ptrs 
   }
 }
 
+// the second scratch set (mono_slot1) of k_mono_bounds_b / k_mono_cells1_b / k_mono_cells2_b for the pair's second scalar
+struct MonoCell2 {
+  double *wdtn, *s_max, *s_min, *flux_tmp, *flux_upwind_tmp, *scalar_old_copy, *scale_arr;
+};
 template <int ME>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds_b(Dims d, Ptrs p, int is, double coef_3rd_order) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds_b(Dims d, Ptrs p, int is, double coef_3rd_order,
+                                                                  int nq = 1, MonoCell2 s2 = MonoCell2{}) {
   const int c = wave_elem(0);
   if (c >= d.nCellsSolve) return;
   const int k = lane_id(), K = d.K, ns = d.ns;
@@ -4171,52 +4176,53 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds_b(Dims d, Ptrs p,
   int cc[ME];
 #pragma unroll
   for (int i = 0; i < ME; ++i) cc[i] = p.cellsOnCell[(size_t)c * ME + i];
-  double so = p.scalars1[SIX(c, kc, is)], sn = p.scalars2[SIX(c, kc, is)];
   const double wwa = p.wwAvg[(size_t)c * K1 + kw];
   const double fnm = p.fzm[kc], fnp = p.fzp[kc];
-  double sv[ME];
+  // nq = 2: the pair's second scalar (is + 1) into the second scratch set (s2), after the first
+#pragma unroll 1
+  for (int q = 0; q < nq; ++q) {
+    const int iq = is + q;
+    double so = p.scalars1[SIX(c, kc, iq)], sn = p.scalars2[SIX(c, kc, iq)];
+    double sv[ME];
 #pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    const double v = p.scalars1[SIX(cc[i], kc, is)];
-    sv[i] = cc[i] < d.nCells ? v : 0.0;  // sold() of the reference's halo loop
-  }
-  if (!act) {
-    so = 0.0;
-    sn = 0.0;
-  }
-  const double som = up1(so), sop = dn1(so);
-  const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
-  double wdtn = 0.0;
-  if (k == 1 || k == K - 1) wdtn = wwa * (fnm * sn + fnp * snm1);
-  else if (k >= 2 && k <= K - 2) wdtn = flux3(snm2, snm1, sn, snp1, wwa, coef_3rd_order);
-  if (k <= K) p.wdtn[(size_t)c * K1 + k] = wdtn;
-  if (!act) return;
-  double smax, smin;
-  if (k == 0) {
-    smax = fmax(so, sop);
-    smin = fmin(so, sop);
-  } else if (k == K - 1) {
-    smax = fmax(so, som);
-    smin = fmin(so, som);
-  } else {
-    smax = fmax(fmax(som, so), sop);
-    smin = fmin(fmin(som, so), sop);
-  }
-#pragma unroll
-  for (int i = 0; i < ME; ++i) {
-    if (i < ne) {
-      smax = fmax(smax, sv[i]);
-      smin = fmin(smin, sv[i]);
+    for (int i = 0; i < ME; ++i) {
+      const double v = p.scalars1[SIX(cc[i], kc, iq)];
+      sv[i] = cc[i] < d.nCells ? v : 0.0;  // sold() of the reference's halo loop
     }
+    if (!act) {
+      so = 0.0;
+      sn = 0.0;
+    }
+    const double som = up1(so), sop = dn1(so);
+    const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
+    double wdtn = 0.0;
+    if (k == 1 || k == K - 1) wdtn = wwa * (fnm * sn + fnp * snm1);
+    else if (k >= 2 && k <= K - 2) wdtn = flux3(snm2, snm1, sn, snp1, wwa, coef_3rd_order);
+    if (k <= K) (q ? s2.wdtn : p.wdtn)[(size_t)c * K1 + k] = wdtn;
+    if (!act) continue;
+    double smax, smin;
+    if (k == 0) {
+      smax = fmax(so, sop);
+      smin = fmin(so, sop);
+    } else if (k == K - 1) {
+      smax = fmax(so, som);
+      smin = fmin(so, som);
+    } else {
+      smax = fmax(fmax(som, so), sop);
+      smin = fmin(fmin(som, so), sop);
+    }
+#pragma unroll
+    for (int i = 0; i < ME; ++i) {
+      if (i < ne) {
+        smax = fmax(smax, sv[i]);
+        smin = fmin(smin, sv[i]);
+      }
+    }
+    (q ? s2.s_max : p.s_max)[o] = smax;
+    (q ? s2.s_min : p.s_min)[o] = smin;
   }
-  p.s_max[o] = smax;
-  p.s_min[o] = smin;
 }
 
-// the second scratch set (mono_slot1) of k_mono_cells1_b for the pair's second scalar
-struct MonoCell2 {
-  double *wdtn, *s_max, *s_min, *flux_tmp, *flux_upwind_tmp, *scalar_old_copy, *scale_arr;
-};
 template <int ME>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p, int is, double dt, int advance_density,
                                                                   int nq = 1, MonoCell2 s2 = MonoCell2{}) {
@@ -4296,7 +4302,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p,
 }
 
 template <int ME>
-__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2_b(Dims d, Ptrs p, int is, int advance_density) {
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2_b(Dims d, Ptrs p, int is, int advance_density,
+                                                                  int nq = 1, MonoCell2 s2 = MonoCell2{},
+                                                                  double* flux_arr2 = nullptr) {
   const int c = wave_elem(0);
   if (c >= d.nCells) return;
   const int k = lane_id(), K = d.K, ns = d.ns;
@@ -4308,37 +4316,44 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells2_b(Dims d, Ptrs p,
   // the mask whether or not config_apply_lbcs is set, as at 2292, 3069 and 3435)
   if (p.bdyMaskCell[c] > N_SPEC_ZONE) return;
   if (c >= d.nCellsSolve) {  // halo cells: scalars_new = max(0, scalar_new) with scalar_new = input copy
-    if (act) p.scalars2[SIX(c, k, is)] = fmax(0.0, p.scalars2[SIX(c, k, is)]);
+    for (int q = 0; q < nq; ++q)
+      if (act) p.scalars2[SIX(c, k, is + q)] = fmax(0.0, p.scalars2[SIX(c, k, is + q)]);
     return;
   }
   const CellSten<ME> st = load_sten<ME>(p, c);
   const double invA = ld_uniform_f64(p.invAreaCell + c);
-  double si = p.scale_arr[((size_t)c * 2 + 0) * K + kc], so_ = p.scale_arr[((size_t)c * 2 + 1) * K + kc];
-  double wd = p.wdtn[ow];
-  const double sold_copy = p.scalar_old_copy[o];
   const double rhoref = advance_density ? p.rho_zz_int[o] : p.rho_zz2[o];
   const double rdzw = p.rdzw[kc];
-  double fa[ME];
+  // nq = 2: the pair's second scalar (is + 1) from the second scratch set (s2, flux_arr2), after the first
+#pragma unroll 1
+  for (int q = 0; q < nq; ++q) {
+    const double* sa = q ? s2.scale_arr : p.scale_arr;
+    const double* far = q ? flux_arr2 : p.flux_arr;
+    double si = sa[((size_t)c * 2 + 0) * K + kc], so_ = sa[((size_t)c * 2 + 1) * K + kc];
+    double wd = (q ? s2.wdtn : p.wdtn)[ow];
+    const double sold_copy = (q ? s2.scalar_old_copy : p.scalar_old_copy)[o];
+    double fa[ME];
 #pragma unroll
-  for (int i = 0; i < ME; ++i) fa[i] = p.flux_arr[(size_t)st.e[i] * K + kc];
-  if (!act) {
-    si = 0.0;
-    so_ = 0.0;
-  }
-  if (k > K) wd = 0.0;
-  const double sim = up1(si), som = up1(so_);
-  if (act && k >= 1) {
-    const double f = wd;
-    wd = fmax(0.0, f) * fmin(som, si) + fmin(0.0, f) * fmin(so_, sim);
-  }
-  const double wdp = dn1(wd);
-  if (!act) return;
-  double snew = sold_copy;
+    for (int i = 0; i < ME; ++i) fa[i] = far[(size_t)st.e[i] * K + kc];
+    if (!act) {
+      si = 0.0;
+      so_ = 0.0;
+    }
+    if (k > K) wd = 0.0;
+    const double sim = up1(si), som = up1(so_);
+    if (act && k >= 1) {
+      const double f = wd;
+      wd = fmax(0.0, f) * fmin(som, si) + fmin(0.0, f) * fmin(so_, sim);
+    }
+    const double wdp = dn1(wd);
+    if (!act) continue;
+    double snew = sold_copy;
 #pragma unroll
-  for (int i = 0; i < ME; ++i)
-    if (i < st.ne) snew = snew - st.sg(i) * fa[i] * invA;
-  snew = (snew + (-rdzw * (wdp - wd))) / rhoref;
-  p.scalars2[SIX(c, k, is)] = fmax(0.0, snew);
+    for (int i = 0; i < ME; ++i)
+      if (i < st.ne) snew = snew - st.sg(i) * fa[i] * invA;
+    snew = (snew + (-rdzw * (wdp - wd))) / rhoref;
+    p.scalars2[SIX(c, k, is + q)] = fmax(0.0, snew);
+  }
 }
 
 template <bool ODD = false>
