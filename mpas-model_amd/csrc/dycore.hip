@@ -160,6 +160,16 @@ struct mpas_dyc_ctx {
   int rank = 0, nranks = 1;
   ncclComm_t comm = nullptr;
   bool rccl_local = false;              // route block-to-block copies of this process through RCCL too
+  // MPAS_DYCORE_LOOPBACK=1 (timing only, tools/rank_emulation.py --exchange): the block of one rank
+  // of an N-way run, with its real lists to the other ranks, alone on one GPU; every message goes to
+  // this rank itself over a one-rank communicator (the halo receives this rank's own send data)
+  bool loopback = false;
+  // MPAS_DYCORE_LATE_ISSUE=1: a split-phase exchange is enqueued on the exchange stream at its
+  // exchange_wait, after the compute kernels it overlaps (the same dependencies; only the order in
+  // which a captured graph's nodes are created changes)
+  bool late_issue = false;
+  std::vector<XField> late_fs;
+  bool late_pending = false;
   bool fused_pack_enabled = true;       // MPAS_DYCORE_FUSED_PACK=0: pack kernel instead (A/B)
   bool plain_exchange = false;          // mpas_dyc_halo_exchange: no fused pack / unpack
   bool lbc = false;                     // config_apply_lbcs (mpas_dyc_set_lbc)
@@ -534,7 +544,7 @@ inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + WAVES_PER_BLOCK - 
 // ---------------------------------------------------------------------------
 // halo exchange (mpas_dmpar_exch_halo_field, framework/mpas_dmpar.F)
 // ---------------------------------------------------------------------------
-bool needs_exchange(const mpas_dyc_ctx* ctx) { return ctx->blk.size() > 1 || ctx->nranks > 1; }
+bool needs_exchange(const mpas_dyc_ctx* ctx) { return ctx->blk.size() > 1 || ctx->nranks > 1 || ctx->loopback; }
 
 // An exchange plan holds the fields' buffers, so its key names them: the time level and, per field,
 // which of the buffers that the step's rotations move it is (buffer index of block 0)
@@ -1074,6 +1084,29 @@ void set_last_key(mpas_dyc_ctx* ctx, const std::string& k) {
   ctx->last_key[n] = 0;
 }
 
+// The RCCL group of an exchange: one send and one receive per peer rank.  Loopback (timing
+// emulation): each peer's pair goes to this rank itself; a send to self and the receive that
+// matches it must have one size, so both move min(send, receive) doubles.
+int rccl_group(mpas_dyc_ctx* ctx, const XPlan& pl) {
+  NCCLCHK(ncclGroupStart());
+  if (ctx->loopback) {
+    for (const XMsg& m : pl.rsend)
+      for (const XMsg& r : pl.rrecv)
+        if (r.peer_rank == m.peer_rank) {
+          const size_t n = (size_t)std::min(m.count, r.count);
+          NCCLCHK(ncclSend(pl.sendbuf + m.off, n, ncclFloat64, ctx->rank, ctx->comm, ctx->stream));
+          NCCLCHK(ncclRecv(pl.recvbuf + r.off, n, ncclFloat64, ctx->rank, ctx->comm, ctx->stream));
+        }
+  } else {
+    for (const XMsg& m : pl.rsend)
+      NCCLCHK(ncclSend(pl.sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
+    for (const XMsg& m : pl.rrecv)
+      NCCLCHK(ncclRecv(pl.recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
+  }
+  NCCLCHK(ncclGroupEnd());
+  return MPAS_DYC_OK;
+}
+
 int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   if (!needs_exchange(ctx)) return MPAS_DYC_OK;
   const std::string key = plan_key(ctx, fs);
@@ -1103,12 +1136,7 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   if (!pl.rsend.empty() || !pl.rrecv.empty()) {
     set_last_key(ctx, key);
     CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
-    NCCLCHK(ncclGroupStart());
-    for (const XMsg& m : pl.rsend)
-      NCCLCHK(ncclSend(pl.sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
-    for (const XMsg& m : pl.rrecv)
-      NCCLCHK(ncclRecv(pl.recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
-    NCCLCHK(ncclGroupEnd());
+    CHK(rccl_group(ctx, pl));
     CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
   }
   if (pl.npost && !pl.fused_unpack)
@@ -1300,14 +1328,12 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
 bool split_phase(const mpas_dyc_ctx* ctx) {
   if (!needs_exchange(ctx)) return false;
   if (ctx->overlap >= 0) return ctx->overlap != 0;
-  return ctx->nranks > 1 || ctx->rccl_local;
+  return ctx->nranks > 1 || ctx->rccl_local || ctx->loopback;
 }
 
 // First half of a split-phase exchange: after everything queued on the compute stream,
 // the exchange stream packs, talks RCCL and unpacks; exchange_wait joins it back.
-int exchange_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
-  if (ctx->planning) return exchange(ctx, fs);
-  HIPCHK(hipEventRecord(ctx->xfork, ctx->stream));
+int issue_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   HIPCHK(hipStreamWaitEvent(ctx->xstream, ctx->xfork, 0));
   hipStream_t s = ctx->stream;
   ctx->stream = ctx->xstream;  // exchange() issues on ctx->stream
@@ -1320,8 +1346,23 @@ int exchange_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   return MPAS_DYC_OK;
 }
 
+int exchange_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
+  if (ctx->planning) return exchange(ctx, fs);
+  HIPCHK(hipEventRecord(ctx->xfork, ctx->stream));
+  if (ctx->late_issue) {
+    ctx->late_fs = fs;
+    ctx->late_pending = true;
+    return MPAS_DYC_OK;
+  }
+  return issue_async(ctx, fs);
+}
+
 int exchange_wait(mpas_dyc_ctx* ctx) {
   if (ctx->planning) return MPAS_DYC_OK;
+  if (ctx->late_pending) {
+    ctx->late_pending = false;
+    CHK(issue_async(ctx, ctx->late_fs));
+  }
   CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));  // the compute stream's work before the join
   HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->xjoin, 0));
   CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));  // ... completes once the join has
@@ -2375,12 +2416,7 @@ int warm_rccl(mpas_dyc_ctx* ctx) {
     pl.warmed = true;
     if (pl.rsend.empty() && pl.rrecv.empty()) continue;
     set_last_key(ctx, "warm_rccl " + kv.first);
-    NCCLCHK(ncclGroupStart());
-    for (const XMsg& m : pl.rsend)
-      NCCLCHK(ncclSend(pl.sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
-    for (const XMsg& m : pl.rrecv)
-      NCCLCHK(ncclRecv(pl.recvbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
-    NCCLCHK(ncclGroupEnd());
+    CHK(rccl_group(ctx, pl));
     // one group at a time: a group that never completes names its plan in last_key
     HIPCHK(hipStreamSynchronize(ctx->stream));
     any = true;
@@ -2499,6 +2535,9 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   g_mono_pairs = 1;
   if (const char* mp = getenv("MPAS_DYCORE_MONO_PAIRS")) g_mono_pairs = std::string(mp) != "0";
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
+  if (const char* lb = getenv("MPAS_DYCORE_LOOPBACK")) ctx->loopback = std::string(lb) == "1";
+  if (const char* li = getenv("MPAS_DYCORE_LATE_ISSUE")) ctx->late_issue = std::string(li) == "1";
+  if (const char* ov = getenv("MPAS_DYCORE_OVERLAP")) ctx->overlap = std::atoi(ov);
   for (auto& b : ctx->blk) {
     build_registry(b);
     for (auto& f : b.fields) {

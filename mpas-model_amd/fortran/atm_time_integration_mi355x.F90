@@ -78,6 +78,11 @@ module atm_time_integration
       integer(c_int32_t) :: k, index
    end type dyc_extreme
 
+   type, bind(C) :: dyc_plan_msg   ! mpas_dyc_plan_msg
+      integer(c_int32_t) :: point, direction, block, peer_rank, peer_block
+      integer(c_int64_t) :: count
+   end type dyc_plan_msg
+
    type, bind(C) :: dyc_summary
       integer(c_int32_t) :: flags
       real(c_double) :: w_min, w_max, u_min, u_max
@@ -89,6 +94,7 @@ module atm_time_integration
    integer(c_int32_t), parameter, private :: PHYS_TENDENCIES = 1, PHYS_RQVDYNTEN = 2, PHYS_MICROPHYSICS = 4
    integer(c_int32_t), parameter, private :: SUM_VEL = 1, SUM_DETAILED = 2, SUM_SCA = 4
    integer, parameter, private :: UP = 1, DOWN = 2
+   integer(c_int), parameter, private :: DYC_HOST_ONLY = -2   ! MPAS_DYC_HOST_ONLY
 
    interface
       integer(c_int) function mpas_dyc_create(dims, cfg, device, ctx) bind(C, name='mpas_dyc_create')
@@ -234,6 +240,15 @@ module atm_time_integration
          integer(c_int32_t), value :: apply
          real(c_double), value :: seconds_to_interval_end
       end function
+      integer(c_int) function mpas_dyc_plan_exchanges(ctx, nranks, rank, dt, msgs, cap, n_msgs, keys, keys_bytes, &
+            keys_len) bind(C, name='mpas_dyc_plan_exchanges')
+         import :: c_int, c_ptr, c_int32_t, c_int64_t, c_double
+         type(c_ptr), value :: ctx, msgs, keys
+         integer(c_int32_t), value :: nranks, rank
+         real(c_double), value :: dt
+         integer(c_int64_t), value :: cap, keys_bytes
+         integer(c_int64_t), intent(out) :: n_msgs, keys_len
+      end function
       type(c_ptr) function mpas_dyc_last_error(ctx) bind(C, name='mpas_dyc_last_error')
          import :: c_ptr
          type(c_ptr), value :: ctx
@@ -247,6 +262,9 @@ module atm_time_integration
    logical, save, private :: wait_every_step = .false.   ! MPAS_DYCORE_WAIT_EVERY_STEP=1 (diagnostics)
    integer(c_int32_t), save, private :: summary_flags = 0, physics_flags = 0
    real (kind=RKIND), save, private :: dt_init = 0.0_RKIND
+   ! atm_dycore_plan_exchanges: the domain context as host-only contexts (no GPU, no uploads)
+   logical, save, private :: plan_only = .false.
+   integer(c_int64_t), save, private :: plan_id_sum = 0
    ! regional runs: the host lbc pool's interval-end arrays last uploaded (mpas_atm_update_bdy_tend
    ! shifts the pool's time levels and reads new ones each time the lbc_in alarm rings), and a
    ! one-column probe block through which mpas_atm_get_bdy_state reports LBC_intv_end - now
@@ -376,6 +394,52 @@ module atm_time_integration
       if (c_associated(dyc)) call check(dyc, mpas_dyc_synchronize(dyc), 'mpas_dyc_synchronize')
    end subroutine atm_dycore_wait
 
+   ! This task's RCCL exchange plan, without a GPU: the domain context is built as the first
+   ! atm_srk3 builds it (create_domain_context: every block of domain%blocklist, the id broadcast
+   ! over dminfo%comm, set_block_lists with parinfo's lists), but as host-only contexts, with no
+   ! uploads and no model init; then mpas_dyc_plan_exchanges runs the planner over one model run's
+   ! exchange calls.  `path` gets one line 'id <n>' (a checksum of the broadcast id words), then
+   ! 'msg <point> <direction> <block> <peer_rank> <peer_block> <count>' per RCCL message and
+   ! 'key <plan key>' per exchange call, in issue order.  The context is destroyed afterwards.
+   subroutine atm_dycore_plan_exchanges(domain, dt, path)
+      type (domain_type), intent(inout) :: domain
+      real (kind=RKIND), intent(in) :: dt
+      character(len=*), intent(in) :: path
+      type(dyc_plan_msg), allocatable, target :: msgs(:)
+      character(kind=c_char), allocatable, target :: keys(:)
+      integer(c_int64_t) :: nm, kl
+      integer(c_int) :: ierr
+      integer :: u, i, j, nprocs, myrank
+      if (c_associated(dyc)) call fatal(dyc, 'atm_dycore_plan_exchanges after the domain context exists')
+      nprocs = domain % dminfo % nprocs
+      myrank = domain % dminfo % my_proc_id
+      plan_only = .true.
+      call create_domain_context(domain)
+      ierr = mpas_dyc_plan_exchanges(dyc, int(nprocs, c_int32_t), int(myrank, c_int32_t), real(dt, c_double), &
+                                     c_null_ptr, 0_c_int64_t, nm, c_null_ptr, 0_c_int64_t, kl)
+      allocate(msgs(max(nm, 1_c_int64_t)), keys(max(kl, 1_c_int64_t)))
+      call check(dyc, mpas_dyc_plan_exchanges(dyc, int(nprocs, c_int32_t), int(myrank, c_int32_t), real(dt, c_double), &
+                                              c_loc(msgs), nm, nm, c_loc(keys), kl, kl), 'mpas_dyc_plan_exchanges')
+      open(newunit=u, file=path, status='replace', action='write', recl=65536)
+      write(u, '(a,i0)') 'id ', plan_id_sum
+      do i = 1, int(nm)
+         write(u, '(a,5(1x,i0),1x,i0)') 'msg', msgs(i) % point, msgs(i) % direction, msgs(i) % block, &
+            msgs(i) % peer_rank, msgs(i) % peer_block, msgs(i) % count
+      end do
+      j = 1   ! keys: NUL-terminated text, one key per line
+      do i = 1, int(kl)
+         if (keys(i) == c_null_char .or. keys(i) == achar(10)) then
+            if (i > j) write(u, '(a,a)') 'key ', transfer(keys(j:i - 1), repeat(' ', i - j))
+            j = i + 1
+            if (keys(i) == c_null_char) exit
+         end if
+      end do
+      close(u)
+      call mpas_dyc_destroy(dyc)
+      dyc = c_null_ptr
+      plan_only = .false.
+   end subroutine atm_dycore_plan_exchanges
+
    ! Copy the host pools' current state (time level 1) and diagnostics into HBM, after the host
    ! changed them between steps (e.g. an analysis increment or a state read from a file).
    subroutine atm_dycore_from_host(domain)
@@ -500,7 +564,7 @@ module atm_time_integration
       nb = count_blocks(domain)
       nprocs = domain % dminfo % nprocs
       myrank = domain % dminfo % my_proc_id
-      if (nb == 1 .and. nprocs == 1 .and. c_associated(dyc_init)) then
+      if (nb == 1 .and. nprocs == 1 .and. c_associated(dyc_init) .and. .not. plan_only) then
          dyc = dyc_init
          dyc_init = c_null_ptr
       else
@@ -517,16 +581,30 @@ module atm_time_integration
             block => block % next
          end do
          call read_config(domain % blocklist % configs, c)
-         call check(dyc, mpas_dyc_create_blocks(int(nb, c_int32_t), d, c, device_index(), dyc), 'mpas_dyc_create_blocks')
+         if (plan_only) then
+            call check(dyc, mpas_dyc_create_blocks(int(nb, c_int32_t), d, c, DYC_HOST_ONLY, dyc), 'mpas_dyc_create_blocks')
+         else
+            call check(dyc, mpas_dyc_create_blocks(int(nb, c_int32_t), d, c, device_index(), dyc), 'mpas_dyc_create_blocks')
+         end if
          if (nprocs > 1) then
             ! RCCL id from task 0 to every task over the model's communicator (dminfo % comm)
             idbytes = mpas_dyc_comm_unique_id_bytes()
             allocate(idwords((idbytes + 3) / 4))
             idwords = 0
-            if (myrank == 0) call check(dyc, mpas_dyc_comm_unique_id(c_loc(idwords), idbytes), 'mpas_dyc_comm_unique_id')
+            if (myrank == 0) then
+               if (plan_only) then   ! no GPU: a known pattern stands for the id (RCCL's needs a device)
+                  idwords = [(7919 * ib + 13, ib = 1, size(idwords))]
+               else
+                  call check(dyc, mpas_dyc_comm_unique_id(c_loc(idwords), idbytes), 'mpas_dyc_comm_unique_id')
+               end if
+            end if
             call mpas_dmpar_bcast_ints(domain % dminfo, size(idwords), idwords)
-            call check(dyc, mpas_dyc_comm_init(dyc, c_loc(idwords), idbytes, int(nprocs, c_int32_t), &
-                                               int(myrank, c_int32_t)), 'mpas_dyc_comm_init')
+            if (plan_only) then
+               plan_id_sum = sum(int(idwords, c_int64_t) * [(int(ib, c_int64_t), ib = 1, size(idwords))])
+            else
+               call check(dyc, mpas_dyc_comm_init(dyc, c_loc(idwords), idbytes, int(nprocs, c_int32_t), &
+                                                  int(myrank, c_int32_t)), 'mpas_dyc_comm_init')
+            end if
          end if
          block => domain % blocklist
          ib = 0
@@ -535,10 +613,11 @@ module atm_time_integration
             call mpas_pool_get_subpool(block % structs, 'state', state)
             call mpas_pool_get_subpool(block % structs, 'diag', diag)
             call set_block_lists(block, ib, myrank, nprocs > 1, nb > 1)
-            call upload_block(dyc, ib, mesh, state, diag)
+            if (.not. plan_only) call upload_block(dyc, ib, mesh, state, diag)
             ib = ib + 1
             block => block % next
          end do
+         if (plan_only) return   ! atm_dycore_plan_exchanges: the lists are in, nothing runs
          if (coupled_init) then
             call check(dyc, mpas_dyc_init_diagnostics(dyc, real(dt_init, c_double)), 'mpas_dyc_init_diagnostics')
          else

@@ -26,6 +26,10 @@ program decomp_harness
    use mpas_log
    use mpas_block_decomp
    use mpas_block_creator
+#ifdef DROPIN_PLAN
+   use mpas_domain_routines, only : mpas_allocate_block
+   use atm_time_integration, only : atm_dycore_plan_exchanges
+#endif
    implicit none
 
    character(len=256) :: indir, outdir
@@ -117,10 +121,125 @@ program decomp_harness
    call dump_location('cell', indexToCellID_Block, nCellsSolveField)
    call dump_location('edge', indexToEdgeID_Block, nEdgesSolveField)
    call dump_location('vertex', indexToVertexID_Block, nVerticesSolveField)
+#ifdef DROPIN_PLAN
+   call plan_dropin()
+#endif
    write(0, '(a)') 'decomp_harness: done'
    call mpas_dmpar_finalize(domain % dminfo)
 
 contains
+
+#ifdef DROPIN_PLAN
+   ! Built as oracle/_ref/dropin_plan_harness (make -C oracle dropin_plan): the Fortran drop-in's
+   ! domain-context path on this task's blocks, without a GPU (tests/test_dropin_multitask.py).  The
+   ! blocks get what mpas_block_creator.F's finalize step gives them (:1000-1147): mpas_allocate_block,
+   ! the pool dimensions, and parinfo's lists, which are the index fields' send / recv / copy lists;
+   ! then the drop-in's atm_dycore_plan_exchanges writes <output_dir>/plan_task<rank>.txt.  The
+   ! optional namelist /plan/ in decomp.nml holds the vertical size, scalars, dt and the namelist
+   ! options that decide the exchange calls.
+   subroutine plan_dropin()
+      type (block_type), pointer :: b
+      type (field1dInteger), pointer :: fc, fe, fv, sc, se, sv
+      type (mpas_pool_type), pointer :: cfg, mesh, state
+      character(len=320) :: path
+      integer :: uu, ios
+      integer :: nVertLevels, maxEdges2, num_scalars, moist_end, config_time_integration_order, &
+                 config_number_of_sub_steps, config_dynamics_split_steps
+      logical :: config_split_dynamics_transport, config_scalar_advection, config_monotonic, config_positive_definite
+      real(kind=RKIND) :: dt
+      namelist /plan/ nVertLevels, maxEdges2, num_scalars, moist_end, dt, config_time_integration_order, &
+                      config_number_of_sub_steps, config_dynamics_split_steps, config_split_dynamics_transport, &
+                      config_scalar_advection, config_monotonic, config_positive_definite
+      nVertLevels = 26
+      maxEdges2 = 2 * maxEdges
+      num_scalars = 1
+      moist_end = 1
+      dt = 600.0_RKIND
+      config_time_integration_order = 2
+      config_number_of_sub_steps = 2
+      config_dynamics_split_steps = 3
+      config_split_dynamics_transport = .true.
+      config_scalar_advection = .true.
+      config_monotonic = .true.
+      config_positive_definite = .false.
+      open(newunit=uu, file=trim(indir)//'/decomp.nml', status='old')
+      read(uu, nml=plan, iostat=ios)
+      close(uu)
+      call mpas_pool_create_pool(cfg)
+      domain % configs => cfg
+      call mpas_pool_add_config_int(cfg, 'config_time_integration_order', config_time_integration_order)
+      call mpas_pool_add_config_int(cfg, 'config_number_of_sub_steps', config_number_of_sub_steps)
+      call mpas_pool_add_config_int(cfg, 'config_dynamics_split_steps', config_dynamics_split_steps)
+      call mpas_pool_add_config_int(cfg, 'config_number_rayleigh_damp_u_levels', 6)
+      call mpas_pool_add_config_logical(cfg, 'config_split_dynamics_transport', config_split_dynamics_transport)
+      call mpas_pool_add_config_logical(cfg, 'config_scalar_advection', config_scalar_advection)
+      call mpas_pool_add_config_logical(cfg, 'config_positive_definite', config_positive_definite)
+      call mpas_pool_add_config_logical(cfg, 'config_monotonic', config_monotonic)
+      call mpas_pool_add_config_logical(cfg, 'config_mix_full', .true.)
+      call mpas_pool_add_config_logical(cfg, 'config_rayleigh_damp_u', .true.)
+      call mpas_pool_add_config_char(cfg, 'config_horiz_mixing', '2d_smagorinsky')
+      call mpas_pool_add_config_real(cfg, 'config_h_mom_eddy_visc2', 0.0_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_h_mom_eddy_visc4', 0.0_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_v_mom_eddy_visc2', 0.0_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_h_theta_eddy_visc2', 0.0_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_h_theta_eddy_visc4', 0.0_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_v_theta_eddy_visc2', 0.0_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_len_disp', 120000.0_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_visc4_2dsmag', 0.05_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_del4u_div_factor', 10.0_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_coef_3rd_order', 0.25_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_smagorinsky_coef', 0.125_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_epssm', 0.1_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_smdiv', 0.1_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_apvm_upwinding', 0.5_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_mpas_cam_coef', 0.0_RKIND)
+      call mpas_pool_add_config_real(cfg, 'config_rayleigh_damp_u_timescale_days', 5.0_RKIND)
+      fc => indexToCellID_Block
+      fe => indexToEdgeID_Block
+      fv => indexToVertexID_Block
+      sc => nCellsSolveField
+      se => nEdgesSolveField
+      sv => nVerticesSolveField
+      do while (associated(fc))
+         b => fc % block
+         call mpas_allocate_block(nHalos, b, domain, b % blockID)
+         b % parinfo % cellsToSend => fc % sendList
+         b % parinfo % cellsToRecv => fc % recvList
+         b % parinfo % cellsToCopy => fc % copyList
+         b % parinfo % edgesToSend => fe % sendList
+         b % parinfo % edgesToRecv => fe % recvList
+         b % parinfo % edgesToCopy => fe % copyList
+         b % parinfo % verticesToSend => fv % sendList
+         b % parinfo % verticesToRecv => fv % recvList
+         b % parinfo % verticesToCopy => fv % copyList
+         call mpas_pool_create_pool(mesh)
+         call mpas_pool_add_subpool(b % structs, 'mesh', mesh)
+         call mpas_pool_create_pool(state)
+         call mpas_pool_add_subpool(b % structs, 'state', state)
+         call mpas_pool_add_dimension(mesh, 'nCells', sc % array(nHalos + 1))
+         call mpas_pool_add_dimension(mesh, 'nEdges', se % array(nHalos + 2))
+         call mpas_pool_add_dimension(mesh, 'nVertices', sv % array(nHalos + 2))
+         call mpas_pool_add_dimension(mesh, 'nCellsSolve', sc % array(1))
+         call mpas_pool_add_dimension(mesh, 'nEdgesSolve', se % array(1))
+         call mpas_pool_add_dimension(mesh, 'nVerticesSolve', sv % array(1))
+         call mpas_pool_add_dimension(mesh, 'nVertLevels', nVertLevels)
+         call mpas_pool_add_dimension(mesh, 'maxEdges', maxEdges)
+         call mpas_pool_add_dimension(mesh, 'maxEdges2', maxEdges2)
+         call mpas_pool_add_dimension(state, 'num_scalars', num_scalars)
+         call mpas_pool_add_dimension(state, 'moist_start', 1)
+         call mpas_pool_add_dimension(state, 'moist_end', moist_end)
+         call mpas_pool_add_dimension(state, 'index_qv', 1)
+         fc => fc % next
+         fe => fe % next
+         fv => fv % next
+         sc => sc % next
+         se => se % next
+         sv => sv % next
+      end do
+      write(path, '(a,a,i0,a)') trim(outdir), '/plan_task', domain % dminfo % my_proc_id, '.txt'
+      call atm_dycore_plan_exchanges(domain, dt, trim(path))
+   end subroutine plan_dropin
+#endif
 
    ! elements s..e of a file of d1 int32 per element
    subroutine read_i(name, a, d1, s, e)

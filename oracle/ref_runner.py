@@ -459,7 +459,16 @@ DECOMP_HARNESS = os.path.join(HERE, "_ref", "decomp_harness")
 MPIRUN = "/opt/conda/bin/mpirun"
 
 
-def run_reference_decomp(case: dict, part, nprocs: int = 1, timeout: int = 600) -> dict:
+def _nml(v):
+    if isinstance(v, bool):
+        return ".true." if v else ".false."
+    if isinstance(v, float):
+        return repr(v).replace("e", "d") if "e" in repr(v) else repr(v) + "d0"
+    return str(v)
+
+
+def run_reference_decomp(case: dict, part, nprocs: int = 1, timeout: int = 600, binary: str = DECOMP_HARNESS,
+                         plan: dict | None = None) -> dict:
     """mpas_block_decomp.F + mpas_block_creator.F on the case's mesh and cell partition ``part``
     (0-based block per cell, written as graph.info.part.N).  With ``nprocs`` > 1 the harness runs
     under mpirun, one task per block.  Returns {block id: {"<loc>_index": global 0-based ids in
@@ -480,7 +489,9 @@ def run_reference_decomp(case: dict, part, nprocs: int = 1, timeout: int = 600) 
         with open(os.path.join(ind, "decomp.nml"), "w") as f:
             f.write(f"&decomp\n nCells={case['nCells']}, nEdges={case['nEdges']}, nVertices={case['nVertices']},\n"
                     f" maxEdges={case['maxEdges']}, nblocks={nblocks}, nHalos=2\n/\n")
-        cmd = [DECOMP_HARNESS, ind, outd]
+            if plan is not None:
+                f.write("&plan\n" + ",\n".join(f" {k}={_nml(v)}" for k, v in plan.items()) + "\n/\n")
+        cmd = [binary, ind, outd]
         if nprocs > 1:
             cmd = [MPIRUN, "-np", str(nprocs)] + cmd
         r = subprocess.run(cmd, cwd=tmp, capture_output=True, text=True, timeout=timeout)
@@ -488,6 +499,9 @@ def run_reference_decomp(case: dict, part, nprocs: int = 1, timeout: int = 600) 
             raise RuntimeError(f"decomp_harness failed ({r.returncode}):\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}")
         out = {}
         for bdir in sorted(os.listdir(outd)):
+            if bdir.startswith("plan_task"):  # dropin_plan_harness: the drop-in's plan of each task
+                out.setdefault("plans", {})[int(bdir[len("plan_task"):-4])] = _read_plan(os.path.join(outd, bdir))
+                continue
             b = int(bdir[len("block"):])
             res = {}
             for fn in sorted(os.listdir(os.path.join(outd, bdir))):
@@ -508,3 +522,32 @@ def run_reference_decomp(case: dict, part, nprocs: int = 1, timeout: int = 600) 
         return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+# ---- the Fortran drop-in's multi-task plan (harness/decomp_harness.F90 -DDROPIN_PLAN, make -C oracle dropin_plan) ----
+DROPIN_PLAN_HARNESS = os.path.join(HERE, "_ref", "dropin_plan_harness")
+
+
+def _read_plan(path):
+    """A plan file of atm_dycore_plan_exchanges: (id checksum, messages as tuples (point, direction,
+    block, peer_rank, peer_block, count), plan keys)."""
+    ident, msgs, keys = None, [], []
+    with open(path) as f:
+        for line in f:
+            tag, _, rest = line.rstrip("\n").partition(" ")
+            if tag == "id":
+                ident = int(rest)
+            elif tag == "msg":
+                msgs.append(tuple(int(x) for x in rest.split()))
+            elif tag == "key":
+                keys.append(rest.strip())
+    return ident, msgs, keys
+
+
+def run_dropin_plan(case: dict, part, nprocs: int, plan: dict, timeout: int = 600) -> dict:
+    """The drop-in's domain-context path on `nprocs` MPI tasks without a GPU: the reference's
+    decomposition of `part` (as run_reference_decomp), each task's blocks handed to
+    atm_dycore_plan_exchanges.  Returns run_reference_decomp's dict plus "plans": {task: (id
+    checksum, messages, keys)}."""
+    cmd_binary = DROPIN_PLAN_HARNESS
+    return run_reference_decomp(case, part, nprocs=nprocs, timeout=timeout, binary=cmd_binary, plan=plan)

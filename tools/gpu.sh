@@ -15,6 +15,9 @@
 #   pmc              two rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE (gpurun_out/pmc_*)
 #   rank             tools/rank_emulation.py --parts 1 2 4 8
 #   prof8            rocprofv3 kernel trace of one rank's block of an 8-way split (rank emulation)
+#   rank8            every block of the 8-way split alone, compute only and then with its real exchange
+#                    lists looped back (tools/rank_emulation.py --exchange), one after the other
+#   prof8e           rocprofv3 kernel traces of rank8's two modes (gpurun_out/prof8c, gpurun_out/prof8e)
 #   blocks8          bench.py --blocks 8 --rccl-local (the 8-GPU decomposition on one device)
 #   prof8b           rocprofv3 kernel trace of blocks8 (gpurun_out/prof8b)
 #   ab8              blocks8 with the fused exchange packs / unpacks off and on (MPAS_DYCORE_FUSED_PACK), AB_ROUNDS rounds
@@ -45,6 +48,22 @@ step() {
          timeout -s KILL 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o write --output-format csv -- python3 bench.py $A > gpurun_out/pmc_write.log 2>&1 && echo "pmc done" ;;
     rank) timeout -k 10 400 python tools/rank_emulation.py --parts 1 2 4 8 > gpurun_out/rank.log 2>&1 && tail -4 gpurun_out/rank.log ;;
     prof8) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8 -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --steps 10 > gpurun_out/prof8.log 2>&1 && echo "prof8 done" ;;
+    rank8) timeout -k 10 400 python tools/rank_emulation.py --parts 1 8 --blocks all > gpurun_out/rank8.log 2>&1 &&
+           timeout -k 10 400 python tools/rank_emulation.py --parts 8 --blocks all --exchange >> gpurun_out/rank8.log 2>&1 &&
+           grep blocks gpurun_out/rank8.log ;;
+    rcclenv) rm -f gpurun_out/rcclenv.log
+           for E in "X=0" "NCCL_P2P_LL_THRESHOLD=1048576" "NCCL_P2P_LL_THRESHOLD=1048576 NCCL_NCHANNELS_PER_PEER=1" "NCCL_NCHANNELS_PER_PEER=4" "NCCL_PROTO=LL" ${RCCL_ENVS}; do
+             echo "== $E" >> gpurun_out/rcclenv.log
+             env $E timeout -k 10 300 python tools/rank_emulation.py --parts 8 --blocks 0 4 --exchange >> gpurun_out/rcclenv.log 2>&1 || return 1
+           done; grep -h "==\|blocks" gpurun_out/rcclenv.log | cut -c1-160 ;;
+    envsweep) rm -f gpurun_out/envsweep.log   # ENVS="A=1 B=2;C=3" (';' between variants), EMU_ARGS for rank_emulation.py
+           IFS=';' read -ra VS <<< "${ENVS:-X=0}"
+           for r in ${AB_ROUNDS:-1}; do for E in "${VS[@]}"; do
+             echo "== $E" >> gpurun_out/envsweep.log
+             env $E timeout -k 10 300 python tools/rank_emulation.py ${EMU_ARGS:---parts 8 --blocks 0 4 --exchange} >> gpurun_out/envsweep.log 2>&1 || return 1
+           done; done; grep -h "==\|blocks" gpurun_out/envsweep.log | cut -c1-160 ;;
+    prof8e) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8c -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks all --steps 3 > gpurun_out/prof8c.log 2>&1 &&
+            timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8e -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks all --steps 3 --exchange > gpurun_out/prof8e.log 2>&1 && echo "prof8e done" ;;
     blocks8) timeout -k 10 400 python bench.py --blocks 8 --rccl-local --steps 5 --warmup 2 $B > gpurun_out/blocks8.log 2>&1 && last gpurun_out/blocks8.log 300 ;;
     ab8) rm -f gpurun_out/ab8.log
         for r in ${AB_ROUNDS:-1 2 3}; do for F in 0 1; do

@@ -1,10 +1,19 @@
 #!/usr/bin/env python3
-"""Time one rank's share of an N-way decomposition on a single GPU (no exchanges).
+"""Time one rank's share of an N-way decomposition on a single GPU.
 
-Builds block 0 of an N-block SFC partition of the x1.<ncells> case and steps it
-alone: the time per dt is the compute a rank would spend at N GPUs, without the
-RCCL traffic (halo values go stale -- timing only, numerics are not checked).
-    python tools/rank_emulation.py [--ncells 163842] [--parts 2 4 8]
+Builds block i of an N-block SFC partition of the x1.<ncells> case and steps it alone: the time
+per dt is what a rank would spend at N GPUs.  Two modes (timing only, numerics are not checked):
+
+  compute only (default)  no exchange lists: the block runs as a one-block domain (halo values
+                          go stale, no split-phase launches, no pack / unpack, no RCCL);
+  --exchange              the block's real exchange lists to the other N-1 ranks, every message
+                          looped back to this rank over a one-rank RCCL communicator
+                          (MPAS_DYCORE_LOOPBACK=1): the split-phase interior / boundary launches,
+                          the fused pack / unpack epilogues, k_halo_copy and the RCCL kernels all
+                          run as on a rank of an N-GPU job; only the transfer over xGMI and the
+                          wait for the slowest peer are missing.
+
+    python tools/rank_emulation.py [--ncells 163842] [--parts 2 4 8] [--exchange] [--blocks all|0 3]
 """
 import argparse
 import json
@@ -19,37 +28,63 @@ sys.path.insert(0, os.path.join(ROOT, "mpas-model_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ncells", type=int, default=163842)
+    ap.add_argument("--levels", type=int, default=56)
     ap.add_argument("--parts", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--order", type=int, default=3)
+    ap.add_argument("--exchange", action="store_true", help="install the block's real lists, messages looped back")
+    ap.add_argument("--blocks", nargs="+", default=["0"], help="which blocks of each split ('all' = every one)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (what a rank without hipGraph costs)")
     a = ap.parse_args()
+    if a.exchange:
+        os.environ["MPAS_DYCORE_LOOPBACK"] = "1"  # read when a context is created
     from mpas_dycore import Dycore, decomp
     from mpas_dycore.cases import jw_case
-    case = jw_case(a.ncells, K=56, order=a.order)
+    case = jw_case(a.ncells, K=a.levels, order=a.order)
     dt = case["dt"]
-    res = {}
+    base = None
     for n in a.parts:
-        if n == 1:
-            dy = Dycore(case, device=0)
-        else:
-            (b,) = decomp.decompose(case, decomp.partition_sfc(case["nCells"], n), parts=[0])
-            dy = Dycore(b.case, device=0, solve=b.solve)
-        dy.init_diagnostics(dt)
-        dy.use_graph(not a.no_graph)
-        for i in range(2):
-            dy.atm_timestep(dt, i + 1)
-            dy.shift_time_levels()
-        dy.synchronize()
-        t0 = time.perf_counter()
-        for i in range(a.steps):
-            dy.atm_timestep(dt, i + 3)
-            dy.shift_time_levels()
-        dy.synchronize()
-        res[n] = (time.perf_counter() - t0) / a.steps * 1e3
-        dy.close()
-        print(json.dumps(dict(parts=n, graph=not a.no_graph, ms_per_dt=res[n], compute_speedup=res[a.parts[0]] / res[n])),
-              flush=True)
+        blocks = [0] if n == 1 else (list(range(n)) if a.blocks == ["all"] else [int(b) for b in a.blocks])
+        part = None if n == 1 else decomp.partition_sfc(case["nCells"], n)
+        times = []
+        for ib in blocks:
+            if n == 1:
+                dy = Dycore(case, device=0)
+            else:
+                (b,) = decomp.decompose(case, part, parts=[ib])
+                if a.exchange:
+                    # the other parts are ranks 1..n (this process is rank 0 of its one-rank communicator,
+                    # so no list names it and every message goes through RCCL)
+                    placement = {p: (p + 1, 0) for p in range(n)}
+                    dy = Dycore.from_blocks([b], device=0, placement=placement, rank=0, nranks=1,
+                                            comm_id=Dycore.comm_unique_id())
+                else:
+                    dy = Dycore(b.case, device=0, solve=b.solve)
+            dy.init_diagnostics(dt)
+            dy.use_graph(not a.no_graph)
+            for i in range(2):
+                dy.atm_timestep(dt, i + 1)
+                dy.shift_time_levels()
+            dy.synchronize()
+            t0 = time.perf_counter()
+            for i in range(a.steps):
+                dy.atm_timestep(dt, i + 3)
+                dy.shift_time_levels()
+            dy.synchronize()
+            ms = (time.perf_counter() - t0) / a.steps * 1e3
+            times.append(ms)
+            out = dict(parts=n, block=ib, exchange=a.exchange and n > 1, graph=not a.no_graph, ms_per_dt=ms)
+            if n > 1:
+                out["owned_cells"] = int(b.solve[0])
+                out["cells"] = int(b.case["nCells"])
+            dy.close()
+            print(json.dumps(out), flush=True)
+        mean = sum(times) / len(times)
+        if base is None:
+            base = mean
+        print(json.dumps(dict(parts=n, blocks=len(blocks), exchange=a.exchange and n > 1, ms_per_dt_mean=mean,
+                              ms_per_dt_max=max(times), ms_per_dt_sum=sum(times), compute_speedup=base / mean,
+                              speedup_slowest=base / max(times))), flush=True)
 
 
 if __name__ == "__main__":
