@@ -169,8 +169,14 @@ int mpas_dyc_set_lbc(mpas_dyc_ctx* ctx, int32_t apply, double seconds_to_interva
  * It reads what the init file holds, set beforehand with mpas_dyc_set_field: the connectivity,
  * dcEdge, dvEdge, zgrid and mesh.deriv_two (15, 2, nEdges+1), mesh.zb / zb3 (nVertLevels+1, 2,
  * nEdges+1), mesh.meshDensity, mesh.areaCell (nCells+1), mesh.areaTriangle (nVertices+1).
- * Bitwise the reference's arithmetic; x**0.25 and sin are correctly rounded (the reference's C library
- * is 1 ulp away for ~0.1 % of arguments).  Synchronous. */
+ * Every + - * / in the reference's order.  Two values are transcendental: meshDensity**0.25 and the
+ * damping layer's sin.  Set them too -- mesh.meshDensity_root4 (nCells+1: meshDensity**0.25),
+ * mesh.meshDensityEdge_root4 (nEdges+1: ((meshDensity(c1) + meshDensity(c2)) / 2)**0.25) and
+ * mesh.dss_sin (nVertLevels, nCells+1: sin(0.5 pi (z - config_zd) / (zt - config_zd)) where z >
+ * config_zd), from the C library as the compiled reference calls it -- and the outputs are the
+ * reference's bits.  Unset, they are computed on the device correctly rounded; the reference's C library
+ * is 1 ulp away for ~0.1 % of arguments, and meshScaling* then differ by up to 2 ulp there, dss by up to
+ * 4.  Cells of more than 10 edges are refused (MPAS_DYC_EINVAL).  Synchronous. */
 int mpas_dyc_model_init(mpas_dyc_ctx* ctx, int32_t h_scale_with_mesh, double config_zd, double config_xnutr);
 /* deriv_two as core_init_atmosphere computes it (mpas_atm_advection.F:21-394,
  * atm_initialize_advection_rk, polynomial_order = 2, on a sphere), into mesh.deriv_two (15, 2, nEdges+1)

@@ -163,11 +163,14 @@ struct mpas_dyc_ctx {
   // MPAS_DYCORE_LOOPBACK=1 (timing only, tools/rank_emulation.py --exchange): the block of one rank
   // of an N-way run, with its real lists to the other ranks, alone on one GPU; every message goes to
   // this rank itself over a one-rank communicator (the halo receives this rank's own send data)
-  bool loopback = false;
+  // (=2: each pair is a hipMemcpyAsync instead of RCCL, to separate RCCL's own cost)
+  int loopback = 0;
   // MPAS_DYCORE_LATE_ISSUE=1: a split-phase exchange is enqueued on the exchange stream at its
   // exchange_wait, after the compute kernels it overlaps (the same dependencies; only the order in
   // which a captured graph's nodes are created changes)
   bool late_issue = false;
+  // MPAS_DYCORE_OVERLAP_ALL=1: split the 642 and 876-887 exchanges even with nothing to overlap (A/B)
+  bool overlap_all = false;
   std::vector<XField> late_fs;
   bool late_pending = false;
   bool fused_pack_enabled = true;       // MPAS_DYCORE_FUSED_PACK=0: pack kernel instead (A/B)
@@ -394,11 +397,17 @@ void build_registry(Block& c) {
   add(c, "mesh", "meshDensity", L_CELL, 1);
   add(c, "mesh", "areaCell", L_CELL, 1);
   add(c, "mesh", "areaTriangle", L_VERTEX, 1);
+  // optional: the C library's values of the two transcendental functions of the precompute, which the
+  // caller computes as the compiled reference does (meshDensity**0.25 per cell and per edge midpoint,
+  // the damping layer's sin per cell and level); unset, the device uses correctly rounded ones
+  add(c, "mesh", "meshDensity_root4", L_CELL, 1);
+  add(c, "mesh", "meshDensityEdge_root4", L_EDGE, 1);
+  add(c, "mesh", "dss_sin", L_CELL, K);
   // inputs of the reconstruction coefficients (mpas_dyc_init_reconstruct), allocated when set
   for (const char* n : {"xCell", "yCell", "zCell"}) add(c, "mesh", n, L_CELL, 1);
   for (const char* n : {"xEdge", "yEdge", "zEdge"}) add(c, "mesh", n, L_EDGE, 1);
   for (const char* n : {"deriv_two", "zb", "zb3", "meshDensity", "areaCell", "areaTriangle", "xCell", "yCell", "zCell",
-                        "xEdge", "yEdge", "zEdge"})
+                        "xEdge", "yEdge", "zEdge", "meshDensity_root4", "meshDensityEdge_root4", "dss_sin"})
     c.fields[c.by_name[std::string("mesh.") + n]].lazy = true;
   // the maxEdges- and maxEdges2-strided mesh arrays (pack_mesh)
   for (const char* n : {"edgesOnCell", "cellsOnCell", "verticesOnCell", "kiteForCell", "coeffs_reconstruct",
@@ -867,6 +876,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   merge_by_rank(pl.rsend, pre_off);
   merge_by_rank(pl.rrecv, post_off);
   if (ctx->host_only) return MPAS_DYC_OK;  // the dry run keeps the message lists only
+  if (ctx->loopback) stotal = rtotal = stotal + rtotal;  // rccl_group's loopback pairs stay inside
   if (stotal) HIPCHK(hipMalloc(&pl.sendbuf, stotal * sizeof(double)));
   // 256 B of slack: a fused unpack (ld_pp) reads the two levels of its lane's pair, one past the
   // last column at an odd K
@@ -1090,13 +1100,22 @@ void set_last_key(mpas_dyc_ctx* ctx, const std::string& k) {
 int rccl_group(mpas_dyc_ctx* ctx, const XPlan& pl) {
   NCCLCHK(ncclGroupStart());
   if (ctx->loopback) {
-    for (const XMsg& m : pl.rsend)
-      for (const XMsg& r : pl.rrecv)
-        if (r.peer_rank == m.peer_rank) {
-          const size_t n = (size_t)std::min(m.count, r.count);
-          NCCLCHK(ncclSend(pl.sendbuf + m.off, n, ncclFloat64, ctx->rank, ctx->comm, ctx->stream));
-          NCCLCHK(ncclRecv(pl.recvbuf + r.off, n, ncclFloat64, ctx->rank, ctx->comm, ctx->stream));
-        }
+    // one self pair per peer rank of max(send, receive) doubles (a peer this rank only sends to or
+    // only receives from gets one too); build_plan sizes both buffers for it
+    std::map<int, std::pair<const XMsg*, const XMsg*>> peers;
+    for (const XMsg& m : pl.rsend) peers[m.peer_rank].first = &m;
+    for (const XMsg& m : pl.rrecv) peers[m.peer_rank].second = &m;
+    for (const auto& kv : peers) {
+      const XMsg *sm = kv.second.first, *rm = kv.second.second;
+      const size_t n = (size_t)std::max(sm ? sm->count : 0, rm ? rm->count : 0);
+      if (ctx->loopback == 2) {
+        HIPCHK(hipMemcpyAsync(pl.recvbuf + (rm ? rm->off : 0), pl.sendbuf + (sm ? sm->off : 0), n * sizeof(double),
+                              hipMemcpyDeviceToDevice, ctx->stream));
+        continue;
+      }
+      NCCLCHK(ncclSend(pl.sendbuf + (sm ? sm->off : 0), n, ncclFloat64, ctx->rank, ctx->comm, ctx->stream));
+      NCCLCHK(ncclRecv(pl.recvbuf + (rm ? rm->off : 0), n, ncclFloat64, ctx->rank, ctx->comm, ctx->stream));
+    }
   } else {
     for (const XMsg& m : pl.rsend)
       NCCLCHK(ncclSend(pl.sendbuf + m.off, (size_t)m.count, ncclFloat64, m.peer_rank, ctx->comm, ctx->stream));
@@ -2040,6 +2059,14 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   // kept after stage 1 only.  Not with LBCs (the reference recomputes h_divergence from the
   // overwritten ru).
   bool hdiv_prev = false;  // the previous stage's w recovery computed this stage's h_divergence
+  // split-phase exchanges that would have work to overlap: 642 when smlstep_pert is not fused into
+  // k_dyn_cells3_r on some block, 876-887 when some block recovers its owned elements separately
+  bool sml_fused = true, rec_overlap = false;
+  for (const auto& b : ctx->blk) {
+    sml_fused = sml_fused && fuse_smlstep(b.d);
+    rec_overlap = rec_overlap || !fused_recover(b.d) || !fused_recover_edges(b.d);
+  }
+  if (ctx->overlap_all) sml_fused = false, rec_overlap = true;
   EACHV(Ppre, vert_imp_coefs(ctx, d, p, rk_sub_timestep[0]));    // 476-510 of dynamics substep 1
   for (int dynamics_substep = 1; dynamics_substep <= dynamics_split; ++dynamics_substep) {
     // 513 (exner): carried by the step-start exchange and by the 1282-1297 exchange below
@@ -2065,10 +2092,15 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
         EACHV(PS, dyn_tend(ctx, d, p, rk_step, dt, 0, hdiv_prev && batched(d), last_stage, tpk(ib_)));  // 561-630
       }
       const double dts = rk_sub_timestep[rk_step - 1];
-      if (split) {  // 642 | 644-678: interior cells overlap the tend_u exchange
+      if (split && !sml_fused) {  // 642 | 644-678: interior cells overlap the tend_u exchange
         CHK(exchange_async(ctx, xtu));
         EACHV(PS, smlstep_pert(ctx, d, p, 1));
         CHK(exchange_wait(ctx));
+        EACHV(PS, smlstep_pert(ctx, d, p, 2, tup(ib_)));
+      } else if (split) {
+        // k_dyn_cells3_r already did the interior cells' smlstep: nothing would overlap the exchange,
+        // so it blocks (a fork and a join of the exchange stream cost more than they could hide)
+        CHK(exchange(ctx, xtu));
         EACHV(PS, smlstep_pert(ctx, d, p, 2, tup(ib_)));
       } else {
         CHK(exchange(ctx, xtu));                                  // 642
@@ -2155,13 +2187,16 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
       const double rdt = rk_timestep[rk_step - 1];
       if (split) {
         // 889-1185: owned cells and interior edges overlap the 876-887 exchange; once every
-        // owned u is final, the u exchange (988) overlaps the w recovery, which does not read u
-        CHK(exchange_async(ctx, xrec));
+        // owned u is final, the u exchange (988) overlaps the w recovery, which does not read u.
+        // When the last cell phase and damping recovered those already (fused_recover,
+        // fused_recover_edges) nothing is left to overlap and the exchange blocks.
+        if (rec_overlap) CHK(exchange_async(ctx, xrec));
+        else CHK((exchange)(ctx, xrec));
         // owned cells: recovered by the last sub-step's cell phase (fused_recover) or here
         EACH(if (!fused_recover(d)) LAUNCH(k_recover_cells1, d.nCells + 1, d, p, rdt, invNs, rk_step, 1, 0));
         // edges with two owned cells: recovered by the last damping (fused_recover_edges) or here
         EACH(if (!fused_recover_edges(d)) LAUNCH(k_recover_edges, d.nEdges, d, p, invNs, 1, XUnpack{}, upk(ib_)));
-        CHK(exchange_wait(ctx));
+        if (rec_overlap) CHK(exchange_wait(ctx));
         EACH(LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2, d.nCellsSolve,
                     ruc(ib_)));
         EACH(LAUNCH(k_recover_edges, d.n_bnd_edges, d, p, invNs, 2, rue(ib_), upk(ib_)));  // phase 2: bnd_edges
@@ -2535,8 +2570,9 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   g_mono_pairs = 1;
   if (const char* mp = getenv("MPAS_DYCORE_MONO_PAIRS")) g_mono_pairs = std::string(mp) != "0";
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
-  if (const char* lb = getenv("MPAS_DYCORE_LOOPBACK")) ctx->loopback = std::string(lb) == "1";
+  if (const char* lb = getenv("MPAS_DYCORE_LOOPBACK")) ctx->loopback = std::atoi(lb);
   if (const char* li = getenv("MPAS_DYCORE_LATE_ISSUE")) ctx->late_issue = std::string(li) == "1";
+  if (const char* oa = getenv("MPAS_DYCORE_OVERLAP_ALL")) ctx->overlap_all = std::string(oa) == "1";
   if (const char* ov = getenv("MPAS_DYCORE_OVERLAP")) ctx->overlap = std::atoi(ov);
   for (auto& b : ctx->blk) {
     build_registry(b);
@@ -2625,6 +2661,9 @@ void* mpas_dyc_block_field_device_ptr(mpas_dyc_ctx* ctx, int32_t block, const ch
   if (!b || !pool || !name) return nullptr;
   Field* f = find(*b, pool, name);
   if (!f) return nullptr;
+  // the kernels read packed copies of the maxEdges-strided mesh fields (pack_mesh) and zb_cell / zb3_cell
+  // through zb_p / zb_m: a caller may write through the pointer, so the next step packs them again
+  if (f->me || (f->pool == "mesh" && (f->name == "zb_cell" || f->name == "zb3_cell"))) ctx->bnd_ready = false;
   return f->buf[slot_of(ctx, *f, time_level)];
 }
 
@@ -3163,7 +3202,19 @@ int mpas_dyc_model_init(mpas_dyc_ctx* ctx, int32_t h_scale_with_mesh, double con
     // the declared-stride images (buf), not the kernels' packed copies: pack_mesh redoes those after
     auto I = [&](const char* n) { return (int*)find(b, "mesh", n)->buf[0]; };
     auto R = [&](const char* n) { return (double*)find(b, "mesh", n)->buf[0]; };
+    // k_mi_adv_compression keeps a cell's stencil list (at most 2 + 2 (maxEdges - 1) cells) in 20 slots and
+    // reads deriv_two's 15 weights per side: cells of more than 10 edges are refused here
+    int maxdeg = 0;
+    for (int c = 0; c < b.d.nCells && c < (int)b.h_noc.size(); ++c) maxdeg = std::max(maxdeg, b.h_noc[c]);
+    if ((int)b.h_noc.size() < b.d.nCells || maxdeg > 10) {
+      ctx->err = "mpas_dyc_model_init: nEdgesOnCell " +
+                 ((int)b.h_noc.size() < b.d.nCells ? std::string("not set") : "max " + std::to_string(maxdeg) + " > 10");
+      return MPAS_DYC_EINVAL;
+    }
     MInit m{};
+    m.root4_cell = R("meshDensity_root4");
+    m.root4_edge = R("meshDensityEdge_root4");
+    m.dss_sin = R("dss_sin");
     m.nEdgesOnCell = I("nEdgesOnCell");
     m.edgesOnCell = I("edgesOnCell");
     m.cellsOnCell = I("cellsOnCell");

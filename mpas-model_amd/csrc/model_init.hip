@@ -8,10 +8,13 @@
 //
 // Arithmetic follows the Fortran statement by statement (same operands, same order, fp64, no
 // contraction).  Two functions go beyond + - * / sqrt: x**0.25 (a runtime pow in the compiled
-// reference) and sin.  Here they are correctly rounded (cr_root4, cr_sin below, both proved against a
-// 60-digit evaluation in tests/test_gpu_model_init.py); the reference's C library rounds them correctly for
-// all but ~0.1 % of arguments and is 1 ulp away there.  x**0.75 is sqrt(x) * sqrt(sqrt(x)), as the
-// reference build lowers it (init_atm._pow).
+// reference) and sin.  The caller may hand in the C library's values (mesh.meshDensity_root4,
+// meshDensityEdge_root4, dss_sin: what the compiled reference gets, so the outputs are its bits --
+// Dycore(model_init="device") does); without them they are computed here correctly rounded (cr_root4,
+// cr_sin below, both proved against a 60-digit evaluation in tests/test_gpu_model_init.py), and the
+// reference's C library, which rounds them correctly for all but ~0.1 % of arguments, is 1 ulp away
+// there: meshScalingDel2 / RegionalCell / RegionalEdge then differ by up to 2 ulp, dss by up to 4.
+// x**0.75 is sqrt(x) * sqrt(sqrt(x)), as the reference build lowers it (init_atm._pow).
 // Included by dycore.hip.
 #pragma once
 #include "dycore.h"
@@ -106,6 +109,9 @@ struct MInit {
   int *kiteForCell, *nAdvCellsForEdge, *advCellsForEdge;
   double *adv_coefs, *adv_coefs_3rd;
   double *meshScalingDel2, *meshScalingDel4, *meshScalingRegionalCell, *meshScalingRegionalEdge, *dss;
+  // the caller's C-library values (mesh.meshDensity_root4, meshDensityEdge_root4, dss_sin), or nullptr:
+  // correctly rounded ones are computed here
+  const double *root4_cell, *root4_edge, *dss_sin;
   int nCells, nEdges, nVertices, K, maxEdges;  // maxEdges: the declared stride
 };
 
@@ -243,7 +249,7 @@ __global__ void k_mi_mesh_scaling(MInit m, int scale) {
     if (scale) {
       const int c1 = m.cellsOnEdge[2 * i], c2 = m.cellsOnEdge[2 * i + 1];
       const double x = (m.meshDensity[c1] + m.meshDensity[c2]) / 2.0;
-      s2 = 1.0 / cr_root4(x);
+      s2 = 1.0 / (m.root4_edge ? m.root4_edge[i] : cr_root4(x));
       s4 = 1.0 / (sqrt(x) * sqrt(sqrt(x)));
       sr = s2;
     }
@@ -251,7 +257,8 @@ __global__ void k_mi_mesh_scaling(MInit m, int scale) {
     m.meshScalingDel4[i] = s4;
     m.meshScalingRegionalEdge[i] = sr;
   }
-  if (i < m.nCells) m.meshScalingRegionalCell[i] = scale ? 1.0 / cr_root4(m.meshDensity[i]) : 1.0;
+  if (i < m.nCells)
+    m.meshScalingRegionalCell[i] = scale ? 1.0 / (m.root4_cell ? m.root4_cell[i] : cr_root4(m.meshDensity[i])) : 1.0;
 }
 
 // atm_compute_damping_coefs, 1105-1116: one thread per (cell, level)
@@ -265,9 +272,9 @@ __global__ void k_mi_damping(MInit m, double zd, double xnutr) {
   const double z = 0.5 * (m.zgrid[(size_t)c * K1 + k] + m.zgrid[(size_t)c * K1 + k + 1]);
   double v = 0.0;
   if (z > zd) {
-    const double s = cr_sin(0.5 * pii * (z - zd) / (zt - zd));
+    const double s = m.dss_sin ? m.dss_sin[(size_t)c * m.K + k] : cr_sin(0.5 * pii * (z - zd) / (zt - zd));
     v = xnutr * (s * s);
-    v = v / cr_root4(m.meshDensity[c]);
+    v = v / (m.root4_cell ? m.root4_cell[c] : cr_root4(m.meshDensity[c]));
   }
   m.dss[(size_t)c * m.K + k] = v;
 }

@@ -154,11 +154,12 @@ class Dycore:
         if rc != 0 or not h.value:
             raise DycoreError(f"mpas_dyc_create_blocks failed ({rc})")
         self.h = h
-        if model_init not in ("host", "device"):
-            raise ValueError("model_init: 'host' (the case's precomputed arrays) or 'device' (mpas_dyc_model_init)")
+        if model_init not in ("host", "device", "device_cr"):
+            raise ValueError("model_init: 'host' (the case's precomputed arrays), 'device' (mpas_dyc_model_init with "
+                             "the C library's x**0.25 / sin from the host) or 'device_cr' (correctly rounded on the device)")
         for ib, c in enumerate(cases):
-            self._upload_case(c, ib, device_init=model_init == "device")
-        if model_init == "device":
+            self._upload_case(c, ib, device_init=model_init != "host", host_libm=model_init == "device")
+        if model_init != "host":
             cfg = self.case["config"]
             self._check(self.lib.mpas_dyc_model_init(self.h, int(bool(cfg.get("config_h_ScaleWithMesh", True))),
                                                      float(cfg["config_zd"]), float(cfg["config_xnutr"])),
@@ -272,7 +273,7 @@ class Dycore:
         self._check(self.lib.mpas_dyc_halo_exchange(self.h, pool.encode(), name.encode(), time_level, mask),
                     f"halo_exchange {pool}.{name}")
 
-    def _upload_case(self, case: dict, block: int = 0, device_init: bool = False):
+    def _upload_case(self, case: dict, block: int = 0, device_init: bool = False, host_libm: bool = True):
         """device_init: leave atm_mpas_init_block's precompute to the device (mpas_dyc_model_init) --
         upload its inputs (the init file's deriv_two, zb, zb3, meshDensity, areaCell, areaTriangle)
         instead of the case's precomputed arrays."""
@@ -280,6 +281,13 @@ class Dycore:
         if device_init:
             for name in MODEL_INIT_IN + (RECONSTRUCT_IN if device_rec else ()):
                 self.set_raw("mesh", name, to_fortran(case, name), block=block)
+            # the C library's meshDensity**0.25 and damping-layer sin, as the compiled reference gets them
+            # (init_atm.model_init_libm): the device's precompute then has the reference's bits
+            if host_libm:
+                from .init_atm import model_init_libm
+                lm = model_init_libm(case, case["config"])
+                for name, a in lm.items():
+                    self.set_raw("mesh", name, to_fortran({**case, name: a}, name), block=block)
         for name in case:
             if name in _SKIP or (device_init and name in MODEL_INIT_OUT) or (device_rec and name == "coeffs_reconstruct"):
                 continue

@@ -13,12 +13,13 @@ LOCATION = {}
 for n in ("latCell lonCell xCell yCell zCell areaCell invAreaCell meshDensity nEdgesOnCell indexToCellID "
           "edgesOnCell cellsOnCell verticesOnCell kiteForCell edgesOnCell_sign defc_a defc_b zgrid zz dss "
           "zb_cell zb3_cell theta rho scalars rho_base theta_base w coeffs_reconstruct t_init "
-          "bdyMaskCell nearestRelaxationCell meshScalingRegionalCell specZoneMaskCell").split():
+          "bdyMaskCell nearestRelaxationCell meshScalingRegionalCell specZoneMaskCell "
+          "meshDensity_root4 dss_sin").split():
     LOCATION[n] = "cell"
 for n in ("latEdge lonEdge xEdge yEdge zEdge dcEdge dvEdge invDcEdge invDvEdge angleEdge fEdge "
           "meshScalingDel2 meshScalingDel4 nEdgesOnEdge nAdvCellsForEdge cellsOnEdge verticesOnEdge "
           "edgesOnEdge advCellsForEdge weightsOnEdge adv_coefs adv_coefs_3rd zxu deriv_two zb zb3 u "
-          "bdyMaskEdge meshScalingRegionalEdge specZoneMaskEdge").split():
+          "bdyMaskEdge meshScalingRegionalEdge specZoneMaskEdge meshDensityEdge_root4").split():
     LOCATION[n] = "edge"
 for n in ("latVertex lonVertex xVertex yVertex zVertex areaTriangle invAreaTriangle fVertex "
           "cellsOnVertex edgesOnVertex edgesOnVertex_sign kiteAreasOnVertex").split():

@@ -125,8 +125,19 @@ try:
         getattr(_HOST, _f).argtypes = [_C.c_void_p, _C.c_void_p, _C.c_int64]
     _HOST.hl_pow_s.argtypes = [_C.c_void_p, _C.c_double, _C.c_void_p, _C.c_int64]
     _HOST.hl_sincos.argtypes = [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_int64]
-except OSError:
+except (OSError, AttributeError) as _e:  # not built, or a stale build without one of the helpers
+    import warnings as _w
+    _w.warn(f"mpas_dycore.init_atm: csrc/libmpas_host.so unusable ({_e}); the case builder falls back to "
+            "numpy / math, whose sin, cos, exp, tan and pow differ from the compiled reference's C library in "
+            "the last bit for some arguments (the JW state, deriv_two and defc are then not the reference's "
+            "bits; rebuild with __graft_entry__.build())", RuntimeWarning, stacklevel=2)
     _HOST = None
+
+
+def host_libm_loaded() -> bool:
+    """True when the case builder uses the C library's functions (csrc/libmpas_host.so), i.e. its
+    initial states are the compiled reference's bits (cases record it as case["host_libm"])."""
+    return _HOST is not None
 
 
 def _sincos(x):
@@ -652,6 +663,24 @@ def build_case(m: dict, K: int = 26, ns: int = 1, moist: bool = False, config: d
     return model_init(out, cfg)
 
 
+def model_init_libm(m: dict, cfg: dict) -> dict:
+    """The transcendental values of the model-init precompute, as the compiled reference gets them
+    from the C library: meshDensity**0.25 per cell (atm_compute_damping_coefs 1113, mesh scaling 979)
+    and per edge midpoint (meshScalingDel2, 963), and sin of the damping layer's argument per cell and
+    level (1111; 0 where z <= config_zd).  model_init uses them, and mpas_dyc_model_init takes them
+    (mesh.meshDensity_root4, meshDensityEdge_root4, dss_sin) so the device's precompute has the same
+    bits."""
+    zgrid, md = np.asarray(m["zgrid"]), np.asarray(m["meshDensity"])
+    coe = np.asarray(m["cellsOnEdge"])
+    zt_c = zgrid[:, m["nVertLevels"]]
+    zmid = 0.5 * (zgrid[:, :-1] + zgrid[:, 1:])
+    zd = cfg["config_zd"]
+    arg = 0.5 * PII * (zmid - zd) / (zt_c[:, None] - zd)
+    return {"meshDensity_root4": _pow(md, 0.25 * 1.0),
+            "meshDensityEdge_root4": _pow((md[coe[:, 0]] + md[coe[:, 1]]) / 2.0, 0.25),
+            "dss_sin": np.where(zmid > zd, np.sin(arg), 0.0)}
+
+
 def model_init(out: dict, cfg: dict) -> dict:
     """The dycore's model-init precompute on the fields of an MPAS input stream
     (mpas_atm_core.F:311-463 and 927-1288): edge signs, zb_cell/zb3_cell, kiteForCell,
@@ -701,15 +730,15 @@ def model_init(out: dict, cfg: dict) -> dict:
         defc_a, defc_b = compute_defc(m)
 
     # damping (mpas_atm_core.F:1105-1116)
-    zt_c = zgrid[:, nz1]
+    lm = model_init_libm(m, cfg)
     zmid = 0.5 * (zgrid[:, :-1] + zgrid[:, 1:])
     zd, xnutr = cfg["config_zd"], cfg["config_xnutr"]
-    sn = np.sin(0.5 * PII * (zmid - zd) / (zt_c[:, None] - zd))
+    sn = lm["dss_sin"]
     dss = np.where(zmid > zd, xnutr * (sn * sn), 0.0)
-    dss = np.where(zmid > zd, dss / _pow(m["meshDensity"], 0.25 * 1.0)[:, None], 0.0)
+    dss = np.where(zmid > zd, dss / lm["meshDensity_root4"][:, None], 0.0)
     md = m["meshDensity"]
     if cfg["config_h_ScaleWithMesh"]:   # mesh scaling (927-984)
-        msd2 = 1.0 / _pow((md[c1] + md[c2]) / 2.0, 0.25)
+        msd2 = 1.0 / lm["meshDensityEdge_root4"]
         msd4 = 1.0 / _pow((md[c1] + md[c2]) / 2.0, 0.75)
     else:
         msd2 = np.ones(nE)

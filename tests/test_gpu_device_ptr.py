@@ -57,3 +57,37 @@ def test_pointers_requeried_after_each_step_hold_the_field(moist_case):
     moved = [k for k in ROTATED if len(seen[k]) > 1]
     print("pointers that moved over 3 steps:", moved)
     dy.close()
+
+
+def test_writes_through_packed_mesh_pointers_reach_the_kernels(moist_case):
+    """The maxEdges-strided mesh fields and zb_cell / zb3_cell are read by the kernels from packed copies
+    (pack_mesh, zb_p / zb_m).  A write through their device pointers must reach the next step as a
+    mpas_dyc_set_field of the same image does: the library packs again after handing out such a pointer."""
+    from mpas_dycore import Dycore
+    hip = _hip()
+    dt = 2880.0
+    scale = {"zb3_cell": 0.5, "defc_a": 1.001}
+    runs = {}
+    for mode in ("none", "set", "ptr"):
+        dy = Dycore(moist_case, device=0, moist_end=3)
+        dy.init_diagnostics(dt)
+        dy.use_graph(True)
+        dy.atm_timestep(dt, 1)
+        dy.shift_time_levels()
+        dy.synchronize()
+        for n, f in scale.items():
+            img = dy.get_raw("mesh", n) * f
+            if mode == "ptr":
+                ptr = dy.lib.mpas_dyc_field_device_ptr(dy.h, b"mesh", n.encode(), 1)
+                assert hip.hipMemcpy(C.c_void_p(ptr), img.ctypes.data_as(C.c_void_p), img.nbytes, 1) == 0
+            elif mode == "set":
+                dy.set_raw("mesh", n, img)
+        for it in range(2):
+            dy.atm_timestep(dt, it + 2)
+            dy.shift_time_levels()
+        dy.synchronize()
+        runs[mode] = {n: dy.get("state", n, 1) for n in ("u", "w", "theta_m")}
+        dy.close()
+    assert not np.array_equal(runs["none"]["w"], runs["set"]["w"]), "the changed fields did not change the run"
+    for n in runs["set"]:
+        assert np.array_equal(runs["set"][n], runs["ptr"][n]), f"{n}: the write through the pointer did not reach the kernels"

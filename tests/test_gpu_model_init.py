@@ -8,11 +8,12 @@ mpas_atm_core.F run by the harness) and against init_atm.model_init (the host re
   * adv_coefs / adv_coefs_3rd: bit for bit (the compression is pure arithmetic on deriv_two, which
     init_atm computes to the reference's bits, tests/test_init_pinned.py);
   * zb_cell / zb3_cell (copies of zb / zb3 times config_coef_3rd_order), inverses: bit for bit vs host;
-  * meshScalingDel2 / Del4, dss: bit for bit, except where the reference's C library does not round
-    x**0.25 or sin correctly -- there the device value is the correctly rounded one (checked against a
-    60-digit evaluation here), 1 ulp from the reference's root / sine, so at most 2 ulp from its
-    meshScalingDel2 and 4 ulp from its dss.
-Then a model run from the device-initialised mesh equals the host-initialised one."""
+  * meshScalingDel2 / Del4, dss: bit for bit when the host hands in the C library's x**0.25 and sin
+    (Dycore(model_init="device"), init_atm.model_init_libm: what the compiled reference computes);
+    without them (model_init="device_cr") the device's correctly rounded values (checked against a
+    60-digit evaluation here), which differ where the reference's C library does not round x**0.25 or
+    sin correctly: 1 ulp in the root / sine, so at most 2 ulp in meshScalingDel2 and 4 ulp in dss.
+Then a model run from the device-initialised mesh equals the host-initialised one bit for bit."""
 import math
 from decimal import Decimal, getcontext
 
@@ -47,9 +48,9 @@ def _cases():
     return make_golden
 
 
-def _device(case, fields):
+def _device(case, fields, mode="device"):
     from mpas_dycore import Dycore
-    dy = Dycore(case, device=0, model_init="device")
+    dy = Dycore(case, device=0, model_init=mode)
     out = {}
     for n in fields:
         nb = dy.lib.mpas_dyc_field_bytes(dy.h, b"mesh", n.encode())
@@ -96,8 +97,9 @@ def _expected_scaling(case):
                 dss=dss), dict(meshScalingDel2=r4 != lib4, dss=dss != dss_lib)
 
 
+@pytest.mark.parametrize("mode", ["device", "device_cr"])
 @pytest.mark.parametrize("fixture", ["init_x1.642_K8.npz", "init_varres2562_K8.npz"])
-def test_model_init_matches_reference(fixture):
+def test_model_init_matches_reference(fixture, mode):
     import os
     from mpas_dycore.layout import to_fortran
     mg = _cases()
@@ -114,7 +116,7 @@ def test_model_init_matches_reference(fixture):
              "adv_coefs", "adv_coefs_3rd", "meshScalingDel2", "meshScalingDel4", "meshScalingRegionalEdge",
              "meshScalingRegionalCell", "dss", "zb_cell", "zb3_cell", "invAreaCell", "invDvEdge", "invDcEdge",
              "invAreaTriangle")
-    got = _device(c, names)
+    got = _device(c, names, mode)
     noc = np.asarray(case["nEdgesOnCell"])
     slot = np.arange(ME)[None, :] < noc[:, None]
     nadv = np.asarray(ref["nAdvCellsForEdge"])
@@ -133,6 +135,16 @@ def test_model_init_matches_reference(fixture):
     for n in ("adv_coefs", "adv_coefs_3rd"):
         a = g[n].reshape(nE + 1, 15)[:nE]
         assert np.array_equal(np.where(aslot, a, 0), np.where(aslot, ref[n], 0)), f"{n} not bit for bit"
+    if mode == "device":  # the C library's x**0.25 and sin from the host: every output is the reference's
+        from mpas_dycore.init_atm import model_init_libm
+        for n in ("meshScalingDel2", "meshScalingDel4"):
+            assert np.array_equal(g[n][:nE], np.asarray(ref[n])), f"{n} not bit for bit"
+        # the regional scalings (mpas_atm_core.F:979-982): the same 1 / x**0.25 as Del2, and per cell
+        assert np.array_equal(g["meshScalingRegionalEdge"][:nE], np.asarray(ref["meshScalingDel2"]))
+        assert np.array_equal(g["meshScalingRegionalCell"][:nC],
+                              1.0 / model_init_libm(case, case["config"])["meshDensity_root4"])
+        assert np.array_equal(g["dss"].reshape(nC + 1, K)[:nC], np.asarray(ref["dss"])), "dss not bit for bit"
+        return
     # pow / sin outputs: the correctly rounded values; the reference's where its C library rounds right
     want, lib_off = _expected_scaling(case)
     for n in ("meshScalingDel2", "meshScalingDel4", "meshScalingRegionalEdge"):
@@ -161,11 +173,9 @@ def test_model_init_matches_reference(fixture):
 
 
 def test_model_run_from_device_init(moist_case):
-    """A moist run whose mesh precompute came from mpas_dyc_model_init: every precomputed array equals
-    the host-initialised one bit for bit except dss, which may differ by a few ulp (<= 4) where the C library's sin
-    is not correctly rounded; the run is bitwise equal when dss is, else within the parity tests' bars
-    (1e-13, w 1e-11)."""
-    from conftest import rel_linf
+    """A moist run whose mesh precompute came from mpas_dyc_model_init (with the host's C-library x**0.25 and
+    sin, Dycore(model_init="device")): every precomputed array and the run equal the host-initialised ones
+    bit for bit."""
     from mpas_dycore import Dycore
     case = moist_case
     dt = 2880.0
@@ -185,17 +195,9 @@ def test_model_run_from_device_init(moist_case):
         dy.close()
     (m0, s0), (m1, s1) = runs
     for n in m0:
-        if n == "dss":
-            off = m0[n] != m1[n]
-            assert np.all(np.abs(m0[n][off] - m1[n][off]) <= 4 * np.spacing(np.abs(m0[n][off]))), "dss beyond 4 ulp"
-            continue
         assert np.array_equal(m0[n], m1[n]), f"{n}: device model init differs from the host's"
-    exact = np.array_equal(m0["dss"], m1["dss"])
     for n in s0:
-        if exact:
-            assert np.array_equal(s0[n], s1[n]), n
-        else:  # the parity tests' 1-step bars: w amplifies a last-bit change of dss the most
-            assert rel_linf(s1[n], s0[n]) <= (1e-11 if n == "w" else 1e-13), n
+        assert np.array_equal(s0[n], s1[n]), n
 
 
 @pytest.mark.parametrize("fixture", ["init_x1.642_K8.npz", "init_varres2562_K8.npz"])

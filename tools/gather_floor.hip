@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -204,6 +206,140 @@ __global__ __launch_bounds__(EDGE_THREADS) void f_dynedges(Dims d, Ptrs p) {
   if (solve && 2 * l < K) st2(p.tend_u + o, q);
 }
 
+// ---- cell-centric advflux (VERDICT r04 Next 3) ---------------------------------------------------
+// One wavefront per cell that is cellsOnEdge(1) of an edge (c1): lanes 0-31 form w's edge values,
+// lanes 32-63 theta_m's, two levels per lane.  advCellsForEdge lists c1, c2, c1's other neighbours in
+// c1's cellsOnCell order, then c2's neighbours not yet listed (atm_adv_coef_compression,
+// mpas_atm_core.F:1154-1191): slots 0 .. ne(c1) are c1's ring, which the wave loads once for all of
+// its c1-edges; only the last slots (c2's far neighbours) are gathered per edge.  The sum runs over
+// the slots in the same order with the same expression as k_dyn_advflux_p: the same bits.
+// list[i] = (cell, bit mask of its edge positions whose edge has it as c1).
+// one c1-edge of the cell (its position IE among the cell's NE edges, both compile-time constants, so
+// every slot's ring column and coefficient offset is static)
+template <int ME, int NE, int IE>
+__device__ __forceinline__ void advflux_c_edge(const Dims& d, const Ptrs& p, const d2 (&col)[ME + 1], int e, int c,
+                                               const double* F, size_t stride, int off, d2 fzm, d2 fzp, int h, int l,
+                                               int lc) {
+  constexpr int NF = ME - 3;
+  const int K = d.K, kx = 2 * l, ky = 2 * l + 1;
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int na = __builtin_amdgcn_readfirstlane(p.nAdvCellsForEdge[e]);
+  const int* ac = p.advCellsForEdge + (size_t)e * 15;
+  const double* A = p.adv_coefs + (size_t)e * 15;
+  const double* B = p.adv_coefs_3rd + (size_t)e * 15;
+  double a[NE + 1 + NF], b[NE + 1 + NF];
+#pragma unroll
+  for (int j = 0; j < NE + 1 + NF; ++j) {
+    a[j] = ld_uniform_f64(A + j);
+    b[j] = ld_uniform_f64(B + j);
+  }
+  d2 far[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int cf = NE + 1 + f < na ? ac[NE + 1 + f] : c;
+    far[f] = ld2(F + (size_t)cf * stride + off);
+  }
+  const d2 rue = ld2(p.ru + o);
+  const d2 rue_m = km1(rue, l);
+  const double rewx = kx < K ? fzm.x * rue.x + fzp.x * rue_m.x : 0.0;
+  const double rewy = ky < K ? fzm.y * rue.y + fzp.y * rue_m.y : 0.0;
+  const double sx = h ? sgn1(rue.x) : sgn1(rewx), sy = h ? sgn1(rue.y) : sgn1(rewy);
+  d2 fl{0.0, 0.0};
+  auto add = [&](int j, d2 v) {
+    fl.x = fl.x + (a[j] + sx * b[j]) * v.x;
+    fl.y = fl.y + (a[j] + sy * b[j]) * v.y;
+  };
+  add(0, col[0]);
+  add(1, col[1 + IE]);
+#pragma unroll
+  for (int m = 0; m < NE; ++m)
+    if (m != IE) add(2 + m - (m > IE ? 1 : 0), col[1 + m]);
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+    if (NE + 1 + f < na) add(NE + 1 + f, far[f]);
+  if (2 * l < K) st2((h ? p.advflux_th : p.advflux_w) + o, fl);
+}
+
+template <int ME, int NE>
+__device__ __forceinline__ void advflux_c_cell(const Dims& d, const Ptrs& p, const d2 (&col)[ME + 1], const int (&eo)[ME],
+                                               int mask, int c, const double* F, size_t stride, int off, d2 fzm,
+                                               d2 fzp, int h, int l, int lc) {
+#define ADVF_E(IE) \
+  if (IE < NE && ((mask >> IE) & 1)) advflux_c_edge<ME, NE, (IE < NE ? IE : 0)>(d, p, col, eo[IE < ME ? IE : 0], c, F, stride, off, fzm, fzp, h, l, lc)
+  ADVF_E(0);
+  ADVF_E(1);
+  ADVF_E(2);
+  ADVF_E(3);
+  ADVF_E(4);
+  ADVF_E(5);
+  ADVF_E(6);
+#undef ADVF_E
+}
+
+template <int ME>
+__global__ __launch_bounds__(EDGE_THREADS) void k_advflux_c(Dims d, Ptrs p, const int2* __restrict__ list, int n) {
+  const int iw = pair_wave();
+  if (iw >= n) return;
+  const int c = __builtin_amdgcn_readfirstlane(list[iw].x), mask = __builtin_amdgcn_readfirstlane(list[iw].y);
+  const int K = d.K, h = pair_half(), l = pair_lane();
+  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  const size_t stride = h ? (size_t)K : (size_t)K + 1;
+  const int off = 2 * (h ? lc : lw);
+  const double* F = h ? p.theta_m2 : p.w2;
+  const int* rec = p.cell_rec + (size_t)c * CELL_REC;
+  const int ne = rec[14];
+  int eo[ME];
+  d2 col[ME + 1];
+  col[0] = ld2(F + (size_t)c * stride + off);
+#pragma unroll
+  for (int m = 0; m < ME; ++m) {
+    eo[m] = rec[m];
+    col[1 + m] = ld2(F + (size_t)rec[7 + m] * stride + off);
+  }
+  const d2 fzm = ld2(p.fzm + 2 * lc), fzp = ld2(p.fzp + 2 * lc);
+  if (ne == 6) advflux_c_cell<ME, 6>(d, p, col, eo, mask, c, F, stride, off, fzm, fzp, h, l, lc);
+  else if (ne == 5) advflux_c_cell<ME, 5>(d, p, col, eo, mask, c, F, stride, off, fzm, fzp, h, l, lc);
+  else if (ME >= 7 && ne == 7) advflux_c_cell<ME, ME>(d, p, col, eo, mask, c, F, stride, off, fzm, fzp, h, l, lc);
+}
+
+// the same loads and stores, a plain sum for the arithmetic
+template <int ME>
+__global__ __launch_bounds__(EDGE_THREADS) void f_advflux_c(Dims d, Ptrs p, const int2* __restrict__ list, int n) {
+  constexpr int NF = ME - 3;
+  const int iw = pair_wave();
+  if (iw >= n) return;
+  const int c = __builtin_amdgcn_readfirstlane(list[iw].x), mask = __builtin_amdgcn_readfirstlane(list[iw].y);
+  const int K = d.K, h = pair_half(), l = pair_lane();
+  const int lc = min(l, K / 2 - 1), lw = min(l, K / 2);
+  const size_t stride = h ? (size_t)K : (size_t)K + 1;
+  const int off = 2 * (h ? lc : lw);
+  const double* F = h ? p.theta_m2 : p.w2;
+  const int* rec = p.cell_rec + (size_t)c * CELL_REC;
+  const int ne = rec[14];
+  d2 acc = ld2(F + (size_t)c * stride + off);
+#pragma unroll
+  for (int m = 0; m < ME; ++m) {
+    const d2 v = ld2(F + (size_t)rec[7 + m] * stride + off);
+    acc.x += v.x;
+    acc.y += v.y;
+  }
+#pragma unroll
+  for (int ie = 0; ie < ME; ++ie) {
+    if (!((mask >> ie) & 1)) continue;
+    const int e = rec[ie];
+    const size_t o = (size_t)e * K + 2 * lc;
+    d2 fl = ld2(p.ru + o);
+    const int* ac = p.advCellsForEdge + (size_t)e * 15;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const d2 v = ld2(F + (size_t)__builtin_amdgcn_readfirstlane(ac[ne + 1 + f]) * stride + off);
+      fl.x += v.x + acc.x;
+      fl.y += v.y + acc.y;
+    }
+    if (2 * l < K) st2((h ? p.advflux_th : p.advflux_w) + o, fl);
+  }
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s DUMPDIR [reps] [rounds]\n", argv[0]);
@@ -244,6 +380,40 @@ int main(int argc, char** argv) {
   p.adv_coefs = dev(load<double>(dir, "adv_coefs.f64", (size_t)(nE + 1) * 15));
   p.adv_coefs_3rd = dev(load<double>(dir, "adv_coefs_3rd.f64", (size_t)(nE + 1) * 15));
   p.weightsOnEdge = dev(load<double>(dir, "weightsOnEdge.f64", (size_t)(nE + 1) * 10));
+  // cell records (k_build_cell_rec's layout) and the c1 list of the cell-centric advflux
+  std::vector<int> crec = load<int>(dir, "cell_rec.i32", (size_t)(nC + 1) * CELL_REC);
+  p.cell_rec = dev(crec);
+  std::vector<int2> c1list;
+  {
+    std::vector<int> coe = load<int>(dir, "cellsOnEdge.i32", (size_t)(nE + 1) * 2);
+    std::vector<int> ace = load<int>(dir, "advCellsForEdge.i32", (size_t)(nE + 1) * 15);
+    std::vector<int> nae = load<int>(dir, "nAdvCellsForEdge.i32", (size_t)nE + 1);
+    std::vector<int> mask(nC, 0);
+    int bad = 0;
+    for (int e = 0; e < nE; ++e) {
+      const int c = coe[2 * e];
+      const int* r = &crec[(size_t)c * CELL_REC];
+      const int ne = r[14];
+      int ie = -1;
+      for (int m = 0; m < ne; ++m)
+        if (r[m] == e) ie = m;
+      // slots 0 .. ne: c, the cell across e, c's other neighbours in order; then at most ne(c2) - 3 more
+      bool ok = ie >= 0 && ace[(size_t)e * 15] == c && ace[(size_t)e * 15 + 1] == r[7 + ie] &&
+                nae[e] - (ne + 1) <= 3 && nae[e] >= ne + 1;
+      for (int m = 0, j = 2; ok && m < ne; ++m)
+        if (m != ie) ok = ace[(size_t)e * 15 + j++] == r[7 + m];
+      if (!ok) {
+        ++bad;
+        continue;
+      }
+      mask[c] |= 1 << ie;
+    }
+    for (int c = 0; c < nC; ++c)
+      if (mask[c]) c1list.push_back(int2{c, mask[c]});
+    printf("cell-centric advflux: %zu c1 cells for %d edges, %d edges off the ring pattern\n", c1list.size(), nE, bad);
+  }
+  int2* d_c1list = dev(c1list);
+  const int n_c1 = (int)c1list.size();
   const size_t cK = (size_t)(nC + 1) * K, cK1 = (size_t)(nC + 1) * (K + 1), eK = (size_t)(nE + 1) * K;
   unsigned seed = 1;
   p.invDcEdge = dev_field(nE + 1, seed++);
@@ -266,6 +436,28 @@ int main(int argc, char** argv) {
   DynTendScal s{};
   s.rk_step = 2;
   const dim3 blk(EDGE_THREADS), grid((unsigned)(((nE + 1) / 2 + EDGE_WPB - 1) / EDGE_WPB));
+  const dim3 gridc((unsigned)((n_c1 + EDGE_WPB - 1) / EDGE_WPB));
+  {  // the cell-centric kernel gives the pair kernel's bits
+    const size_t eKb = (size_t)(nE + 1) * K * sizeof(double);
+    std::vector<double> w0(eKb / 8), t0(eKb / 8), w1(eKb / 8), t1(eKb / 8);
+    CK(hipMemset(p.advflux_w, 0, eKb));
+    CK(hipMemset(p.advflux_th, 0, eKb));
+    hipLaunchKernelGGL((k_dyn_advflux_p<10, false>), grid, blk, 0, 0, d, p);
+    CK(hipMemcpy(w0.data(), p.advflux_w, eKb, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(t0.data(), p.advflux_th, eKb, hipMemcpyDeviceToHost));
+    CK(hipMemset(p.advflux_w, 0, eKb));
+    CK(hipMemset(p.advflux_th, 0, eKb));
+    hipLaunchKernelGGL(k_advflux_c<6>, gridc, blk, 0, 0, d, p, d_c1list, n_c1);
+    CK(hipMemcpy(w1.data(), p.advflux_w, eKb, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(t1.data(), p.advflux_th, eKb, hipMemcpyDeviceToHost));
+    size_t dw = 0, dtt = 0;
+    for (size_t i = 0; i < (size_t)nE * K; ++i) {
+      dw += memcmp(&w0[i], &w1[i], 8) != 0;
+      dtt += memcmp(&t0[i], &t1[i], 8) != 0;
+    }
+    printf("cell-centric vs pair kernel: %zu / %zu w values and %zu theta values differ in any bit\n", dw,
+           (size_t)nE * K, dtt);
+  }
   struct V {
     const char* name;
     std::function<void()> run;
@@ -275,6 +467,8 @@ int main(int argc, char** argv) {
       {"advflux kernel", [&] { hipLaunchKernelGGL((k_dyn_advflux_p<10, false>), grid, blk, 0, 0, d, p); }, {}},
       {"advflux floor", [&] { hipLaunchKernelGGL(f_advflux, grid, blk, 0, 0, d, p); }, {}},
       {"advflux stream", [&] { hipLaunchKernelGGL(s_advflux, grid, blk, 0, 0, d, p, W10, T10); }, {}},
+      {"advflux cell", [&] { hipLaunchKernelGGL(k_advflux_c<6>, gridc, blk, 0, 0, d, p, d_c1list, n_c1); }, {}},
+      {"advflux cell fl", [&] { hipLaunchKernelGGL(f_advflux_c<6>, gridc, blk, 0, 0, d, p, d_c1list, n_c1); }, {}},
       {"scalars kernel", [&] { hipLaunchKernelGGL((k_scalars_edges_p<10, false>), grid, blk, 0, 0, d, p); }, {}},
       {"scalars floor", [&] { hipLaunchKernelGGL(f_scalars, grid, blk, 0, 0, d, p); }, {}},
       {"dynedges kernel",

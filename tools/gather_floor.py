@@ -29,14 +29,30 @@ def dump(case, out):
         return np.concatenate([a, np.zeros((1, width))])
     files = {
         "advCellsForEdge.i32": idx(case["advCellsForEdge"], nC, 15),
-        "nAdvCellsForEdge.i32": np.append(np.asarray(case["nAdvCellsForEdge"], np.int32), 0),
+        "nAdvCellsForEdge.i32": np.append(np.asarray(case["nAdvCellsForEdge"]), 0).astype(np.int32),
         "cellsOnEdge.i32": idx(case["cellsOnEdge"], nC, 2),
         "edgesOnEdge.i32": idx(case["edgesOnEdge"], nE, 10),
-        "nEdgesOnEdge.i32": np.append(np.asarray(case["nEdgesOnEdge"], np.int32), 0),
+        "nEdgesOnEdge.i32": np.append(np.asarray(case["nEdgesOnEdge"]), 0).astype(np.int32),
         "adv_coefs.f64": real(case["adv_coefs"], 15),
         "adv_coefs_3rd.f64": real(case["adv_coefs_3rd"], 15),
         "weightsOnEdge.f64": real(case["weightsOnEdge"], 10),
     }
+    # k_build_cell_rec's records: [0, 7) edgesOnCell, [7, 14) the cell across each edge, [14] nEdgesOnCell
+    ne = np.asarray(case["nEdgesOnCell"])
+    eoc = np.asarray(case["edgesOnCell"])[:, :7]
+    coe = np.asarray(case["cellsOnEdge"])
+    rec = np.zeros((nC + 1, 16), np.int32)
+    rec[:, :7] = nE
+    rec[:, 7:14] = nC
+    for m in range(eoc.shape[1]):
+        live = m < ne
+        e = np.where(live, eoc[:, m], 0)
+        other = np.where(coe[e, 0] == np.arange(nC), coe[e, 1], coe[e, 0])
+        rec[:nC, m] = np.where(live, e, nE)
+        rec[:nC, 7 + m] = np.where(live & (other >= 0), other, nC)
+    rec[:nC, 14] = ne
+    rec[nC, 14] = 0
+    files["cell_rec.i32"] = rec
     for n, a in files.items():
         np.ascontiguousarray(a).tofile(os.path.join(out, n))
     return nC, nE, nV, K

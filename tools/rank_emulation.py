@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager launches (what a rank without hipGraph costs)")
     a = ap.parse_args()
     if a.exchange:
-        os.environ["MPAS_DYCORE_LOOPBACK"] = "1"  # read when a context is created
+        os.environ.setdefault("MPAS_DYCORE_LOOPBACK", "1")  # read when a context is created (2: memcpy pairs)
     from mpas_dycore import Dycore, decomp
     from mpas_dycore.cases import jw_case
     case = jw_case(a.ncells, K=a.levels, order=a.order)
