@@ -1824,7 +1824,7 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
       const Dims& d = ctx->blk[b].d;
       const bool bt = batched(d), m6 = d.maxEdges == 6;
       // the pair's second scratch set for the kernels that take both scalars in one launch
-      const MonoCell2 s2 = nq == 2 ? MonoCell2{P1[b].wdtn, P1[b].s_max, P1[b].s_min, P1[b].flux_tmp,
+      const MonoCell2 s2 = nq == 2 ? MonoCell2{P1[b].wdtn, P1[b].s_max, P1[b].s_min, P1[b].flux_arr,
                                                P1[b].flux_upwind_tmp, P1[b].scalar_old_copy, P1[b].scale_arr}
                                    : MonoCell2{};
       const double c3 = ctx->cf.coef_3rd_order;
@@ -1843,8 +1843,9 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
         for (int q = 0; q < nq; ++q) LAUNCH(k_mono_edges1, d.nEdges, d, q ? P1[b] : P[b], is + q, dt);
       }
       if (bt) {  // both scalars of the pair in one launch (the cell's own columns read once)
-        if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2);
-        else LAUNCH(k_mono_cells1_b<7>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2);
+        const int pr = pair_layout(d) ? 1 : 0;  // which edge kernel formed the fluxes
+        if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2, pr);
+        else LAUNCH(k_mono_cells1_b<7>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2, pr);
       } else {
         for (int q = 0; q < nq; ++q) LAUNCH(k_mono_cells1, d.nCellsSolve, d, q ? P1[b] : P[b], is + q, dt, ad);
       }
@@ -1868,7 +1869,7 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
         if (pair_layout(d)) LAUNCH_PE((k_mono_edges2_p<false>), (k_mono_edges2_p<true>), d.nEdges, d, pq, dt);
         else LAUNCH(k_mono_edges2, d.nEdges, d, pq, dt);
       }
-      const MonoCell2 s2 = nq == 2 ? MonoCell2{P1[b].wdtn, P1[b].s_max, P1[b].s_min, P1[b].flux_tmp,
+      const MonoCell2 s2 = nq == 2 ? MonoCell2{P1[b].wdtn, P1[b].s_max, P1[b].s_min, P1[b].flux_arr,
                                                P1[b].flux_upwind_tmp, P1[b].scalar_old_copy, P1[b].scale_arr}
                                    : MonoCell2{};
       double* fa2 = nq == 2 ? P1[b].flux_arr : nullptr;
@@ -2041,7 +2042,8 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
   relayout(true);                                                 // time level 2 via stage_pre
   EACH(rk_integration_setup(ctx, d, p));
   EACH(LAUNCH(k_moist_cells, d.nCells, d, p));                    // 383-422
-  EACH(LAUNCH(k_moist_edges, d.nEdges, d, p));
+  EACH(if (pair_layout(d)) LAUNCH_PE((k_moist_edges_p<false>), (k_moist_edges_p<true>), d.nEdges, d, p);
+       else LAUNCH(k_moist_edges, d.nEdges, d, p));
   // physics tendencies are zero without DO_PHYSICS (450-457): scratch arrays stay zero.
 
   // Deferred exchanges.  With split-phase exchanges, the exchange after the diagnostics

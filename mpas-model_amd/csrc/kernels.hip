@@ -2528,6 +2528,30 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
   }
 }
 
+// k_moist_edges in the pair layout (two edges per wave, two levels per lane): the 2 x (moist species)
+// column gathers as 16-byte loads, the sum over the species in the same order (1920-1926)
+template <bool ODD = false>
+__global__ __launch_bounds__(PAIR_THREADS) void k_moist_edges_p(Dims d, Ptrs p) {
+  int eA, eB;
+  bool hasB;
+  if (!pair_edges(d, p, 0, eA, eB, hasB)) return;
+  const int K = d.K, h = pair_half(), l = pair_lane();
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int e = sel(h, eA, eB);
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
+  const bool on = (c1 < d.nCellsSolve || c2 < d.nCellsSolve) && (h == 0 || hasB);
+  d2 q{0.0, 0.0};
+  for (int iq = d.moist_start; iq <= d.moist_end; ++iq) {
+    const d2 s1 = ld2(p.scalars2 + SIX(c1, 2 * lc, iq)), s2 = ld2(p.scalars2 + SIX(c2, 2 * lc, iq));
+    q.x = q.x + 0.5 * (s1.x + s2.x);
+    q.y = q.y + 0.5 * (s1.y + s2.y);
+  }
+  if (on && 2 * l < K) pst(p.cqu + (size_t)e * K + 2 * lc, d2{1.0 / (1.0 + q.x), 1.0 / (1.0 + q.y)}, two);
+}
+
 // (a two-scalar variant -- both scalars' gathers from one pass over the stencil indices and
 // coefficients -- needs 197 VGPRs, runs 2 waves per SIMD instead of 4 and took exactly the time
 // of two launches: the in-flight gathers per SIMD, not the index loads, bound this kernel)
@@ -2613,7 +2637,8 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
     if ((h == 0 || hasB) && 2 * l < K) {
       pst((q ? f2.flux_arr : p.flux_arr) + o, upw ? fu : fa, two);
       pst((q ? f2.flux_upwind_tmp : p.flux_upwind_tmp) + o, fu, two);
-      pst((q ? f2.flux_tmp : p.flux_tmp) + o, upw ? d2{0.0, 0.0} : d2{dt * fa.x - fu.x, dt * fa.y - fu.y}, two);
+      // flux_tmp (upw ? 0 : dt fa - fu) is not stored: k_mono_cells1_b, its only reader, forms it from
+      // flux_arr and flux_upwind_tmp with the same operations (one edge array less written per scalar)
     }
   }
 }
@@ -4160,7 +4185,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_scalars_cells_b(Dims d, Ptrs 
 
 // the second scratch set (mono_slot1) of k_mono_bounds_b / k_mono_cells1_b / k_mono_cells2_b for the pair's second scalar
 struct MonoCell2 {
-  double *wdtn, *s_max, *s_min, *flux_tmp, *flux_upwind_tmp, *scalar_old_copy, *scale_arr;
+  double *wdtn, *s_max, *s_min, *flux_arr, *flux_upwind_tmp, *scalar_old_copy, *scale_arr;
 };
 template <int ME>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds_b(Dims d, Ptrs p, int is, double coef_3rd_order,
@@ -4223,9 +4248,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds_b(Dims d, Ptrs p,
   }
 }
 
+// pair_rule: the edge fluxes come from k_mono_edges1_p, whose flux_arr holds the upwind flux on the
+// outer relaxation rows (upw, 4017-4020) -- flux_tmp is 0 there; else from k_mono_edges1 (no such rows)
 template <int ME>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p, int is, double dt, int advance_density,
-                                                                  int nq = 1, MonoCell2 s2 = MonoCell2{}) {
+                                                                  int nq = 1, MonoCell2 s2 = MonoCell2{},
+                                                                  int pair_rule = 1) {
   const int c = wave_elem(0);
   if (c >= d.nCellsSolve) return;
   const int k = lane_id(), K = d.K, ns = d.ns;
@@ -4245,7 +4273,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p,
   for (int q = 0; q < nq; ++q) {
     const int iq = is + q;
     double* wdtn = q ? s2.wdtn : p.wdtn;
-    const double* ftmp = q ? s2.flux_tmp : p.flux_tmp;
+    const double* farr = q ? s2.flux_arr : p.flux_arr;
     const double* fup = q ? s2.flux_upwind_tmp : p.flux_upwind_tmp;
     double so = p.scalars1[SIX(c, kc, iq)];
     double rzo = rzo_l;
@@ -4254,8 +4282,12 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p,
     double ft[ME], fu[ME];
 #pragma unroll
     for (int i = 0; i < ME; ++i) {
-      ft[i] = ftmp[(size_t)st.e[i] * K + kc];
+      const double fa = farr[(size_t)st.e[i] * K + kc];
       fu[i] = fup[(size_t)st.e[i] * K + kc];
+      // flux_tmp of k_mono_edges1(_p) (4014, 4017-4020): dt flux_arr - flux_upwind, 0 on the upwind-only rows
+      const int bm = pair_rule ? p.bdyMaskEdge[st.e[i]] : 0;
+      const bool upw = (d.lbc && bm == N_RELAX_ZONE) || bm == N_RELAX_ZONE - 1;
+      ft[i] = upw ? 0.0 : dt * fa - fu[i];
     }
     if (!act) {
       so = 0.0;

@@ -92,7 +92,7 @@ step() {
         echo "== bench --init (maxEdges 10)" >> gpurun_out/maxedges.log
         timeout -k 10 400 python bench.py --steps 10 --warmup 2 $B --init /tmp/x1.163842.me10.init.nc --dt 360 --len-disp 60000 >> gpurun_out/maxedges.log 2>&1 || return 1
         grep -h "==\|ms_per_step" gpurun_out/maxedges.log | sed 's/.*"ms_per_step": \([0-9.]*\).*"kernel_layout": \({[^}]*}\).*/ms_per_step \1 \2/' ;;
-    floor) timeout -k 10 400 python tools/gather_floor.py > gpurun_out/floor.log 2>&1; r=$?; cat gpurun_out/floor.log; return $r ;;
+    floor) timeout -k 10 400 python tools/gather_floor.py ${FLOOR_ARGS} > gpurun_out/floor.log 2>&1; r=$?; cat gpurun_out/floor.log; return $r ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && last gpurun_out/smoke.log ;;
     *) echo "unknown step $1"; return 2 ;;
   esac

@@ -2,7 +2,11 @@
 """Whole-dt roofline table: every kernel of one atm_timestep, its algorithmic bytes per launch
 (SURVEY.md §8d's rule), its measured time, and the PMC-counted HBM traffic.
 
-    python tools/kernel_roofline.py KERNEL_STATS.csv PMC.json STEPS [NCELLS LEVELS] > profiles/r03_kernel_roofline.csv
+    python tools/kernel_roofline.py KERNEL_STATS.csv PMC.json STEPS [NCELLS LEVELS [NS]] > profiles/r03_kernel_roofline.csv
+
+With NS > 1 (the moist transport, scalar-major scalars): the monotone pipeline's kernels (k_mono_*
+but k_mono_prep) run one launch per pair of scalars (MonoFlux2, a second set of scratch), so their
+scalars / scalars_tend count 2 of NS scalar columns and their per-scalar scratch twice.
 
 Algorithmic bytes of a launch = the sum, over the arrays the kernel reads and over those it writes
 (tools/kernel_access.py, resolved per template variant below), of the array's size over the
@@ -122,7 +126,10 @@ def field_key(member, reg):
     return None
 
 
-def alg_bytes(kernel_full, amap, reg):
+PER_SCALAR_FIELDS = {"state.scalars", "tend.scalars_tend"}
+
+
+def alg_bytes(kernel_full, amap, reg, ns=1):
     base = kernel_full.split("<")[0].replace("void ", "").strip()
     if base not in amap:
         return None
@@ -140,13 +147,22 @@ def alg_bytes(kernel_full, amap, reg):
         return (k, m.rstrip("_rd")[-1] if k and k.startswith("state.") else "")
     keys_r = {arr(m) for m in reads} | {(k, "x") for k in EXTRA_READS.get(base, set())}
     keys_w = {arr(m) for m in writes}
+    pair = ns > 1 and base.startswith("k_mono_") and base != "k_mono_prep"
+
+    def size(k):
+        b = reg[k][0] * reg[k][1] * (4 if k.split(".")[1] in INT_FIELDS else 8)
+        if pair and k in PER_SCALAR_FIELDS:
+            return b * 2 // ns  # two of the ns scalars
+        if pair and k.startswith("scratch."):
+            return 2 * b  # the pair's second set of scratch
+        return b
     tot = 0
     for k, tag in keys_r:
         if k and k in reg:
-            tot += reg[k][0] * reg[k][1] * (4 if k.split(".")[1] in INT_FIELDS else 8)
+            tot += size(k)
     for k, tag in keys_w:
         if k and k in reg:
-            tot += reg[k][0] * reg[k][1] * 8
+            tot += size(k)
     return tot
 
 
@@ -159,7 +175,8 @@ def main():
     stats, pmc_path, steps = sys.argv[1], sys.argv[2], int(sys.argv[3])
     nC = int(sys.argv[4]) if len(sys.argv) > 4 else 163842
     K = int(sys.argv[5]) if len(sys.argv) > 5 else 56
-    reg = registry(nC, K)
+    ns = int(sys.argv[6]) if len(sys.argv) > 6 else 1
+    reg = registry(nC, K, ns=ns)
     amap = access_map()
     pmc = {}
     if os.path.isfile(pmc_path):
@@ -176,7 +193,7 @@ def main():
         if name.startswith("__amd") or "init" in name or "build" in name or calls < 0.5:
             continue
         # launches over a halo / boundary remainder (one element on one block) have no whole-array count
-        b = alg_bytes(name, amap, reg) if us >= 20.0 else None
+        b = alg_bytes(name, amap, reg, ns) if us >= 20.0 else None
         pb = pmc.get(name)
         row = [name, f"{calls:.2f}", f"{us:.1f}"]
         if b:
