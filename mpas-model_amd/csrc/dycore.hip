@@ -1799,6 +1799,12 @@ Ptrs mono_slot1(mpas_dyc_ctx* c, Block& b, Ptrs p) {
 
 // MPAS_DYCORE_MONO_PAIRS=0 (read when a context is created): one scalar at a time
 int g_mono_pairs = 1;
+// the monotone limiter's bounds (s_max, s_min, wdtn) inside the first cell pass k_mono_cells1_b<ME, true>
+// (MPAS_DYCORE_MONO_FUSE=0, read when a context is created: the separate k_mono_bounds_b).  (The flux
+// rescaling of k_mono_edges2_p inside k_mono_cells2_b, each edge formed by both of its cells, was bitwise
+// but no faster: profiles/r05_ab_mono_fuse_edges2_rejected.log.)
+constexpr int MONO_FUSE_BOUNDS = 1;
+int g_mono_fuse = MONO_FUSE_BOUNDS;
 
 // The reference's per-scalar loop (3798-4210): bounds, fluxes, limiter factors, the scale_arr
 // exchange (4098), rescale and update, one scalar after the other.  Each scalar's pipeline reads and
@@ -1828,8 +1834,10 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
                                                P1[b].flux_upwind_tmp, P1[b].scalar_old_copy, P1[b].scale_arr}
                                    : MonoCell2{};
       const double c3 = ctx->cf.coef_3rd_order;
+      const bool fb = bt && (g_mono_fuse & MONO_FUSE_BOUNDS);  // the bounds inside k_mono_cells1_b<ME, true>
       if (!bt) {
         for (int q = 0; q < nq; ++q) LAUNCH(k_mono_bounds, d.nCellsSolve, d, q ? P1[b] : P[b], is + q, c3);
+      } else if (fb) {
       } else if (m6) {
         LAUNCH(k_mono_bounds_b<6>, d.nCellsSolve, d, P[b], is, c3, nq, s2);
       } else {
@@ -1844,7 +1852,9 @@ int advance_scalars_mono(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double d
       }
       if (bt) {  // both scalars of the pair in one launch (the cell's own columns read once)
         const int pr = pair_layout(d) ? 1 : 0;  // which edge kernel formed the fluxes
-        if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2, pr);
+        if (fb && m6) LAUNCH((k_mono_cells1_b<6, true>), d.nCellsSolve, d, P[b], is, dt, ad, nq, s2, pr, c3);
+        else if (fb) LAUNCH((k_mono_cells1_b<7, true>), d.nCellsSolve, d, P[b], is, dt, ad, nq, s2, pr, c3);
+        else if (m6) LAUNCH(k_mono_cells1_b<6>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2, pr);
         else LAUNCH(k_mono_cells1_b<7>, d.nCellsSolve, d, P[b], is, dt, ad, nq, s2, pr);
       } else {
         for (int q = 0; q < nq; ++q) LAUNCH(k_mono_cells1, d.nCellsSolve, d, q ? P1[b] : P[b], is + q, dt, ad);
@@ -2571,6 +2581,8 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   if (const char* fs = getenv("MPAS_DYCORE_FUSE_SMLSTEP")) g_fuse_smlstep = std::string(fs) != "0";
   g_mono_pairs = 1;
   if (const char* mp = getenv("MPAS_DYCORE_MONO_PAIRS")) g_mono_pairs = std::string(mp) != "0";
+  g_mono_fuse = MONO_FUSE_BOUNDS;
+  if (const char* mf = getenv("MPAS_DYCORE_MONO_FUSE")) g_mono_fuse = std::atoi(mf);
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
   if (const char* lb = getenv("MPAS_DYCORE_LOOPBACK")) ctx->loopback = std::atoi(lb);
   if (const char* li = getenv("MPAS_DYCORE_LATE_ISSUE")) ctx->late_issue = std::string(li) == "1";

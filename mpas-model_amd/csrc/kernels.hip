@@ -4250,10 +4250,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds_b(Dims d, Ptrs p,
 
 // pair_rule: the edge fluxes come from k_mono_edges1_p, whose flux_arr holds the upwind flux on the
 // outer relaxation rows (upw, 4017-4020) -- flux_tmp is 0 there; else from k_mono_edges1 (no such rows)
-template <int ME>
+// FB: k_mono_bounds_b fused in (3798-3850 + 3857-3907 before 3969-4076): the cell forms its own s_max /
+// s_min from the old scalar of its column and ring and its vertical flux wdtn from the new scalar, with
+// k_mono_bounds_b's expressions, instead of reading them back (nothing else reads s_max / s_min, and the
+// edge pass in between touches none of the inputs); coef_3rd_order only for FB
+template <int ME, bool FB = false>
 __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p, int is, double dt, int advance_density,
                                                                   int nq = 1, MonoCell2 s2 = MonoCell2{},
-                                                                  int pair_rule = 1) {
+                                                                  int pair_rule = 1, double coef_3rd_order = 0.0) {
   const int c = wave_elem(0);
   if (c >= d.nCellsSolve) return;
   const int k = lane_id(), K = d.K, ns = d.ns;
@@ -4267,6 +4271,14 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p,
   const double rzo_l = p.rho_zz1[o];
   const double wwa = p.wwAvg[ow], rdnw = p.rdzw[kc];
   const double rhoref = advance_density ? p.rho_zz_int[o] : p.rho_zz2[o];
+  int cc[ME];  // FB: cellsOnCell, as k_mono_bounds_b reads it
+  double fnm = 0.0, fnp = 0.0;
+  if (FB) {
+#pragma unroll
+    for (int i = 0; i < ME; ++i) cc[i] = p.cellsOnCell[(size_t)c * ME + i];
+    fnm = p.fzm[kc];
+    fnp = p.fzp[kc];
+  }
   // nq = 2: the pair's second scalar (is + 1) with the second scratch set (s2), after the first --
   // the cell's own columns and stencil read once
 #pragma unroll 1
@@ -4277,8 +4289,46 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_cells1_b(Dims d, Ptrs p,
     const double* fup = q ? s2.flux_upwind_tmp : p.flux_upwind_tmp;
     double so = p.scalars1[SIX(c, kc, iq)];
     double rzo = rzo_l;
-    double wd = wdtn[ow];
-    const double smx = (q ? s2.s_max : p.s_max)[o], smn = (q ? s2.s_min : p.s_min)[o];
+    double wd, smx, smn;
+    if (FB) {  // k_mono_bounds_b
+      double sn = p.scalars2[SIX(c, kc, iq)], sb = so;
+      double sv[ME];
+#pragma unroll
+      for (int i = 0; i < ME; ++i) {
+        const double v = p.scalars1[SIX(cc[i], kc, iq)];
+        sv[i] = cc[i] < d.nCells ? v : 0.0;  // sold() of the reference's halo loop
+      }
+      if (!act) {
+        sb = 0.0;
+        sn = 0.0;
+      }
+      const double som = up1(sb), sop = dn1(sb);
+      const double snm1 = up1(sn), snm2 = up2(sn), snp1 = dn1(sn);
+      wd = 0.0;
+      if (k == 1 || k == K - 1) wd = wwa * (fnm * sn + fnp * snm1);
+      else if (k >= 2 && k <= K - 2) wd = flux3(snm2, snm1, sn, snp1, wwa, coef_3rd_order);
+      if (k == 0) {
+        smx = fmax(sb, sop);
+        smn = fmin(sb, sop);
+      } else if (k == K - 1) {
+        smx = fmax(sb, som);
+        smn = fmin(sb, som);
+      } else {
+        smx = fmax(fmax(som, sb), sop);
+        smn = fmin(fmin(som, sb), sop);
+      }
+#pragma unroll
+      for (int i = 0; i < ME; ++i) {
+        if (i < st.ne) {
+          smx = fmax(smx, sv[i]);
+          smn = fmin(smn, sv[i]);
+        }
+      }
+    } else {
+      wd = wdtn[ow];
+      smx = (q ? s2.s_max : p.s_max)[o];
+      smn = (q ? s2.s_min : p.s_min)[o];
+    }
     double ft[ME], fu[ME];
 #pragma unroll
     for (int i = 0; i < ME; ++i) {

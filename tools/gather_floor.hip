@@ -340,6 +340,39 @@ __global__ __launch_bounds__(EDGE_THREADS) void f_advflux_c(Dims d, Ptrs p, cons
   }
 }
 
+// the acoustic edge phase with the previous sub-step's damping (k_acoustic_edges_p<true>): 5 columns of
+// the edge and 6 fields at both of its cells, two stores -- a plain sum for the arithmetic
+__global__ __launch_bounds__(EDGE_THREADS) void f_acoustic_edges(Dims d, Ptrs p) {
+  int eA, eB;
+  bool hasB;
+  if (!pair_edges(d, p, 0, eA, eB, hasB)) return;
+  const int K = d.K, h = pair_half(), l = pair_lane();
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  const bool onA = ceA.x < d.nCellsSolve || ceA.y < d.nCellsSolve;
+  const bool onB = hasB && (ceB.x < d.nCellsSolve || ceB.y < d.nCellsSolve);
+  if (!onA && !onB) return;
+  const d2 tu = ld2(p.tend_u + o), rp = ld2(p.ru_p + o), ra = ld2(p.ruAvg + o), cq = ld2(p.cqu + o),
+           zx = ld2(p.zxu + o);
+  const double mask = sel(h, ld_uniform_f64(p.specZoneMaskEdge + eA), ld_uniform_f64(p.specZoneMaskEdge + eB));
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
+  const size_t o1 = (size_t)c1 * K + 2 * lc, o2 = (size_t)c2 * K + 2 * lc;
+  d2 acc{tu.x + rp.x + cq.x + zx.x + mask, tu.y + rp.y + cq.y + zx.y};
+  const double* fs[6] = {p.rtheta_pp, p.zz, p.exner, p.rho_pp, p.rtheta_pp_old, p.theta_m1};
+  for (const double* f : fs) {
+    const d2 v1 = ld2(f + o1), v2 = ld2(f + o2);
+    acc.x += v1.x + v2.x;
+    acc.y += v1.y + v2.y;
+  }
+  if (2 * l < K && (h ? onB : onA)) {
+    st2(p.ru_p + o, acc);
+    st2(p.ruAvg + o, d2{ra.x + acc.x, ra.y + acc.y});
+  }
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s DUMPDIR [reps] [rounds]\n", argv[0]);
@@ -427,8 +460,15 @@ int main(int argc, char** argv) {
   p.h_divergence = dev_field(cK, seed++);
   p.scalars2 = dev_field(cK * ns, seed++);
   for (double** f : {&p.ru, &p.ruAvg, &p.advflux_w, &p.advflux_th, &p.rho_edge, &p.u2, &p.pv_edge, &p.tend_u_euler,
-                     &p.tend_u})
+                     &p.tend_u, &p.ru_p, &p.cqu})
     *f = dev_field(eK, seed++);
+  p.zxu = dev_field(eK, seed++);
+  for (double** f : {&p.rtheta_pp, &p.exner, &p.rho_pp, &p.rtheta_pp_old, &p.theta_m1}) *f = dev_field(cK, seed++);
+  p.zz = dev_field(cK, seed++);
+  {
+    std::vector<double> zmask(nE + 1, 0.0);
+    p.specZoneMaskEdge = dev(zmask);
+  }
   p.horiz_flux_array = dev_field(eK * ns, seed++);
   double* W10 = dev_field((size_t)nE * 10 * (K + 1), seed++);
   double* T10 = dev_field((size_t)nE * 10 * K, seed++);
@@ -475,6 +515,11 @@ int main(int argc, char** argv) {
        [&] { hipLaunchKernelGGL((k_dyn_edges_p<false, 10, false, false>), grid, blk, 0, 0, d, p, cf, s, 0, XPack{}); },
        {}},
       {"dynedges floor", [&] { hipLaunchKernelGGL(f_dynedges, grid, blk, 0, 0, d, p); }, {}},
+      {"acoustic edges",
+       [&] { hipLaunchKernelGGL((k_acoustic_edges_p<true, false, false>), grid, blk, 0, 0, d, p, 30.0, 2, 0.1, 0, 0,
+                                UnpackMap{}); },
+       {}},
+      {"acoustic edges fl", [&] { hipLaunchKernelGGL(f_acoustic_edges, grid, blk, 0, 0, d, p); }, {}},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));

@@ -56,6 +56,12 @@ step() {
              echo "== $E" >> gpurun_out/rcclenv.log
              env $E timeout -k 10 300 python tools/rank_emulation.py --parts 8 --blocks 0 4 --exchange >> gpurun_out/rcclenv.log 2>&1 || return 1
            done; grep -h "==\|blocks" gpurun_out/rcclenv.log | cut -c1-160 ;;
+    abenv) rm -f gpurun_out/abenv.log   # same library, ENVS="A=1;A=0" variants, AB_ROUNDS rounds of tools/kbench.py
+           IFS=';' read -ra VS <<< "${ENVS:-X=0}"
+           for r in ${AB_ROUNDS:-1 2 3}; do for E in "${VS[@]}"; do
+             echo "== $E" >> gpurun_out/abenv.log
+             env $E timeout -k 10 250 python tools/kbench.py --steps ${AB_STEPS:-10} ${AB_ARGS} >> gpurun_out/abenv.log 2>&1 || return 1
+           done; done; grep -h "==\|ms_dt" gpurun_out/abenv.log | cut -c1-130 ;;
     envsweep) rm -f gpurun_out/envsweep.log   # ENVS="A=1 B=2;C=3" (';' between variants), EMU_ARGS for rank_emulation.py
            IFS=';' read -ra VS <<< "${ENVS:-X=0}"
            for r in ${AB_ROUNDS:-1}; do for E in "${VS[@]}"; do
