@@ -373,6 +373,46 @@ __global__ __launch_bounds__(EDGE_THREADS) void f_acoustic_edges(Dims d, Ptrs p)
   }
 }
 
+// k_mono_edges1_p's loads and stores for a pair of scalars (nq = 2): the stencil rows once, per scalar
+// 10 stencil columns of the new scalar and the edge's two cells of the old one, three flux arrays
+// stored (round 5: two), a plain sum for the arithmetic
+__global__ __launch_bounds__(EDGE_THREADS) void f_mono_edges1(Dims d, Ptrs p, int is, int nq, MonoFlux2 f2) {
+  const int eA = PAIR_EPW * pair_wave();
+  if (eA >= d.nEdges) return;
+  const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
+  const int eB = hasB ? eA + 1 : eA;
+  const int K = d.K, h = pair_half(), l = pair_lane();
+  const int lc = min(l, K / 2 - 1);
+  const int e = sel(h, eA, eB);
+  const size_t o = (size_t)e * K + 2 * lc;
+  const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
+  const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
+  int ic[10];
+  double a[10], b[10];
+  ld_row(p.advCellsForEdge + (size_t)e * 15, ic);
+  ld_row(p.adv_coefs + (size_t)e * 15, a);
+  ld_row(p.adv_coefs_3rd + (size_t)e * 15, b);
+  const d2 uh = ld2(p.ruAvg + o);
+  const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
+  const int ns = d.ns;
+#pragma unroll 1
+  for (int q = 0; q < nq; ++q) {
+    const int iq = is + q;
+    d2 acc = uh;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const d2 v = ld2(p.scalars2 + SIX(ic[j], 2 * lc, iq));
+      acc.x += (a[j] + b[j]) * v.x;
+      acc.y += (a[j] - b[j]) * v.y;
+    }
+    const d2 s1 = ld2(p.scalars1 + SIX(c1, 2 * lc, iq)), s2 = ld2(p.scalars1 + SIX(c2, 2 * lc, iq));
+    if ((h == 0 || hasB) && 2 * l < K) {
+      st2((q ? f2.flux_arr : p.flux_arr) + o, acc);
+      st2((q ? f2.flux_upwind_tmp : p.flux_upwind_tmp) + o, d2{s1.x + s2.x, s1.y + s2.y});
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: %s DUMPDIR [reps] [rounds]\n", argv[0]);
@@ -459,6 +499,15 @@ int main(int argc, char** argv) {
   p.ke = dev_field(cK, seed++);
   p.h_divergence = dev_field(cK, seed++);
   p.scalars2 = dev_field(cK * ns, seed++);
+  p.scalars1 = dev_field(cK * ns, seed++);
+  double* fl2[3];
+  for (double*& f : fl2) f = dev_field(eK, seed++);
+  const MonoFlux2 mf2{fl2[0], fl2[1], fl2[2]};
+  p.flux_arr = dev_field(eK, seed++);
+  p.flux_upwind_tmp = dev_field(eK, seed++);
+  p.flux_tmp = dev_field(eK, seed++);
+  p.bdyMaskEdge = dev(std::vector<int>(nE + 1, 0));
+  p.dvEdge = dev_field(nE + 1, seed++);  // k_mono_edges1_p's upwind flux
   for (double** f : {&p.ru, &p.ruAvg, &p.advflux_w, &p.advflux_th, &p.rho_edge, &p.u2, &p.pv_edge, &p.tend_u_euler,
                      &p.tend_u, &p.ru_p, &p.cqu})
     *f = dev_field(eK, seed++);
@@ -520,6 +569,10 @@ int main(int argc, char** argv) {
                                 UnpackMap{}); },
        {}},
       {"acoustic edges fl", [&] { hipLaunchKernelGGL(f_acoustic_edges, grid, blk, 0, 0, d, p); }, {}},
+      {"mono edges1 x2", [&] { hipLaunchKernelGGL((k_mono_edges1_p<10, false>), grid, blk, 0, 0, d, p, 0, 30.0,
+                                                  ns >= 2 ? 2 : 1, mf2); }, {}},
+      {"mono edges1 x2 fl", [&] { hipLaunchKernelGGL(f_mono_edges1, grid, blk, 0, 0, d, p, 0, ns >= 2 ? 2 : 1, mf2); },
+       {}},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
