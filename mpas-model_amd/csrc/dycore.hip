@@ -16,6 +16,7 @@
 #include <string>
 #include <tuple>
 #include <vector>
+#include <unistd.h>
 
 // The library links two builds of this file (gen_api.py): MPAS_API_TAG=n, one wavefront per
 // column (nVertLevels 4..63), and MPAS_API_TAG=w with MPAS_WIDE, one workgroup per column
@@ -127,6 +128,18 @@ struct XPlan {
   int fused_rec = 0;  // 1: the 876-887 exchange, 2: the tend_u exchange (642)
   std::vector<XPack> rpk_cell, rpk_edge;
   std::vector<XUnpack> rup_cell, rup_edge;
+  // one-sided transfer (mpas_dyc_ctx::p2p, halo.hip k_p2p_post / k_p2p_get): the send buffer is
+  // uncached memory the peers map; p2p_id < 0 until p2p_setup has exchanged the mappings
+  bool p2p = false;
+  int p2p_id = -1;
+  unsigned long long* p2p_cnt = nullptr;  // [0] use counter, [1 + i] chunks pulled from get peer i
+  P2PGet* d_get = nullptr;
+  int nget = 0, get_chunks = 0;
+  unsigned long long** d_ready = nullptr;  // the ready flags this rank raises (one per receiving rank)
+  int nready = 0;
+  const unsigned long long** d_cons = nullptr;  // the consumed flags this rank waits for
+  int ncons = 0;
+  std::vector<void*> p2p_mapped;  // the peers' send buffers mapped here (IPC)
 };
 
 // One field of an exchange point: mpas_dmpar_exch_halo_field(field[, haloLayers]).
@@ -165,6 +178,17 @@ struct mpas_dyc_ctx {
   // this rank itself over a one-rank communicator (the halo receives this rank's own send data)
   // (=2: each pair is a hipMemcpyAsync instead of RCCL, to separate RCCL's own cost)
   int loopback = 0;
+  // MPAS_DYCORE_P2P=1: messages between ranks of one node are pulled over xGMI by the receiving
+  // rank's kernel (halo.hip k_p2p_get) instead of RCCL groups; RCCL stays for the set-up all-gathers
+  int p2p = 0;
+  unsigned long long* p2p_flags = nullptr;          // this rank's flag arena (uncached): [id][rank][2]
+  std::vector<unsigned long long*> p2p_peer_flags;  // by rank: the arenas of the peers, mapped here
+  std::vector<void*> p2p_mapped;                    // IPC mappings of the peers' arenas
+  int p2p_nr = 0;                                   // rank stride of the arena
+  int p2p_next = 0;                                 // the next exchange point's id
+  int* p2p_status = nullptr;                        // set by a wait that timed out (halo.hip)
+  std::vector<XField> p2p_open;                     // a split-phase p2p exchange between post and get
+  bool p2p_pending = false;
   // MPAS_DYCORE_LATE_ISSUE=1: a split-phase exchange is enqueued on the exchange stream at its
   // exchange_wait, after the compute kernels it overlaps (the same dependencies; only the order in
   // which a captured graph's nodes are created changes)
@@ -576,7 +600,9 @@ const XList* find_list(const Block& b, int loc, int layer, int dir, int peer_ran
 }
 
 void free_plan(XPlan& pl) {
-  for (void* p : {(void*)pl.d_pre, (void*)pl.d_post, (void*)pl.sendbuf, (void*)pl.recvbuf})
+  for (void* p : pl.p2p_mapped) (void)hipIpcCloseMemHandle(p);
+  for (void* p : {(void*)pl.d_pre, (void*)pl.d_post, (void*)pl.sendbuf, (void*)pl.recvbuf, (void*)pl.p2p_cnt,
+                  (void*)pl.d_get, (void*)pl.d_ready, (void*)pl.d_cons})
     if (p) (void)hipFree(p);
   for (void* p : pl.pack_mem) (void)hipFree(p);
   pl = XPlan{};
@@ -877,7 +903,14 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   merge_by_rank(pl.rrecv, post_off);
   if (ctx->host_only) return MPAS_DYC_OK;  // the dry run keeps the message lists only
   if (ctx->loopback) stotal = rtotal = stotal + rtotal;  // rccl_group's loopback pairs stay inside
-  if (stotal) HIPCHK(hipMalloc(&pl.sendbuf, stotal * sizeof(double)));
+  pl.p2p = ctx->p2p && (!pl.rsend.empty() || !pl.rrecv.empty());
+  if (pl.p2p) {
+    // read by the peers over xGMI: uncached, so the producer's stores are in HBM when its kernel ends
+    HIPCHK(hipExtMallocWithFlags((void**)&pl.sendbuf, std::max<int64_t>(stotal, 1) * sizeof(double) + 256,
+                                 hipDeviceMallocUncached));
+  } else if (stotal) {
+    HIPCHK(hipMalloc(&pl.sendbuf, stotal * sizeof(double)));
+  }
   // 256 B of slack: a fused unpack (ld_pp) reads the two levels of its lane's pair, one past the
   // last column at an odd K
   if (rtotal) HIPCHK(hipMalloc(&pl.recvbuf, rtotal * sizeof(double) + 256));
@@ -1126,7 +1159,215 @@ int rccl_group(mpas_dyc_ctx* ctx, const XPlan& pl) {
   return MPAS_DYC_OK;
 }
 
-int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
+// ---------------------------------------------------------------------------
+// one-sided transfer set-up (MPAS_DYCORE_P2P, halo.hip): collective, outside graph capture
+// ---------------------------------------------------------------------------
+constexpr int P2P_MAX_POINTS = 4096;  // exchange points per context (a run builds ~60)
+
+// nbytes from every rank, in rank order, over the library's communicator
+int allgather_bytes(mpas_dyc_ctx* ctx, const void* mine, size_t nbytes, std::vector<char>& all) {
+  all.assign(nbytes * ctx->nranks, 0);
+  if (ctx->nranks == 1) {
+    memcpy(all.data(), mine, nbytes);
+    return MPAS_DYC_OK;
+  }
+  char* d = nullptr;
+  HIPCHK(hipMalloc(&d, nbytes * (ctx->nranks + 1)));
+  const int r = [&]() -> int {
+    HIPCHK(hipMemcpy(d, mine, nbytes, hipMemcpyHostToDevice));
+    NCCLCHK(ncclAllGather(d, d + nbytes, nbytes, ncclUint8, ctx->comm, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMemcpy(all.data(), d + nbytes, nbytes * ctx->nranks, hipMemcpyDeviceToHost));
+    return MPAS_DYC_OK;
+  }();
+  (void)hipFree(d);
+  return r;
+}
+
+// the node a rank runs on: IPC mappings exist only between processes of one node
+uint64_t node_id() {
+  char buf[512] = {0};
+  (void)gethostname(buf, 255);
+  if (FILE* f = fopen("/proc/sys/kernel/random/boot_id", "r")) {
+    const size_t n = strlen(buf);
+    if (!fgets(buf + n, (int)(sizeof(buf) - n - 1), f)) buf[n] = 0;
+    fclose(f);
+  }
+  uint64_t h = 1469598103934665603ull;
+  for (const char* c = buf; *c; ++c) h = (h ^ (unsigned char)*c) * 1099511628211ull;
+  return h;
+}
+
+// the flag arenas: this rank's, and every peer's mapped here
+int p2p_init(mpas_dyc_ctx* ctx) {
+  if (ctx->p2p_flags) return MPAS_DYC_OK;
+  if (!ctx->comm) {
+    ctx->err = "MPAS_DYCORE_P2P: no communicator for the set-up (mpas_dyc_comm_init)";
+    return MPAS_DYC_ECOMM;
+  }
+  int nr = ctx->nranks;
+  if (ctx->loopback)  // the emulated peers are ranks the lists name, beyond this one-rank communicator
+    for (const auto& b : ctx->blk)
+      for (const auto& x : b.xl) nr = std::max(nr, x.peer_rank + 1);
+  ctx->p2p_nr = nr;
+  const size_t bytes = (size_t)P2P_MAX_POINTS * nr * 2 * sizeof(unsigned long long);
+  HIPCHK(hipExtMallocWithFlags((void**)&ctx->p2p_flags, bytes, hipDeviceMallocUncached));
+  HIPCHK(hipMemset(ctx->p2p_flags, 0, bytes));
+  HIPCHK(hipMalloc(&ctx->p2p_status, sizeof(int)));
+  HIPCHK(hipMemset(ctx->p2p_status, 0, sizeof(int)));
+  HIPCHK(hipDeviceSynchronize());
+  ctx->p2p_peer_flags.assign(ctx->nranks, nullptr);
+  ctx->p2p_peer_flags[ctx->rank] = ctx->p2p_flags;
+  if (ctx->nranks == 1) return MPAS_DYC_OK;
+  struct Rec {
+    hipIpcMemHandle_t h;
+    uint64_t node;
+  } rec{};
+  HIPCHK(hipIpcGetMemHandle(&rec.h, ctx->p2p_flags));
+  rec.node = node_id();
+  std::vector<char> all;
+  CHK(allgather_bytes(ctx, &rec, sizeof(rec), all));
+  for (int r = 0; r < ctx->nranks; ++r) {
+    const Rec& o = *(const Rec*)(all.data() + r * sizeof(Rec));
+    if (o.node != rec.node) {
+      ctx->err = "MPAS_DYCORE_P2P: rank " + std::to_string(r) + " runs on another node (one-sided transfer is intra-node)";
+      return MPAS_DYC_ECOMM;
+    }
+    if (r == ctx->rank) continue;
+    void* p = nullptr;
+    HIPCHK(hipIpcOpenMemHandle(&p, o.h, hipIpcMemLazyEnablePeerAccess));
+    ctx->p2p_mapped.push_back(p);
+    ctx->p2p_peer_flags[r] = (unsigned long long*)p;
+  }
+  return MPAS_DYC_OK;
+}
+
+// Maps the send buffers of the exchange points built since the last call and uploads their get /
+// post tables.  Every rank builds the same exchange points in the same (plan key) order; the count
+// is checked, and every message's size against its sender's.
+int p2p_setup(mpas_dyc_ctx* ctx) {
+  std::vector<XPlan*> todo;
+  for (auto& kv : ctx->plans)
+    if (kv.second.p2p && kv.second.p2p_id < 0) todo.push_back(&kv.second);
+  CHK(p2p_init(ctx));
+  const int nr = ctx->nranks, me = ctx->rank;
+  {
+    int64_t n = (int64_t)todo.size();
+    std::vector<char> all;
+    CHK(allgather_bytes(ctx, &n, sizeof(n), all));
+    for (int r = 0; r < nr; ++r)
+      if (((const int64_t*)all.data())[r] != n) {
+        ctx->err = "MPAS_DYCORE_P2P: rank " + std::to_string(r) + " built a different number of exchange points";
+        return MPAS_DYC_ECOMM;
+      }
+  }
+  if (todo.empty()) return MPAS_DYC_OK;
+  // per exchange point: the send buffer's IPC handle, then per rank (offset, count) of the message to it
+  const size_t per = sizeof(hipIpcMemHandle_t) + 2 * sizeof(int64_t) * nr;
+  std::vector<char> mine(per * todo.size(), 0), all;
+  for (size_t i = 0; i < todo.size(); ++i) {
+    char* r = mine.data() + per * i;
+    if (nr > 1) HIPCHK(hipIpcGetMemHandle((hipIpcMemHandle_t*)r, todo[i]->sendbuf));
+    int64_t* oc = (int64_t*)(r + sizeof(hipIpcMemHandle_t));
+    for (int q = 0; q < nr; ++q) oc[2 * q] = oc[2 * q + 1] = -1;
+    for (const XMsg& m : todo[i]->rsend) {
+      oc[2 * m.peer_rank] = m.off;
+      oc[2 * m.peer_rank + 1] = m.count;
+    }
+  }
+  CHK(allgather_bytes(ctx, mine.data(), mine.size(), all));
+  for (size_t i = 0; i < todo.size(); ++i) {
+    XPlan& pl = *todo[i];
+    if (ctx->p2p_next >= P2P_MAX_POINTS) {
+      ctx->err = "MPAS_DYCORE_P2P: more than " + std::to_string(P2P_MAX_POINTS) + " exchange points";
+      return MPAS_DYC_ESTATE;
+    }
+    pl.p2p_id = ctx->p2p_next++;
+    auto flag = [&](unsigned long long* arena, int r, int k) {
+      return arena + ((size_t)pl.p2p_id * ctx->p2p_nr + r) * 2 + k;
+    };
+    auto nchunk = [](int64_t n) { return (int)std::max<int64_t>(1, (n + P2P_CHUNK - 1) / P2P_CHUNK); };
+    std::vector<P2PGet> gets;
+    std::vector<unsigned long long*> ready;
+    std::vector<const unsigned long long*> cons;
+    if (ctx->loopback) {
+      // as rccl_group: one pair per emulated peer of max(send, receive) doubles, all in this rank
+      std::map<int, std::pair<const XMsg*, const XMsg*>> peers;
+      for (const XMsg& m : pl.rsend) peers[m.peer_rank].first = &m;
+      for (const XMsg& m : pl.rrecv) peers[m.peer_rank].second = &m;
+      for (const auto& kv : peers) {
+        const XMsg *sm = kv.second.first, *rm = kv.second.second;
+        const int64_t n = std::max(sm ? sm->count : 0, rm ? rm->count : 0);
+        gets.push_back(P2PGet{pl.sendbuf + (sm ? sm->off : 0), pl.recvbuf + (rm ? rm->off : 0), n,
+                              flag(ctx->p2p_flags, kv.first, 0), flag(ctx->p2p_flags, kv.first, 1), nullptr, nchunk(n)});
+        ready.push_back(flag(ctx->p2p_flags, kv.first, 0));
+        cons.push_back(flag(ctx->p2p_flags, kv.first, 1));
+      }
+    } else {
+      for (const XMsg& m : pl.rsend) {
+        ready.push_back(flag(ctx->p2p_peer_flags[m.peer_rank], me, 0));
+        cons.push_back(flag(ctx->p2p_flags, m.peer_rank, 1));
+      }
+      for (const XMsg& m : pl.rrecv) {
+        const char* rr = all.data() + (size_t)m.peer_rank * mine.size() + per * i;
+        const int64_t* oc = (const int64_t*)(rr + sizeof(hipIpcMemHandle_t));
+        if (oc[2 * me + 1] != m.count) {
+          ctx->err = "MPAS_DYCORE_P2P: rank " + std::to_string(m.peer_rank) + " sends " + std::to_string(oc[2 * me + 1]) +
+                     " doubles where this rank receives " + std::to_string(m.count);
+          return MPAS_DYC_ECOMM;
+        }
+        const double* base = pl.sendbuf;
+        if (m.peer_rank != me) {
+          void* p = nullptr;
+          HIPCHK(hipIpcOpenMemHandle(&p, *(const hipIpcMemHandle_t*)rr, hipIpcMemLazyEnablePeerAccess));
+          pl.p2p_mapped.push_back(p);
+          base = (const double*)p;
+        }
+        gets.push_back(P2PGet{base + oc[2 * me], pl.recvbuf + m.off, m.count, flag(ctx->p2p_flags, m.peer_rank, 0),
+                              flag(ctx->p2p_peer_flags[m.peer_rank], me, 1), nullptr, nchunk(m.count)});
+      }
+    }
+    if (cons.size() > 256) {
+      ctx->err = "MPAS_DYCORE_P2P: more than 256 peers";
+      return MPAS_DYC_EINVAL;
+    }
+    HIPCHK(hipMalloc(&pl.p2p_cnt, (1 + gets.size()) * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(pl.p2p_cnt, 0, (1 + gets.size()) * sizeof(unsigned long long)));
+    for (size_t j = 0; j < gets.size(); ++j) {
+      gets[j].done = pl.p2p_cnt + 1 + j;
+      pl.get_chunks = std::max(pl.get_chunks, gets[j].nchunk);
+    }
+    pl.nget = (int)gets.size();
+    pl.nready = (int)ready.size();
+    pl.ncons = (int)cons.size();
+    auto upload = [&](const void* h, size_t bytes, void** d) -> int {
+      HIPCHK(hipMalloc(d, std::max<size_t>(bytes, 8)));
+      if (bytes) HIPCHK(hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice));
+      return MPAS_DYC_OK;
+    };
+    CHK(upload(gets.data(), gets.size() * sizeof(P2PGet), (void**)&pl.d_get));
+    CHK(upload(ready.data(), ready.size() * sizeof(void*), (void**)&pl.d_ready));
+    CHK(upload(cons.data(), cons.size() * sizeof(void*), (void**)&pl.d_cons));
+  }
+  return MPAS_DYC_OK;
+}
+
+// p2p_status: a wait of k_p2p_get that timed out
+int p2p_check(mpas_dyc_ctx* ctx) {
+  if (!ctx->p2p_status) return MPAS_DYC_OK;
+  int st = 0;
+  HIPCHK(hipMemcpy(&st, ctx->p2p_status, sizeof(int), hipMemcpyDeviceToHost));
+  if (st) {
+    ctx->err = std::string("MPAS_DYCORE_P2P: a peer's halo message did not arrive within 30 s (last exchange: ") +
+               ctx->last_key + ")";
+    return MPAS_DYC_ECOMM;
+  }
+  return MPAS_DYC_OK;
+}
+
+// part: 0 the whole exchange; with one-sided transfer a split-phase exchange runs as 1 (pack and
+// post, at exchange_async) and 2 (get and unpack, at exchange_wait), all on the compute stream
+int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, int part = 0) {
   if (!needs_exchange(ctx)) return MPAS_DYC_OK;
   const std::string key = plan_key(ctx, fs);
   if (ctx->record) ctx->record->push_back(key);
@@ -1148,6 +1389,36 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   }
   if (ctx->planning) return MPAS_DYC_OK;
   XPlan& pl = it->second;
+  if (pl.p2p) {
+    if (pl.p2p_id < 0) {  // built outside plan_all (mpas_dyc_halo_exchange): every rank is here too
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(ctx->stream, &cs);
+      if (cs != hipStreamCaptureStatusNone) {
+        ctx->err = "internal: one-sided exchange set up during graph capture";
+        return MPAS_DYC_ESTATE;
+      }
+      CHK(p2p_setup(ctx));
+    }
+    if (part != 2) {
+      if (part == 0) CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
+      if (pl.npre && !pl.fused_pack)
+        hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_pre + 3) / 4, pl.npre), dim3(256), 0, ctx->stream, pl.d_pre);
+      set_last_key(ctx, key);
+      hipLaunchKernelGGL(k_p2p_post, dim3(1), dim3(64), 0, ctx->stream, pl.p2p_cnt, pl.d_ready, pl.nready);
+    }
+    if (part != 1) {
+      CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
+      hipLaunchKernelGGL(k_p2p_get, dim3(std::max(pl.get_chunks, 1), pl.nget + 1), dim3(256), 0, ctx->stream,
+                         (const P2PGet*)pl.d_get, pl.nget, (const unsigned long long* const*)pl.d_cons, pl.ncons,
+                         (const unsigned long long*)pl.p2p_cnt, ctx->p2p_status);
+      CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
+      if (pl.npost && !pl.fused_unpack)
+        hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_post + 3) / 4, pl.npost), dim3(256), 0, ctx->stream, pl.d_post);
+      if (part == 0) CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
+    }
+    return MPAS_DYC_OK;
+  }
+  if (part == 2) return MPAS_DYC_OK;  // in-process copies only: done at part 1
   const bool whole = !ctx->in_async;  // a blocking exchange: all of it is exposed
   if (whole) CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
   if (pl.npre && !pl.fused_pack)
@@ -1347,6 +1618,7 @@ int compute_bnd(mpas_dyc_ctx* ctx) {
 bool split_phase(const mpas_dyc_ctx* ctx) {
   if (!needs_exchange(ctx)) return false;
   if (ctx->overlap >= 0) return ctx->overlap != 0;
+  if (ctx->p2p) return false;  // the transfer is the receiver's kernel: nothing to overlap it with
   return ctx->nranks > 1 || ctx->rccl_local || ctx->loopback;
 }
 
@@ -1367,6 +1639,11 @@ int issue_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
 
 int exchange_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
   if (ctx->planning) return exchange(ctx, fs);
+  if (ctx->p2p) {  // no second stream: pack and post now, the get at exchange_wait
+    ctx->p2p_open = fs;
+    ctx->p2p_pending = true;
+    return exchange(ctx, fs, 1);
+  }
   HIPCHK(hipEventRecord(ctx->xfork, ctx->stream));
   if (ctx->late_issue) {
     ctx->late_fs = fs;
@@ -1378,6 +1655,13 @@ int exchange_async(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
 
 int exchange_wait(mpas_dyc_ctx* ctx) {
   if (ctx->planning) return MPAS_DYC_OK;
+  if (ctx->p2p_pending) {
+    ctx->p2p_pending = false;
+    CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
+    CHK(exchange(ctx, ctx->p2p_open, 2));
+    CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
+    return MPAS_DYC_OK;
+  }
   if (ctx->late_pending) {
     ctx->late_pending = false;
     CHK(issue_async(ctx, ctx->late_fs));
@@ -2461,7 +2745,7 @@ int warm_rccl(mpas_dyc_ctx* ctx) {
     XPlan& pl = kv.second;
     if (pl.warmed) continue;
     pl.warmed = true;
-    if (pl.rsend.empty() && pl.rrecv.empty()) continue;
+    if (pl.p2p || (pl.rsend.empty() && pl.rrecv.empty())) continue;
     set_last_key(ctx, "warm_rccl " + kv.first);
     CHK(rccl_group(ctx, pl));
     // one group at a time: a group that never completes names its plan in last_key
@@ -2519,7 +2803,8 @@ int plan_all(mpas_dyc_ctx* ctx, double dt) {
   restore_layout(l);
   if (r == MPAS_DYC_OK) {
     ctx->planned.insert(sig);
-    r = warm_rccl(ctx);
+    r = ctx->p2p ? p2p_setup(ctx) : MPAS_DYC_OK;
+    if (r == MPAS_DYC_OK) r = warm_rccl(ctx);
   }
   return r;
 }
@@ -2585,6 +2870,7 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   if (const char* mf = getenv("MPAS_DYCORE_MONO_FUSE")) g_mono_fuse = std::atoi(mf);
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
   if (const char* lb = getenv("MPAS_DYCORE_LOOPBACK")) ctx->loopback = std::atoi(lb);
+  if (const char* pp = getenv("MPAS_DYCORE_P2P")) ctx->p2p = std::atoi(pp);
   if (const char* li = getenv("MPAS_DYCORE_LATE_ISSUE")) ctx->late_issue = std::string(li) == "1";
   if (const char* oa = getenv("MPAS_DYCORE_OVERLAP_ALL")) ctx->overlap_all = std::string(oa) == "1";
   if (const char* ov = getenv("MPAS_DYCORE_OVERLAP")) ctx->overlap = std::atoi(ov);
@@ -2641,6 +2927,9 @@ void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
     if (b.sum_out) (void)hipFree(b.sum_out);
   }
   if (ctx->sum_gather) (void)hipFree(ctx->sum_gather);
+  for (void* p : ctx->p2p_mapped) (void)hipIpcCloseMemHandle(p);
+  if (ctx->p2p_flags) (void)hipFree(ctx->p2p_flags);
+  if (ctx->p2p_status) (void)hipFree(ctx->p2p_status);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -3628,7 +3917,7 @@ int mpas_dyc_synchronize(mpas_dyc_ctx* ctx) {
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->xstream));
-  return MPAS_DYC_OK;
+  return p2p_check(ctx);
 }
 
 int mpas_dyc_set_overlap(mpas_dyc_ctx* ctx, int32_t on) {

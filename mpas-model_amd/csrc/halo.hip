@@ -36,6 +36,94 @@ __global__ __launch_bounds__(256) void k_halo_copy(const XSeg* __restrict__ segs
   for (int j = threadIdx.x & 63; j < inner; j += 64) dst[j] = src[j];
 }
 
+// ---------------------------------------------------------------------------
+// One-sided halo transfer between the ranks of one node (MPAS_DYCORE_P2P): the messages of an
+// exchange point are pulled over xGMI by the receiving rank's kernel, with no RCCL group, no second
+// stream and no host involvement, so a step stays one captured graph of kernels.
+//
+// Per exchange point and rank: a send buffer in uncached device memory (fine-grained, so the peers'
+// reads see the producer's stores once its kernel has ended), mapped into every peer that reads it
+// (IPC); and a flag arena of the same kind per rank, [plan][sender rank][ready, consumed].  A use n
+// of an exchange point (the n-th time the step runs it; every rank runs the same sequence):
+//   k_p2p_post (after the pack or the fused producer): n = ++use counter; ready[plan][me] = n in the
+//     arena of every rank this rank sends to;
+//   k_p2p_get (where the halo is needed): per peer, wait for ready[plan][peer] >= n in this rank's
+//     arena, copy the peer's message from its send buffer into this rank's receive buffer (ordinary
+//     device memory: the unpack or the fused consumer reads it as before), and when the last chunk
+//     of that peer is in, set consumed[plan][me] = n in the peer's arena; one more workgroup waits
+//     for consumed[plan][r] >= n from every rank r this rank sends to, so the kernel ends only when
+//     this rank's send buffer may be written again (the next use's producer comes after it).
+// Every rank raises its flags before it waits on its peers', and all ranks run the exchange points
+// in one order, so the waits resolve.  A wait that has not resolved after P2P_TIMEOUT_S seconds sets
+// the context's status word and gives up (and so does every later wait): the host reports the error
+// (mpas_dyc_synchronize) instead of a hung GPU.
+constexpr unsigned long long P2P_TIMEOUT_TICKS = 30ull * 100000000ull;  // wall_clock64 runs at 100 MHz
+constexpr int P2P_CHUNK = 8192;                                          // doubles per workgroup
+
+struct P2PGet {
+  const double* src;                  // the peer's send buffer: its message to this rank
+  double* dst;                        // this rank's receive buffer: the message from that peer
+  long long count;                    // doubles
+  const unsigned long long* ready;    // raised by the peer's post (this rank's arena)
+  unsigned long long* consumed;       // raised here once the message is copied (the peer's arena)
+  unsigned long long* done;           // chunks copied so far, over all uses (local)
+  int nchunk;
+};
+
+__device__ inline bool p2p_wait_geq(const unsigned long long* f, unsigned long long n, int* status) {
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < n) {
+    if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    if (wall_clock64() - t0 > P2P_TIMEOUT_TICKS) {
+      atomicOr(status, 1);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  return true;
+}
+
+// use[0]: this exchange point's use counter (read by the get of the same use, later on the stream)
+__global__ __launch_bounds__(64) void k_p2p_post(unsigned long long* use, unsigned long long* const* ready, int npeer) {
+  const unsigned long long n = use[0] + 1;
+  __syncthreads();
+  if (threadIdx.x == 0) use[0] = n;
+  for (int i = threadIdx.x; i < npeer; i += 64) {
+    __threadfence_system();
+    __hip_atomic_store(ready[i], n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// grid (max chunks, nget + 1): row y < nget pulls chunk x of peer y; row nget waits for the peers
+// that pull from this rank (one lane per peer)
+__global__ __launch_bounds__(256) void k_p2p_get(const P2PGet* __restrict__ g, int nget,
+                                                 const unsigned long long* const* consumed, int ncons,
+                                                 const unsigned long long* use, int* status) {
+  const unsigned long long n = use[0];
+  if ((int)blockIdx.y == nget) {
+    if (blockIdx.x == 0 && (int)threadIdx.x < ncons) (void)p2p_wait_geq(consumed[threadIdx.x], n, status);
+    return;
+  }
+  const P2PGet& p = g[blockIdx.y];
+  if ((int)blockIdx.x >= p.nchunk) return;
+  __shared__ int ok;
+  if (threadIdx.x == 0) ok = p2p_wait_geq(p.ready, n, status);
+  __syncthreads();
+  if (!ok) return;
+  const long long c0 = (long long)blockIdx.x * P2P_CHUNK;
+  const long long c1 = min(p.count, c0 + P2P_CHUNK);
+  for (long long i = c0 + threadIdx.x; i < c1; i += 256) p.dst[i] = p.src[i];
+  __syncthreads();  // every lane's loads have returned (their values are stored)
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned long long old = atomicAdd(p.done, 1ull);
+    if (old + 1 == n * (unsigned long long)p.nchunk) {
+      __threadfence_system();
+      __hip_atomic_store(p.consumed, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // atm_rk_integration_setup (mpas_atm_time_integration.F:1847-1857): the ten state/diag
 // copies of one block in a single launch; blockIdx.y selects the copy.
 struct CopyList {

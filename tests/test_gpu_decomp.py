@@ -189,3 +189,27 @@ def test_fused_exchanges_keep_halo_fields(small_case):
         dy.close()
     for key in runs[1]:
         assert np.array_equal(runs[0][key], runs[1][key]), f"{key}: fused exchange differs from pack/unpack kernels"
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("which", ["small_case", "moist_case"])
+def test_p2p_transport_bitwise(which, overlap, request):
+    """One-sided transfer (MPAS_DYCORE_P2P=1; halo.hip k_p2p_post / k_p2p_get): 4 blocks of one rank
+    whose messages all go through the one-sided protocol -- the post raises this rank's ready flags,
+    the get pulls each message from the uncached send buffer, raises the consumed flag and waits for
+    the others' -- equal one block bit for bit, graph replay, blocking exchanges (the p2p default) and
+    split-phase (post at the exchange, get where the halo is read)."""
+    import os
+    case = request.getfixturevalue(which)
+    one = _single(case, 3)
+    old = os.environ.get("MPAS_DYCORE_P2P")
+    os.environ["MPAS_DYCORE_P2P"] = "1"
+    try:
+        got = _blocks(case, 4, 3, graph=True, rccl_local=True, overlap=overlap)
+    finally:
+        if old is None:
+            os.environ.pop("MPAS_DYCORE_P2P", None)
+        else:
+            os.environ["MPAS_DYCORE_P2P"] = old
+    for name in one:
+        assert np.array_equal(got[name], one[name]), f"{name}: p2p blocks differ from one block"
