@@ -190,6 +190,9 @@ def main():
     ap.add_argument("--acoustic-reps", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=1, help="blocks per GPU (MPAS blocks with halos)")
     ap.add_argument("--rccl-local", action="store_true", help="route in-process block exchanges through RCCL")
+    ap.add_argument("--transport", choices=("rccl", "p2p"), default="rccl",
+                    help="halo messages between ranks: RCCL send/recv groups, or the one-sided intra-node "
+                         "transfer (mpas_dyc_set_p2p: pulled over xGMI by the receiving rank's kernel)")
     ap.add_argument("--no-configs1", action="store_true",
                     help="skip the secondary x1.10242 (BASELINE.json configs[1]) measurement")
     ap.add_argument("--preflight-only", action="store_true",
@@ -288,7 +291,8 @@ def main():
         torch.cuda.set_device(device)
         wd.phase("rccl_init (ncclCommInitRank) and upload", args.phase_timeout)
         dy = Dycore.from_blocks(blocks, device=device, placement=placement, rank=rank, nranks=world,
-                                comm_id=comm_id, moist_end=moist_end, rccl_local=args.rccl_local)
+                                comm_id=comm_id, moist_end=moist_end, rccl_local=args.rccl_local,
+                                p2p=args.transport == "p2p")
         owned = sum(b.solve[0] for b in blocks)
         halo = sum(b.case["nCells"] - b.solve[0] for b in blocks)
     else:
@@ -404,7 +408,9 @@ def main():
             "dt": dt, "time_integration_order": case["config"]["config_time_integration_order"],
             "split_steps": case["config"]["config_dynamics_split_steps"], "acoustic_substeps": nss,
             "parallelism": (f"domain decomposition: {nparts} SFC blocks with 2-layer halos, "
-                            f"{args.blocks} per GPU, halo exchange over RCCL" if nparts > 1 else "single block"),
+                            f"{args.blocks} per GPU, halo exchange " +
+                            ("one-sided over xGMI (IPC)" if args.transport == "p2p" else "over RCCL")
+                            if nparts > 1 else "single block"),
             "owned_cells_rank0": owned, "halo_cells_rank0": halo,
             "hip_graph": graph,
             "maxEdges_declared": [case["maxEdges"], case["maxEdges2"]],

@@ -301,6 +301,17 @@ int mpas_dyc_comm_unique_id(void* id, int64_t nbytes);
 int mpas_dyc_comm_init(mpas_dyc_ctx* ctx, const void* id, int64_t nbytes, int32_t nranks, int32_t rank);
 /* Test hook: route block-to-block exchanges inside this process through RCCL (send to self). */
 int mpas_dyc_set_transport(mpas_dyc_ctx* ctx, int32_t rccl_for_local_blocks);
+/* One-sided transfer between the ranks of one node (on = 1; 0 = RCCL groups; -1 = the environment
+ * variable MPAS_DYCORE_P2P, read at context creation, default 0).  Replaces the ncclSend / ncclRecv
+ * groups of every exchange point by two kernels (halo.hip): after the pack, k_p2p_post raises a flag
+ * in each receiving rank's arena; where the halo is needed, k_p2p_get pulls each peer's message from
+ * the peer's send buffer (uncached device memory, IPC-mapped at set-up) and waits until this rank's
+ * own buffer has been pulled.  Same messages, buffer layouts and order as the RCCL path (the plans
+ * are the ones mpas_dyc_plan_exchanges reports).  Set-up runs once per exchange-plan build, over the
+ * communicator of mpas_dyc_comm_init (all-gathers of IPC handles); all ranks must be on one node
+ * (checked: MPAS_DYC_ECOMM otherwise).  A message that does not arrive within 30 s makes
+ * mpas_dyc_synchronize return MPAS_DYC_ECOMM.  Collective: every rank calls it with the same value. */
+int mpas_dyc_set_p2p(mpas_dyc_ctx* ctx, int32_t on);
 /* Split-phase exchanges: at the tend_u, rho_pp and rtheta_pp exchanges the interior
  * elements are computed while the halo traffic runs on a second stream.  on = 1 / 0;
  * -1 (default) = automatic: on when exchanges go through RCCL (more than one rank). */

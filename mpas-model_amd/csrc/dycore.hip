@@ -1271,6 +1271,7 @@ int p2p_setup(mpas_dyc_ctx* ctx) {
     int64_t* oc = (int64_t*)(r + sizeof(hipIpcMemHandle_t));
     for (int q = 0; q < nr; ++q) oc[2 * q] = oc[2 * q + 1] = -1;
     for (const XMsg& m : todo[i]->rsend) {
+      if (m.peer_rank >= nr) continue;  // loopback: emulated ranks beyond the communicator
       oc[2 * m.peer_rank] = m.off;
       oc[2 * m.peer_rank + 1] = m.count;
     }
@@ -3918,6 +3919,14 @@ int mpas_dyc_synchronize(mpas_dyc_ctx* ctx) {
   HIPCHK(hipStreamSynchronize(ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->xstream));
   return p2p_check(ctx);
+}
+
+int mpas_dyc_set_p2p(mpas_dyc_ctx* ctx, int32_t on) {
+  if (!ctx) return MPAS_DYC_EINVAL;
+  if (on < 0) return MPAS_DYC_OK;  // keep what the environment chose at creation
+  invalidate_plans(ctx);
+  ctx->p2p = on != 0;
+  return MPAS_DYC_OK;
 }
 
 int mpas_dyc_set_overlap(mpas_dyc_ctx* ctx, int32_t on) {

@@ -54,11 +54,11 @@ __global__ __launch_bounds__(256) void k_halo_copy(const XSeg* __restrict__ segs
 //     for consumed[plan][r] >= n from every rank r this rank sends to, so the kernel ends only when
 //     this rank's send buffer may be written again (the next use's producer comes after it).
 // Every rank raises its flags before it waits on its peers', and all ranks run the exchange points
-// in one order, so the waits resolve.  A wait that has not resolved after P2P_TIMEOUT_S seconds sets
+// in one order, so the waits resolve.  A wait that has not resolved after 30 s (P2P_TIMEOUT_TICKS) sets
 // the context's status word and gives up (and so does every later wait): the host reports the error
 // (mpas_dyc_synchronize) instead of a hung GPU.
 constexpr unsigned long long P2P_TIMEOUT_TICKS = 30ull * 100000000ull;  // wall_clock64 runs at 100 MHz
-constexpr int P2P_CHUNK = 8192;                                          // doubles per workgroup
+constexpr int P2P_CHUNK = 4096;                                          // doubles per workgroup
 
 struct P2PGet {
   const double* src;                  // the peer's send buffer: its message to this rank
@@ -112,7 +112,15 @@ __global__ __launch_bounds__(256) void k_p2p_get(const P2PGet* __restrict__ g, i
   if (!ok) return;
   const long long c0 = (long long)blockIdx.x * P2P_CHUNK;
   const long long c1 = min(p.count, c0 + P2P_CHUNK);
-  for (long long i = c0 + threadIdx.x; i < c1; i += 256) p.dst[i] = p.src[i];
+  // four loads in flight per lane before the stores (the source is another GPU's memory)
+  for (long long i = c0 + threadIdx.x; i < c1; i += 4 * 256) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = i + u * 256 < c1 ? p.src[i + u * 256] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * 256 < c1) p.dst[i + u * 256] = v[u];
+  }
   __syncthreads();  // every lane's loads have returned (their values are stored)
   if (threadIdx.x == 0) {
     __threadfence();

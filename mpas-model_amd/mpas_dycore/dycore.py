@@ -170,12 +170,13 @@ class Dycore:
     @classmethod
     def from_blocks(cls, blocks: list, device: int = 0, moist_end: int = 1, placement: dict | None = None,
                     rank: int = 0, nranks: int = 1, comm_id: bytes | None = None, rccl_local: bool = False,
-                    positional: bool = False):
+                    positional: bool = False, p2p: bool | None = None):
         """Blocks of this process (``decomp.decompose(..., parts=...)``) on one GPU.
 
         ``placement`` maps every block (part) id to (rank, local block index); by
         default all blocks live in this process, in the given order.  With
-        ``nranks`` > 1, ``comm_id`` is the RCCL unique id created on rank 0."""
+        ``nranks`` > 1, ``comm_id`` is the RCCL unique id created on rank 0.  ``p2p``: one-sided
+        transfer between the ranks of the node (mpas_dyc_set_p2p; None = MPAS_DYCORE_P2P)."""
         if placement is None:
             placement = {b.part: (0, i) for i, b in enumerate(blocks)}
         self = cls(device=device, moist_end=moist_end, _blocks=blocks)
@@ -184,6 +185,8 @@ class Dycore:
             self._check(self.lib.mpas_dyc_comm_init(self.h, idb, len(comm_id), int(nranks), int(rank)), "comm_init")
         if rccl_local:
             self._check(self.lib.mpas_dyc_set_transport(self.h, 1), "set_transport")
+        if p2p is not None:
+            self._check(self.lib.mpas_dyc_set_p2p(self.h, int(bool(p2p))), "set_p2p")
         # positional: the lists with other ranks as mpas_dmpar keeps them for tasks of several blocks (with
         # rccl_local, this process's block pairs too) -- the Fortran drop-in's path
         _install_lists(self.lib, self.h, blocks, placement, self._check, positional_rank=rank if positional else None,
