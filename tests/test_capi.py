@@ -12,7 +12,7 @@ HEADER = os.path.join(ROOT, "include", "mpas_dycore.h")
 
 def declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(mpas_dyc_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(mpas_dyc_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_boundary():
