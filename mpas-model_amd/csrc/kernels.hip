@@ -2563,6 +2563,11 @@ struct MonoFlux2 {
 template <int NA, bool ODD = false>
 __global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, int is, double dt, int nq = 1,
                                                                 MonoFlux2 f2 = MonoFlux2{}) {
+  // the stencil weights of the wave's two edges, a + b and a - b (the two values a + sgn(u) b takes),
+  // in LDS: one row per half-wave, written by its first NA lanes and read as half-wave broadcasts
+  // where the sums use them.  Held in registers, the two rows took 40 VGPRs for the whole kernel
+  // (146 VGPRs, 3 waves per SIMD).
+  __shared__ d2 wts[PAIR_WPB][PAIR_EPW][NA];
   const int eA = PAIR_EPW * pair_wave();
   if (eA >= d.nEdges) return;
   const bool hasB = PAIR_EPW == 2 && eA + 1 < d.nEdges;
@@ -2575,12 +2580,13 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
   const int2 ceA = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eA);
   const int2 ceB = *reinterpret_cast<const int2*>(p.cellsOnEdge + 2 * eB);
   const int na = sel(h, p.nAdvCellsForEdge[eA], p.nAdvCellsForEdge[eB]);
+  d2 (&w)[NA] = wts[threadIdx.x >> 6][h];
+  if (l < NA) {
+    const double a = p.adv_coefs[(size_t)e * 15 + l], b = p.adv_coefs_3rd[(size_t)e * 15 + l];
+    w[l] = d2{a + b, a - b};
+  }
   int ic[NA];
-  double a[NA], b[NA];
-  // the stencil rows as vector loads: 394-404 -> 364-368 us per call
   ld_row(p.advCellsForEdge + (size_t)e * 15, ic);
-  ld_row(p.adv_coefs + (size_t)e * 15, a);
-  ld_row(p.adv_coefs_3rd + (size_t)e * 15, b);
   const double dv = sel(h, ld_uniform_f64(p.dvEdge + eA), ld_uniform_f64(p.dvEdge + eB));
   const d2 uh = ld2(p.ruAvg + o);
   const int c1 = sel(h, ceA.x, ceB.x), c2 = sel(h, ceA.y, ceB.y);
@@ -2589,15 +2595,14 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
   // two outer relaxation rows keep only the upwind flux
   const int bm = sel(h, p.bdyMaskEdge[eA], p.bdyMaskEdge[eB]);
   const bool upw = (d.lbc && bm == N_RELAX_ZONE) || bm == N_RELAX_ZONE - 1;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // nq = 2: the pair's second scalar (is + 1) from the same rows, into the second scratch set
   // (f2), one after the other -- each scalar's operations as in its own launch
 #pragma unroll 1
   for (int q = 0; q < nq; ++q) {
     const int iq = is + q;
-    // the weights a +- b formed per scalar, not hoisted out of the loop (hoisted, they stay live
-    // across it: 180 VGPRs, half the occupancy)
-#pragma unroll
-    for (int j = 0; j < NA; ++j) asm volatile("" : "+v"(a[j]), "+v"(b[j]));
     // scalars outside the block (the garbage slot) read as 0, as the reference's halo loops see them
     auto val = [&](const double* arr, int cc) {
       const d2 v = ld2(arr + SIX(cc, 2 * lc, iq));
@@ -2607,29 +2612,32 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_mono_edges1_p(Dims d, Ptrs p, 
 #pragma unroll
     for (int j = 0; j < NA; ++j) sv[j] = val(p.scalars2, ic[j]);
     const d2 so1 = val(p.scalars1, c1), so2 = val(p.scalars1, c2);
-    auto flux = [&](double u, int lev) {
-      double acc = 0.0;
-      if (na == 10) {
-        const bool up = u > 0;
-#pragma unroll
-        for (int j = 0; j < 10 && j < NA; ++j) {
-          const double swa = up ? (a[j] + b[j]) : (a[j] - b[j]);
-          const double term = swa * (lev ? sv[j].y : sv[j].x);
-          acc = (j == 0) ? term : acc + term;
-        }
-        return u * (acc);
-      }
-      double fa = 0.0;
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        if (j < na) fa = fa + (u * (a[j] + sgn1(u) * b[j])) * (lev ? sv[j].y : sv[j].x);
-      }
-      return fa;
-    };
     d2 fa{0.0, 0.0};
     if (on) {
-      fa.x = flux(uh.x, 0);
-      fa.y = flux(uh.y, 1);
+      if (na == 10) {
+        // sum_j (a_j +- b_j) q_j, then times u (the reference's 10-cell tree)
+        const bool upx = uh.x > 0, upy = uh.y > 0;
+        double ax = 0.0, ay = 0.0;
+#pragma unroll
+        for (int j = 0; j < 10 && j < NA; ++j) {
+          const d2 wj = w[j];
+          const double tx = (upx ? wj.x : wj.y) * sv[j].x, ty = (upy ? wj.x : wj.y) * sv[j].y;
+          ax = (j == 0) ? tx : ax + tx;
+          ay = (j == 0) ? ty : ay + ty;
+        }
+        fa = d2{uh.x * ax, uh.y * ay};
+      } else {
+        // sum_j u (a_j + sgn(u) b_j) q_j over the edge's na cells
+        const bool px = sgn1(uh.x) > 0.0, py = sgn1(uh.y) > 0.0;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+          if (j < na) {
+            const d2 wj = w[j];
+            fa.x = fa.x + (uh.x * (px ? wj.x : wj.y)) * sv[j].x;
+            fa.y = fa.y + (uh.y * (py ? wj.x : wj.y)) * sv[j].y;
+          }
+        }
+      }
     }
     d2 fu;
     fu.x = dv * dt * (fmax(0.0, uh.x) * so1.x + fmin(0.0, uh.x) * so2.x);
