@@ -70,9 +70,17 @@ struct P2PGet {
   int nchunk;
 };
 
+// The flags and the send buffers are uncached memory: a system-scope load or store of them goes to
+// memory, and no cache holds a stale copy of a peer's send buffer.  So the waits poll with relaxed
+// system-scope loads and the signals are relaxed system-scope stores -- no acquire / release fences,
+// which on gfx950 invalidate or write back the whole L2 (4.7 us per post with them, and every kernel
+// after a get starting on a cold L2).  Ordering that the fences would give comes from elsewhere:
+// the data a post announces was stored by earlier kernels on the stream (complete when they end),
+// a get's copy loads issue after the poll loop has seen the flag (control dependency), and a
+// consumed flag is raised after every copy load of the message has returned its value.
 __device__ inline bool p2p_wait_geq(const unsigned long long* f, unsigned long long n, int* status) {
   const unsigned long long t0 = wall_clock64();
-  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < n) {
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < n) {
     if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
     if (wall_clock64() - t0 > P2P_TIMEOUT_TICKS) {
       atomicOr(status, 1);
@@ -88,10 +96,7 @@ __global__ __launch_bounds__(64) void k_p2p_post(unsigned long long* use, unsign
   const unsigned long long n = use[0] + 1;
   __syncthreads();
   if (threadIdx.x == 0) use[0] = n;
-  for (int i = threadIdx.x; i < npeer; i += 64) {
-    __threadfence_system();
-    __hip_atomic_store(ready[i], n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  for (int i = threadIdx.x; i < npeer; i += 64) __hip_atomic_store(ready[i], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // grid (max chunks, nget + 1): row y < nget pulls chunk x of peer y; row nget waits for the peers
@@ -123,12 +128,9 @@ __global__ __launch_bounds__(256) void k_p2p_get(const P2PGet* __restrict__ g, i
   }
   __syncthreads();  // every lane's loads have returned (their values are stored)
   if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned long long old = atomicAdd(p.done, 1ull);
-    if (old + 1 == n * (unsigned long long)p.nchunk) {
-      __threadfence_system();
-      __hip_atomic_store(p.consumed, n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    const unsigned long long old = __hip_atomic_fetch_add(p.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1 == n * (unsigned long long)p.nchunk)
+      __hip_atomic_store(p.consumed, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -17,6 +17,7 @@
 #   prof8            rocprofv3 kernel trace of one rank's block of an 8-way split (rank emulation)
 #   rank8            every block of the 8-way split alone, compute only and then with its real exchange
 #                    lists looped back (tools/rank_emulation.py --exchange), one after the other
+#   prof8p           the same with the one-sided transfer (MPAS_DYCORE_P2P=1) in the exchange run (gpurun_out/prof8p)
 #   prof8e           rocprofv3 kernel traces of rank8's two modes (gpurun_out/prof8c, gpurun_out/prof8e)
 #   blocks8          bench.py --blocks 8 --rccl-local (the 8-GPU decomposition on one device)
 #   prof8b           rocprofv3 kernel trace of blocks8 (gpurun_out/prof8b)
@@ -69,8 +70,10 @@ step() {
              echo "== $E" >> gpurun_out/envsweep.log
              env $E timeout -k 10 300 python tools/rank_emulation.py ${EMU_ARGS:---parts 8 --blocks 0 4 --exchange} >> gpurun_out/envsweep.log 2>&1 || return 1
            done; done; grep -h "==\|blocks" gpurun_out/envsweep.log | cut -c1-160 ;;
-    prof8e) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8c -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks all --steps 3 > gpurun_out/prof8c.log 2>&1 &&
+    prof8e) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8c -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks ${PROF_BLOCKS:-all} --steps 3 > gpurun_out/prof8c.log 2>&1 &&
             timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8e -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks all --steps 3 --exchange > gpurun_out/prof8e.log 2>&1 && echo "prof8e done" ;;
+    prof8p) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8c -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks ${PROF_BLOCKS:-all} --steps 3 > gpurun_out/prof8c.log 2>&1 &&
+            MPAS_DYCORE_P2P=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8p -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks ${PROF_BLOCKS:-all} --steps 3 --exchange > gpurun_out/prof8p.log 2>&1 && echo "prof8p done" ;;
     blocks8) timeout -k 10 400 python bench.py --blocks 8 --rccl-local --steps 5 --warmup 2 $B > gpurun_out/blocks8.log 2>&1 && last gpurun_out/blocks8.log 300 ;;
     ab8) rm -f gpurun_out/ab8.log
         for r in ${AB_ROUNDS:-1 2 3}; do for F in 0 1; do

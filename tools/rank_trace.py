@@ -22,7 +22,7 @@ def kname(r):
 
 
 def is_exchange(n):
-    return "k_halo_copy" in n or "nccl" in n.lower() or "rccl" in n.lower()
+    return "k_halo_copy" in n or "k_p2p" in n or "nccl" in n.lower() or "rccl" in n.lower()
 
 
 def union(iv):
