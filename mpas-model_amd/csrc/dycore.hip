@@ -189,6 +189,7 @@ struct mpas_dyc_ctx {
   int* p2p_status = nullptr;                        // set by a wait that timed out (halo.hip)
   std::vector<XField> p2p_open;                     // a split-phase p2p exchange between post and get
   bool p2p_pending = false;
+  bool p2p_merge = true;                            // MPAS_DYCORE_P2P_MERGE=0: post and get as two launches
   // MPAS_DYCORE_LATE_ISSUE=1: a split-phase exchange is enqueued on the exchange stream at its
   // exchange_wait, after the compute kernels it overlaps (the same dependencies; only the order in
   // which a captured graph's nodes are created changes)
@@ -1249,6 +1250,8 @@ int p2p_setup(mpas_dyc_ctx* ctx) {
   std::vector<XPlan*> todo;
   for (auto& kv : ctx->plans)
     if (kv.second.p2p && kv.second.p2p_id < 0) todo.push_back(&kv.second);
+  // nothing to map and no peer process to agree with (a single block, or only in-process copies)
+  if (todo.empty() && ctx->nranks == 1) return MPAS_DYC_OK;
   CHK(p2p_init(ctx));
   const int nr = ctx->nranks, me = ctx->rank;
   {
@@ -1332,8 +1335,9 @@ int p2p_setup(mpas_dyc_ctx* ctx) {
       ctx->err = "MPAS_DYCORE_P2P: more than 256 peers";
       return MPAS_DYC_EINVAL;
     }
-    HIPCHK(hipMalloc(&pl.p2p_cnt, (1 + gets.size()) * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(pl.p2p_cnt, 0, (1 + gets.size()) * sizeof(unsigned long long)));
+    // [0] uses, [1 + i] chunks pulled from get peer i, [1 + nget] finished workgroups of k_p2p_exchange
+    HIPCHK(hipMalloc(&pl.p2p_cnt, (2 + gets.size()) * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(pl.p2p_cnt, 0, (2 + gets.size()) * sizeof(unsigned long long)));
     for (size_t j = 0; j < gets.size(); ++j) {
       gets[j].done = pl.p2p_cnt + 1 + j;
       pl.get_chunks = std::max(pl.get_chunks, gets[j].nchunk);
@@ -1400,8 +1404,26 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, int part = 0) {
       }
       CHK(p2p_setup(ctx));
     }
-    if (part != 2) {
-      if (part == 0) CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
+    if (part == 0 && !ctx->p2p_merge) {  // the two launches (A/B of the merged one)
+      CHK(exchange(ctx, fs, 1));
+      return exchange(ctx, fs, 2);
+    }
+    if (part == 0) {  // blocking: post and get as one launch (k_p2p_exchange)
+      CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
+      if (pl.npre && !pl.fused_pack)
+        hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_pre + 3) / 4, pl.npre), dim3(256), 0, ctx->stream, pl.d_pre);
+      set_last_key(ctx, key);
+      CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
+      hipLaunchKernelGGL(k_p2p_exchange, dim3(std::max(pl.get_chunks, 1), pl.nget + 1), dim3(256), 0, ctx->stream,
+                         (const P2PGet*)pl.d_get, pl.nget, (unsigned long long* const*)pl.d_ready, pl.nready,
+                         (const unsigned long long* const*)pl.d_cons, pl.ncons, pl.p2p_cnt, ctx->p2p_status);
+      CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
+      if (pl.npost && !pl.fused_unpack)
+        hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_post + 3) / 4, pl.npost), dim3(256), 0, ctx->stream, pl.d_post);
+      CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
+      return MPAS_DYC_OK;
+    }
+    if (part == 1) {
       if (pl.npre && !pl.fused_pack)
         hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_pre + 3) / 4, pl.npre), dim3(256), 0, ctx->stream, pl.d_pre);
       set_last_key(ctx, key);
@@ -1415,7 +1437,6 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, int part = 0) {
       CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
       if (pl.npost && !pl.fused_unpack)
         hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_post + 3) / 4, pl.npost), dim3(256), 0, ctx->stream, pl.d_post);
-      if (part == 0) CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
     }
     return MPAS_DYC_OK;
   }
@@ -2872,6 +2893,7 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";
   if (const char* lb = getenv("MPAS_DYCORE_LOOPBACK")) ctx->loopback = std::atoi(lb);
   if (const char* pp = getenv("MPAS_DYCORE_P2P")) ctx->p2p = std::atoi(pp);
+  if (const char* pm = getenv("MPAS_DYCORE_P2P_MERGE")) ctx->p2p_merge = std::atoi(pm) != 0;
   if (const char* li = getenv("MPAS_DYCORE_LATE_ISSUE")) ctx->late_issue = std::string(li) == "1";
   if (const char* oa = getenv("MPAS_DYCORE_OVERLAP_ALL")) ctx->overlap_all = std::string(oa) == "1";
   if (const char* ov = getenv("MPAS_DYCORE_OVERLAP")) ctx->overlap = std::atoi(ov);

@@ -134,6 +134,54 @@ __global__ __launch_bounds__(256) void k_p2p_get(const P2PGet* __restrict__ g, i
   }
 }
 
+// A blocking exchange (post then get, nothing between them): both in one launch.  Every row's first
+// workgroup raises the ready flags before it waits for anything (the send buffer was completed by the
+// kernels before this one), so no workgroup depends on another being scheduled first; the use
+// counter is read by every workgroup at its start and advanced by the last one to finish
+// (use[1 + nget] counts finished workgroups over all uses).
+__global__ __launch_bounds__(256) void k_p2p_exchange(const P2PGet* __restrict__ g, int nget,
+                                                      unsigned long long* const* ready, int nready,
+                                                      const unsigned long long* const* consumed, int ncons,
+                                                      unsigned long long* use, int* status) {
+  const unsigned long long n = use[0] + 1;
+  if (blockIdx.x == 0 && (int)threadIdx.x < nready)
+    __hip_atomic_store(ready[threadIdx.x], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((int)blockIdx.y == nget) {
+    if (blockIdx.x == 0 && (int)threadIdx.x < ncons) (void)p2p_wait_geq(consumed[threadIdx.x], n, status);
+  } else {
+    const P2PGet& p = g[blockIdx.y];
+    if ((int)blockIdx.x < p.nchunk) {
+      __shared__ int ok;
+      if (threadIdx.x == 0) ok = p2p_wait_geq(p.ready, n, status);
+      __syncthreads();
+      if (ok) {
+        const long long c0 = (long long)blockIdx.x * P2P_CHUNK;
+        const long long c1 = min(p.count, c0 + P2P_CHUNK);
+        for (long long i = c0 + threadIdx.x; i < c1; i += 4 * 256) {
+          double v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = i + u * 256 < c1 ? p.src[i + u * 256] : 0.0;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (i + u * 256 < c1) p.dst[i + u * 256] = v[u];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          const unsigned long long old = __hip_atomic_fetch_add(p.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (old + 1 == n * (unsigned long long)p.nchunk)
+            __hip_atomic_store(p.consumed, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long total = (unsigned long long)gridDim.x * gridDim.y;
+    const unsigned long long old = __hip_atomic_fetch_add(use + 1 + nget, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1 == n * total) __hip_atomic_store(use, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // atm_rk_integration_setup (mpas_atm_time_integration.F:1847-1857): the ten state/diag
 // copies of one block in a single launch; blockIdx.y selects the copy.
 struct CopyList {
