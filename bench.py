@@ -190,7 +190,7 @@ def main():
     ap.add_argument("--acoustic-reps", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=1, help="blocks per GPU (MPAS blocks with halos)")
     ap.add_argument("--rccl-local", action="store_true", help="route in-process block exchanges through RCCL")
-    ap.add_argument("--transport", choices=("rccl", "p2p"), default="rccl",
+    ap.add_argument("--transport", choices=("rccl", "p2p"), default="p2p",
                     help="halo messages between ranks: RCCL send/recv groups, or the one-sided intra-node "
                          "transfer (mpas_dyc_set_p2p: pulled over xGMI by the receiving rank's kernel)")
     ap.add_argument("--no-configs1", action="store_true",
@@ -330,6 +330,7 @@ def main():
     elapsed = t1 - t0
     graph = dy.graph_active()
     layout = dy.layout()
+    transport = ("one-sided over xGMI (IPC)" if dy.p2p_active() else "RCCL send/recv groups") if nparts > 1 else None
     ranks = None
     if nparts > 1:
         # one more step, eager, with HIP events around every exchange's exposed part (outside the
@@ -408,9 +409,7 @@ def main():
             "dt": dt, "time_integration_order": case["config"]["config_time_integration_order"],
             "split_steps": case["config"]["config_dynamics_split_steps"], "acoustic_substeps": nss,
             "parallelism": (f"domain decomposition: {nparts} SFC blocks with 2-layer halos, "
-                            f"{args.blocks} per GPU, halo exchange " +
-                            ("one-sided over xGMI (IPC)" if args.transport == "p2p" else "over RCCL")
-                            if nparts > 1 else "single block"),
+                            f"{args.blocks} per GPU, halo exchange {transport}" if nparts > 1 else "single block"),
             "owned_cells_rank0": owned, "halo_cells_rank0": halo,
             "hip_graph": graph,
             "maxEdges_declared": [case["maxEdges"], case["maxEdges2"]],

@@ -312,6 +312,9 @@ int mpas_dyc_set_transport(mpas_dyc_ctx* ctx, int32_t rccl_for_local_blocks);
  * (checked: MPAS_DYC_ECOMM otherwise).  A message that does not arrive within 30 s makes
  * mpas_dyc_synchronize return MPAS_DYC_ECOMM.  Collective: every rank calls it with the same value. */
 int mpas_dyc_set_p2p(mpas_dyc_ctx* ctx, int32_t on);
+/* 1 while the one-sided transfer is on (0 after the set-up found it unavailable on some rank -- IPC
+ * refused, ranks on several nodes -- and every rank went back to RCCL, with a line on stderr). */
+int mpas_dyc_get_p2p(const mpas_dyc_ctx* ctx);
 /* Split-phase exchanges: at the tend_u, rho_pp and rtheta_pp exchanges the interior
  * elements are computed while the halo traffic runs on a second stream.  on = 1 / 0;
  * -1 (default) = automatic: on when exchanges go through RCCL (more than one rank). */

@@ -1199,6 +1199,26 @@ uint64_t node_id() {
   return h;
 }
 
+// p2p_init / p2p_setup return this when the one-sided transfer cannot run on some rank (IPC
+// unsupported, ranks on several nodes, a mapping refused): every rank learns it from the same
+// all-gathers, drops the transfer and plans again with RCCL (plan_all, p2p_fallback)
+constexpr int P2P_UNAVAILABLE = 1;
+
+// every rank's verdict on a local step of the set-up (collective): P2P_UNAVAILABLE on all ranks if
+// any rank failed, with the first failing rank's reason in ctx->err
+int p2p_vote(mpas_dyc_ctx* ctx, int local, const std::string& what) {
+  int32_t mine = local == MPAS_DYC_OK ? 0 : 1;
+  std::vector<char> all;
+  CHK(allgather_bytes(ctx, &mine, sizeof(mine), all));
+  for (int r = 0; r < ctx->nranks; ++r)
+    if (((const int32_t*)all.data())[r]) {
+      ctx->err = "one-sided transfer unavailable (" + what + " failed on rank " + std::to_string(r) +
+                 (r == ctx->rank ? ": " + ctx->err : std::string()) + ")";
+      return P2P_UNAVAILABLE;
+    }
+  return MPAS_DYC_OK;
+}
+
 // the flag arenas: this rank's, and every peer's mapped here
 int p2p_init(mpas_dyc_ctx* ctx) {
   if (ctx->p2p_flags) return MPAS_DYC_OK;
@@ -1211,36 +1231,43 @@ int p2p_init(mpas_dyc_ctx* ctx) {
     for (const auto& b : ctx->blk)
       for (const auto& x : b.xl) nr = std::max(nr, x.peer_rank + 1);
   ctx->p2p_nr = nr;
-  const size_t bytes = (size_t)P2P_MAX_POINTS * nr * 2 * sizeof(unsigned long long);
-  HIPCHK(hipExtMallocWithFlags((void**)&ctx->p2p_flags, bytes, hipDeviceMallocUncached));
-  HIPCHK(hipMemset(ctx->p2p_flags, 0, bytes));
-  HIPCHK(hipMalloc(&ctx->p2p_status, sizeof(int)));
-  HIPCHK(hipMemset(ctx->p2p_status, 0, sizeof(int)));
-  HIPCHK(hipDeviceSynchronize());
-  ctx->p2p_peer_flags.assign(ctx->nranks, nullptr);
-  ctx->p2p_peer_flags[ctx->rank] = ctx->p2p_flags;
-  if (ctx->nranks == 1) return MPAS_DYC_OK;
   struct Rec {
     hipIpcMemHandle_t h;
     uint64_t node;
   } rec{};
-  HIPCHK(hipIpcGetMemHandle(&rec.h, ctx->p2p_flags));
+  const int local = [&]() -> int {
+    const size_t bytes = (size_t)P2P_MAX_POINTS * nr * 2 * sizeof(unsigned long long);
+    HIPCHK(hipExtMallocWithFlags((void**)&ctx->p2p_flags, bytes, hipDeviceMallocUncached));
+    HIPCHK(hipMemset(ctx->p2p_flags, 0, bytes));
+    HIPCHK(hipMalloc(&ctx->p2p_status, sizeof(int)));
+    HIPCHK(hipMemset(ctx->p2p_status, 0, sizeof(int)));
+    HIPCHK(hipDeviceSynchronize());
+    if (ctx->nranks > 1) HIPCHK(hipIpcGetMemHandle(&rec.h, ctx->p2p_flags));
+    return MPAS_DYC_OK;
+  }();
+  ctx->p2p_peer_flags.assign(ctx->nranks, nullptr);
+  ctx->p2p_peer_flags[ctx->rank] = ctx->p2p_flags;
+  if (ctx->nranks == 1) return local;
+  CHK(p2p_vote(ctx, local, "flag arena allocation"));
   rec.node = node_id();
   std::vector<char> all;
   CHK(allgather_bytes(ctx, &rec, sizeof(rec), all));
-  for (int r = 0; r < ctx->nranks; ++r) {
-    const Rec& o = *(const Rec*)(all.data() + r * sizeof(Rec));
-    if (o.node != rec.node) {
-      ctx->err = "MPAS_DYCORE_P2P: rank " + std::to_string(r) + " runs on another node (one-sided transfer is intra-node)";
-      return MPAS_DYC_ECOMM;
+  for (int r = 0; r < ctx->nranks; ++r)
+    if (((const Rec*)all.data())[r].node != rec.node) {
+      ctx->err = "one-sided transfer unavailable (rank " + std::to_string(r) + " runs on another node)";
+      return P2P_UNAVAILABLE;
     }
-    if (r == ctx->rank) continue;
-    void* p = nullptr;
-    HIPCHK(hipIpcOpenMemHandle(&p, o.h, hipIpcMemLazyEnablePeerAccess));
-    ctx->p2p_mapped.push_back(p);
-    ctx->p2p_peer_flags[r] = (unsigned long long*)p;
-  }
-  return MPAS_DYC_OK;
+  const int opened = [&]() -> int {
+    for (int r = 0; r < ctx->nranks; ++r) {
+      if (r == ctx->rank) continue;
+      void* p = nullptr;
+      HIPCHK(hipIpcOpenMemHandle(&p, ((const Rec*)all.data())[r].h, hipIpcMemLazyEnablePeerAccess));
+      ctx->p2p_mapped.push_back(p);
+      ctx->p2p_peer_flags[r] = (unsigned long long*)p;
+    }
+    return MPAS_DYC_OK;
+  }();
+  return p2p_vote(ctx, opened, "mapping the peers' flag arenas");
 }
 
 // Maps the send buffers of the exchange points built since the last call and uploads their get /
@@ -1268,93 +1295,115 @@ int p2p_setup(mpas_dyc_ctx* ctx) {
   // per exchange point: the send buffer's IPC handle, then per rank (offset, count) of the message to it
   const size_t per = sizeof(hipIpcMemHandle_t) + 2 * sizeof(int64_t) * nr;
   std::vector<char> mine(per * todo.size(), 0), all;
-  for (size_t i = 0; i < todo.size(); ++i) {
-    char* r = mine.data() + per * i;
-    if (nr > 1) HIPCHK(hipIpcGetMemHandle((hipIpcMemHandle_t*)r, todo[i]->sendbuf));
-    int64_t* oc = (int64_t*)(r + sizeof(hipIpcMemHandle_t));
-    for (int q = 0; q < nr; ++q) oc[2 * q] = oc[2 * q + 1] = -1;
-    for (const XMsg& m : todo[i]->rsend) {
-      if (m.peer_rank >= nr) continue;  // loopback: emulated ranks beyond the communicator
-      oc[2 * m.peer_rank] = m.off;
-      oc[2 * m.peer_rank + 1] = m.count;
+  const int handles = [&]() -> int {
+    for (size_t i = 0; i < todo.size(); ++i) {
+      char* r = mine.data() + per * i;
+      if (nr > 1) HIPCHK(hipIpcGetMemHandle((hipIpcMemHandle_t*)r, todo[i]->sendbuf));
+      int64_t* oc = (int64_t*)(r + sizeof(hipIpcMemHandle_t));
+      for (int q = 0; q < nr; ++q) oc[2 * q] = oc[2 * q + 1] = -1;
+      for (const XMsg& m : todo[i]->rsend) {
+        if (m.peer_rank >= nr) continue;  // loopback: emulated ranks beyond the communicator
+        oc[2 * m.peer_rank] = m.off;
+        oc[2 * m.peer_rank + 1] = m.count;
+      }
     }
-  }
+    return MPAS_DYC_OK;
+  }();
+  if (nr > 1) CHK(p2p_vote(ctx, handles, "exporting the send buffers"));
+  else CHK(handles);
   CHK(allgather_bytes(ctx, mine.data(), mine.size(), all));
-  for (size_t i = 0; i < todo.size(); ++i) {
-    XPlan& pl = *todo[i];
-    if (ctx->p2p_next >= P2P_MAX_POINTS) {
-      ctx->err = "MPAS_DYCORE_P2P: more than " + std::to_string(P2P_MAX_POINTS) + " exchange points";
-      return MPAS_DYC_ESTATE;
-    }
-    pl.p2p_id = ctx->p2p_next++;
-    auto flag = [&](unsigned long long* arena, int r, int k) {
-      return arena + ((size_t)pl.p2p_id * ctx->p2p_nr + r) * 2 + k;
-    };
-    auto nchunk = [](int64_t n) { return (int)std::max<int64_t>(1, (n + P2P_CHUNK - 1) / P2P_CHUNK); };
-    std::vector<P2PGet> gets;
-    std::vector<unsigned long long*> ready;
-    std::vector<const unsigned long long*> cons;
-    if (ctx->loopback) {
-      // as rccl_group: one pair per emulated peer of max(send, receive) doubles, all in this rank
-      std::map<int, std::pair<const XMsg*, const XMsg*>> peers;
-      for (const XMsg& m : pl.rsend) peers[m.peer_rank].first = &m;
-      for (const XMsg& m : pl.rrecv) peers[m.peer_rank].second = &m;
-      for (const auto& kv : peers) {
-        const XMsg *sm = kv.second.first, *rm = kv.second.second;
-        const int64_t n = std::max(sm ? sm->count : 0, rm ? rm->count : 0);
-        gets.push_back(P2PGet{pl.sendbuf + (sm ? sm->off : 0), pl.recvbuf + (rm ? rm->off : 0), n,
-                              flag(ctx->p2p_flags, kv.first, 0), flag(ctx->p2p_flags, kv.first, 1), nullptr, nchunk(n)});
-        ready.push_back(flag(ctx->p2p_flags, kv.first, 0));
-        cons.push_back(flag(ctx->p2p_flags, kv.first, 1));
+  const int built = [&]() -> int {
+    for (size_t i = 0; i < todo.size(); ++i) {
+      XPlan& pl = *todo[i];
+      if (ctx->p2p_next >= P2P_MAX_POINTS) {
+        ctx->err = "MPAS_DYCORE_P2P: more than " + std::to_string(P2P_MAX_POINTS) + " exchange points";
+        return MPAS_DYC_ESTATE;
       }
-    } else {
-      for (const XMsg& m : pl.rsend) {
-        ready.push_back(flag(ctx->p2p_peer_flags[m.peer_rank], me, 0));
-        cons.push_back(flag(ctx->p2p_flags, m.peer_rank, 1));
-      }
-      for (const XMsg& m : pl.rrecv) {
-        const char* rr = all.data() + (size_t)m.peer_rank * mine.size() + per * i;
-        const int64_t* oc = (const int64_t*)(rr + sizeof(hipIpcMemHandle_t));
-        if (oc[2 * me + 1] != m.count) {
-          ctx->err = "MPAS_DYCORE_P2P: rank " + std::to_string(m.peer_rank) + " sends " + std::to_string(oc[2 * me + 1]) +
-                     " doubles where this rank receives " + std::to_string(m.count);
-          return MPAS_DYC_ECOMM;
+      pl.p2p_id = ctx->p2p_next++;
+      auto flag = [&](unsigned long long* arena, int r, int k) {
+        return arena + ((size_t)pl.p2p_id * ctx->p2p_nr + r) * 2 + k;
+      };
+      auto nchunk = [](int64_t n) { return (int)std::max<int64_t>(1, (n + P2P_CHUNK - 1) / P2P_CHUNK); };
+      std::vector<P2PGet> gets;
+      std::vector<unsigned long long*> ready;
+      std::vector<const unsigned long long*> cons;
+      if (ctx->loopback) {
+        // as rccl_group: one pair per emulated peer of max(send, receive) doubles, all in this rank
+        std::map<int, std::pair<const XMsg*, const XMsg*>> peers;
+        for (const XMsg& m : pl.rsend) peers[m.peer_rank].first = &m;
+        for (const XMsg& m : pl.rrecv) peers[m.peer_rank].second = &m;
+        for (const auto& kv : peers) {
+          const XMsg *sm = kv.second.first, *rm = kv.second.second;
+          const int64_t n = std::max(sm ? sm->count : 0, rm ? rm->count : 0);
+          gets.push_back(P2PGet{pl.sendbuf + (sm ? sm->off : 0), pl.recvbuf + (rm ? rm->off : 0), n,
+                                flag(ctx->p2p_flags, kv.first, 0), flag(ctx->p2p_flags, kv.first, 1), nullptr,
+                                nchunk(n)});
+          ready.push_back(flag(ctx->p2p_flags, kv.first, 0));
+          cons.push_back(flag(ctx->p2p_flags, kv.first, 1));
         }
-        const double* base = pl.sendbuf;
-        if (m.peer_rank != me) {
-          void* p = nullptr;
-          HIPCHK(hipIpcOpenMemHandle(&p, *(const hipIpcMemHandle_t*)rr, hipIpcMemLazyEnablePeerAccess));
-          pl.p2p_mapped.push_back(p);
-          base = (const double*)p;
+      } else {
+        for (const XMsg& m : pl.rsend) {
+          ready.push_back(flag(ctx->p2p_peer_flags[m.peer_rank], me, 0));
+          cons.push_back(flag(ctx->p2p_flags, m.peer_rank, 1));
         }
-        gets.push_back(P2PGet{base + oc[2 * me], pl.recvbuf + m.off, m.count, flag(ctx->p2p_flags, m.peer_rank, 0),
-                              flag(ctx->p2p_peer_flags[m.peer_rank], me, 1), nullptr, nchunk(m.count)});
+        for (const XMsg& m : pl.rrecv) {
+          const char* rr = all.data() + (size_t)m.peer_rank * mine.size() + per * i;
+          const int64_t* oc = (const int64_t*)(rr + sizeof(hipIpcMemHandle_t));
+          if (oc[2 * me + 1] != m.count) {
+            ctx->err = "MPAS_DYCORE_P2P: rank " + std::to_string(m.peer_rank) + " sends " +
+                       std::to_string(oc[2 * me + 1]) + " doubles where this rank receives " + std::to_string(m.count);
+            return MPAS_DYC_ECOMM;
+          }
+          const double* base = pl.sendbuf;
+          if (m.peer_rank != me) {
+            void* p = nullptr;
+            HIPCHK(hipIpcOpenMemHandle(&p, *(const hipIpcMemHandle_t*)rr, hipIpcMemLazyEnablePeerAccess));
+            pl.p2p_mapped.push_back(p);
+            base = (const double*)p;
+          }
+          gets.push_back(P2PGet{base + oc[2 * me], pl.recvbuf + m.off, m.count, flag(ctx->p2p_flags, m.peer_rank, 0),
+                                flag(ctx->p2p_peer_flags[m.peer_rank], me, 1), nullptr, nchunk(m.count)});
+        }
       }
+      if (cons.size() > 256 || ready.size() > 256) {
+        ctx->err = "MPAS_DYCORE_P2P: more than 256 peers";
+        return MPAS_DYC_EINVAL;
+      }
+      // [0] uses, [1 + i] chunks pulled from get peer i, [1 + nget] finished workgroups of k_p2p_exchange
+      HIPCHK(hipMalloc(&pl.p2p_cnt, (2 + gets.size()) * sizeof(unsigned long long)));
+      HIPCHK(hipMemset(pl.p2p_cnt, 0, (2 + gets.size()) * sizeof(unsigned long long)));
+      for (size_t j = 0; j < gets.size(); ++j) {
+        gets[j].done = pl.p2p_cnt + 1 + j;
+        pl.get_chunks = std::max(pl.get_chunks, gets[j].nchunk);
+      }
+      pl.nget = (int)gets.size();
+      pl.nready = (int)ready.size();
+      pl.ncons = (int)cons.size();
+      auto upload = [&](const void* h, size_t bytes, void** d) -> int {
+        HIPCHK(hipMalloc(d, std::max<size_t>(bytes, 8)));
+        if (bytes) HIPCHK(hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice));
+        return MPAS_DYC_OK;
+      };
+      CHK(upload(gets.data(), gets.size() * sizeof(P2PGet), (void**)&pl.d_get));
+      CHK(upload(ready.data(), ready.size() * sizeof(void*), (void**)&pl.d_ready));
+      CHK(upload(cons.data(), cons.size() * sizeof(void*), (void**)&pl.d_cons));
     }
-    if (cons.size() > 256) {
-      ctx->err = "MPAS_DYCORE_P2P: more than 256 peers";
-      return MPAS_DYC_EINVAL;
-    }
-    // [0] uses, [1 + i] chunks pulled from get peer i, [1 + nget] finished workgroups of k_p2p_exchange
-    HIPCHK(hipMalloc(&pl.p2p_cnt, (2 + gets.size()) * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(pl.p2p_cnt, 0, (2 + gets.size()) * sizeof(unsigned long long)));
-    for (size_t j = 0; j < gets.size(); ++j) {
-      gets[j].done = pl.p2p_cnt + 1 + j;
-      pl.get_chunks = std::max(pl.get_chunks, gets[j].nchunk);
-    }
-    pl.nget = (int)gets.size();
-    pl.nready = (int)ready.size();
-    pl.ncons = (int)cons.size();
-    auto upload = [&](const void* h, size_t bytes, void** d) -> int {
-      HIPCHK(hipMalloc(d, std::max<size_t>(bytes, 8)));
-      if (bytes) HIPCHK(hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice));
-      return MPAS_DYC_OK;
-    };
-    CHK(upload(gets.data(), gets.size() * sizeof(P2PGet), (void**)&pl.d_get));
-    CHK(upload(ready.data(), ready.size() * sizeof(void*), (void**)&pl.d_ready));
-    CHK(upload(cons.data(), cons.size() * sizeof(void*), (void**)&pl.d_cons));
-  }
-  return MPAS_DYC_OK;
+    return MPAS_DYC_OK;
+  }();
+  return nr > 1 ? p2p_vote(ctx, built, "mapping the peers' send buffers") : built;
+}
+
+// the one-sided transfer dropped on every rank (P2P_UNAVAILABLE): its mappings and arena freed, the
+// plans rebuilt for RCCL by the caller
+void p2p_fallback(mpas_dyc_ctx* ctx) {
+  fprintf(stderr, "mpas_dycore rank %d: %s; halo exchanges go through RCCL\n", ctx->rank, ctx->err.c_str());
+  invalidate_plans(ctx);
+  for (void* p : ctx->p2p_mapped) (void)hipIpcCloseMemHandle(p);
+  ctx->p2p_mapped.clear();
+  if (ctx->p2p_flags) (void)hipFree(ctx->p2p_flags);
+  ctx->p2p_flags = nullptr;
+  ctx->p2p_peer_flags.clear();
+  ctx->p2p = 0;
 }
 
 // p2p_status: a wait of k_p2p_get that timed out
@@ -1402,7 +1451,12 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, int part = 0) {
         ctx->err = "internal: one-sided exchange set up during graph capture";
         return MPAS_DYC_ESTATE;
       }
-      CHK(p2p_setup(ctx));
+      const int r = p2p_setup(ctx);
+      if (r == P2P_UNAVAILABLE) {  // every rank is here: this exchange, and the rest, through RCCL
+        p2p_fallback(ctx);
+        return exchange(ctx, fs, part);
+      }
+      CHK(r);
     }
     if (part == 0 && !ctx->p2p_merge) {  // the two launches (A/B of the merged one)
       CHK(exchange(ctx, fs, 1));
@@ -2826,6 +2880,10 @@ int plan_all(mpas_dyc_ctx* ctx, double dt) {
   if (r == MPAS_DYC_OK) {
     ctx->planned.insert(sig);
     r = ctx->p2p ? p2p_setup(ctx) : MPAS_DYC_OK;
+    if (r == P2P_UNAVAILABLE) {  // every rank is here: plan again for RCCL
+      p2p_fallback(ctx);
+      return plan_all(ctx, dt);
+    }
     if (r == MPAS_DYC_OK) r = warm_rccl(ctx);
   }
   return r;
@@ -3950,6 +4008,8 @@ int mpas_dyc_set_p2p(mpas_dyc_ctx* ctx, int32_t on) {
   ctx->p2p = on != 0;
   return MPAS_DYC_OK;
 }
+
+int mpas_dyc_get_p2p(const mpas_dyc_ctx* ctx) { return ctx && ctx->p2p ? 1 : 0; }
 
 int mpas_dyc_set_overlap(mpas_dyc_ctx* ctx, int32_t on) {
   if (!ctx) return MPAS_DYC_EINVAL;

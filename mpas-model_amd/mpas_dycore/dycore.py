@@ -193,6 +193,10 @@ class Dycore:
                        include_self=positional and rccl_local)
         return self
 
+    def p2p_active(self) -> bool:
+        """True while halo messages between ranks use the one-sided transfer (mpas_dyc_get_p2p)."""
+        return bool(self.lib.mpas_dyc_get_p2p(self.h))
+
     def graph_active(self) -> bool:
         """True if the last step replayed its captured hipGraph (False: it ran eagerly)."""
         return bool(self.lib.mpas_dyc_graph_active(self.h))
