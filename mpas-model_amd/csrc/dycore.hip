@@ -140,6 +140,19 @@ struct XPlan {
   const unsigned long long** d_cons = nullptr;  // the consumed flags this rank waits for
   int ncons = 0;
   std::vector<void*> p2p_mapped;  // the peers' send buffers mapped here (IPC)
+  // pull (k_p2p_pull): block-pair lists, blocking exchanges -- the receiver copies the peers' owned
+  // columns from their fields; no buffers, no pack / unpack kernels, no fused pack / unpack
+  bool pull = false;
+  std::vector<XSeg> h_pre, h_post;        // the pack / unpack segments (host), in buffer order
+  std::vector<const std::vector<int32_t>*> h_pre_idx;  // each pack segment's send list (host)
+  std::vector<int64_t> h_pre_off, h_post_off;
+  XSeg* d_local = nullptr;                // in-process block-to-block copies of a pull plan
+  int nlocal = 0, maxn_local = 0;
+  P2PSeg* d_pseg = nullptr;
+  int2* d_chunk = nullptr;                // (segment, first column) per workgroup of k_p2p_pull
+  int npseg = 0, nchunk = 0, npeer_work = 0;
+  P2PPeer* d_peer = nullptr;
+  std::vector<void*> pull_mem;            // device copies of the peers' send lists
 };
 
 // One field of an exchange point: mpas_dmpar_exch_halo_field(field[, haloLayers]).
@@ -190,6 +203,8 @@ struct mpas_dyc_ctx {
   std::vector<XField> p2p_open;                     // a split-phase p2p exchange between post and get
   bool p2p_pending = false;
   bool p2p_merge = true;                            // MPAS_DYCORE_P2P_MERGE=0: post and get as two launches
+  bool p2p_pull = true;                             // MPAS_DYCORE_P2P_PULL=0: buffers + k_p2p_exchange instead
+  std::map<std::pair<int, uint64_t>, void*> p2p_fields;  // (rank, its field buffer) -> mapped here
   // MPAS_DYCORE_LATE_ISSUE=1: a split-phase exchange is enqueued on the exchange stream at its
   // exchange_wait, after the compute kernels it overlaps (the same dependencies; only the order in
   // which a captured graph's nodes are created changes)
@@ -606,6 +621,9 @@ void free_plan(XPlan& pl) {
                   (void*)pl.d_get, (void*)pl.d_ready, (void*)pl.d_cons})
     if (p) (void)hipFree(p);
   for (void* p : pl.pack_mem) (void)hipFree(p);
+  for (void* p : pl.pull_mem) (void)hipFree(p);
+  for (void* p : {(void*)pl.d_local, (void*)pl.d_pseg, (void*)pl.d_peer, (void*)pl.d_chunk})
+    if (p) (void)hipFree(p);
   pl = XPlan{};
 }
 
@@ -638,6 +656,7 @@ std::vector<std::pair<int, int>> peers_of(const Block& b, int dir) {
 
 inline bool batched(const Dims& d);
 inline bool pair_layout(const Dims& d);
+bool split_phase(const mpas_dyc_ctx* ctx);
 
 // Message layout: per block, peers in (rank, block) order; per peer, the fields in call
 // order and per field the halo layers in ascending order (both sides agree on it).
@@ -645,6 +664,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   const int nb = (int)ctx->blk.size();
   std::vector<XSeg> pre, post;
   std::vector<int64_t> pre_off, post_off;  // buffer offsets, patched once the buffers exist (-1: direct)
+  std::vector<const std::vector<int32_t>*> pre_hidx;  // host send list of each block-pair pre segment
   int64_t stotal = 0, rtotal = 0;
   // the fused pack applies to the per-sub-step exchange (diag rtheta_pp [+ rho_pp], halo layer 1)
   bool fusable = !fs.empty() && fs.size() <= 2 && !ctx->plain_exchange;
@@ -739,6 +759,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
               if (recfuse) rec_pack.push_back(RecSeg{bi, rec_fid(f), F->loc, sx, pre.size()});
             }
             pre.push_back(sg);
+            pre_hidx.push_back(&sx->h_idx);
           }
           pl.maxn_pre = std::max(pl.maxn_pre, sx->n);
         }
@@ -786,6 +807,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
       if (!local && rtotal > start) pl.rrecv.push_back(XMsg{bi, pr.first, pr.second, start, rtotal - start});
     }
   }
+  bool positional = false;
   // positional lists (mpas_dyc_set_exchange_positions): per peer rank one message, laid out as
   // mpas_dmpar lays out its buffer (mpas_dmpar.F:5448-5535): per field, per halo layer a region whose
   // slots the blocks of this process fill at their positions; the receiver reads its blocks' slots
@@ -849,6 +871,7 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
         if (total > start) (dir == MPAS_DYC_SEND ? pl.rsend : pl.rrecv).push_back(XMsg{-1, pr, -1, start, total - start});
       }
     if (!pos_ranks.empty()) {
+      positional = true;
       fusable = false;
       recfuse = false;
       for (const auto& m : pl.rsend)
@@ -905,6 +928,29 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   if (ctx->host_only) return MPAS_DYC_OK;  // the dry run keeps the message lists only
   if (ctx->loopback) stotal = rtotal = stotal + rtotal;  // rccl_group's loopback pairs stay inside
   pl.p2p = ctx->p2p && (!pl.rsend.empty() || !pl.rrecv.empty());
+  pl.pull = pl.p2p && ctx->p2p_pull && !positional && !split_phase(ctx);
+  if (pl.pull) {
+    // the receiver copies from the fields: no buffers, and the kernels store and read the fields
+    // themselves (no fused pack / unpack)
+    fusable = recfuse = false;
+    pl.h_pre = pre;
+    pl.h_pre_off = pre_off;
+    pl.h_pre_idx = pre_hidx;
+    pl.h_post = post;
+    pl.h_post_off = post_off;
+    std::vector<XSeg> loc;
+    for (size_t i = 0; i < pre.size(); ++i)
+      if (pre_off[i] < 0) {
+        loc.push_back(pre[i]);
+        pl.maxn_local = std::max(pl.maxn_local, pre[i].n);
+      }
+    pl.nlocal = (int)loc.size();
+    if (pl.nlocal) {
+      HIPCHK(hipMalloc(&pl.d_local, loc.size() * sizeof(XSeg)));
+      HIPCHK(hipMemcpy(pl.d_local, loc.data(), loc.size() * sizeof(XSeg), hipMemcpyHostToDevice));
+    }
+    return MPAS_DYC_OK;
+  }
   if (pl.p2p) {
     // read by the peers over xGMI: uncached, so the producer's stores are in HBM when its kernel ends
     HIPCHK(hipExtMallocWithFlags((void**)&pl.sendbuf, std::max<int64_t>(stotal, 1) * sizeof(double) + 256,
@@ -1273,13 +1319,16 @@ int p2p_init(mpas_dyc_ctx* ctx) {
 // Maps the send buffers of the exchange points built since the last call and uploads their get /
 // post tables.  Every rank builds the same exchange points in the same (plan key) order; the count
 // is checked, and every message's size against its sender's.
+int p2p_setup_pull(mpas_dyc_ctx* ctx, const std::vector<XPlan*>& todo);
+
 int p2p_setup(mpas_dyc_ctx* ctx) {
-  std::vector<XPlan*> todo;
+  std::vector<XPlan*> todo, pulls;
   for (auto& kv : ctx->plans)
-    if (kv.second.p2p && kv.second.p2p_id < 0) todo.push_back(&kv.second);
+    if (kv.second.p2p && kv.second.p2p_id < 0) (kv.second.pull ? pulls : todo).push_back(&kv.second);
   // nothing to map and no peer process to agree with (a single block, or only in-process copies)
-  if (todo.empty() && ctx->nranks == 1) return MPAS_DYC_OK;
+  if (todo.empty() && pulls.empty() && ctx->nranks == 1) return MPAS_DYC_OK;
   CHK(p2p_init(ctx));
+  CHK(p2p_setup_pull(ctx, pulls));
   const int nr = ctx->nranks, me = ctx->rank;
   {
     int64_t n = (int64_t)todo.size();
@@ -1393,6 +1442,313 @@ int p2p_setup(mpas_dyc_ctx* ctx) {
   return nr > 1 ? p2p_vote(ctx, built, "mapping the peers' send buffers") : built;
 }
 
+// variable-size all-gather: every rank's bytes, in rank order
+int allgatherv_bytes(mpas_dyc_ctx* ctx, const std::vector<char>& mine, std::vector<std::vector<char>>& out) {
+  int64_t n = (int64_t)mine.size();
+  std::vector<char> sizes;
+  CHK(allgather_bytes(ctx, &n, sizeof(n), sizes));
+  int64_t mx = 0;
+  for (int r = 0; r < ctx->nranks; ++r) mx = std::max(mx, ((const int64_t*)sizes.data())[r]);
+  std::vector<char> pad(mine);
+  pad.resize(std::max<int64_t>(mx, 1), 0);
+  std::vector<char> all;
+  CHK(allgather_bytes(ctx, pad.data(), pad.size(), all));
+  out.assign(ctx->nranks, {});
+  for (int r = 0; r < ctx->nranks; ++r) {
+    const char* b = all.data() + (size_t)r * pad.size();
+    out[r].assign(b, b + ((const int64_t*)sizes.data())[r]);
+  }
+  return MPAS_DYC_OK;
+}
+
+// Pull plans: every rank exports, per exchange point and message, its pack segments (the field
+// buffer -- IPC handle, mapped once per peer and buffer -- the sub-field offset, the send list);
+// the receiver pairs them in message order with its unpack segments into k_p2p_pull's segments.
+int p2p_setup_pull(mpas_dyc_ctx* ctx, const std::vector<XPlan*>& todo) {
+  const int nr = ctx->nranks, me = ctx->rank;
+  if (todo.empty()) return MPAS_DYC_OK;
+  // the field buffer a pack segment reads
+  auto base_of = [&](const double* p, size_t& bytes) -> const double* {
+    for (const auto& b : ctx->blk)
+      for (const auto& f : b.fields)
+        for (int t = 0; t < f.ntl; ++t) {
+          const char* q = (const char*)f.buf[t];
+          if (!q || f.is_int) continue;
+          const size_t nb = (size_t)field_bytes(b, f) + 256;
+          if ((const char*)p >= q && (const char*)p < q + nb) {
+            bytes = nb;
+            return (const double*)q;
+          }
+        }
+    return nullptr;
+  };
+  std::vector<char> rec;
+  auto put = [&](const void* v, size_t n) { rec.insert(rec.end(), (const char*)v, (const char*)v + n); };
+  std::vector<const double*> bases;
+  std::map<const double*, int32_t> base_id;
+  std::vector<char> body;
+  const int exported = [&]() -> int {
+    std::vector<char> hdr;
+    for (XPlan* pp : todo) {
+      const XPlan& pl = *pp;
+      const int32_t nmsg = (int32_t)pl.rsend.size();
+      body.insert(body.end(), (const char*)&nmsg, (const char*)&nmsg + 4);
+      for (const XMsg& m : pl.rsend) {
+        std::vector<size_t> segs;  // in buffer order: the receiver pairs them with its unpack segments so
+        for (size_t i = 0; i < pl.h_pre.size(); ++i)
+          if (pl.h_pre_off[i] >= m.off && pl.h_pre_off[i] < m.off + m.count) segs.push_back(i);
+        std::sort(segs.begin(), segs.end(), [&](size_t a, size_t b) { return pl.h_pre_off[a] < pl.h_pre_off[b]; });
+        const int32_t dest = m.peer_rank, ns = (int32_t)segs.size();
+        body.insert(body.end(), (const char*)&dest, (const char*)&dest + 4);
+        body.insert(body.end(), (const char*)&ns, (const char*)&ns + 4);
+        for (size_t i : segs) {
+          const XSeg& sg = pl.h_pre[i];
+          size_t nb = 0;
+          const double* b = base_of(sg.src, nb);
+          if (!b) {
+            ctx->err = "internal: pack segment outside every field";
+            return MPAS_DYC_ESTATE;
+          }
+          if (!base_id.count(b)) {
+            base_id[b] = (int32_t)bases.size();
+            bases.push_back(b);
+          }
+          const int32_t id = base_id[b], n = sg.n, inner = sg.inner;
+          const int64_t off = (const char*)sg.src - (const char*)b;
+          const std::vector<int32_t>& idx = *pl.h_pre_idx[i];
+          body.insert(body.end(), (const char*)&id, (const char*)&id + 4);
+          body.insert(body.end(), (const char*)&off, (const char*)&off + 8);
+          body.insert(body.end(), (const char*)&n, (const char*)&n + 4);
+          body.insert(body.end(), (const char*)&inner, (const char*)&inner + 4);
+          body.insert(body.end(), (const char*)idx.data(), (const char*)(idx.data() + n));
+        }
+      }
+    }
+    const int32_t nbase = (int32_t)bases.size();
+    put(&nbase, 4);
+    for (const double* b : bases) {
+      const uint64_t a = (uint64_t)(uintptr_t)b;
+      hipIpcMemHandle_t h{};
+      if (nr > 1) HIPCHK(hipIpcGetMemHandle(&h, (void*)b));
+      put(&a, 8);
+      put(&h, sizeof(h));
+    }
+    rec.insert(rec.end(), body.begin(), body.end());
+    return MPAS_DYC_OK;
+  }();
+  if (nr > 1) CHK(p2p_vote(ctx, exported, "exporting the field buffers"));
+  else CHK(exported);
+  std::vector<std::vector<char>> all;
+  CHK(allgatherv_bytes(ctx, rec, all));
+  // per rank: its buffer table and a cursor over its per-plan messages
+  struct Reader {
+    const char* p;
+    std::vector<std::pair<uint64_t, hipIpcMemHandle_t>> bases;
+  };
+  std::vector<Reader> rd(nr);
+  for (int r = 0; r < nr; ++r) {
+    const char* p = all[r].data();
+    int32_t nb;
+    memcpy(&nb, p, 4);
+    p += 4;
+    for (int i = 0; i < nb; ++i) {
+      std::pair<uint64_t, hipIpcMemHandle_t> e;
+      memcpy(&e.first, p, 8);
+      memcpy(&e.second, p + 8, sizeof(hipIpcMemHandle_t));
+      p += 8 + sizeof(hipIpcMemHandle_t);
+      rd[r].bases.push_back(e);
+    }
+    rd[r].p = p;
+  }
+  struct SegIn {
+    int32_t id, n, inner;
+    int64_t off;
+    const int32_t* idx;
+  };
+  // a mapped field buffer of rank r (each buffer opened once per context)
+  auto mapped = [&](int r, int32_t id, const double*& out) -> int {
+    const auto& e = rd[r].bases.at(id);
+    if (r == me) {
+      out = (const double*)(uintptr_t)e.first;
+      return MPAS_DYC_OK;
+    }
+    auto key = std::make_pair(r, e.first);
+    auto it = ctx->p2p_fields.find(key);
+    if (it == ctx->p2p_fields.end()) {
+      void* p = nullptr;
+      HIPCHK(hipIpcOpenMemHandle(&p, e.second, hipIpcMemLazyEnablePeerAccess));
+      ctx->p2p_mapped.push_back(p);
+      it = ctx->p2p_fields.emplace(key, p).first;
+    }
+    out = (const double*)it->second;
+    return MPAS_DYC_OK;
+  };
+  const int built = [&]() -> int {
+    for (XPlan* pp : todo) {
+      XPlan& pl = *pp;
+      if (ctx->p2p_next >= P2P_MAX_POINTS) {
+        ctx->err = "MPAS_DYCORE_P2P: more than " + std::to_string(P2P_MAX_POINTS) + " exchange points";
+        return MPAS_DYC_ESTATE;
+      }
+      pl.p2p_id = ctx->p2p_next++;
+      auto flag = [&](unsigned long long* arena, int r, int k) {
+        return arena + ((size_t)pl.p2p_id * ctx->p2p_nr + r) * 2 + k;
+      };
+      // every rank's messages of this exchange point: rank -> destination -> its pack segments
+      std::vector<std::map<int, std::vector<SegIn>>> from(nr);
+      for (int r = 0; r < nr; ++r) {
+        const char*& q = rd[r].p;
+        int32_t nmsg;
+        memcpy(&nmsg, q, 4);
+        q += 4;
+        for (int m = 0; m < nmsg; ++m) {
+          int32_t dest, ns;
+          memcpy(&dest, q, 4);
+          memcpy(&ns, q + 4, 4);
+          q += 8;
+          auto& v = from[r][dest];
+          for (int k = 0; k < ns; ++k) {
+            SegIn si{};
+            memcpy(&si.id, q, 4);
+            memcpy(&si.off, q + 4, 8);
+            memcpy(&si.n, q + 12, 4);
+            memcpy(&si.inner, q + 16, 4);
+            si.idx = (const int32_t*)(q + 20);
+            q += 20 + 4 * (size_t)si.n;
+            v.push_back(si);
+          }
+        }
+      }
+      std::vector<P2PSeg> segs;
+      std::vector<P2PPeer> peers;
+      std::vector<unsigned long long*> ready;
+      std::vector<const unsigned long long*> cons;
+      std::map<int, int> peer_ix;
+      auto peer_of = [&](int src) -> int {
+        auto it = peer_ix.find(src);
+        if (it != peer_ix.end()) return it->second;
+        const int ix = (int)peers.size();
+        peer_ix[src] = ix;
+        const bool here = ctx->loopback || src == me;
+        peers.push_back(P2PPeer{flag(ctx->p2p_flags, src, 0),
+                                here ? flag(ctx->p2p_flags, src, 1) : flag(ctx->p2p_peer_flags[src], me, 1), nullptr, 0});
+        return ix;
+      };
+      auto upload = [&](const void* h, size_t bytes) -> void* {
+        void* d = nullptr;
+        if (hipMalloc(&d, std::max<size_t>(bytes, 8)) != hipSuccess) return nullptr;
+        if (bytes && hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+          (void)hipFree(d);
+          return nullptr;
+        }
+        pl.pull_mem.push_back(d);
+        return d;
+      };
+      std::set<int> loop_peers;  // loopback: every emulated peer
+      for (const XMsg& m : pl.rrecv) {
+        std::vector<size_t> mine_post;  // in buffer order, as the sender exported its pack segments
+        for (size_t i = 0; i < pl.h_post.size(); ++i)
+          if (pl.h_post_off[i] >= m.off && pl.h_post_off[i] < m.off + m.count) mine_post.push_back(i);
+        std::sort(mine_post.begin(), mine_post.end(),
+                  [&](size_t a, size_t b) { return pl.h_post_off[a] < pl.h_post_off[b]; });
+        const int src = m.peer_rank;
+        const int ix = peer_of(src);
+        if (ctx->loopback) {
+          // timing only: the peer's segments are this rank's own pack segments to that peer
+          loop_peers.insert(src);
+          std::vector<size_t> theirs;
+          for (const XMsg& sm : pl.rsend)
+            if (sm.peer_rank == src)
+              for (size_t i = 0; i < pl.h_pre.size(); ++i)
+                if (pl.h_pre_off[i] >= sm.off && pl.h_pre_off[i] < sm.off + sm.count) theirs.push_back(i);
+          std::sort(theirs.begin(), theirs.end(), [&](size_t a, size_t b) { return pl.h_pre_off[a] < pl.h_pre_off[b]; });
+          for (size_t k = 0; k < std::min(theirs.size(), mine_post.size()); ++k) {
+            const XSeg &a = pl.h_pre[theirs[k]], &b = pl.h_post[mine_post[k]];
+            const int n = std::min(a.n, b.n);
+            segs.push_back(P2PSeg{a.src, b.dst, a.sidx, b.didx, n, std::min(a.inner, b.inner), ix});
+          }
+          continue;
+        }
+        auto f = from[src].find(me);
+        if (f == from[src].end() || f->second.size() != mine_post.size()) {
+          ctx->err = "MPAS_DYCORE_P2P: rank " + std::to_string(src) + "'s message to rank " + std::to_string(me) +
+                     " does not match this rank's receive lists";
+          return MPAS_DYC_ECOMM;
+        }
+        for (size_t k = 0; k < mine_post.size(); ++k) {
+          const SegIn& a = f->second[k];
+          const XSeg& b = pl.h_post[mine_post[k]];
+          if (a.n != b.n || a.inner != b.inner) {
+            ctx->err = "MPAS_DYCORE_P2P: rank " + std::to_string(src) + " sends " + std::to_string(a.n) +
+                       " elements where rank " + std::to_string(me) + " receives " + std::to_string(b.n);
+            return MPAS_DYC_ECOMM;
+          }
+          const double* base = nullptr;
+          CHK(mapped(src, a.id, base));
+          const int* sidx = (const int*)upload(a.idx, sizeof(int32_t) * (size_t)a.n);
+          if (!sidx) {
+            ctx->err = "hipMalloc for a peer's send list failed";
+            return MPAS_DYC_EHIP;
+          }
+          segs.push_back(P2PSeg{(const double*)((const char*)base + a.off), b.dst, sidx, b.didx, a.n, a.inner, ix});
+        }
+      }
+      if (ctx->loopback) {
+        for (const XMsg& m : pl.rsend) {
+          loop_peers.insert(m.peer_rank);
+          (void)peer_of(m.peer_rank);
+        }
+        for (int q : loop_peers) ready.push_back(flag(ctx->p2p_flags, q, 0));
+      } else {
+        for (const XMsg& m : pl.rsend) {
+          ready.push_back(flag(ctx->p2p_peer_flags[m.peer_rank], me, 0));
+          cons.push_back(flag(ctx->p2p_flags, m.peer_rank, 1));
+        }
+      }
+      std::vector<int2> chunks;
+      for (size_t k = 0; k < segs.size(); ++k)
+        for (int c = 0; c < segs[k].n; c += P2P_PULL_COLS) {
+          chunks.push_back(make_int2((int)k, c));
+          peers[segs[k].peer].nwg += 1;
+        }
+      pl.nchunk = (int)chunks.size();
+      pl.npeer_work = 0;
+      for (const P2PPeer& pr : peers) pl.npeer_work += pr.nwg ? 1 : 0;
+      if (ctx->loopback)  // the emulated readers of this rank: the peers with segments here
+        for (const P2PPeer& pr : peers)
+          if (pr.nwg) cons.push_back(pr.consumed);
+      if (cons.size() > 256 || ready.size() > 256) {
+        ctx->err = "MPAS_DYCORE_P2P: more than 256 peers";
+        return MPAS_DYC_EINVAL;
+      }
+      // [0] uses, [1] finished workgroups of k_p2p_pull, [2 + i] workgroups done for peer i
+      HIPCHK(hipMalloc(&pl.p2p_cnt, (2 + peers.size()) * sizeof(unsigned long long)));
+      HIPCHK(hipMemset(pl.p2p_cnt, 0, (2 + peers.size()) * sizeof(unsigned long long)));
+      for (size_t j = 0; j < peers.size(); ++j) peers[j].done = pl.p2p_cnt + 2 + j;
+      pl.npseg = (int)segs.size();
+      pl.nready = (int)ready.size();
+      pl.ncons = (int)cons.size();
+      pl.d_pseg = (P2PSeg*)upload(segs.data(), segs.size() * sizeof(P2PSeg));
+      pl.d_chunk = (int2*)upload(chunks.data(), chunks.size() * sizeof(int2));
+      pl.d_peer = (P2PPeer*)upload(peers.data(), peers.size() * sizeof(P2PPeer));
+      pl.d_ready = (unsigned long long**)upload(ready.data(), ready.size() * sizeof(void*));
+      pl.d_cons = (const unsigned long long**)upload(cons.data(), cons.size() * sizeof(void*));
+      if (!pl.d_pseg || !pl.d_chunk || !pl.d_peer || !pl.d_ready || !pl.d_cons) {
+        ctx->err = "hipMalloc for a pull plan failed";
+        return MPAS_DYC_EHIP;
+      }
+      // d_ready / d_cons are freed with the plan (free_plan); keep them out of pull_mem
+      pl.pull_mem.erase(std::remove_if(pl.pull_mem.begin(), pl.pull_mem.end(),
+                                       [&](void* q) { return q == (void*)pl.d_ready || q == (void*)pl.d_cons ||
+                                                             q == (void*)pl.d_pseg || q == (void*)pl.d_peer ||
+                                                             q == (void*)pl.d_chunk; }),
+                        pl.pull_mem.end());
+    }
+    return MPAS_DYC_OK;
+  }();
+  return nr > 1 ? p2p_vote(ctx, built, "mapping the peers' fields") : built;
+}
+
 // the one-sided transfer dropped on every rank (P2P_UNAVAILABLE): its mappings and arena freed, the
 // plans rebuilt for RCCL by the caller
 void p2p_fallback(mpas_dyc_ctx* ctx) {
@@ -1400,6 +1756,7 @@ void p2p_fallback(mpas_dyc_ctx* ctx) {
   invalidate_plans(ctx);
   for (void* p : ctx->p2p_mapped) (void)hipIpcCloseMemHandle(p);
   ctx->p2p_mapped.clear();
+  ctx->p2p_fields.clear();
   if (ctx->p2p_flags) (void)hipFree(ctx->p2p_flags);
   ctx->p2p_flags = nullptr;
   ctx->p2p_peer_flags.clear();
@@ -1457,6 +1814,21 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, int part = 0) {
         return exchange(ctx, fs, part);
       }
       CHK(r);
+    }
+    if (pl.pull) {  // blocking only (build_plan): the whole exchange at the first call
+      if (part == 2) return MPAS_DYC_OK;
+      CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
+      if (pl.nlocal)
+        hipLaunchKernelGGL(k_halo_copy, dim3((pl.maxn_local + 3) / 4, pl.nlocal), dim3(256), 0, ctx->stream, pl.d_local);
+      set_last_key(ctx, key);
+      CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
+      hipLaunchKernelGGL(k_p2p_pull, dim3(pl.nchunk + 1), dim3(256), 0, ctx->stream, (const P2PSeg*)pl.d_pseg,
+                         (const int2*)pl.d_chunk, pl.nchunk, (const P2PPeer*)pl.d_peer, pl.npeer_work,
+                         (unsigned long long* const*)pl.d_ready, pl.nready, (const unsigned long long* const*)pl.d_cons,
+                         pl.ncons, pl.p2p_cnt, ctx->p2p_status);
+      CHK(prof_mark(ctx, ctx->prof_rccl, ctx->stream));
+      CHK(prof_mark(ctx, ctx->prof_exposed, ctx->stream));
+      return MPAS_DYC_OK;
     }
     if (part == 0 && !ctx->p2p_merge) {  // the two launches (A/B of the merged one)
       CHK(exchange(ctx, fs, 1));
@@ -2952,6 +3324,7 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   if (const char* lb = getenv("MPAS_DYCORE_LOOPBACK")) ctx->loopback = std::atoi(lb);
   if (const char* pp = getenv("MPAS_DYCORE_P2P")) ctx->p2p = std::atoi(pp);
   if (const char* pm = getenv("MPAS_DYCORE_P2P_MERGE")) ctx->p2p_merge = std::atoi(pm) != 0;
+  if (const char* pu = getenv("MPAS_DYCORE_P2P_PULL")) ctx->p2p_pull = std::atoi(pu) != 0;
   if (const char* li = getenv("MPAS_DYCORE_LATE_ISSUE")) ctx->late_issue = std::string(li) == "1";
   if (const char* oa = getenv("MPAS_DYCORE_OVERLAP_ALL")) ctx->overlap_all = std::string(oa) == "1";
   if (const char* ov = getenv("MPAS_DYCORE_OVERLAP")) ctx->overlap = std::atoi(ov);

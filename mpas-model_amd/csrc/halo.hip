@@ -182,6 +182,90 @@ __global__ __launch_bounds__(256) void k_p2p_exchange(const P2PGet* __restrict__
   }
 }
 
+// Pull exchange (blocking one-sided exchanges with block-pair lists): the receiving rank copies each
+// peer's owned columns straight from the peer's field (IPC-mapped) into its own halo columns -- the
+// peer's pack segment and this rank's unpack segment of one message slot, fused -- so an exchange is
+// this one launch: no pack, no send or receive buffer, no unpack.  The protocol is k_p2p_exchange's:
+// ready raised at the start (the peer's field is final: its producer has ended), per peer the last
+// workgroup raises consumed, and the kernel ends only when every rank that reads this rank's fields
+// has finished (the next kernel may overwrite them).  The peer's field is ordinary device memory:
+// its producer's stores reach memory when that kernel ends (the L2 write-back that makes them
+// visible to the other XCDs), and the loads here are system-scope so that no cache of this GPU
+// holds a stale copy from the previous exchange.
+struct P2PSeg {
+  const double* src;  // the peer's field (mapped), sub-field base
+  double* dst;        // this rank's field
+  const int* sidx;    // the peer's send list (0-based owned elements), a copy in this rank's memory
+  const int* didx;    // this rank's receive list (halo elements)
+  int n, inner, peer;
+};
+struct P2PPeer {
+  const unsigned long long* ready;  // raised by the peer (this rank's arena)
+  unsigned long long* consumed;     // raised here when all of the peer's segments are copied (its arena)
+  unsigned long long* done;         // workgroups done, over all uses (local)
+  unsigned long long nwg;           // workgroups per use with work for this peer
+};
+
+__device__ inline double sys_load(const double* a) {
+  const unsigned long long v = __hip_atomic_load((const unsigned long long*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __longlong_as_double((long long)v);
+}
+
+constexpr int P2P_PULL_COLS = 16;  // element columns per workgroup (4 per wave)
+
+// grid (nchunk + 1): workgroup x < nchunk copies columns chunk[x].y .. +15 of segment chunk[x].x (a
+// chunk never spans two segments, so one peer); workgroup nchunk waits for the ranks that read this
+// rank's fields.  Completion is counted per peer (one atomic per workgroup) and, by the last
+// workgroup of each peer and the waiting one, per launch: the last of those advances the use
+// counter, after every workgroup has read it.
+__global__ __launch_bounds__(256) void k_p2p_pull(const P2PSeg* __restrict__ segs, const int2* __restrict__ chunk,
+                                                  int nchunk, const P2PPeer* __restrict__ peers, int npeer_work,
+                                                  unsigned long long* const* ready, int nready,
+                                                  const unsigned long long* const* consumed, int ncons,
+                                                  unsigned long long* use, int* status) {
+  const unsigned long long n = use[0] + 1;
+  bool last = false;  // this workgroup closes a peer (or is the waiting one)
+  if ((blockIdx.x == 0 || (int)blockIdx.x == nchunk) && (int)threadIdx.x < nready)
+    __hip_atomic_store(ready[threadIdx.x], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((int)blockIdx.x == nchunk) {
+    if ((int)threadIdx.x < ncons) (void)p2p_wait_geq(consumed[threadIdx.x], n, status);
+    last = true;
+  } else {
+    const int2 ch = chunk[blockIdx.x];
+    const P2PSeg& sg = segs[ch.x];
+    const P2PPeer& pr = peers[sg.peer];
+    __shared__ int ok;
+    if (threadIdx.x == 0) ok = p2p_wait_geq(pr.ready, n, status);
+    __syncthreads();
+    if (ok) {
+      const int inner = sg.inner;
+#pragma unroll
+      for (int c = 0; c < P2P_PULL_COLS / 4; ++c) {
+        const int i = __builtin_amdgcn_readfirstlane(ch.y + c * 4 + (int)(threadIdx.x >> 6));
+        if (i < sg.n) {
+          const int si = __builtin_amdgcn_readfirstlane(sg.sidx[i]), di = __builtin_amdgcn_readfirstlane(sg.didx[i]);
+          const double* src = sg.src + (size_t)si * inner;
+          double* dst = sg.dst + (size_t)di * inner;
+          for (int j = threadIdx.x & 63; j < inner; j += 64) dst[j] = sys_load(src + j);
+        }
+      }
+    }
+    __syncthreads();  // every lane's loads have returned
+    if (threadIdx.x == 0) {
+      const unsigned long long old = __hip_atomic_fetch_add(pr.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (old + 1 == n * pr.nwg) {
+        __hip_atomic_store(pr.consumed, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = true;
+      }
+    }
+  }
+  if (threadIdx.x == 0 && last) {
+    const unsigned long long old = __hip_atomic_fetch_add(use + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1 == n * (unsigned long long)(npeer_work + 1))
+      __hip_atomic_store(use, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // atm_rk_integration_setup (mpas_atm_time_integration.F:1847-1857): the ten state/diag
 // copies of one block in a single launch; blockIdx.y selects the copy.
 struct CopyList {

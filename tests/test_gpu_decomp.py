@@ -191,25 +191,28 @@ def test_fused_exchanges_keep_halo_fields(small_case):
         assert np.array_equal(runs[0][key], runs[1][key]), f"{key}: fused exchange differs from pack/unpack kernels"
 
 
-@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("mode", ["pull", "buffers", "split"])
 @pytest.mark.parametrize("which", ["small_case", "moist_case"])
-def test_p2p_transport_bitwise(which, overlap, request):
-    """One-sided transfer (MPAS_DYCORE_P2P=1; halo.hip k_p2p_post / k_p2p_get): 4 blocks of one rank
-    whose messages all go through the one-sided protocol -- the post raises this rank's ready flags,
-    the get pulls each message from the uncached send buffer, raises the consumed flag and waits for
-    the others' -- equal one block bit for bit, graph replay, blocking exchanges (the p2p default) and
-    split-phase (post at the exchange, get where the halo is read)."""
+def test_p2p_transport_bitwise(which, mode, request):
+    """One-sided transfer (MPAS_DYCORE_P2P=1; halo.hip): 4 blocks of one rank whose messages all go
+    through the one-sided protocol equal one block bit for bit, graph replay.  pull: blocking
+    exchanges, the receiver copies the sender's owned columns from its fields (k_p2p_pull, the p2p
+    default); buffers: blocking, send buffers pulled into receive buffers with the fused packs and
+    unpacks (k_p2p_exchange, MPAS_DYCORE_P2P_PULL=0); split: split-phase exchanges (k_p2p_post at the
+    exchange, k_p2p_get where the halo is read)."""
     import os
     case = request.getfixturevalue(which)
     one = _single(case, 3)
-    old = os.environ.get("MPAS_DYCORE_P2P")
-    os.environ["MPAS_DYCORE_P2P"] = "1"
+    env = {"MPAS_DYCORE_P2P": "1", "MPAS_DYCORE_P2P_PULL": "0" if mode == "buffers" else "1"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
-        got = _blocks(case, 4, 3, graph=True, rccl_local=True, overlap=overlap)
+        got = _blocks(case, 4, 3, graph=True, rccl_local=True, overlap=mode == "split")
     finally:
-        if old is None:
-            os.environ.pop("MPAS_DYCORE_P2P", None)
-        else:
-            os.environ["MPAS_DYCORE_P2P"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     for name in one:
         assert np.array_equal(got[name], one[name]), f"{name}: p2p blocks differ from one block"
