@@ -299,6 +299,15 @@ int mpas_dyc_set_exchange_positions(mpas_dyc_ctx* ctx, int32_t block, int32_t lo
 int64_t mpas_dyc_comm_unique_id_bytes(void);
 int mpas_dyc_comm_unique_id(void* id, int64_t nbytes);
 int mpas_dyc_comm_init(mpas_dyc_ctx* ctx, const void* id, int64_t nbytes, int32_t nranks, int32_t rank);
+/* Ranks without RCCL: the host's own all-gather (MPI_Allgather, a torch.distributed gloo group, ...)
+ * for the few set-up collectives, and the one-sided transfer (mpas_dyc_set_p2p, switched on here) for
+ * every halo message -- all ranks on one node.  fn(send, recv, nbytes, user) must place every rank's
+ * nbytes in recv in rank order and return 0; it is called from mpas_dyc_timestep /
+ * mpas_dyc_init_diagnostics / mpas_dyc_halo_exchange (set-up of new exchange points, on every rank at
+ * the same call) and from mpas_dyc_get_summary, never during graph capture.  Instead of
+ * mpas_dyc_comm_init; a context has one or the other. */
+typedef int (*mpas_dyc_allgather_fn)(const void* send, void* recv, int64_t nbytes, void* user);
+int mpas_dyc_comm_init_host(mpas_dyc_ctx* ctx, int32_t nranks, int32_t rank, mpas_dyc_allgather_fn fn, void* user);
 /* Test hook: route block-to-block exchanges inside this process through RCCL (send to self). */
 int mpas_dyc_set_transport(mpas_dyc_ctx* ctx, int32_t rccl_for_local_blocks);
 /* One-sided transfer between the ranks of one node (on = 1; 0 = RCCL groups; -1 = the environment

@@ -243,6 +243,9 @@ struct mpas_dyc_ctx {
   // the exchange whose RCCL group was enqueued last (a watchdog's report when a group hangs)
   char last_key[256] = {0};
   double* sum_gather = nullptr;         // RCCL all-gather buffer of the per-rank records
+  // mpas_dyc_comm_init_host: the host's all-gather instead of an RCCL communicator (one-sided transfer)
+  mpas_dyc_allgather_fn host_allgather = nullptr;
+  void* host_user = nullptr;
 };
 
 namespace {
@@ -882,7 +885,8 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
           }
     }
   }
-  if ((!pl.rsend.empty() || !pl.rrecv.empty()) && !ctx->comm && !ctx->host_only) {
+  if ((!pl.rsend.empty() || !pl.rrecv.empty()) && !ctx->comm && !(ctx->host_allgather && ctx->p2p) &&
+      !ctx->host_only) {
     ctx->err = "exchange lists name other processes but no communicator was set (mpas_dyc_comm_init)";
     return MPAS_DYC_ECOMM;
   }
@@ -1218,6 +1222,13 @@ int allgather_bytes(mpas_dyc_ctx* ctx, const void* mine, size_t nbytes, std::vec
     memcpy(all.data(), mine, nbytes);
     return MPAS_DYC_OK;
   }
+  if (!ctx->comm && ctx->host_allgather) {
+    if (ctx->host_allgather(mine, all.data(), (int64_t)nbytes, ctx->host_user) != 0) {
+      ctx->err = "the host's all-gather (mpas_dyc_comm_init_host) failed";
+      return MPAS_DYC_ECOMM;
+    }
+    return MPAS_DYC_OK;
+  }
   char* d = nullptr;
   HIPCHK(hipMalloc(&d, nbytes * (ctx->nranks + 1)));
   const int r = [&]() -> int {
@@ -1268,8 +1279,8 @@ int p2p_vote(mpas_dyc_ctx* ctx, int local, const std::string& what) {
 // the flag arenas: this rank's, and every peer's mapped here
 int p2p_init(mpas_dyc_ctx* ctx) {
   if (ctx->p2p_flags) return MPAS_DYC_OK;
-  if (!ctx->comm) {
-    ctx->err = "MPAS_DYCORE_P2P: no communicator for the set-up (mpas_dyc_comm_init)";
+  if (!ctx->comm && !ctx->host_allgather) {
+    ctx->err = "MPAS_DYCORE_P2P: no communicator for the set-up (mpas_dyc_comm_init / _comm_init_host)";
     return MPAS_DYC_ECOMM;
   }
   int nr = ctx->nranks;
@@ -1810,6 +1821,7 @@ int exchange(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, int part = 0) {
       }
       const int r = p2p_setup(ctx);
       if (r == P2P_UNAVAILABLE) {  // every rank is here: this exchange, and the rest, through RCCL
+        if (!ctx->comm) return MPAS_DYC_ECOMM;
         p2p_fallback(ctx);
         return exchange(ctx, fs, part);
       }
@@ -3253,6 +3265,7 @@ int plan_all(mpas_dyc_ctx* ctx, double dt) {
     ctx->planned.insert(sig);
     r = ctx->p2p ? p2p_setup(ctx) : MPAS_DYC_OK;
     if (r == P2P_UNAVAILABLE) {  // every rank is here: plan again for RCCL
+      if (!ctx->comm) return MPAS_DYC_ECOMM;  // mpas_dyc_comm_init_host: nothing to fall back to
       p2p_fallback(ctx);
       return plan_all(ctx, dt);
     }
@@ -3729,6 +3742,18 @@ int mpas_dyc_comm_init(mpas_dyc_ctx* ctx, const void* id, int64_t nbytes, int32_
   return MPAS_DYC_OK;
 }
 
+int mpas_dyc_comm_init_host(mpas_dyc_ctx* ctx, int32_t nranks, int32_t rank, mpas_dyc_allgather_fn fn, void* user) {
+  if (!ctx || !fn || nranks < 1 || rank < 0 || rank >= nranks) return MPAS_DYC_EINVAL;
+  if (ctx->host_only || ctx->comm) return MPAS_DYC_ESTATE;
+  invalidate_plans(ctx);
+  ctx->host_allgather = fn;
+  ctx->host_user = user;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  ctx->p2p = 1;
+  return MPAS_DYC_OK;
+}
+
 int mpas_dyc_set_transport(mpas_dyc_ctx* ctx, int32_t rccl_for_local_blocks) {
   if (!ctx) return MPAS_DYC_EINVAL;
   invalidate_plans(ctx);
@@ -3829,6 +3854,15 @@ static int get_summary(mpas_dyc_ctx* ctx, int32_t blocks, mpas_dyc_summary* out,
       if (first_block) std::copy(x, x + PL, acc);
       else fold(acc, x);
     }
+  }
+  if (!ctx->comm && ctx->host_allgather && ctx->nranks > 1) {  // the host's all-gather, folded in rank order
+    std::vector<char> all;
+    CHK(allgather_bytes(ctx, pay.data(), pay.size() * sizeof(double), all));
+    const size_t cnt = pay.size();
+    const double* a = (const double*)all.data();
+    std::copy(a, a + cnt, pay.begin());
+    for (int r = 1; r < ctx->nranks; ++r)
+      for (int f = 0; f < nf; ++f) fold(&pay[(size_t)f * PL], &a[cnt * r + (size_t)f * PL]);
   }
   if (ctx->comm && ctx->nranks > 1) {
     // all ranks' payloads to every rank (RCCL all-gather, in place), folded in rank order

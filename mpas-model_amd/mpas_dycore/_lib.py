@@ -9,6 +9,9 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+# int fn(const void* send, void* recv, int64_t nbytes, void* user) -- mpas_dyc_comm_init_host
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.environ.get("MPAS_DYCORE_LIB") or os.path.join(os.path.dirname(HERE), "csrc", "libmpas_dycore.so")
 
@@ -19,7 +22,7 @@ EXPORTS = (
     "mpas_dyc_acoustic_bytes", "mpas_dyc_create_blocks", "mpas_dyc_num_blocks", "mpas_dyc_set_block_field",
     "mpas_dyc_get_block_field", "mpas_dyc_block_field_bytes", "mpas_dyc_block_field_device_ptr",
     "mpas_dyc_set_exchange_list", "mpas_dyc_comm_unique_id_bytes", "mpas_dyc_comm_unique_id", "mpas_dyc_comm_init",
-    "mpas_dyc_set_transport", "mpas_dyc_set_p2p", "mpas_dyc_get_p2p", "mpas_dyc_halo_exchange", "mpas_dyc_set_overlap", "mpas_dyc_output_diagnostics",
+    "mpas_dyc_set_transport", "mpas_dyc_set_p2p", "mpas_dyc_get_p2p", "mpas_dyc_comm_init_host", "mpas_dyc_halo_exchange", "mpas_dyc_set_overlap", "mpas_dyc_output_diagnostics",
     "mpas_dyc_set_physics", "mpas_dyc_set_summary", "mpas_dyc_get_summary", "mpas_dyc_plan_exchanges",
     "mpas_dyc_graph_active", "mpas_dyc_solve_diagnostics", "mpas_dyc_set_lbc", "mpas_dyc_finish_step",
     "mpas_dyc_get_block_summary", "mpas_dyc_block_layout", "mpas_dyc_set_profile", "mpas_dyc_get_profile",
@@ -144,6 +147,7 @@ def load() -> C.CDLL:
     lib.mpas_dyc_set_transport.argtypes = [vp, i32]
     lib.mpas_dyc_set_p2p.argtypes = [vp, i32]
     lib.mpas_dyc_get_p2p.argtypes = [vp]
+    lib.mpas_dyc_comm_init_host.argtypes = [vp, i32, i32, ALLGATHER_FN, vp]
     lib.mpas_dyc_halo_exchange.argtypes = [vp, C.c_char_p, C.c_char_p, i32, i32]
     lib.mpas_dyc_set_overlap.argtypes = [vp, i32]
     lib.mpas_dyc_set_summary.argtypes = [vp, i32]

@@ -38,6 +38,27 @@ _SKIP = set(STATE_INPUTS) | set(DIAG_INPUTS) | {"xCell", "yCell", "zCell", "xEdg
                                                 "meshDensity", "indexToCellID", "deriv_two", "zb", "zb3"}
 
 
+def _host_allgather_fn(group, nranks: int):
+    """mpas_dyc_comm_init_host's all-gather over a torch.distributed group: every rank's bytes, in rank
+    order (CPU tensors, so gloo carries them)."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(send, recv, nbytes, user):
+        try:
+            mine = torch.frombuffer(bytearray(C.string_at(send, nbytes)), dtype=torch.uint8) if nbytes else \
+                torch.zeros(0, dtype=torch.uint8)
+            outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(nranks)]
+            dist.all_gather(outs, mine, group=group)
+            buf = b"".join(bytes(o.numpy().tobytes()) for o in outs)
+            C.memmove(recv, buf, len(buf))
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the library as a failed all-gather
+            return 1
+
+    return _lib.ALLGATHER_FN(fn)
+
+
 class DycoreError(RuntimeError):
     pass
 
@@ -170,19 +191,26 @@ class Dycore:
     @classmethod
     def from_blocks(cls, blocks: list, device: int = 0, moist_end: int = 1, placement: dict | None = None,
                     rank: int = 0, nranks: int = 1, comm_id: bytes | None = None, rccl_local: bool = False,
-                    positional: bool = False, p2p: bool | None = None):
+                    positional: bool = False, p2p: bool | None = None, host_group=None):
         """Blocks of this process (``decomp.decompose(..., parts=...)``) on one GPU.
 
         ``placement`` maps every block (part) id to (rank, local block index); by
         default all blocks live in this process, in the given order.  With
         ``nranks`` > 1, ``comm_id`` is the RCCL unique id created on rank 0.  ``p2p``: one-sided
-        transfer between the ranks of the node (mpas_dyc_set_p2p; None = MPAS_DYCORE_P2P)."""
+        transfer between the ranks of the node (mpas_dyc_set_p2p; None = MPAS_DYCORE_P2P).
+        ``host_group``: a torch.distributed process group (gloo) of the ranks instead of ``comm_id``: no
+        RCCL communicator, the set-up all-gathers go through the group (mpas_dyc_comm_init_host) and
+        every halo message through the one-sided transfer."""
         if placement is None:
             placement = {b.part: (0, i) for i, b in enumerate(blocks)}
         self = cls(device=device, moist_end=moist_end, _blocks=blocks)
         if comm_id is not None:
             idb = C.create_string_buffer(bytes(comm_id), len(comm_id))
             self._check(self.lib.mpas_dyc_comm_init(self.h, idb, len(comm_id), int(nranks), int(rank)), "comm_init")
+        elif host_group is not None:
+            self._host_allgather = _host_allgather_fn(host_group, int(nranks))  # kept alive with the context
+            self._check(self.lib.mpas_dyc_comm_init_host(self.h, int(nranks), int(rank), self._host_allgather, None),
+                        "comm_init_host")
         if rccl_local:
             self._check(self.lib.mpas_dyc_set_transport(self.h, 1), "set_transport")
         if p2p is not None:

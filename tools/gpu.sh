@@ -29,6 +29,7 @@
 #                    eager tools/kbench.py dt for each of AB_LIBS (gpurun_out/kpmc_<lib>_<set>)
 #   maxedges         bench.py with the mesh declared maxEdges 6 vs 10 (AB_ROUNDS rounds), and from an init file
 #                    declaring maxEdges 10 (tools/write_init.py)
+#   tworanks         tools/p2p_two_ranks.py: two ranks on the GPU, one-sided transfer over IPC, bitwise vs one block
 #   ipc              tools/p2p_ipc_check: the one-sided protocol between two processes on the GPU (IPC)
 #   floor            tools/gather_floor: the gather kernels next to load-only replays of their index streams
 #   smoke            __graft_entry__.smoke()
@@ -103,6 +104,10 @@ step() {
         timeout -k 10 400 python bench.py --steps 10 --warmup 2 $B --init /tmp/x1.163842.me10.init.nc --dt 360 --len-disp 60000 >> gpurun_out/maxedges.log 2>&1 || return 1
         grep -h "==\|ms_per_step" gpurun_out/maxedges.log | sed 's/.*"ms_per_step": \([0-9.]*\).*"kernel_layout": \({[^}]*}\).*/ms_per_step \1 \2/' ;;
     floor) timeout -k 10 400 python tools/gather_floor.py ${FLOOR_ARGS} > gpurun_out/floor.log 2>&1; r=$?; cat gpurun_out/floor.log; return $r ;;
+    tworanks) rm -f gpurun_out/tworanks.log   # two ranks on the one GPU, one-sided transfer, no RCCL
+              for A in "" "--moist" "--pull 0"; do
+                timeout -k 10 300 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 tools/p2p_two_ranks.py $A >> gpurun_out/tworanks.log 2>&1 || { tail -30 gpurun_out/tworanks.log; return 1; }
+              done; grep bitwise gpurun_out/tworanks.log ;;
     ipc) timeout -k 10 600 python tools/p2p_ipc_check.py ${IPC_ARGS} > gpurun_out/ipc.log 2>&1; r=$?; cat gpurun_out/ipc.log; return $r ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && last gpurun_out/smoke.log ;;
     *) echo "unknown step $1"; return 2 ;;
