@@ -190,6 +190,9 @@ def main():
     ap.add_argument("--acoustic-reps", type=int, default=20)
     ap.add_argument("--blocks", type=int, default=1, help="blocks per GPU (MPAS blocks with halos)")
     ap.add_argument("--rccl-local", action="store_true", help="route in-process block exchanges through RCCL")
+    ap.add_argument("--same-device", action="store_true",
+                    help="test: every rank on GPU 0, no RCCL (the host's all-gather over gloo, one-sided "
+                         "transfer between the processes) -- exercises the multi-rank path on a one-GPU box")
     ap.add_argument("--transport", choices=("rccl", "p2p"), default="p2p",
                     help="halo messages between ranks: RCCL send/recv groups, or the one-sided intra-node "
                          "transfer (mpas_dyc_set_p2p: pulled over xGMI by the receiving rank's kernel)")
@@ -211,7 +214,7 @@ def main():
         # exchanges of the dycore itself run over the library's own RCCL communicator
         import torch.distributed as dist
         dist.init_process_group("gloo")
-    device = local
+    device = 0 if args.same_device else local
 
     from mpas_dycore import Dycore, decomp
     from mpas_dycore.cases import jw_case
@@ -283,7 +286,10 @@ def main():
         comm_id = None
         # --rccl-local: blocks of this process also exchange through RCCL (send to self), to
         # measure the cost of the RCCL path on one GPU
-        if world > 1 or args.rccl_local:
+        if args.same_device:
+            if args.transport != "p2p" or args.rccl_local:
+                raise SystemExit("--same-device needs --transport p2p and no --rccl-local")
+        elif world > 1 or args.rccl_local:
             obj = [Dycore.comm_unique_id() if rank == 0 else None]
             if dist:
                 dist.broadcast_object_list(obj, src=0)
@@ -292,7 +298,8 @@ def main():
         wd.phase("rccl_init (ncclCommInitRank) and upload", args.phase_timeout)
         dy = Dycore.from_blocks(blocks, device=device, placement=placement, rank=rank, nranks=world,
                                 comm_id=comm_id, moist_end=moist_end, rccl_local=args.rccl_local,
-                                p2p=args.transport == "p2p")
+                                p2p=args.transport == "p2p",
+                                host_group=dist.group.WORLD if (args.same_device and dist) else None)
         owned = sum(b.solve[0] for b in blocks)
         halo = sum(b.case["nCells"] - b.solve[0] for b in blocks)
     else:

@@ -30,6 +30,7 @@
 #   maxedges         bench.py with the mesh declared maxEdges 6 vs 10 (AB_ROUNDS rounds), and from an init file
 #                    declaring maxEdges 10 (tools/write_init.py)
 #   tworanks         tools/p2p_two_ranks.py: two ranks on the GPU, one-sided transfer over IPC, bitwise vs one block
+#   bench2same       bench.py --gpus 2 --same-device: the multi-rank bench path (torchrun, two processes) on the one GPU
 #   ipc              tools/p2p_ipc_check: the one-sided protocol between two processes on the GPU (IPC)
 #   floor            tools/gather_floor: the gather kernels next to load-only replays of their index streams
 #   smoke            __graft_entry__.smoke()
@@ -108,6 +109,7 @@ step() {
               for A in "" "--moist" "--pull 0"; do
                 timeout -k 10 300 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 tools/p2p_two_ranks.py $A >> gpurun_out/tworanks.log 2>&1 || { tail -30 gpurun_out/tworanks.log; return 1; }
               done; grep bitwise gpurun_out/tworanks.log ;;
+    bench2same) timeout -k 10 400 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 2 --same-device --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --no-configs1 ${B} > gpurun_out/bench2same.log 2>&1 && last gpurun_out/bench2same.log 400 ;;
     ipc) timeout -k 10 600 python tools/p2p_ipc_check.py ${IPC_ARGS} > gpurun_out/ipc.log 2>&1; r=$?; cat gpurun_out/ipc.log; return $r ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && last gpurun_out/smoke.log ;;
     *) echo "unknown step $1"; return 2 ;;
