@@ -44,13 +44,16 @@ extern "C" {
 #define MPAS_DYC_ESTATE -3    /* call out of sequence */
 #define MPAS_DYC_ECOMM -4     /* halo exchange failure */
 
-/* nVertLevels: 4..MPAS_DYC_MAX_LEVELS, every kernel family and regional LBCs at any of them.  Up to
- * MPAS_DYC_MAX_LEVELS_WAVE a column is one 64-lane wavefront (lane = level), or half of one in the
- * pair layout (two levels per lane); above, the pair-layout kernels give a whole wavefront to one
- * column (two levels per lane) and the per-cell kernels one 128-lane workgroup, whose cross-level
- * moves go through LDS. */
+/* nVertLevels: 4..MPAS_DYC_MAX_LEVELS.  Up to MPAS_DYC_MAX_LEVELS_WAVE a column is one 64-lane
+ * wavefront (lane = level), or half of one in the pair layout (two levels per lane); up to
+ * MPAS_DYC_MAX_LEVELS_WIDE the pair-layout kernels give a whole wavefront to one column (two levels
+ * per lane) and the per-cell kernels one 128-lane workgroup, whose cross-level moves go through LDS;
+ * above, every kernel runs one column per 256-lane workgroup (the batched per-cell and one-column
+ * edge kernels; no pair layout, so no regional LBCs there).  Every kernel family and regional LBCs
+ * run at any nVertLevels up to MPAS_DYC_MAX_LEVELS_WIDE. */
 #define MPAS_DYC_MAX_LEVELS_WAVE 63
-#define MPAS_DYC_MAX_LEVELS 127
+#define MPAS_DYC_MAX_LEVELS_WIDE 127
+#define MPAS_DYC_MAX_LEVELS 255
 
 typedef struct mpas_dyc_ctx mpas_dyc_ctx;
 
@@ -403,7 +406,8 @@ int32_t mpas_dyc_rccl_version(void);
  * family (0 one column per element, 1 batched stencil records, 2 pair layout: two elements per
  * wavefront, two levels per lane -- one element per wavefront above MPAS_DYC_MAX_LEVELS_WAVE),
  * out[3] = column shape (0 one wavefront, 1 nVertLevels > MPAS_DYC_MAX_LEVELS_WAVE: one 128-lane
- * workgroup per column in the per-cell kernels, one wavefront per column in the pair layout). */
+ * workgroup per column in the per-cell kernels, one wavefront per column in the pair layout; 2
+ * nVertLevels > MPAS_DYC_MAX_LEVELS_WIDE: one 256-lane workgroup per column in every kernel). */
 int mpas_dyc_block_layout(mpas_dyc_ctx* ctx, int32_t block, int32_t* out /* [4] */);
 
 #ifdef __cplusplus

@@ -18,10 +18,12 @@
 namespace mpas {
 
 #ifdef MPAS_WIDE
-// Wide columns (the library's second build, nVertLevels 64..WIDE_THREADS-1; dycore.hip picks the
-// build per context): one column per workgroup of WIDE_THREADS lanes, lane = level, and the
-// cross-lane moves below go through LDS.  The kernel bodies are the same source.
+// Wide columns (the library's second and third builds, nVertLevels 64..127 and 128..255; dycore.hip
+// picks the build per context): one column per workgroup of WIDE_THREADS lanes (128 / 256), lane =
+// level, and the cross-lane moves below go through LDS.  The kernel bodies are the same source.
+#ifndef WIDE_THREADS
 #define WIDE_THREADS 128
+#endif
 #define WAVES_PER_BLOCK 1
 #define BLOCK_THREADS WIDE_THREADS
 #else
@@ -203,11 +205,13 @@ __device__ __forceinline__ double wave_shl1(double v) {
 }
 // The column's tridiagonal sweeps (2675-2682) in the wide build: forward x(k) = (x(k) - a(k) x(k-1))
 // alpha(k) for k = 1..K-1, then backward x(k) = x(k) - gamma(k) x(k+1) for k = K-1..0; x(K) is read,
-// never written.  The column goes through LDS to the first wavefront, which holds levels 2l, 2l+1
-// on lane l and runs thomas_column's lane sweep over the lane pairs: every iteration each lane
-// re-evaluates its two updates from its neighbour's current value, so after (K+1)/2 iterations each
-// level holds what the sequential loop computes, from the same operands, bit for bit.
+// never written.  The column goes through LDS to the first wavefront, which holds levels
+// NL l .. NL l + NL-1 on lane l (NL = WIDE_THREADS / 64: 2 or 4) and runs thomas_column's lane sweep
+// over them: every iteration each lane re-evaluates its NL updates in level order, the first from its
+// neighbour's current value, so after ceil(K / NL) iterations each level holds what the sequential
+// loop computes, from the same operands, bit for bit.
 __device__ __forceinline__ double column_solve(double x, double a, double alpha, double gamma, int k, int K) {
+  constexpr int NL = WIDE_THREADS / 64;
   __syncthreads();
   wide_lds[0][threadIdx.x] = x;
   wide_lds[1][threadIdx.x] = a;
@@ -215,25 +219,39 @@ __device__ __forceinline__ double column_solve(double x, double a, double alpha,
   wide_lds[3][threadIdx.x] = gamma;
   __syncthreads();
   if (threadIdx.x < 64) {
-    const int kx = 2 * threadIdx.x, ky = kx + 1;
-    const double rx = wide_lds[0][kx], ry = wide_lds[0][ky];
-    const double ax = wide_lds[1][kx], ay = wide_lds[1][ky], alx = wide_lds[2][kx], aly = wide_lds[2][ky];
-    const double gx = wide_lds[3][kx], gy = wide_lds[3][ky];
-    const bool fx = kx >= 1 && kx < K, fy = ky < K;
-    double xx = rx, xy = ry;
-    for (int it = 0; it < (K + 1) / 2; ++it) {
-      const double m = wave_shr1(xy);  // level kx - 1
-      if (fx) xx = (rx - ax * m) * alx;
-      if (fy) xy = (ry - ay * xx) * aly;
+    double r[NL], aa[NL], al[NL], g[NL], xv[NL], xf[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int kj = NL * threadIdx.x + j;
+      r[j] = wide_lds[0][kj];
+      aa[j] = wide_lds[1][kj];
+      al[j] = wide_lds[2][kj];
+      g[j] = wide_lds[3][kj];
+      xv[j] = r[j];
     }
-    const double fxx = xx, fxy = xy;
-    for (int it = 0; it < (K + 1) / 2; ++it) {
-      const double q = wave_shl1(xx);  // level ky + 1
-      if (fy) xy = fxy - gy * q;
-      if (kx < K) xx = fxx - gx * xy;
+    const int nit = (K + NL - 1) / NL;
+    for (int it = 0; it < nit; ++it) {
+      double prev = wave_shr1(xv[NL - 1]);  // level NL l - 1
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        const int kj = NL * threadIdx.x + j;
+        if (kj >= 1 && kj < K) xv[j] = (r[j] - aa[j] * prev) * al[j];
+        prev = xv[j];
+      }
     }
-    wide_lds[0][kx] = xx;
-    wide_lds[0][ky] = xy;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) xf[j] = xv[j];
+    for (int it = 0; it < nit; ++it) {
+      double next = wave_shl1(xv[0]);  // level NL (l + 1)
+#pragma unroll
+      for (int j = NL - 1; j >= 0; --j) {
+        const int kj = NL * threadIdx.x + j;
+        if (kj < K) xv[j] = xf[j] - g[j] * next;
+        next = xv[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) wide_lds[0][NL * threadIdx.x + j] = xv[j];
   }
   __syncthreads();
   return wide_lds[0][k];
