@@ -238,16 +238,29 @@ __global__ __launch_bounds__(256) void k_p2p_pull(const P2PSeg* __restrict__ seg
     if (threadIdx.x == 0) ok = p2p_wait_geq(pr.ready, n, status);
     __syncthreads();
     if (ok) {
-      const int inner = sg.inner;
+      // the wave's four columns: every load issued before the first store (over xGMI each is a
+      // round trip of a microsecond or more); columns of up to 64 levels in one load per lane,
+      // taller ones (the wide builds) in a loop
+      const int inner = sg.inner, lane = threadIdx.x & 63;
+      constexpr int NC = P2P_PULL_COLS / 4;
+      int di[NC];
+      const double* src[NC];
+      double v[NC];
 #pragma unroll
-      for (int c = 0; c < P2P_PULL_COLS / 4; ++c) {
+      for (int c = 0; c < NC; ++c) {
         const int i = __builtin_amdgcn_readfirstlane(ch.y + c * 4 + (int)(threadIdx.x >> 6));
-        if (i < sg.n) {
-          const int si = __builtin_amdgcn_readfirstlane(sg.sidx[i]), di = __builtin_amdgcn_readfirstlane(sg.didx[i]);
-          const double* src = sg.src + (size_t)si * inner;
-          double* dst = sg.dst + (size_t)di * inner;
-          for (int j = threadIdx.x & 63; j < inner; j += 64) dst[j] = sys_load(src + j);
-        }
+        const bool in = i < sg.n;
+        const int si = in ? __builtin_amdgcn_readfirstlane(sg.sidx[i]) : 0;
+        di[c] = in ? __builtin_amdgcn_readfirstlane(sg.didx[i]) : -1;
+        src[c] = sg.src + (size_t)si * inner;
+        v[c] = (in && lane < inner) ? sys_load(src[c] + lane) : 0.0;
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (di[c] < 0) continue;
+        double* dst = sg.dst + (size_t)di[c] * inner;
+        if (lane < inner) dst[lane] = v[c];
+        for (int j = lane + 64; j < inner; j += 64) dst[j] = sys_load(src[c] + j);
       }
     }
     __syncthreads();  // every lane's loads have returned
