@@ -2485,12 +2485,21 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
   const int e = sel(h, eA, eB);
   const size_t o = (size_t)e * K + 2 * lc;
   const int na = sel(h, p.nAdvCellsForEdge[eA], p.nAdvCellsForEdge[eB]);
+  // VROW (one scalar): the weights a + b and a - b of the wave's two edges in LDS, one row per
+  // half-wave (the two values a + sgn(u) b takes: sgn is +-1, so the sum is the same either way), read
+  // as half-wave broadcasts in the sums, as in k_mono_edges1_p: the two rows no longer take 40 VGPRs
+  // (108 -> 84), 35.86-36.03 -> 35.68-35.88 ms per dt.  With six scalars the scalar-cache rows stay
+  // (the LDS rows measured no faster there, 42.23-42.26 against 42.26-42.37 ms per dt).
+  __shared__ d2 wts[PAIR_WPB][PAIR_EPW][NA];
+  d2 (&w)[NA] = wts[threadIdx.x >> 6][h];
   int ic[NA];
   double a[NA], b[NA];
-  if (VROW) {
+  if constexpr (VROW) {
+    if (l < NA) {
+      const double aa = p.adv_coefs[(size_t)e * 15 + l], bb = p.adv_coefs_3rd[(size_t)e * 15 + l];
+      w[l] = d2{aa + bb, aa - bb};
+    }
     ld_row(p.advCellsForEdge + (size_t)e * 15, ic);
-    ld_row(p.adv_coefs + (size_t)e * 15, a);
-    ld_row(p.adv_coefs_3rd + (size_t)e * 15, b);
   } else {
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
@@ -2500,8 +2509,23 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
                  ld_uniform_f64(p.adv_coefs_3rd + (size_t)eB * 15 + j));
     }
   }
+  // the weight of stencil cell j at the lane's two levels: w[j] picked by the sign, or a + sgn b
+  auto wt = [&](int j, double sg, bool pos) -> double {
+    if constexpr (VROW) {
+      const d2 wj = w[j];
+      return pos ? wj.x : wj.y;
+    } else {
+      return a[j] + sg * b[j];
+    }
+  };
   const d2 uh = ld2(p.ruAvg + o);
   const double sgx = sgn1(uh.x), sgy = sgn1(uh.y);
+  const bool px = sgx > 0.0, py = sgy > 0.0;
+  if constexpr (VROW) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
   const bool hex = na == 10;  // the reference's unrolled hexagon form (3363-3390)
   bool st = (h == 0 || hasB) && 2 * l < K;
   // regional: edges of the two outer relaxation rows take a first-order upwind flux, and
@@ -2526,19 +2550,19 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_scalars_edges_p(Dims d, Ptrs p
     for (int j = 0; j < NA; ++j) sv[j] = ld2(p.scalars2 + SIX(ic[j], 2 * lc, is));
     d2 acc{0.0, 0.0};
     if (hex) {
-      acc.x = (a[0] + sgx * b[0]) * sv[0].x;
-      acc.y = (a[0] + sgy * b[0]) * sv[0].y;
+      acc.x = wt(0, sgx, px) * sv[0].x;
+      acc.y = wt(0, sgy, py) * sv[0].y;
 #pragma unroll
       for (int j = 1; j < 10 && j < NA; ++j) {
-        acc.x = acc.x + (a[j] + sgx * b[j]) * sv[j].x;
-        acc.y = acc.y + (a[j] + sgy * b[j]) * sv[j].y;
+        acc.x = acc.x + wt(j, sgx, px) * sv[j].x;
+        acc.y = acc.y + wt(j, sgy, py) * sv[j].y;
       }
     } else {
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
         if (j < na) {
-          acc.x = acc.x + (a[j] + sgx * b[j]) * sv[j].x;
-          acc.y = acc.y + (a[j] + sgy * b[j]) * sv[j].y;
+          acc.x = acc.x + wt(j, sgx, px) * sv[j].x;
+          acc.y = acc.y + wt(j, sgy, py) * sv[j].y;
         }
       }
     }
