@@ -931,7 +931,9 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   merge_by_rank(pl.rrecv, post_off);
   if (ctx->host_only) return MPAS_DYC_OK;  // the dry run keeps the message lists only
   if (ctx->loopback) stotal = rtotal = stotal + rtotal;  // rccl_group's loopback pairs stay inside
-  pl.p2p = ctx->p2p && (!pl.rsend.empty() || !pl.rrecv.empty());
+  // with other ranks, every exchange point is a one-sided one on every rank, messages or not: the
+  // set-up numbers the exchange points in the same order on every rank (flag indices, records)
+  pl.p2p = ctx->p2p && (!pl.rsend.empty() || !pl.rrecv.empty() || ctx->nranks > 1);
   pl.pull = pl.p2p && ctx->p2p_pull && !positional && !split_phase(ctx);
   if (pl.pull) {
     // the receiver copies from the fields: no buffers, and the kernels store and read the fields
