@@ -235,7 +235,14 @@ __global__ __launch_bounds__(256) void k_p2p_pull(const P2PSeg* __restrict__ seg
     const P2PSeg& sg = segs[ch.x];
     const P2PPeer& pr = peers[sg.peer];
     __shared__ int ok;
-    if (threadIdx.x == 0) ok = p2p_wait_geq(pr.ready, n, status);
+    if (threadIdx.x == 0) {
+      ok = p2p_wait_geq(pr.ready, n, status);
+      // the peer's field is ordinary (cacheable) memory: one system-scope acquire per workgroup after
+      // the poll, so that no line of it this GPU cached at an earlier exchange is read again
+      // (MI355X_MICROARCH.md, consumer: one relaxed poll, one acquire, vmcnt(0), barrier)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
     if (ok) {
       // the wave's four columns: every load issued before the first store (over xGMI each is a
