@@ -40,11 +40,12 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
         _lib.load()
 
 
-def test_two_builds_are_dispatched_by_level_count():
-    """The library links two builds of dycore.hip (one wavefront per column up to
-    MPAS_DYC_MAX_LEVELS_WAVE levels, one workgroup per column above): the public entry points
-    (api_dispatch.cpp) and the builds' renames (api_rename.h) are generated from the header and
-    up to date, every public function forwards to both builds, and both builds are in the library."""
+def test_three_builds_are_dispatched_by_level_count():
+    """The library links three builds of dycore.hip (one wavefront per column up to
+    MPAS_DYC_MAX_LEVELS_WAVE levels, one 128-lane workgroup per column up to
+    MPAS_DYC_MAX_LEVELS_WIDE, one 256-lane workgroup up to MPAS_DYC_MAX_LEVELS): the public entry
+    points (api_dispatch.cpp) and the builds' renames (api_rename.h) are generated from the header and
+    up to date, every public function forwards to the builds, and every build is in the library."""
     import subprocess
     import sys
     gen = os.path.join(ROOT, "mpas-model_amd", "csrc", "gen_api.py")
@@ -52,7 +53,8 @@ def test_two_builds_are_dispatched_by_level_count():
     assert r.returncode == 0, r.stdout + r.stderr
     src = open(HEADER).read()
     assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS_WAVE (\d+)", src).group(1)) == 63
-    assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS (\d+)", src).group(1)) == 127
+    assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS_WIDE (\d+)", src).group(1)) == 127
+    assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS (\d+)", src).group(1)) == 255
     disp = open(os.path.join(ROOT, "mpas-model_amd", "csrc", "api_dispatch.cpp")).read()
     for f in declared_functions():
         assert re.search(rf"\b{f}\(", disp), f
@@ -60,6 +62,6 @@ def test_two_builds_are_dispatched_by_level_count():
     if not os.path.isfile(_lib.LIBPATH):
         pytest.skip("libmpas_dycore.so not built (__graft_entry__.build())")
     lib = ctypes.CDLL(_lib.LIBPATH)
-    for tag in ("n", "w"):
+    for tag in ("n", "w", "x"):
         missing = [f for f in declared_functions() if not hasattr(lib, f.replace("mpas_dyc_", f"mpas_dyc{tag}_"))]
         assert not missing, (tag, missing)
