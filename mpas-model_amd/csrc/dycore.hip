@@ -129,7 +129,7 @@ struct XPlan {
   std::vector<XPack> rpk_cell, rpk_edge;
   std::vector<XUnpack> rup_cell, rup_edge;
   // one-sided transfer (mpas_dyc_ctx::p2p, halo.hip k_p2p_post / k_p2p_get): the send buffer is
-  // uncached memory the peers map; p2p_id < 0 until p2p_setup has exchanged the mappings
+  // device memory the peers map; p2p_id < 0 until p2p_setup has exchanged the mappings
   bool p2p = false;
   int p2p_id = -1;
   unsigned long long* p2p_cnt = nullptr;  // [0] use counter, [1 + i] chunks pulled from get peer i
@@ -935,6 +935,17 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
   // set-up numbers the exchange points in the same order on every rank (flag indices, records)
   pl.p2p = ctx->p2p && (!pl.rsend.empty() || !pl.rrecv.empty() || ctx->nranks > 1);
   pl.pull = pl.p2p && ctx->p2p_pull && !positional && !split_phase(ctx);
+  if (pl.pull)
+    if (const char* bk = getenv("MPAS_DYCORE_P2P_BUFFERS")) {  // debugging: these exchange points (key substrings) in buffers mode
+      const std::string key = plan_key(ctx, fs), list = bk;
+      size_t a = 0;
+      while (a <= list.size()) {
+        size_t e = list.find(',', a);
+        if (e == std::string::npos) e = list.size();
+        if (e > a && key.find(list.substr(a, e - a)) != std::string::npos) pl.pull = false;
+        a = e + 1;
+      }
+    }
   if (pl.pull) {
     // the receiver copies from the fields: no buffers, and the kernels store and read the fields
     // themselves (no fused pack / unpack)
@@ -958,9 +969,11 @@ int build_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs, XPlan& pl) {
     return MPAS_DYC_OK;
   }
   if (pl.p2p) {
-    // read by the peers over xGMI: uncached, so the producer's stores are in HBM when its kernel ends
-    HIPCHK(hipExtMallocWithFlags((void**)&pl.sendbuf, std::max<int64_t>(stotal, 1) * sizeof(double) + 256,
-                                 hipDeviceMallocUncached));
+    // read by the peers (IPC): ordinary device memory, as the fields a pull reads -- the producer's
+    // stores reach memory when its kernel ends (the L2 write-back that makes them visible to the
+    // other XCDs), and the peers load it with system-scope loads (an uncached allocation here was
+    // read stale by a peer process now and then: halo.hip)
+    HIPCHK(hipMalloc(&pl.sendbuf, std::max<int64_t>(stotal, 1) * sizeof(double) + 256));
   } else if (stotal) {
     HIPCHK(hipMalloc(&pl.sendbuf, stotal * sizeof(double)));
   }
@@ -2968,6 +2981,9 @@ int srk3(mpas_dyc_ctx* ctx, double dt) {
           CHK(exchange_wait(ctx));
         }
       } else {
+        // (The w recovery of the owned cells away from the halo before this exchange, straight after
+        // the damping that recovered their edges' ru, and the rest after it: bitwise, but 2.5 % slower
+        // per dt on the 8-way emulation -- profiles/r05_ab_early_w_rejected.log.)
         CHK((exchange)(ctx, xrec));
         // 889-930: the owned cells were recovered by the last sub-step if fused_recover
         EACH(if (fused_recover(d)) LAUNCH(k_recover_cells1, d.nCells + 1 - d.nCellsSolve, d, p, rdt, invNs, rk_step, 2,
@@ -3382,6 +3398,14 @@ void mpas_dyc_destroy(mpas_dyc_ctx* ctx) {
   }
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (getenv("MPAS_DYCORE_P2P_DEBUG"))  // every one-sided exchange point's use count (ranks compare them)
+    for (const auto& kv : ctx->plans)
+      if (kv.second.p2p_id >= 0 && kv.second.p2p_cnt) {
+        unsigned long long c[2] = {0, 0};
+        (void)hipMemcpy(c, kv.second.p2p_cnt, sizeof(c), hipMemcpyDeviceToHost);
+        printf("p2pdbg rank %d id %d uses %llu wg %llu nget %d %s\n", ctx->rank, kv.second.p2p_id, c[0], c[1],
+               kv.second.nget, kv.first.c_str());
+      }
   invalidate_plans(ctx);
   for (auto& b : ctx->blk) {
     for (auto& f : b.fields) {

@@ -41,9 +41,10 @@ __global__ __launch_bounds__(256) void k_halo_copy(const XSeg* __restrict__ segs
 // exchange point are pulled over xGMI by the receiving rank's kernel, with no RCCL group, no second
 // stream and no host involvement, so a step stays one captured graph of kernels.
 //
-// Per exchange point and rank: a send buffer in uncached device memory (fine-grained, so the peers'
-// reads see the producer's stores once its kernel has ended), mapped into every peer that reads it
-// (IPC); and a flag arena of the same kind per rank, [plan][sender rank][ready, consumed].  A use n
+// Per exchange point and rank: a send buffer in ordinary device memory (the producer's stores are in
+// memory once its kernel has ended: the L2 write-back that makes them visible to the other XCDs),
+// mapped into every peer that reads it (IPC); and a flag arena in uncached memory per rank,
+// [plan][sender rank][ready, consumed].  A use n
 // of an exchange point (the n-th time the step runs it; every rank runs the same sequence):
 //   k_p2p_post (after the pack or the fused producer): n = ++use counter; ready[plan][me] = n in the
 //     arena of every rank this rank sends to;
@@ -70,14 +71,16 @@ struct P2PGet {
   int nchunk;
 };
 
-// The flags and the send buffers are uncached memory: a system-scope load or store of them goes to
-// memory, and no cache holds a stale copy of a peer's send buffer.  So the waits poll with relaxed
-// system-scope loads and the signals are relaxed system-scope stores -- no acquire / release fences,
-// which on gfx950 invalidate or write back the whole L2 (4.7 us per post with them, and every kernel
-// after a get starting on a cold L2).  Ordering that the fences would give comes from elsewhere:
-// the data a post announces was stored by earlier kernels on the stream (complete when they end),
-// a get's copy loads issue after the poll loop has seen the flag (control dependency), and a
-// consumed flag is raised after every copy load of the message has returned its value.
+// The flags are uncached memory: the waits poll with relaxed system-scope loads and the signals are
+// relaxed system-scope stores, with no release fence (a write-back of the whole L2: 4.7 us per post
+// with one).  The data a post announces was stored by earlier kernels on the stream (in memory when
+// they end); after its poll has seen the flag, a copy workgroup runs one system-scope acquire and
+// reads the peer's buffer with system-scope loads, so no cache of this GPU serves a stale copy of
+// it; and a consumed flag is raised after every copy load of the message has returned its value.
+// (Send buffers in uncached memory gave a peer process stale halo values in about one run in four
+// with two ranks on one GPU, whatever the reading side did: the producers' stores into them were not
+// all in memory when the next kernel raised the ready flag -- a release fence at the end of the pack
+// cured it, and so does ordinary memory; tools/p2p_repeat.sh.)
 __device__ inline bool p2p_wait_geq(const unsigned long long* f, unsigned long long n, int* status) {
   const unsigned long long t0 = wall_clock64();
   while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < n) {
@@ -89,6 +92,13 @@ __device__ inline bool p2p_wait_geq(const unsigned long long* f, unsigned long l
     __builtin_amdgcn_s_sleep(4);
   }
   return true;
+}
+
+// a system-scope load of a double: the peer's data as it is in memory, whatever a cache of this GPU
+// holds from an earlier exchange (an IPC mapping of another process's memory need not be uncached)
+__device__ inline double sys_load(const double* a) {
+  const unsigned long long v = __hip_atomic_load((const unsigned long long*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __longlong_as_double((long long)v);
 }
 
 // use[0]: this exchange point's use counter (read by the get of the same use, later on the stream)
@@ -112,7 +122,13 @@ __global__ __launch_bounds__(256) void k_p2p_get(const P2PGet* __restrict__ g, i
   const P2PGet& p = g[blockIdx.y];
   if ((int)blockIdx.x >= p.nchunk) return;
   __shared__ int ok;
-  if (threadIdx.x == 0) ok = p2p_wait_geq(p.ready, n, status);
+  if (threadIdx.x == 0) {
+    ok = p2p_wait_geq(p.ready, n, status);
+    // as in k_p2p_pull: one system-scope acquire after the poll, then system-scope loads of the
+    // peer's buffer (another process's memory, mapped here over IPC)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
   if (!ok) return;
   const long long c0 = (long long)blockIdx.x * P2P_CHUNK;
@@ -121,7 +137,7 @@ __global__ __launch_bounds__(256) void k_p2p_get(const P2PGet* __restrict__ g, i
   for (long long i = c0 + threadIdx.x; i < c1; i += 4 * 256) {
     double v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = i + u * 256 < c1 ? p.src[i + u * 256] : 0.0;
+    for (int u = 0; u < 4; ++u) v[u] = i + u * 256 < c1 ? sys_load(p.src + i + u * 256) : 0.0;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (i + u * 256 < c1) p.dst[i + u * 256] = v[u];
@@ -152,7 +168,11 @@ __global__ __launch_bounds__(256) void k_p2p_exchange(const P2PGet* __restrict__
     const P2PGet& p = g[blockIdx.y];
     if ((int)blockIdx.x < p.nchunk) {
       __shared__ int ok;
-      if (threadIdx.x == 0) ok = p2p_wait_geq(p.ready, n, status);
+      if (threadIdx.x == 0) {
+        ok = p2p_wait_geq(p.ready, n, status);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // as in k_p2p_get
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __syncthreads();
       if (ok) {
         const long long c0 = (long long)blockIdx.x * P2P_CHUNK;
@@ -160,7 +180,7 @@ __global__ __launch_bounds__(256) void k_p2p_exchange(const P2PGet* __restrict__
         for (long long i = c0 + threadIdx.x; i < c1; i += 4 * 256) {
           double v[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) v[u] = i + u * 256 < c1 ? p.src[i + u * 256] : 0.0;
+          for (int u = 0; u < 4; ++u) v[u] = i + u * 256 < c1 ? sys_load(p.src + i + u * 256) : 0.0;
 #pragma unroll
           for (int u = 0; u < 4; ++u)
             if (i + u * 256 < c1) p.dst[i + u * 256] = v[u];
@@ -206,10 +226,6 @@ struct P2PPeer {
   unsigned long long nwg;           // workgroups per use with work for this peer
 };
 
-__device__ inline double sys_load(const double* a) {
-  const unsigned long long v = __hip_atomic_load((const unsigned long long*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return __longlong_as_double((long long)v);
-}
 
 constexpr int P2P_PULL_COLS = 16;  // element columns per workgroup (4 per wave)
 

@@ -72,10 +72,10 @@ step() {
              echo "== $E" >> gpurun_out/envsweep.log
              env $E timeout -k 10 300 python tools/rank_emulation.py ${EMU_ARGS:---parts 8 --blocks 0 4 --exchange} >> gpurun_out/envsweep.log 2>&1 || return 1
            done; done; grep -h "==\|blocks" gpurun_out/envsweep.log | cut -c1-160 ;;
-    prof8e) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8c -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks ${PROF_BLOCKS:-all} --steps 3 > gpurun_out/prof8c.log 2>&1 &&
+    prof8e) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8c -o run --output-format csv -- python3 tools/rank_emulation.py --parts ${PROF_PARTS:-8} --blocks ${PROF_BLOCKS:-all} --steps 3 > gpurun_out/prof8c.log 2>&1 &&
             timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8e -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks all --steps 3 --exchange > gpurun_out/prof8e.log 2>&1 && echo "prof8e done" ;;
-    prof8p) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8c -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks ${PROF_BLOCKS:-all} --steps 3 > gpurun_out/prof8c.log 2>&1 &&
-            MPAS_DYCORE_P2P=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8p -o run --output-format csv -- python3 tools/rank_emulation.py --parts 8 --blocks ${PROF_BLOCKS:-all} --steps 3 --exchange > gpurun_out/prof8p.log 2>&1 && echo "prof8p done" ;;
+    prof8p) timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8c -o run --output-format csv -- python3 tools/rank_emulation.py --parts ${PROF_PARTS:-8} --blocks ${PROF_BLOCKS:-all} --steps 3 > gpurun_out/prof8c.log 2>&1 &&
+            MPAS_DYCORE_P2P=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof8p -o run --output-format csv -- python3 tools/rank_emulation.py --parts ${PROF_PARTS:-8} --blocks ${PROF_BLOCKS:-all} --steps 3 --exchange > gpurun_out/prof8p.log 2>&1 && echo "prof8p done" ;;
     blocks8) timeout -k 10 400 python bench.py --blocks 8 --rccl-local --steps 5 --warmup 2 $B > gpurun_out/blocks8.log 2>&1 && last gpurun_out/blocks8.log 300 ;;
     ab8) rm -f gpurun_out/ab8.log
         for r in ${AB_ROUNDS:-1 2 3}; do for F in 0 1; do

@@ -81,7 +81,7 @@ int main(int argc, char** argv) {
   double *send = nullptr, *recv = nullptr;
   unsigned long long *flags = nullptr, *cnt = nullptr, *bad = nullptr;
   int* status = nullptr;
-  CK(hipExtMallocWithFlags((void**)&send, n * sizeof(double), hipDeviceMallocUncached));
+  CK(hipMalloc(&send, n * sizeof(double)));  // ordinary device memory, as the library's send buffers
   CK(hipExtMallocWithFlags((void**)&flags, 4 * sizeof(unsigned long long), hipDeviceMallocUncached));
   CK(hipMemset(flags, 0, 4 * sizeof(unsigned long long)));
   CK(hipMalloc(&recv, n * sizeof(double)));

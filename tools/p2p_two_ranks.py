@@ -23,9 +23,9 @@ FIELDS = [("state", "u", "edge"), ("state", "theta_m", "cell"), ("state", "rho_z
           ("state", "w", "cell"), ("state", "scalars", "cell")]
 
 
-def run(dy, dt, steps):
+def run(dy, dt, steps, graph=True):
     dy.init_diagnostics(dt)
-    dy.use_graph(True)
+    dy.use_graph(graph)
     for it in range(steps):
         dy.atm_timestep(dt, it + 1)
         dy.shift_time_levels()
@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--levels", type=int, default=26)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--moist", action="store_true")
+    ap.add_argument("--graph", type=int, default=1, help="0: launch the kernels one by one (no hipGraph)")
     ap.add_argument("--pull", type=int, default=1, help="0: send / receive buffers (MPAS_DYCORE_P2P_PULL=0)")
     a = ap.parse_args()
     os.environ["MPAS_DYCORE_P2P_PULL"] = str(a.pull)
@@ -54,7 +55,7 @@ def main():
     blocks = decomp.decompose(case, part, parts=[rank], placement=placement)
     dy = Dycore.from_blocks(blocks, device=0, placement=placement, rank=rank, nranks=world,
                             host_group=dist.group.WORLD)
-    run(dy, dt, a.steps)
+    run(dy, dt, a.steps, bool(a.graph))
     active = dy.p2p_active()
     mine = {n: dy.get(p, n, 1) for p, n, _ in FIELDS}
     dy.close()
@@ -70,13 +71,20 @@ def main():
         one.close()
         allb = decomp.decompose(case, part, placement=placement)
         n_glob = {"cell": case["nCells"], "edge": case["nEdges"]}
-        diffs = {}
+        diffs, where = {}, {}
         for p, n, loc in FIELDS:
             got = decomp.gather_owned(allb, [allv[r][n] for r in range(world)], loc, n_glob[loc])
             same = bool(np.array_equal(got, ref[n]))
             diffs[n] = 0.0 if same else float(np.nanmax(np.abs(got - ref[n])))
+            if not same:  # where it differs: which side holds non-finite values, how many columns
+                bad = np.atleast_2d(got != ref[n])
+                where[n] = {"nonfinite_split": int((~np.isfinite(got)).sum()),
+                            "nonfinite_one": int((~np.isfinite(ref[n])).sum()),
+                            "columns": int(bad.any(axis=tuple(range(1, bad.ndim))).sum()) if bad.ndim > 1 else int(bad.sum())}
             ok = ok and same
         out.update(bitwise=ok, max_abs_diff=diffs)
+        if where:
+            out["where"] = where
         print(json.dumps(out), flush=True)
     flag = [ok and active]
     dist.broadcast_object_list(flag, src=0)
