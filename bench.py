@@ -283,44 +283,72 @@ def main():
                 if dist:
                     dist.destroy_process_group()
                 raise SystemExit(0 if preflight["ok"] else 2)
-        comm_id = None
         # --rccl-local: blocks of this process also exchange through RCCL (send to self), to
         # measure the cost of the RCCL path on one GPU
-        if args.same_device:
-            if args.transport != "p2p" or args.rccl_local:
-                raise SystemExit("--same-device needs --transport p2p and no --rccl-local")
-        elif world > 1 or args.rccl_local:
-            obj = [Dycore.comm_unique_id() if rank == 0 else None]
-            if dist:
-                dist.broadcast_object_list(obj, src=0)
-            comm_id = obj[0]
+        if args.same_device and (args.transport != "p2p" or args.rccl_local):
+            raise SystemExit("--same-device needs --transport p2p and no --rccl-local")
         torch.cuda.set_device(device)
-        wd.phase("rccl_init (ncclCommInitRank) and upload", args.phase_timeout)
-        dy = Dycore.from_blocks(blocks, device=device, placement=placement, rank=rank, nranks=world,
-                                comm_id=comm_id, moist_end=moist_end, rccl_local=args.rccl_local,
-                                p2p=args.transport == "p2p",
-                                host_group=dist.group.WORLD if (args.same_device and dist) else None)
+
+        def build(transport):
+            comm_id = None
+            if not args.same_device and (world > 1 or args.rccl_local):
+                obj = [Dycore.comm_unique_id() if rank == 0 else None]
+                if dist:
+                    dist.broadcast_object_list(obj, src=0)
+                comm_id = obj[0]
+            wd.phase("rccl_init (ncclCommInitRank) and upload", args.phase_timeout)
+            return Dycore.from_blocks(blocks, device=device, placement=placement, rank=rank, nranks=world,
+                                      comm_id=comm_id, moist_end=moist_end, rccl_local=args.rccl_local,
+                                      p2p=transport == "p2p",
+                                      host_group=dist.group.WORLD if (args.same_device and dist) else None)
+        dy = build(args.transport)
         owned = sum(b.solve[0] for b in blocks)
         halo = sum(b.case["nCells"] - b.solve[0] for b in blocks)
     else:
         dy = Dycore(case, device=device, moist_end=moist_end)
         owned, halo = case["nCells"], 0
-    wd.dy = dy
-    wd.phase("model init (init_diagnostics)", args.phase_timeout)
-    dy.init_diagnostics(dt)
-    dy.synchronize()
-    if not args.no_graph:
-        dy.use_graph(True)
 
     def step(i):
         dy.atm_timestep(dt, i)
         dy.shift_time_levels()
 
-    for i in range(args.warmup):
-        wd.phase(f"warmup step {i + 1}" + (" (exchange plans, RCCL warm-up, hipGraph capture)" if i == 0 else ""),
-                 args.phase_timeout)
-        step(i + 1)
+    def warm_up():
+        wd.dy = dy
+        wd.phase("model init (init_diagnostics)", args.phase_timeout)
+        dy.init_diagnostics(dt)
         dy.synchronize()
+        if not args.no_graph:
+            dy.use_graph(True)
+        for i in range(args.warmup):
+            wd.phase(f"warmup step {i + 1}" + (" (exchange plans, RCCL warm-up, hipGraph capture)" if i == 0 else ""),
+                     args.phase_timeout)
+            step(i + 1)
+            dy.synchronize()
+
+    # the one-sided transfer's first run between separate GPUs may be the driver's: if any rank's
+    # warm-up fails with it (a wait that timed out, a refused mapping at run time), every rank drops
+    # it together and runs again over RCCL, and the line says so (config.transport_fallback)
+    fallback = None
+    if nparts > 1 and world > 1 and args.transport == "p2p" and not args.same_device:
+        err = ""
+        try:
+            warm_up()
+        except Exception as e:  # noqa: BLE001 -- any failure: decided collectively below
+            err = f"rank {rank}: {str(e)[:300]}"
+        errs = [None] * world
+        dist.all_gather_object(errs, err)
+        bad = [e for e in errs if e]
+        if bad:
+            fallback = {"from": "p2p", "to": "rccl", "error": bad[0]}
+            wd.done()
+            try:
+                dy.close()
+            except Exception:  # noqa: BLE001
+                pass
+            dy = build("rccl")
+            warm_up()
+    else:
+        warm_up()
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
@@ -419,6 +447,7 @@ def main():
                             f"{args.blocks} per GPU, halo exchange {transport}" if nparts > 1 else "single block"),
             "owned_cells_rank0": owned, "halo_cells_rank0": halo,
             "hip_graph": graph,
+            "transport_fallback": fallback,
             "maxEdges_declared": [case["maxEdges"], case["maxEdges2"]],
             "kernel_layout": layout,
         },
