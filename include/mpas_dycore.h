@@ -48,12 +48,14 @@ extern "C" {
  * wavefront (lane = level), or half of one in the pair layout (two levels per lane); up to
  * MPAS_DYC_MAX_LEVELS_WIDE the pair-layout kernels give a whole wavefront to one column (two levels
  * per lane) and the per-cell kernels one 128-lane workgroup, whose cross-level moves go through LDS;
- * above, every kernel runs one column per 256-lane workgroup (the batched per-cell and one-column
- * edge kernels; no pair layout, so no regional LBCs there).  Every kernel family and regional LBCs
- * run at any nVertLevels up to MPAS_DYC_MAX_LEVELS_WIDE. */
+ * above, every kernel runs one column per 256-lane workgroup up to MPAS_DYC_MAX_LEVELS_256, and per
+ * 512-lane workgroup above (the batched per-cell and one-column edge kernels; no pair layout, so no
+ * regional LBCs there).  Every kernel family and regional LBCs run at any nVertLevels up to
+ * MPAS_DYC_MAX_LEVELS_WIDE. */
 #define MPAS_DYC_MAX_LEVELS_WAVE 63
 #define MPAS_DYC_MAX_LEVELS_WIDE 127
-#define MPAS_DYC_MAX_LEVELS 255
+#define MPAS_DYC_MAX_LEVELS_256 255
+#define MPAS_DYC_MAX_LEVELS 511
 
 typedef struct mpas_dyc_ctx mpas_dyc_ctx;
 
@@ -407,7 +409,8 @@ int32_t mpas_dyc_rccl_version(void);
  * wavefront, two levels per lane -- one element per wavefront above MPAS_DYC_MAX_LEVELS_WAVE),
  * out[3] = column shape (0 one wavefront, 1 nVertLevels > MPAS_DYC_MAX_LEVELS_WAVE: one 128-lane
  * workgroup per column in the per-cell kernels, one wavefront per column in the pair layout; 2
- * nVertLevels > MPAS_DYC_MAX_LEVELS_WIDE: one 256-lane workgroup per column in every kernel). */
+ * nVertLevels > MPAS_DYC_MAX_LEVELS_WIDE: one 256-lane workgroup per column in every kernel; 3
+ * nVertLevels > MPAS_DYC_MAX_LEVELS_256: one 512-lane workgroup per column). */
 int mpas_dyc_block_layout(mpas_dyc_ctx* ctx, int32_t block, int32_t* out /* [4] */);
 
 #ifdef __cplusplus

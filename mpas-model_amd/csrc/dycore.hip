@@ -3128,11 +3128,13 @@ namespace {
 int fill_dims(Dims& d, const mpas_dyc_dims* dims) {
 #ifdef MPAS_WIDE
   // column = one workgroup of WIDE_THREADS lanes (levels 0..K of w)
-  // (the 128-lane build: 64..127 levels; the 256-lane build: 128..255)
-  constexpr int lo = WIDE_THREADS == 128 ? MPAS_DYC_MAX_LEVELS_WAVE : MPAS_DYC_MAX_LEVELS_WIDE;
+  // (the 128-lane build: 64..127 levels; the 256-lane build: 128..255; the 512-lane build: 256..511)
+  constexpr int lo = WIDE_THREADS == 128 ? MPAS_DYC_MAX_LEVELS_WAVE
+                     : WIDE_THREADS == 256 ? MPAS_DYC_MAX_LEVELS_WIDE : MPAS_DYC_MAX_LEVELS_256;
   if (dims->nVertLevels <= lo || dims->nVertLevels >= WIDE_THREADS || dims->nVertLevels > MPAS_DYC_MAX_LEVELS)
     return MPAS_DYC_EINVAL;
-  static_assert(WIDE_THREADS == 128 || WIDE_THREADS == 256, "wide builds: 128 or 256 lanes per column");
+  static_assert(WIDE_THREADS == 128 || WIDE_THREADS == 256 || WIDE_THREADS == 512,
+                "wide builds: 128, 256 or 512 lanes per column");
 #else
   // column = one wavefront (levels 0..K of w)
   if (dims->nVertLevels < 4 || dims->nVertLevels > MPAS_DYC_MAX_LEVELS_WAVE) return MPAS_DYC_EINVAL;
@@ -4469,7 +4471,7 @@ int mpas_dyc_block_layout(mpas_dyc_ctx* ctx, int32_t block, int32_t* out) {
   out[1] = b->d.maxEdges2;
   out[2] = pair_layout(b->d) ? 2 : batched(b->d) ? 1 : 0;
 #ifdef MPAS_WIDE
-  out[3] = WIDE_THREADS == 128 ? 1 : 2;
+  out[3] = WIDE_THREADS == 128 ? 1 : WIDE_THREADS == 256 ? 2 : 3;
 #else
   out[3] = 0;
 #endif

@@ -449,11 +449,11 @@ class Dycore:
         with, the kernel family and the column shape ("wavefront": nVertLevels <= 63, a column per
         wavefront or half of one; "wide": 64..127, a wavefront per column in the pair layout, a
         128-lane workgroup in the per-cell kernels; "wide256": 128..255, a 256-lane workgroup per
-        column in every kernel)."""
+        column in every kernel; "wide512": 256..511, a 512-lane workgroup)."""
         out = (C.c_int32 * 4)()
         self._check(self.lib.mpas_dyc_block_layout(self.h, int(block), out), "block_layout")
         return {"maxEdges": out[0], "maxEdges2": out[1], "family": ("general", "batched", "pair")[out[2]],
-                "column": ("wavefront", "wide", "wide256")[out[3]]}
+                "column": ("wavefront", "wide", "wide256", "wide512")[out[3]]}
 
     def exchange_profile(self, dt: float, itimestep: int = 1) -> dict:
         """One eager atm_timestep with HIP events around every exchange's exposed part and every

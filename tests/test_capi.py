@@ -40,10 +40,11 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
         _lib.load()
 
 
-def test_three_builds_are_dispatched_by_level_count():
-    """The library links three builds of dycore.hip (one wavefront per column up to
+def test_four_builds_are_dispatched_by_level_count():
+    """The library links four builds of dycore.hip (one wavefront per column up to
     MPAS_DYC_MAX_LEVELS_WAVE levels, one 128-lane workgroup per column up to
-    MPAS_DYC_MAX_LEVELS_WIDE, one 256-lane workgroup up to MPAS_DYC_MAX_LEVELS): the public entry
+    MPAS_DYC_MAX_LEVELS_WIDE, one 256-lane workgroup up to MPAS_DYC_MAX_LEVELS_256, one 512-lane
+    workgroup up to MPAS_DYC_MAX_LEVELS): the public entry
     points (api_dispatch.cpp) and the builds' renames (api_rename.h) are generated from the header and
     up to date, every public function forwards to the builds, and every build is in the library."""
     import subprocess
@@ -54,7 +55,8 @@ def test_three_builds_are_dispatched_by_level_count():
     src = open(HEADER).read()
     assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS_WAVE (\d+)", src).group(1)) == 63
     assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS_WIDE (\d+)", src).group(1)) == 127
-    assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS (\d+)", src).group(1)) == 255
+    assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS_256 (\d+)", src).group(1)) == 255
+    assert int(re.search(r"#define MPAS_DYC_MAX_LEVELS (\d+)", src).group(1)) == 511
     disp = open(os.path.join(ROOT, "mpas-model_amd", "csrc", "api_dispatch.cpp")).read()
     for f in declared_functions():
         assert re.search(rf"\b{f}\(", disp), f
@@ -62,6 +64,6 @@ def test_three_builds_are_dispatched_by_level_count():
     if not os.path.isfile(_lib.LIBPATH):
         pytest.skip("libmpas_dycore.so not built (__graft_entry__.build())")
     lib = ctypes.CDLL(_lib.LIBPATH)
-    for tag in ("n", "w", "x"):
+    for tag in ("n", "w", "x", "y"):
         missing = [f for f in declared_functions() if not hasattr(lib, f.replace("mpas_dyc_", f"mpas_dyc{tag}_"))]
         assert not missing, (tag, missing)
