@@ -317,14 +317,19 @@ int mpas_dyc_comm_init_host(mpas_dyc_ctx* ctx, int32_t nranks, int32_t rank, mpa
 int mpas_dyc_set_transport(mpas_dyc_ctx* ctx, int32_t rccl_for_local_blocks);
 /* One-sided transfer between the ranks of one node (on = 1; 0 = RCCL groups; -1 = the environment
  * variable MPAS_DYCORE_P2P, read at context creation, default 0).  Replaces the ncclSend / ncclRecv
- * groups of every exchange point by two kernels (halo.hip): after the pack, k_p2p_post raises a flag
- * in each receiving rank's arena; where the halo is needed, k_p2p_get pulls each peer's message from
- * the peer's send buffer (uncached device memory, IPC-mapped at set-up) and waits until this rank's
- * own buffer has been pulled.  Same messages, buffer layouts and order as the RCCL path (the plans
- * are the ones mpas_dyc_plan_exchanges reports).  Set-up runs once per exchange-plan build, over the
- * communicator of mpas_dyc_comm_init (all-gathers of IPC handles); all ranks must be on one node
- * (checked: MPAS_DYC_ECOMM otherwise).  A message that does not arrive within 30 s makes
- * mpas_dyc_synchronize return MPAS_DYC_ECOMM.  Collective: every rank calls it with the same value. */
+ * groups of every exchange point by kernels that move the halo themselves (halo.hip), with flags in
+ * each rank's arena (ready / consumed counters, IPC-mapped by the peers at set-up).  Blocking
+ * exchanges with block-pair lists (the default) are pulls: k_p2p_pull copies the peer's owned
+ * columns from its fields (IPC-mapped) straight into this rank's halo columns.  Positional lists and
+ * split-phase exchanges (MPAS_DYCORE_P2P_PULL=0 for all) keep the send / receive buffers: the pack
+ * fills this rank's send buffer (device memory the peers map), k_p2p_post raises ready, and
+ * k_p2p_get pulls each peer's message and waits until this rank's own buffer has been pulled.  Same
+ * messages and order as the RCCL path (the plans are the ones mpas_dyc_plan_exchanges reports).
+ * Set-up runs once per exchange-plan build, over the communicator of mpas_dyc_comm_init (or the host
+ * all-gather of mpas_dyc_comm_init_host); if IPC is refused or the ranks span several nodes, every
+ * rank drops the transfer together and plans for RCCL (mpas_dyc_get_p2p then returns 0).  A message
+ * that does not arrive within 30 s makes mpas_dyc_synchronize return MPAS_DYC_ECOMM.  Collective:
+ * every rank calls it with the same value. */
 int mpas_dyc_set_p2p(mpas_dyc_ctx* ctx, int32_t on);
 /* 1 while the one-sided transfer is on (0 after the set-up found it unavailable on some rank -- IPC
  * refused, ranks on several nodes -- and every rank went back to RCCL, with a line on stderr). */
