@@ -113,6 +113,15 @@ class Watchdog:
                 os._exit(3)
 
 
+def agree_on_failure(dist, world, err):
+    """Every rank's warm-up outcome over the host group (gloo): the first failing rank's message on
+    every rank, or None when all succeeded -- the ranks then drop the one-sided transfer together."""
+    errs = [None] * world
+    dist.all_gather_object(errs, err or "")
+    bad = [e for e in errs if e]
+    return bad[0] if bad else None
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -335,11 +344,9 @@ def main():
             warm_up()
         except Exception as e:  # noqa: BLE001 -- any failure: decided collectively below
             err = f"rank {rank}: {str(e)[:300]}"
-        errs = [None] * world
-        dist.all_gather_object(errs, err)
-        bad = [e for e in errs if e]
-        if bad:
-            fallback = {"from": "p2p", "to": "rccl", "error": bad[0]}
+        first = agree_on_failure(dist, world, err)
+        if first:
+            fallback = {"from": "p2p", "to": "rccl", "error": first}
             wd.done()
             try:
                 dy.close()

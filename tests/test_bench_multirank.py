@@ -53,3 +53,32 @@ def test_watchdog_names_the_phase():
     assert r.returncode == 3
     j = _json_lines(r.stdout)[0]
     assert j["rank"] == 1 and j["phase"].startswith("rccl_init") and j["value"] is None
+
+
+_AGREE = """
+import os, sys
+sys.path.insert(0, %r)
+import torch.distributed as dist
+import bench
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+err = "rank %%d: one-sided wait timed out" %% r if r == w - 1 else ""
+first = bench.agree_on_failure(dist, w, err)
+ok = bench.agree_on_failure(dist, w, "")
+open(os.path.join(%r, "r%%d.txt" %% r), "w").write("%%s|%%s" %% (first, ok))
+dist.destroy_process_group()
+"""
+
+
+def test_transport_fallback_is_agreed_by_every_rank(tmp_path):
+    """bench.py's fallback from the one-sided transfer to RCCL: when one rank's warm-up fails, every
+    rank gets the same (first failing rank's) message and rebuilds over RCCL together; when none
+    fails, none does."""
+    script = tmp_path / "agree.py"
+    script.write_text(_AGREE % (ROOT, str(tmp_path)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+                        "--master-addr", "127.0.0.1", "--master-port", "29617", str(script)],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = [(tmp_path / f"r{i}.txt").read_text() for i in range(3)]
+    assert got == ["rank 2: one-sided wait timed out|None"] * 3, got
