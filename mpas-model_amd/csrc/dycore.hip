@@ -1933,6 +1933,9 @@ const XPlan* fused_rec_plan(mpas_dyc_ctx* ctx, const std::vector<XField>& fs) {
 // (tests/test_gpu_kernels.py); the environment variable MPAS_DYCORE_KERNELS=general|batched|pair,
 // read when a context is created, caps the family (default pair).
 int g_kernel_tier = 2;
+// k_dyn_delsq_vc in the pair layout (MPAS_DYCORE_DELSQ_PAIR=0, read when a context is created: the
+// batched kernel)
+int g_delsq_pair = 1;
 inline bool batched(const Dims& d) {
   return g_kernel_tier >= 1 && (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
 }
@@ -2326,9 +2329,16 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
       LAUNCH(k_dyn_cells2, d.nCells, d, p);
     } else {
       if (s.h_mom_eddy_visc4 > 0.0) {
-        const int nvc = 3 * std::max((d.nVertices + 1) / 2, d.nCells);  // interleaved (k_dyn_delsq_vc_b)
-        if (m6) LAUNCH(k_dyn_delsq_vc_b<6>, nvc, d, p);
-        else LAUNCH(k_dyn_delsq_vc_b<7>, nvc, d, p);
+        if (pair_layout(d) && g_delsq_pair) {  // interleaved, PAIR_EPW elements per wavefront
+          const int64_t nw = 3 * std::max<int64_t>((d.nVertices + 2 * PAIR_EPW - 1) / (2 * PAIR_EPW),
+                                                   (d.nCells + PAIR_EPW - 1) / PAIR_EPW);
+          if (m6) LAUNCH_PE((k_dyn_delsq_vc_p<6, false>), (k_dyn_delsq_vc_p<6, true>), nw * PAIR_EPW, d, p);
+          else LAUNCH_PE((k_dyn_delsq_vc_p<7, false>), (k_dyn_delsq_vc_p<7, true>), nw * PAIR_EPW, d, p);
+        } else {
+          const int nvc = 3 * std::max((d.nVertices + 1) / 2, d.nCells);  // interleaved (k_dyn_delsq_vc_b)
+          if (m6) LAUNCH(k_dyn_delsq_vc_b<6>, nvc, d, p);
+          else LAUNCH(k_dyn_delsq_vc_b<7>, nvc, d, p);
+        }
       }
       LAUNCH(k_dyn_edges_rk1b_b, d.nEdgesSolve, d, p, cf, s, tp);
       if (m6) LAUNCH(k_dyn_cells2_b<6>, d.nCells, d, p);
@@ -3353,6 +3363,8 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   if (const char* fs = getenv("MPAS_DYCORE_FUSE_SMLSTEP")) g_fuse_smlstep = std::string(fs) != "0";
   g_mono_pairs = 1;
   if (const char* mp = getenv("MPAS_DYCORE_MONO_PAIRS")) g_mono_pairs = std::string(mp) != "0";
+  g_delsq_pair = 1;
+  if (const char* dp = getenv("MPAS_DYCORE_DELSQ_PAIR")) g_delsq_pair = std::string(dp) != "0";
   g_mono_fuse = MONO_FUSE_BOUNDS;
   if (const char* mf = getenv("MPAS_DYCORE_MONO_FUSE")) g_mono_fuse = std::atoi(mf);
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";

@@ -2281,6 +2281,77 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_diag_vertices_p(Dims d, Ptrs p
   }
 }
 
+// k_dyn_delsq_vc_b in the pair layout: each group of three wavefronts holds 2 PAIR_EPW vertices
+// (two wavefronts) and PAIR_EPW cells (one), the vertices 2c, 2c+1 next to cell c as there; two
+// levels per lane, 16-byte gathers of delsq_u; same expressions in the same order.  Launch over
+// PAIR_EPW * 3 * max(ceil(nVertices / (2 PAIR_EPW)), ceil(nCells / PAIR_EPW)) elements.
+template <int ME, bool ODD = false>
+__global__ __launch_bounds__(PAIR_THREADS) void k_dyn_delsq_vc_p(Dims d, Ptrs p) {
+  const int wv = pair_wave();
+  const int j3 = wv / 3, t3 = wv - 3 * j3;
+  const int K = d.K, h = pair_half(), l = pair_lane();
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  if (t3 < 2) {
+    const int vA = PAIR_EPW * (2 * j3 + t3);
+    if (vA >= d.nVertices) return;
+    const bool hasB = PAIR_EPW == 2 && vA + 1 < d.nVertices;
+    const int vB = hasB ? vA + 1 : vA;
+    const int v = sel(h, vA, vB);
+    int ei[3];
+    double cf[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int eA = p.edgesOnVertex[3 * vA + i], eB = p.edgesOnVertex[3 * vB + i];
+      // iat * dc * sg, left to right as k_dyn_delsq_vc_b
+      const double cA = ld_uniform_f64(p.invAreaTriangle + vA) * ld_uniform_f64(p.dcEdge + eA) *
+                        ld_uniform_f64(p.edgesOnVertex_sign + 3 * vA + i);
+      const double cB = ld_uniform_f64(p.invAreaTriangle + vB) * ld_uniform_f64(p.dcEdge + eB) *
+                        ld_uniform_f64(p.edgesOnVertex_sign + 3 * vB + i);
+      cf[i] = sel(h, cA, cB);
+      ei[i] = sel(h, eA, eB);
+    }
+    d2 du[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) du[i] = ld2(p.delsq_u + (size_t)ei[i] * K + 2 * lc);
+    d2 dv{0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      dv.x = dv.x + cf[i] * du[i].x;
+      dv.y = dv.y + cf[i] * du[i].y;
+    }
+    if ((h == 0 || hasB) && 2 * l < K) pst(p.delsq_vorticity + (size_t)v * K + 2 * lc, dv, two);
+  } else {
+    const int cA = PAIR_EPW * j3;
+    if (cA >= d.nCells) return;
+    const bool hasB = PAIR_EPW == 2 && cA + 1 < d.nCells;
+    const int cB = hasB ? cA + 1 : cA;
+    const int c = sel(h, cA, cB);
+    const CellSten<ME> sA = load_sten<ME>(p, cA), sB = load_sten<ME>(p, cB);
+    const double rA = ld_uniform_f64(p.invAreaCell + cA), rB = ld_uniform_f64(p.invAreaCell + cB);
+    const int ne = sel(h, sA.ne, sB.ne);
+    double cf[ME];
+    int ei[ME];
+#pragma unroll
+    for (int i = 0; i < ME; ++i) {
+      // r * dvEdge * edgesOnCell_sign (cell_sdv), as k_dyn_delsq_vc_b
+      cf[i] = sel(h, rA * ld_uniform_f64(p.cell_sdv + (size_t)cA * ME + i), rB * ld_uniform_f64(p.cell_sdv + (size_t)cB * ME + i));
+      ei[i] = sel(h, sA.e[i], sB.e[i]);
+    }
+    d2 du[ME];
+#pragma unroll
+    for (int i = 0; i < ME; ++i) du[i] = ld2(p.delsq_u + (size_t)ei[i] * K + 2 * lc);
+    d2 dd{0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < ME; ++i)
+      if (i < ne) {
+        dd.x = dd.x + cf[i] * du[i].x;
+        dd.y = dd.y + cf[i] * du[i].y;
+      }
+    if ((h == 0 || hasB) && 2 * l < K) pst(p.delsq_divergence + (size_t)c * K + 2 * lc, dd, two);
+  }
+}
+
 // k_diag_edges_b in the pair layout
 template <int NE2, bool ODD = false>
 __global__ __launch_bounds__(PAIR_THREADS) void k_diag_edges_p(Dims d, Ptrs p, const double* __restrict__ u,
