@@ -1936,6 +1936,8 @@ int g_kernel_tier = 2;
 // k_dyn_delsq_vc in the pair layout (MPAS_DYCORE_DELSQ_PAIR=0, read when a context is created: the
 // batched kernel)
 int g_delsq_pair = 1;
+// k_dyn_cells2 in the pair layout (MPAS_DYCORE_CELLS2_PAIR=0: the batched kernel)
+int g_cells2_pair = 1;
 inline bool batched(const Dims& d) {
   return g_kernel_tier >= 1 && (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
 }
@@ -2341,8 +2343,14 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
         }
       }
       LAUNCH(k_dyn_edges_rk1b_b, d.nEdgesSolve, d, p, cf, s, tp);
-      if (m6) LAUNCH(k_dyn_cells2_b<6>, d.nCells, d, p);
-      else LAUNCH(k_dyn_cells2_b<7>, d.nCells, d, p);
+      if (pair_layout(d) && g_cells2_pair) {
+        if (m6) LAUNCH_PE((k_dyn_cells2_p<6, false>), (k_dyn_cells2_p<6, true>), d.nCells, d, p);
+        else LAUNCH_PE((k_dyn_cells2_p<7, false>), (k_dyn_cells2_p<7, true>), d.nCells, d, p);
+      } else if (m6) {
+        LAUNCH(k_dyn_cells2_b<6>, d.nCells, d, p);
+      } else {
+        LAUNCH(k_dyn_cells2_b<7>, d.nCells, d, p);
+      }
     }
   }
   if (!batched(d)) LAUNCH(k_dyn_advflux, d.nEdges, d, p);
@@ -3365,6 +3373,8 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   if (const char* mp = getenv("MPAS_DYCORE_MONO_PAIRS")) g_mono_pairs = std::string(mp) != "0";
   g_delsq_pair = 1;
   if (const char* dp = getenv("MPAS_DYCORE_DELSQ_PAIR")) g_delsq_pair = std::string(dp) != "0";
+  g_cells2_pair = 1;
+  if (const char* cp = getenv("MPAS_DYCORE_CELLS2_PAIR")) g_cells2_pair = std::string(cp) != "0";
   g_mono_fuse = MONO_FUSE_BOUNDS;
   if (const char* mf = getenv("MPAS_DYCORE_MONO_FUSE")) g_mono_fuse = std::atoi(mf);
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";

@@ -2281,6 +2281,112 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_diag_vertices_p(Dims d, Ptrs p
   }
 }
 
+// k_dyn_cells2_b in the pair layout: two cells per wavefront, two levels per lane (16-byte gathers
+// of rho_edge at the cell's edges and of kdiff, w, theta_m at its neighbours); same expressions in the
+// same order.  Level 0 of delsq_w / tend_w_euler is 0 (the w fluxes start at level 1) and level K of
+// tend_w_euler is 0, as there.
+template <int ME, bool ODD = false>
+__global__ __launch_bounds__(PAIR_THREADS) void k_dyn_cells2_p(Dims d, Ptrs p) {
+  const int cA = PAIR_EPW * pair_wave();
+  if (cA >= d.nCells) return;
+  const bool hasB = PAIR_EPW == 2 && cA + 1 < d.nCells;
+  const int cB = hasB ? cA + 1 : cA;
+  const int K = d.K, h = pair_half(), l = pair_lane();
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const bool two = !ODD || 2 * l + 1 < K;  // odd K: the last pair holds level K-1 only
+  const int c = sel(h, cA, cB);
+  const size_t K1 = K + 1;
+  const CellSten<ME> sA = load_sten<ME>(p, cA), sB = load_sten<ME>(p, cB);
+  const double rA = ld_uniform_f64(p.invAreaCell + cA), rB = ld_uniform_f64(p.invAreaCell + cB);
+  const double prandtl_inv = 1.0 / PRANDTL;
+  const int ne = sel(h, sA.ne, sB.ne);
+  double est[ME], msd[ME];
+  int eo[ME], co[ME];
+  bool fi[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const int eA = sA.e[i], eB = sB.e[i];
+    const double sdA = ld_uniform_f64(p.cell_sdv + (size_t)cA * ME + i), sdB = ld_uniform_f64(p.cell_sdv + (size_t)cB * ME + i);
+    const double idA = ld_uniform_f64(p.invDcEdge + eA), idB = ld_uniform_f64(p.invDcEdge + eB);
+    const double mA = ld_uniform_f64(p.meshScalingDel2 + eA), mB = ld_uniform_f64(p.meshScalingDel2 + eB);
+    // r_areaCell*sign*dvEdge*invDcEdge; the w fluxes' 0.5*r_areaCell*... is 0.5 times it exactly (a
+    // power-of-two factor: ((0.5 r) s) i and 0.5 ((r s) i) round alike)
+    est[i] = sel(h, rA * sdA * idA, rB * sdB * idB);
+    msd[i] = sel(h, mA, mB);
+    eo[i] = sel(h, eA, eB);
+    co[i] = sel(h, sA.o[i], sB.o[i]);
+    fi[i] = h ? sB.first(i) : sA.first(i);
+  }
+  const d2 kds = ld2(p.kdiff + (size_t)c * K + 2 * lc), ws = ld2(p.w2 + (size_t)c * K1 + 2 * lc),
+           ths = ld2(p.theta_m2 + (size_t)c * K + 2 * lc);
+  // two passes (the w fluxes, then the theta fluxes, each summed in edge order as there): theta_m's
+  // gathers are issued after the w pass (fewer live registers: 138 VGPRs against 160 in one pass)
+  d2 re[ME], kdo[ME], wo[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    re[i] = ld2(p.rho_edge + (size_t)eo[i] * K + 2 * lc);
+    kdo[i] = ld2(p.kdiff + (size_t)co[i] * K + 2 * lc);
+    wo[i] = ld2(p.w2 + (size_t)co[i] * K1 + 2 * lc);
+  }
+  d2 dw{0.0, 0.0}, tw{0.0, 0.0}, dth{0.0, 0.0}, tth{0.0, 0.0};
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    // cellsOnEdge(1/2) of edge i: this cell and the one across, in the edge's order
+    const bool f = fi[i];
+    const d2 kd1 = f ? kds : kdo[i], kd2 = f ? kdo[i] : kds;
+    const d2 w1 = f ? ws : wo[i], w2 = f ? wo[i] : ws;
+    const d2 re_m = km1(re[i], l), kd1m = km1(kd1, l), kd2m = km1(kd2, l);
+    if (i < ne) {
+      const double esw = 0.5 * est[i];
+      double wtf = esw * (re[i].x + re_m.x) * (w2.x - w1.x);
+      dw.x = dw.x + wtf;
+      wtf = wtf * msd[i] * 0.25 * (kd1.x + kd2.x + kd1m.x + kd2m.x);
+      tw.x = tw.x + wtf;
+      wtf = esw * (re[i].y + re_m.y) * (w2.y - w1.y);
+      dw.y = dw.y + wtf;
+      wtf = wtf * msd[i] * 0.25 * (kd1.y + kd2.y + kd1m.y + kd2m.y);
+      tw.y = tw.y + wtf;
+    }
+  }
+  d2 tho[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) tho[i] = ld2(p.theta_m2 + (size_t)co[i] * K + 2 * lc);
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const bool f = fi[i];
+    const d2 kd1 = f ? kds : kdo[i], kd2 = f ? kdo[i] : kds;
+    const d2 t1 = f ? ths : tho[i], t2 = f ? tho[i] : ths;
+    if (i < ne) {
+      const double prs = prandtl_inv * msd[i];
+      double ttf = est[i] * (t2.x - t1.x) * re[i].x;
+      dth.x = dth.x + ttf;
+      ttf = ttf * 0.5 * (kd1.x + kd2.x) * prs;
+      tth.x = tth.x + ttf;
+      ttf = est[i] * (t2.y - t1.y) * re[i].y;
+      dth.y = dth.y + ttf;
+      ttf = ttf * 0.5 * (kd1.y + kd2.y) * prs;
+      tth.y = tth.y + ttf;
+    }
+  }
+  if (!(h == 0 || hasB)) return;
+  if (l == 0) {  // level 0: no w flux
+    dw.x = 0.0;
+    tw.x = 0.0;
+  }
+  if (2 * l < K) {
+    const size_t o = (size_t)c * K + 2 * lc;
+    pst(p.delsq_w + o, dw, two);
+    pst(p.delsq_theta + o, dth, two);
+    pst(p.tend_theta_euler + o, tth, two);
+  }
+  if (2 * l <= K) {  // tend_w_euler, levels 0..K (level K: 0)
+    double* tw_out = p.tend_w_euler + (size_t)c * K1 + 2 * l;
+    const double x = 2 * l < K ? tw.x : 0.0;
+    if (2 * l + 1 <= K) st2(tw_out, d2{x, 2 * l + 1 < K ? tw.y : 0.0});
+    else tw_out[0] = x;
+  }
+}
+
 // k_dyn_delsq_vc_b in the pair layout: each group of three wavefronts holds 2 PAIR_EPW vertices
 // (two wavefronts) and PAIR_EPW cells (one), the vertices 2c, 2c+1 next to cell c as there; two
 // levels per lane, 16-byte gathers of delsq_u; same expressions in the same order.  Launch over
