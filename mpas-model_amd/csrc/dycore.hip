@@ -1938,6 +1938,8 @@ int g_kernel_tier = 2;
 int g_delsq_pair = 1;
 // k_dyn_cells2 in the pair layout (MPAS_DYCORE_CELLS2_PAIR=0: the batched kernel)
 int g_cells2_pair = 1;
+// k_dyn_cells1 in the pair layout (MPAS_DYCORE_CELLS1_PAIR=0: the batched kernel)
+int g_cells1_pair = 1;
 inline bool batched(const Dims& d) {
   return g_kernel_tier >= 1 && (d.maxEdges == 6 || d.maxEdges == 7) && d.maxEdges2 >= 2 * d.maxEdges - 2;
 }
@@ -2304,6 +2306,10 @@ void dyn_tend(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, int rk_step, doub
   const bool bt = batched(d), m6 = d.maxEdges == 6;
   if (part != 2 && !(hdiv_done && rk_step > 1)) {
     if (!bt) LAUNCH(k_dyn_cells1, d.nCells, d, p, cf, s);
+    else if (pair_layout(d) && g_cells1_pair && m6)
+      LAUNCH_PE((k_dyn_cells1_p<6, false>), (k_dyn_cells1_p<6, true>), d.nCells, d, p, cf, s);
+    else if (pair_layout(d) && g_cells1_pair)
+      LAUNCH_PE((k_dyn_cells1_p<7, false>), (k_dyn_cells1_p<7, true>), d.nCells, d, p, cf, s);
     else if (m6) LAUNCH(k_dyn_cells1_b<6>, d.nCells, d, p, cf, s);
     else LAUNCH(k_dyn_cells1_b<7>, d.nCells, d, p, cf, s);
   }
@@ -3375,6 +3381,8 @@ int mpas_dyc_create_blocks(int32_t nblocks, const mpas_dyc_dims* dims, const mpa
   if (const char* dp = getenv("MPAS_DYCORE_DELSQ_PAIR")) g_delsq_pair = std::string(dp) != "0";
   g_cells2_pair = 1;
   if (const char* cp = getenv("MPAS_DYCORE_CELLS2_PAIR")) g_cells2_pair = std::string(cp) != "0";
+  g_cells1_pair = 1;
+  if (const char* c1 = getenv("MPAS_DYCORE_CELLS1_PAIR")) g_cells1_pair = std::string(c1) != "0";
   g_mono_fuse = MONO_FUSE_BOUNDS;
   if (const char* mf = getenv("MPAS_DYCORE_MONO_FUSE")) g_mono_fuse = std::atoi(mf);
   if (const char* fp = getenv("MPAS_DYCORE_FUSED_PACK")) ctx->fused_pack_enabled = std::string(fp) != "0";

@@ -2281,6 +2281,112 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_diag_vertices_p(Dims d, Ptrs p
   }
 }
 
+// k_dyn_cells1_b in the pair layout: two cells per wavefront, two levels per lane (16-byte gathers
+// of ru, and for the Smagorinsky kdiff of u and v, at the cell's edges); same expressions in the
+// same order.  rw has K+1 levels: with an even K its lanes run one further than the K-level fields'
+// (level K, which the top level's rw(k+1) reads).
+template <int ME, bool ODD = false>
+__global__ __launch_bounds__(PAIR_THREADS) void k_dyn_cells1_p(Dims d, Ptrs p, Config cf, DynTendScal s) {
+  const int cA = PAIR_EPW * pair_wave();
+  if (cA >= d.nCells) return;
+  const bool hasB = PAIR_EPW == 2 && cA + 1 < d.nCells;
+  const int cB = hasB ? cA + 1 : cA;
+  const int K = d.K, h = pair_half(), l = pair_lane();
+  const int lc = min(l, (ODD ? K + 1 : K) / 2 - 1);
+  const int lw = ODD ? lc : min(l, K / 2);  // rw: levels 0..K
+  const bool two = !ODD || 2 * l + 1 < K;   // odd K: the last pair holds level K-1 only
+  const int c = sel(h, cA, cB);
+  const size_t o = (size_t)c * K + 2 * lc;
+  const bool rk1 = s.rk_step == 1, smag = rk1 && cf.horiz_mixing_smag;
+  const CellSten<ME> sA = load_sten<ME>(p, cA), sB = load_sten<ME>(p, cB);
+  const int ne = sel(h, sA.ne, sB.ne);
+  double sdv[ME], da[ME], db[ME];
+  int ei[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    sdv[i] = sel(h, ld_uniform_f64(p.cell_sdv + (size_t)cA * ME + i), ld_uniform_f64(p.cell_sdv + (size_t)cB * ME + i));
+    da[i] = smag ? sel(h, ld_uniform_f64(p.defc_a + (size_t)cA * ME + i), ld_uniform_f64(p.defc_a + (size_t)cB * ME + i)) : 0.0;
+    db[i] = smag ? sel(h, ld_uniform_f64(p.defc_b + (size_t)cA * ME + i), ld_uniform_f64(p.defc_b + (size_t)cB * ME + i)) : 0.0;
+    ei[i] = sel(h, sA.e[i], sB.e[i]);
+  }
+  const double invA = sel(h, ld_uniform_f64(p.invAreaCell + cA), ld_uniform_f64(p.invAreaCell + cB));
+  d2 rwk{0.0, 0.0}, qt{0.0, 0.0}, rb{0.0, 0.0}, rps{0.0, 0.0};
+  if (rk1) {
+    rwk = ld2(p.rw + (size_t)c * (K + 1) + 2 * lw);
+    qt = ld2(p.qtot + o);
+    rb = ld2(p.rho_base + o);
+    rps = ld2(p.rho_p_save + o);
+  }
+  d2 rue[ME], ue[ME], ve[ME];
+#pragma unroll
+  for (int i = 0; i < ME; ++i) {
+    const size_t oe = (size_t)ei[i] * K + 2 * lc;
+    rue[i] = ld2(p.ru + oe);
+    ue[i] = smag ? ld2(p.u2 + oe) : d2{0.0, 0.0};
+    ve[i] = smag ? ld2(p.v + oe) : d2{0.0, 0.0};
+  }
+  const bool st = (h == 0 || hasB) && 2 * l < K;
+  // 2d Smagorinsky kdiff + cam filter (rk1, 4677-4720)
+  if (rk1) {
+    d2 kd;
+    if (smag) {
+      d2 dd{0.0, 0.0}, df{0.0, 0.0};
+#pragma unroll
+      for (int i = 0; i < ME; ++i) {
+        if (i < ne) {
+          dd.x = dd.x + da[i] * ue[i].x - db[i] * ve[i].x;
+          df.x = df.x + db[i] * ue[i].x + da[i] * ve[i].x;
+          dd.y = dd.y + da[i] * ue[i].y - db[i] * ve[i].y;
+          df.y = df.y + db[i] * ue[i].y + da[i] * ve[i].y;
+        }
+      }
+      const double csl = s.c_s * cf.len_disp;
+      const double cap = (0.01 * (cf.len_disp * cf.len_disp)) * s.invDt;
+      kd.x = fmin((csl * csl) * sqrt(dd.x * dd.x + df.x * df.x), cap);
+      kd.y = fmin((csl * csl) * sqrt(dd.y * dd.y + df.y * df.y), cap);
+    } else {
+      kd = d2{cf.h_theta_eddy_visc2, cf.h_theta_eddy_visc2};
+    }
+    if (cf.mpas_cam_coef > 0.0) {
+      const int k0 = 2 * l, k1 = 2 * l + 1;
+      const double c3 = 2.0833 * cf.len_disp * cf.mpas_cam_coef, c2 = 2.0 * 2.0833 * cf.len_disp * cf.mpas_cam_coef,
+                   c1 = 4.0 * 2.0833 * cf.len_disp * cf.mpas_cam_coef;
+      if (k0 == K - 3) kd.x = fmax(kd.x, c3);
+      if (k0 == K - 2) kd.x = fmax(kd.x, c2);
+      if (k0 == K - 1) kd.x = fmax(kd.x, c1);
+      if (k1 == K - 3) kd.y = fmax(kd.y, c3);
+      if (k1 == K - 2) kd.y = fmax(kd.y, c2);
+      if (k1 == K - 1) kd.y = fmax(kd.y, c1);
+    }
+    if (st) pst(p.kdiff + o, kd, two);
+  }
+  // h_divergence (4729-4748)
+  d2 hd{0.0, 0.0};
+#pragma unroll
+  for (int i = 0; i < ME; ++i)
+    if (i < ne) {  // edgesOnCell_sign * dvEdge * ru
+      hd.x = hd.x + sdv[i] * rue[i].x;
+      hd.y = hd.y + sdv[i] * rue[i].y;
+    }
+  hd.x = hd.x * invA;
+  hd.y = hd.y * invA;
+  if (st) pst(p.h_divergence + o, hd, two);
+  // tend_rho and dpdz (rk1, 4755-4766)
+  if (rk1) {
+    const d2 rwp = kp1(rwk);
+    const d2 rz = ld2(p.rdzw + 2 * lc);
+    d2 tr, dz;
+    tr.x = -hd.x - rz.x * (rwp.x - rwk.x) + PHYS(p.tend_rho_physics, o);
+    tr.y = -hd.y - rz.y * (rwp.y - rwk.y) + PHYS(p.tend_rho_physics, o + 1);
+    dz.x = -GRAVITY * (rb.x * (qt.x) + rps.x * (1. + qt.x));
+    dz.y = -GRAVITY * (rb.y * (qt.y) + rps.y * (1. + qt.y));
+    if (st) {
+      pst(p.tend_rho + o, tr, two);
+      pst(p.dpdz + o, dz, two);
+    }
+  }
+}
+
 // k_dyn_cells2_b in the pair layout: two cells per wavefront, two levels per lane (16-byte gathers
 // of rho_edge at the cell's edges and of kdiff, w, theta_m at its neighbours); same expressions in the
 // same order.  Level 0 of delsq_w / tend_w_euler is 0 (the w fluxes start at level 1) and level K of
