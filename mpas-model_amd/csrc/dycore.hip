@@ -2515,7 +2515,9 @@ void solve_diagnostics(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double d
   if (pair_layout(d)) {
     LAUNCH_PE((k_diag_vertices_p<false>), (k_diag_vertices_p<true>), d.nVertices, d, p, u, store_dv, uu_up,
               (tl == 1) ? p.u1 : p.u2);
-    // (a pair-layout k_diag_cells, two cells per wave, measured 18 % slower than the batched one)
+    // (a pair-layout k_diag_cells, two cells per wave, measured 18 % slower than the batched one; a
+    // round-5 version with the edge and vertex sums in two passes, 66 VGPRs, bitwise: 206 against
+    // 202 us per call, profiles/r05_ab_diag_cells_pair_rejected.log)
     if (d.maxEdges == 6) LAUNCH(k_diag_cells_b<6>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     else LAUNCH(k_diag_cells_b<7>, d.nCells, d, p, u, ctx->cf.apvm_upwinding, store_dv);
     const int64_t nw = d.nEdges;
