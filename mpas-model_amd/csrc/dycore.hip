@@ -2563,7 +2563,9 @@ void advance_scalars(mpas_dyc_ctx* ctx, const Dims& d, const Ptrs& p, double dt,
 void mono_prep(mpas_dyc_ctx* ctx, const std::vector<Ptrs>& P, double dt, bool advance_density) {
   for (size_t b = 0; b < ctx->blk.size(); ++b) {
     const Dims& d = ctx->blk[b].d;
-    LAUNCH(k_mono_prep, d.nCells, d, P[b], dt, advance_density ? 1 : 0);
+    if (!batched(d)) LAUNCH(k_mono_prep, d.nCells, d, P[b], dt, advance_density ? 1 : 0);
+    else if (d.maxEdges == 6) LAUNCH(k_mono_prep_b<6>, d.nCells, d, P[b], dt, advance_density ? 1 : 0);
+    else LAUNCH(k_mono_prep_b<7>, d.nCells, d, P[b], dt, advance_density ? 1 : 0);
   }
 }
 

@@ -4281,6 +4281,53 @@ __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_prep(Dims d, Ptrs p, dou
   }
 }
 
+// k_mono_prep for the batched families: the cell's edge record and every gather of ruAvg issued
+// before the sums (the general kernel's edge loop waits on each edge in turn), and without physics
+// the zeroed scalars_tend is not read back (its value there is 0.0 either way); same expressions in
+// the same order.
+template <int ME>
+__global__ __launch_bounds__(BLOCK_THREADS) void k_mono_prep_b(Dims d, Ptrs p, double dt, int advance_density) {
+  const int c = wave_elem(0);
+  const int k = lane_id(), K = d.K, ns = d.ns;
+  const bool act = k < K;
+  const int kc = min(k, K - 1);
+  const size_t K1 = K + 1;
+  if (c >= d.nCells) return;
+  const size_t o = (size_t)c * K + k;
+  if (c >= d.nCellsSolve) {  // rho_zz_int(:,iCell) = 0 on all cells (3772-3774)
+    if (advance_density && act) p.rho_zz_int[o] = 0.0;
+    return;
+  }
+  const CellSten<ME> st = load_sten<ME>(p, c);
+  double ra[ME], dv[ME];
+  if (advance_density) {
+#pragma unroll
+    for (int i = 0; i < ME; ++i) {
+      const int e = uni(st.e[i]);
+      ra[i] = p.ruAvg[(size_t)e * K + kc];
+      dv[i] = ld_uniform_f64(p.dvEdge + e);
+    }
+  }
+  if (act) {
+    const double rzo = p.rho_zz1[o];
+    for (int is = 0; is < ns; ++is) {
+      const size_t so = SIX(c, k, is);
+      const double tend = d.physics ? p.scalars_tend[so] : 0.0;  // 3743-3747: zeroed only without physics
+      p.scalars1[so] = p.scalars1[so] + dt * tend / rzo;
+      p.scalars_tend[so] = 0.0;
+    }
+  }
+  if (advance_density) {
+    double rzi = 0.0;
+    const double ia = ld_uniform_f64(p.invAreaCell + c);
+#pragma unroll
+    for (int i = 0; i < ME; ++i)
+      if (i < st.ne) rzi = rzi - st.sg(i) * ra[i] * dv[i] * ia;
+    const double wwa = (k <= K) ? p.wwAvg[(size_t)c * K1 + k] : 0.0, wwap = dn1(wwa);
+    if (act) p.rho_zz_int[o] = p.rho_zz1[o] + dt * (rzi - p.rdzw[k] * (wwap - wwa));
+  }
+}
+
 // per scalar iScalar, cells (solve): vertical flux and min/max bounds (3843-3908)
 __global__ __launch_bounds__(BLOCK_THREADS) void k_mono_bounds(Dims d, Ptrs p, int is, double coef_3rd_order) {
   const int c = wave_elem(0);
